@@ -1,0 +1,86 @@
+# mxk8s native build — gfx950 (MI355X) only.
+#
+#   make            build every native artefact in-tree
+#   make kernels    HIP kernel library  mxk8s/_lib/libmxkernels.so
+#   make node       C++ node library    mxk8s/_lib/libmxnode.so (+ CLIs in bin/)
+#   make tools      validator binaries  bin/mx-vector-add bin/mx-gemm-bench bin/mx-allreduce-perf
+#   make test-native  host unit tests of libmxnode (ASan+UBSan build)
+#
+# Everything lands inside the repo so `gpurun` snapshots carry it to the box.
+
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+CXX       ?= g++
+ARCH      ?= gfx950
+OUT_LIB   := mxk8s/_lib
+OUT_BIN   := bin
+BUILD     := build
+
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
+             -Inative/kernels
+CXXFLAGS  := -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -Inative/libmxnode
+LDLIBS_NODE := -ldl -lpthread
+
+KERNEL_SRCS := native/kernels/gemm_bf16.hip native/kernels/vector_add.hip \
+               native/kernels/fused_ops.hip
+KERNEL_OBJS := $(patsubst native/kernels/%.hip,$(BUILD)/kernels/%.o,$(KERNEL_SRCS))
+KERNEL_HDRS := $(wildcard native/kernels/*.h)
+
+NODE_SRCS := $(wildcard native/libmxnode/*.cc)
+NODE_OBJS := $(patsubst native/libmxnode/%.cc,$(BUILD)/node/%.o,$(NODE_SRCS))
+NODE_HDRS := $(wildcard native/libmxnode/*.h)
+
+.PHONY: all kernels node tools clean test-native
+all: kernels node tools
+
+kernels: $(OUT_LIB)/libmxkernels.so
+
+$(BUILD)/kernels/%.o: native/kernels/%.hip $(KERNEL_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OUT_LIB)/libmxkernels.so: $(KERNEL_OBJS)
+	@mkdir -p $(OUT_LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+# ---- node library + CLIs (plain C++17, no GPU needed to build or test) ----
+node: $(OUT_LIB)/libmxnode.so $(OUT_BIN)/mx-gpu-enum $(OUT_BIN)/mx-cdi-gen
+
+$(BUILD)/node/%.o: native/libmxnode/%.cc $(NODE_HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(OUT_LIB)/libmxnode.so: $(NODE_OBJS)
+	@mkdir -p $(OUT_LIB)
+	$(CXX) -shared -o $@ $^ $(LDLIBS_NODE)
+
+$(OUT_BIN)/mx-%: native/tools/mx_%.cc $(NODE_OBJS)
+	@mkdir -p $(OUT_BIN)
+	$(CXX) $(CXXFLAGS) -o $@ $< $(NODE_OBJS) $(LDLIBS_NODE)
+
+# ---- validator binaries (HIP / RCCL / rocBLAS) ----
+tools: $(OUT_BIN)/mx-vector-add $(OUT_BIN)/mx-gemm-bench $(OUT_BIN)/mx-allreduce-perf
+
+$(OUT_BIN)/mx-vector-add: native/tools/vector_add_main.hip $(BUILD)/kernels/vector_add.o $(KERNEL_HDRS)
+	@mkdir -p $(OUT_BIN)
+	$(HIPCC) $(HIPFLAGS) -o $@ $< $(BUILD)/kernels/vector_add.o
+
+$(OUT_BIN)/mx-gemm-bench: native/tools/gemm_bench_main.hip $(BUILD)/kernels/gemm_bf16.o $(KERNEL_HDRS)
+	@mkdir -p $(OUT_BIN)
+	$(HIPCC) $(HIPFLAGS) -o $@ $< $(BUILD)/kernels/gemm_bf16.o -L$(ROCM)/lib -lrocblas
+
+$(OUT_BIN)/mx-allreduce-perf: native/rccl_bench/allreduce_perf.cc
+	@mkdir -p $(OUT_BIN)
+	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -L$(ROCM)/lib -lrccl -lpthread
+
+# ---- host tests (sanitized) ----
+test-native: $(BUILD)/asan/test_mxnode
+	$(BUILD)/asan/test_mxnode tests/fixtures/sysfs
+
+$(BUILD)/asan/test_mxnode: native/libmxnode/tests/test_mxnode.cc $(NODE_SRCS) $(NODE_HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -g -fsanitize=address,undefined -fno-omit-frame-pointer -o $@ \
+	    native/libmxnode/tests/test_mxnode.cc $(NODE_SRCS) $(LDLIBS_NODE)
+
+clean:
+	rm -rf $(BUILD) $(OUT_LIB)/*.so $(OUT_BIN)

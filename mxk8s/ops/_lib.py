@@ -1,0 +1,86 @@
+"""ctypes binding to the in-tree HIP kernel library ``mxk8s/_lib/libmxkernels.so``.
+
+The kernels are plain C-ABI launchers (``native/kernels/*.hip``) that take raw
+device pointers and a ``hipStream_t``.  Binding them with ctypes instead of a
+torch C++ extension keeps the build to one ``hipcc`` link (seconds, no torch
+headers) and lets the same ``.so`` serve the standalone validator binaries.
+
+There is deliberately NO silent fallback for GPU tensors: if the library is
+missing or a launch fails, the op raises.  CPU tensors take the PyTorch
+reference path (that is what the CPU test tier exercises).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
+KERNEL_LIB_PATH = os.path.join(_LIB_DIR, "libmxkernels.so")
+
+_lock = threading.Lock()
+_lib = None
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_l = ctypes.c_long
+_f = ctypes.c_float
+_fp = ctypes.POINTER(ctypes.c_float)
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "mxk_gemm_bf16_tn": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp]),
+    "mxk_gemm_bf16_tn_is_fast": (_i, [_i, _i, _i]),
+    "mxk_vector_add_f32": (_i, [_vp, _vp, _vp, _l, _vp]),
+    "mxk_vector_add_bf16": (_i, [_vp, _vp, _vp, _l, _vp]),
+    "mxk_error_string": (ctypes.c_char_p, [_i]),
+    "mxk_rmsnorm_fwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _f, _vp]),
+    "mxk_rmsnorm_bwd_workspace": (_l, [_i, _i]),
+    "mxk_rmsnorm_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
+    "mxk_swiglu_fwd": (_i, [_vp, _vp, _l, _i, _vp]),
+    "mxk_swiglu_bwd": (_i, [_vp, _vp, _vp, _l, _i, _vp]),
+    "mxk_rope": (_i, [_vp, _vp, _vp, _vp, _l, _i, _i, _i, _f, _vp]),
+}
+
+
+class KernelLibraryMissing(RuntimeError):
+    pass
+
+
+def kernels_available() -> bool:
+    return os.path.exists(KERNEL_LIB_PATH)
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the kernel library; raise if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(KERNEL_LIB_PATH):
+            raise KernelLibraryMissing(
+                f"{KERNEL_LIB_PATH} not built: run `make kernels` (or "
+                "`python -c 'import __graft_entry__ as g; g.build()'`)")
+        # torch must be loaded first so libamdhip64.so.7 is already resident and
+        # our NEEDED entry binds to the same HIP runtime instance as torch.
+        import torch  # noqa: F401
+        handle = ctypes.CDLL(KERNEL_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = lib().mxk_error_string(status)
+        raise RuntimeError(f"{what} failed: hip error {status} ({msg.decode() if msg else '?'})")
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

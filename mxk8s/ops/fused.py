@@ -1,0 +1,171 @@
+"""Fused RMSNorm / SwiGLU / RoPE with autograd (``native/kernels/fused_ops.hip``).
+
+Each op has a native HIP forward and backward for GPU tensors and a PyTorch
+fp32 reference for CPU tensors (``*_ref``), which the numerics tests compare
+the kernels against.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+# ----------------------------------------------------------------------------
+# references (fp32 math, output in the input dtype)
+# ----------------------------------------------------------------------------
+
+
+def rmsnorm_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    rstd = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (xf * rstd * w.float()).to(x.dtype)
+
+
+def swiglu_ref(gu: torch.Tensor) -> torch.Tensor:
+    g, u = gu.float().chunk(2, dim=-1)
+    return (torch.nn.functional.silu(g) * u).to(gu.dtype)
+
+
+def rope_tables(seq_len: int, head_dim: int, theta: float = 500000.0,
+                device=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """cos/sin tables [S, D/2] fp32 (host-precomputed; no device trig)."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    ang = torch.arange(seq_len, dtype=torch.float64)[:, None] * inv[None, :]
+    return (ang.cos().float().contiguous().to(device), ang.sin().float().contiguous().to(device))
+
+
+def rope_ref(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, sign: float = 1.0) -> torch.Tensor:
+    """x: [B, S, H, D]; rotate-half pairing (i, i + D/2)."""
+    S = x.shape[1]
+    xf = x.float()
+    half = x.shape[-1] // 2
+    a, b = xf[..., :half], xf[..., half:]
+    c = cos[:S].float()[None, :, None, :]
+    s = sign * sin[:S].float()[None, :, None, :]
+    return torch.cat([a * c - b * s, b * c + a * s], dim=-1).to(x.dtype)
+
+
+# ----------------------------------------------------------------------------
+# RMSNorm
+# ----------------------------------------------------------------------------
+
+
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        H = x.shape[-1]
+        x2 = x.contiguous().view(-1, H)
+        rows = x2.shape[0]
+        y = torch.empty_like(x2)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        st = _lib.lib().mxk_rmsnorm_fwd(x2.data_ptr(), w.data_ptr(), y.data_ptr(),
+                                        rstd.data_ptr(), rows, H, float(eps),
+                                        _lib.stream_ptr(x.device))
+        _lib.check(st, "mxk_rmsnorm_fwd")
+        ctx.save_for_backward(x2, w, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, rstd = ctx.saved_tensors
+        rows, H = x2.shape
+        dy2 = dy.contiguous().view(rows, H)
+        dx = torch.empty_like(x2)
+        dw = torch.empty_like(w)
+        L = _lib.lib()
+        ws = torch.empty(L.mxk_rmsnorm_bwd_workspace(rows, H) // 4, dtype=torch.float32,
+                         device=x2.device)
+        st = L.mxk_rmsnorm_bwd(dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), rstd.data_ptr(),
+                               dx.data_ptr(), dw.data_ptr(), None, ws.data_ptr(), rows, H,
+                               _lib.stream_ptr(x2.device))
+        _lib.check(st, "mxk_rmsnorm_bwd")
+        return dx.view(ctx.shape), dw, None
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    if x.device.type == "cpu" or x.dtype != torch.bfloat16:
+        xf = x.float()
+        rstd = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+        return (xf * rstd * w.float()).to(x.dtype)
+    return _RMSNorm.apply(x, w, eps)
+
+
+# ----------------------------------------------------------------------------
+# SwiGLU over a fused [.., 2F] gate|up tensor
+# ----------------------------------------------------------------------------
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        F2 = gu.shape[-1]
+        F = F2 // 2
+        g2 = gu.contiguous().view(-1, F2)
+        rows = g2.shape[0]
+        h = torch.empty((rows, F), dtype=gu.dtype, device=gu.device)
+        st = _lib.lib().mxk_swiglu_fwd(g2.data_ptr(), h.data_ptr(), rows, F,
+                                       _lib.stream_ptr(gu.device))
+        _lib.check(st, "mxk_swiglu_fwd")
+        ctx.save_for_backward(g2)
+        ctx.shape = gu.shape
+        return h.view(*gu.shape[:-1], F)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (g2,) = ctx.saved_tensors
+        rows, F2 = g2.shape
+        dgu = torch.empty_like(g2)
+        dh2 = dh.contiguous().view(rows, F2 // 2)
+        st = _lib.lib().mxk_swiglu_bwd(g2.data_ptr(), dh2.data_ptr(), dgu.data_ptr(), rows,
+                                       F2 // 2, _lib.stream_ptr(g2.device))
+        _lib.check(st, "mxk_swiglu_bwd")
+        return dgu.view(ctx.shape)
+
+
+def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    if gu.device.type == "cpu" or gu.dtype != torch.bfloat16:
+        g, u = gu.chunk(2, dim=-1)
+        return torch.nn.functional.silu(g) * u
+    return _SwiGLU.apply(gu)
+
+
+# ----------------------------------------------------------------------------
+# RoPE on [B, S, H, D]
+# ----------------------------------------------------------------------------
+
+
+def _rope_launch(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, sign: float) -> torch.Tensor:
+    B, S, H, D = x.shape
+    xc = x.contiguous()
+    y = torch.empty_like(xc)
+    st = _lib.lib().mxk_rope(xc.data_ptr(), y.data_ptr(), cos.data_ptr(), sin.data_ptr(),
+                             B * S, H, D, S, float(sign), _lib.stream_ptr(x.device))
+    _lib.check(st, "mxk_rope")
+    return y
+
+
+class _RoPE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin):
+        ctx.save_for_backward(cos, sin)
+        return _rope_launch(x, cos, sin, 1.0)
+
+    @staticmethod
+    def backward(ctx, dy):
+        cos, sin = ctx.saved_tensors
+        return _rope_launch(dy, cos, sin, -1.0), None, None
+
+
+def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """Apply rotary embedding to x [B, S, H, D] with tables [>=S, D/2]."""
+    if x.device.type == "cpu" or x.dtype != torch.bfloat16:
+        return rope_ref(x, cos, sin)
+    S = x.shape[1]
+    cos_s = cos[:S].contiguous()
+    sin_s = sin[:S].contiguous()
+    return _RoPE.apply(x, cos_s, sin_s)
+
+
+__all__ = ["rmsnorm", "swiglu", "rope", "rope_tables", "rmsnorm_ref", "swiglu_ref",
+           "rope_ref"]

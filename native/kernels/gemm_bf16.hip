@@ -1,0 +1,268 @@
+// CDNA4 bf16 MFMA GEMM — the validator's compute payload (BASELINE config 3).
+//
+//   C[M][N] (bf16) = A[M][K] (bf16, row-major) · Bt[N][K]^T (bf16, row-major)
+//   fp32 accumulation in the MFMA accumulators.
+//
+// "Bt" is the nn.Linear weight layout ([out][in]); both operands are read
+// K-contiguous, which is what the MFMA A/B lane maps want, so neither tile
+// needs a transpose on the way into LDS.
+//
+// Design (MI355X-first, see /opt/skills/guides/cdna_hip_programming.md §5):
+//  * 256x256 macro tile, BK = 64, 512 threads = 8 waves laid out 2 (M) x 4 (N);
+//    each wave owns a 128 x 64 output block = 8 x 4 tiles of 16x16.
+//  * v_mfma_f32_16x16x32_bf16: on random data this shape holds a higher clock
+//    than 32x32x16 at equal cycles/FLOP (MI355X_MICROARCH 'DVFS give-back' 7).
+//  * Operands are swapped in the MFMA (D' = Bt·A^T) so every lane ends up
+//    holding 4 consecutive N-columns of one C row -> one 8-byte store per
+//    16x16 tile instead of four 2-byte stores.
+//  * Global -> LDS by LDS-DMA (global_load_lds_dwordx4): the LDS image is
+//    lane-linear, so the bank-conflict swizzle is applied to the per-lane
+//    SOURCE address and undone on the ds_read address (rule 21).
+//    Swizzle: 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7); every
+//    16-lane ds_read_b128 group then touches 16 distinct 16-B bank slots
+//    (checked by tests/test_gemm_swizzle.py against the §LDS lane groups).
+//  * Phased software pipeline: each 64-deep K tile is split into four phases
+//    (k-step x M-half, 16 MFMAs each); every phase issues one quarter of the
+//    NEXT K tile's LDS-DMA (one glds per operand per thread) right after its
+//    fragment reads, so the DMA streams under the MFMAs.  Two 64 KiB stages
+//    (128 KiB LDS, 1 workgroup/CU); one wait + raw s_barrier per K tile.
+//  * XCD-aware bijective block remap + GROUP_M tile ordering so the blocks
+//    that share an XCD's L2 share A/B panels (T1).
+#include "mx_common.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int NTHREADS = 512;
+constexpr int TILE_BYTES = BM * BK * 2;          // 32 KiB per operand per stage
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;      // A + B
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;       // double buffered: 128 KiB
+constexpr int GROUP_M = 8;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// One quarter of an operand tile (64 rows x 64 k = 8 KiB) per call:
+// 512 lanes x 16 B.  Lane t of the block writes LDS bytes [q*8192 + t*16, +16)
+// (lane-linear per wave: wave base + lane*16), i.e. row q*64 + t/8, physical
+// chunk t%8, which must hold logical chunk (t%8) ^ ((row>>1)&7).
+__device__ __forceinline__ void stage_quarter(const uint16_t* __restrict__ src, int ld,
+                                              int row0, int k0, char* lds_tile,
+                                              int q, int tid) {
+  const int row = q * 64 + (tid >> 3);
+  const int pc = tid & 7;
+  const int c = pc ^ ((row >> 1) & 7);
+  const uint16_t* g = src + static_cast<size_t>(row0 + row) * ld + k0 + c * 8;
+  char* dst = lds_tile + q * 8192 + (tid >> 6) * 1024;   // wave-uniform base
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)dst, 16, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8_t lds_read_b128(const char* p) {
+  return *reinterpret_cast<const bf16x8_t*>(p);
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(NTHREADS, 2)
+mxk_gemm_bf16_tn_256x256(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                         uint16_t* __restrict__ C, int M, int N, int K,
+                         int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2;   // 0..1 -> 128 rows each
+  const int wn = wave & 3;    // 0..3 -> 64 cols each
+
+  // ---- block -> output tile (XCD remap, then GROUP_M swizzle) ----
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int wgid = mxk::xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  const int tm = first_m + in_group % gsize;
+  const int tn = in_group / gsize;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- fragment read offsets (bytes, within a 16-row block of a tile) ----
+  // lane l reads row (l & 15), logical chunk ks*4 + (l >> 4), stored at
+  // physical chunk (ks*4 + (l>>4)) ^ ((l & 15) >> 1).
+  const int frow = lane & 15;
+  const int fch0 = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch0 * 16;
+  const int off_k1 = frow * 128 + (fch0 ^ 4) * 16;
+  const int a_wave = wm * 128 * 128;   // byte offset of this wave's first A row
+  const int b_wave = wn * 64 * 128;
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = K / BK;
+
+  // prologue: stage K tile 0 into buffer 0
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    stage_quarter(A, lda, m0, 0, smem, q, tid);
+    stage_quarter(Bt, ldb, n0, 0, smem + TILE_BYTES, q, tid);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int t = 0; t < nt; ++t) {
+    char* cur = smem + (t & 1) * STAGE_BYTES;
+    char* nxt = smem + ((t + 1) & 1) * STAGE_BYTES;
+    const bool more = (t + 1) < nt;
+    const int kn = (t + 1) * BK;
+    const char* As = cur + a_wave;
+    const char* Bs = cur + TILE_BYTES + b_wave;
+
+    // Four phases: (ks, m-half).  Each phase prefetches one quarter of the
+    // next K tile (A quarter + B quarter) ahead of its 16 MFMAs.
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int ks = ph >> 1;
+      const int mh = ph & 1;
+      const int koff = ks ? off_k1 : off_k0;
+      bf16x8_t a[4], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = lds_read_b128(Bs + j * 2048 + koff);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = lds_read_b128(As + (mh * 4 + i) * 2048 + koff);
+      if (more) {
+        stage_quarter(A, lda, m0, kn, nxt, ph, tid);
+        stage_quarter(Bt, ldb, n0, kn, nxt + TILE_BYTES, ph, tid);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[mh * 4 + i][j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[mh * 4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    // Retire the next tile's DMA (issued by this wave), then a barrier so every
+    // wave's DMA has landed and every wave is done reading `cur` before it is
+    // overwritten by the tile after next.
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // ---- epilogue: lane holds C[m][n..n+3] for each 16x16 tile ----
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + crow;
+    uint16_t* crow_ptr = C + static_cast<size_t>(m) * ldc + n0 + wn * 64 + ccol;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4_t v = acc[i][j];
+      uint2 pk;
+      pk.x = mxk::pack2bf(v[0], v[1]);
+      pk.y = mxk::pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(crow_ptr + j * 16) = pk;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generic bounds-checked MFMA GEMM (any M, N, K; K-contiguous operands).
+// 64x64 tile, 256 threads (2x2 waves of 32x32), register-staged through LDS.
+// Used for shapes the 256x256 kernel does not tile exactly.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                         uint16_t* __restrict__ C, int M, int N, int K,
+                         int lda, int ldb, int ldc) {
+  constexpr int T = 64, TK = 32;
+  __shared__ __attribute__((aligned(16))) uint16_t sA[T][TK + 8];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[T][TK + 8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * T, n0 = blockIdx.x * T;
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < K; k0 += TK) {
+    // 64 rows x 32 k per operand = 2048 elements; 256 threads x 8 elements.
+    {
+      const int r = tid >> 2, c = (tid & 3) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int gm = m0 + r, gk = k0 + c + e;
+        sA[r][c + e] = (gm < M && gk < K) ? A[static_cast<size_t>(gm) * lda + gk] : 0;
+        const int gn = n0 + r;
+        sB[r][c + e] = (gn < N && gk < K) ? Bt[static_cast<size_t>(gn) * ldb + gk] : 0;
+      }
+    }
+    __syncthreads();
+    const int fr = lane & 15, fk = (lane >> 4) * 8;
+    bf16x8_t a[2], b[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a[i][e] = static_cast<short>(sA[wm * 32 + i * 16 + fr][fk + e]);
+        b[i][e] = static_cast<short>(sB[wn * 32 + i * 16 + fr][fk + e]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+    __syncthreads();
+  }
+  const int crow = lane & 15, ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m = m0 + wm * 32 + i * 16 + crow;
+      if (m >= M) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 32 + j * 16 + ccol + r;
+        if (n < N) C[static_cast<size_t>(m) * ldc + n] = mxk::f2bf(acc[i][j][r]);
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers (C ABI, stream-ordered, capture-safe: no sync, no malloc).
+// ---------------------------------------------------------------------------
+MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,
+                             int lda, int ldb, int ldc, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return static_cast<int>(hipErrorInvalidValue);
+  const bool fast = (M % BM == 0) && (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) &&
+                    (ldb % 8 == 0) && (ldc % 4 == 0) &&
+                    (reinterpret_cast<uintptr_t>(A) % 16 == 0) &&
+                    (reinterpret_cast<uintptr_t>(Bt) % 16 == 0) &&
+                    (reinterpret_cast<uintptr_t>(C) % 8 == 0);
+  if (fast) {
+    const int nwg = (M / BM) * (N / BN);
+    hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256, dim3(nwg), dim3(NTHREADS), 0, stream,
+                       static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
+                       static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
+  } else {
+    dim3 grid((N + 63) / 64, (M + 63) / 64);
+    hipLaunchKernelGGL(mxk_gemm_bf16_tn_generic, grid, dim3(256), 0, stream,
+                       static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
+                       static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
+  }
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// 1 if (M, N, K) takes the tiled MFMA fast path.
+MXK_API int mxk_gemm_bf16_tn_is_fast(int M, int N, int K) {
+  return (M % BM == 0) && (N % BN == 0) && (K % BK == 0);
+}

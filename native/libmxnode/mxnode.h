@@ -1,0 +1,138 @@
+// libmxnode — MI355X node discovery / CDI / allocation / health / metrics core.
+//
+// Plain C ABI so the same shared object serves the Python device plugin,
+// labeller and exporter (ctypes) and the C++ CLIs (mx-gpu-enum, mx-cdi-gen).
+//
+// Every host path is taken relative to a caller-supplied ROOT ("" or "/" for
+// the real host), so all of it is testable against fake sysfs trees
+// (tests/fixtures/sysfs/*) without root, a cluster or a GPU.
+//
+// Replaces, MI355X-first, the native pieces the reference's runbook pulls in
+// through the NVIDIA GPU Operator (/root/reference/README.md:264-272):
+// NVML enumeration (device plugin + GFD), libnvidia-container / nvidia-ctk
+// (README.md:138-149), NVML Xid health, DCGM sampling.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MX_MAX_GPUS 64
+#define MX_MAX_LINKS 64
+
+typedef struct mx_gpu_info {
+  int index;                    // 0..n-1, ordered by DRM render minor (HIP order)
+  int kfd_node;                 // /sys/class/kfd/kfd/topology/nodes/<kfd_node>
+  uint32_t gpu_id;              // KFD gpu_id
+  uint32_t gfx_target_version;  // e.g. 90500 for gfx950
+  char gfx_arch[16];            // "gfx950"
+  int drm_render_minor;         // 128 + i -> /dev/dri/renderD<minor>
+  int drm_card;                 // /dev/dri/card<drm_card>, -1 if unknown
+  uint32_t vendor_id;           // 0x1002
+  uint32_t device_id;           // PCI device id
+  uint32_t domain;
+  uint32_t location_id;         // bus << 8 | dev << 3 | fn
+  char pci_bdf[20];             // "0000:05:00.0"
+  int numa_node;                // -1 if unknown
+  uint32_t simd_count;
+  uint32_t simd_per_cu;
+  uint32_t cu_count;
+  uint64_t vram_bytes;          // sum of KFD mem_banks (local heap)
+  uint64_t unique_id;
+  uint64_t hive_id;             // xGMI hive id (0 if none)
+  uint32_t max_engine_clk_mhz;
+  int num_xgmi_links;
+  char product[48];             // "MI355X", from the device-id table
+  char uuid[40];                // "GPU-<unique_id hex>"
+} mx_gpu_info;
+
+typedef struct mx_link {
+  int from_index;
+  int to_index;                 // GPU index of the peer, -1 if the peer is a CPU node
+  int type;                     // KFD io_link type: 2 = PCIe, 11 = xGMI
+  uint32_t weight;
+  uint32_t min_bandwidth_mbps;
+  uint32_t max_bandwidth_mbps;
+} mx_link;
+
+// Library version string.
+const char* mx_version(void);
+
+// Enumerate AMD GPUs under ROOT.  Returns the count (>= 0) or -1 on error
+// (message in err).  Fills at most `max` entries.
+int mx_enumerate(const char* root, mx_gpu_info* out, int max, char* err, size_t errlen);
+
+// GPU<->GPU and GPU->CPU io_links.  Returns the number of links written.
+int mx_links(const char* root, mx_link* out, int max, char* err, size_t errlen);
+
+// Write the CDI spec (JSON, cdiVersion 0.6.0, kind `kind`, e.g. "amd.com/gpu")
+// into buf.  Returns the full length needed (excluding NUL) or -1 on error;
+// if the return is >= buflen the output was truncated.
+long mx_cdi_spec(const char* root, const char* kind, char* buf, size_t buflen, char* err,
+                 size_t errlen);
+
+// Preferred allocation (kubelet GetPreferredAllocation):
+// choose `size` GPU indices from `available` (must contain all of
+// `must_include`), preferring one xGMI hive, then the fewest NUMA nodes, then
+// the most xGMI-connected set, then the lowest indices.  Writes `size`
+// indices (ascending) into out; returns size or -1.
+int mx_preferred_allocation(const char* root, const int* available, int navail,
+                            const int* must_include, int nmust, int size, int* out, char* err,
+                            size_t errlen);
+
+// Same policy over explicit topology arrays (no sysfs): numa[i], hive[i] and a
+// row-major n x n xGMI adjacency matrix for device ids 0..n-1.
+int mx_preferred_allocation_topo(int n, const int* numa, const uint64_t* hive,
+                                 const int* xgmi_adj, const int* available, int navail,
+                                 const int* must_include, int nmust, int size, int* out);
+
+// Health of GPU `index`: 0 = healthy, >0 = reason code (see MX_UNHEALTHY_*).
+// Checks: KFD node still present, render node present under ROOT/dev/dri,
+// and the optional fault-injection file (one index per line, or "all").
+#define MX_HEALTHY 0
+#define MX_UNHEALTHY_NO_KFD_NODE 1
+#define MX_UNHEALTHY_NO_RENDER_NODE 2
+#define MX_UNHEALTHY_FAULT_INJECTED 3
+#define MX_UNHEALTHY_SMI_EVENT 4
+#define MX_UNHEALTHY_ECC 5
+int mx_health_check(const char* root, int index, const char* fault_file);
+const char* mx_health_reason(int code);
+
+// ---- amd-smi backed sampling (dlopen("libamd_smi.so"); no link dependency) ----
+typedef struct mx_gpu_sample {
+  int index;
+  int valid;                        // 0 if amd-smi could not sample this GPU
+  uint32_t gfx_activity_pct;
+  uint32_t umc_activity_pct;
+  uint64_t vram_used_bytes;
+  uint64_t vram_total_bytes;
+  int64_t temp_edge_mc;             // milli-degrees C, INT64_MIN if unsupported
+  int64_t temp_hotspot_mc;
+  int64_t temp_mem_mc;
+  uint64_t power_w;
+  uint32_t power_limit_w;
+  uint32_t sclk_mhz;
+  uint32_t mclk_mhz;
+  uint64_t ecc_correctable;
+  uint64_t ecc_uncorrectable;
+  uint32_t num_processes;
+  char bdf[20];
+} mx_gpu_sample;
+
+// 1 if amd-smi could be loaded and initialised, 0 otherwise (msg in err).
+int mx_smi_open(char* err, size_t errlen);
+void mx_smi_close(void);
+// Number of GPUs amd-smi sees (after mx_smi_open), -1 if not open.
+int mx_smi_count(void);
+// Sample GPU i (amd-smi enumeration order, matched to BDF by the caller).
+int mx_smi_sample(int i, mx_gpu_sample* out);
+// Block up to timeout_ms for amd-smi GPU events (reset / thermal / VM fault).
+// Writes up to `max` (gpu_bdf_index, event_code) pairs; returns count or -1.
+int mx_smi_wait_events(int timeout_ms, int* gpu_out, int* event_out, int max);
+const char* mx_smi_driver_version(void);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,131 @@
+"""Numerics of the hand-written HIP kernels vs plain PyTorch fp32 references.
+
+All tests here need an MI355X (``-m gpu``); they run the native kernels only
+(the loader raises if libmxkernels.so is missing — no silent fallback).
+"""
+import pytest
+import torch
+
+from mxk8s.ops import gemm_bf16_tn, vector_add, rmsnorm, swiglu, rope, rope_tables
+from mxk8s.ops.fused import rmsnorm_ref, swiglu_ref, rope_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(shape, dev, seed, scale=1.0):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    return ((torch.rand(shape, device=dev, generator=g) * 2 - 1) * scale)
+
+
+@pytest.mark.parametrize("n", [1, 3, 50000, 1 << 20, (1 << 20) + 5])
+def test_vector_add_f32_exact(cuda_device, n):
+    a = _rand((n,), cuda_device, 1)
+    b = _rand((n,), cuda_device, 2)
+    c = vector_add(a, b)
+    assert torch.equal(c.cpu(), a.cpu() + b.cpu())
+
+
+def test_vector_add_bf16(cuda_device):
+    n = (1 << 20) + 7
+    a = _rand((n,), cuda_device, 3).bfloat16()
+    b = _rand((n,), cuda_device, 4).bfloat16()
+    c = vector_add(a, b)
+    ref = (a.float() + b.float()).bfloat16()
+    assert torch.equal(c, ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 256), (1024, 1024, 1024),
+                                   (2048, 4096, 512)])
+def test_gemm_fast_path_vs_fp32(cuda_device, M, N, K):
+    a = _rand((M, K), cuda_device, 5).bfloat16()
+    bt = _rand((N, K), cuda_device, 6).bfloat16()
+    c = gemm_bf16_tn(a, bt)
+    ref = a.float() @ bt.float().t()
+    err = (c.float() - ref).abs().max().item()
+    # bf16 output rounding: |ref| <= K, relative 2^-8
+    assert err <= ref.abs().max().item() * 2 ** -7 + 1e-3, err
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (17, 33, 65), (100, 300, 200), (255, 257, 63)])
+def test_gemm_generic_path_vs_fp32(cuda_device, M, N, K):
+    a = _rand((M, K), cuda_device, 7).bfloat16()
+    bt = _rand((N, K), cuda_device, 8).bfloat16()
+    c = gemm_bf16_tn(a, bt)
+    ref = a.float() @ bt.float().t()
+    err = (c.float() - ref).abs().max().item()
+    assert err <= ref.abs().max().item() * 2 ** -7 + 1e-3, err
+
+
+def test_gemm_identity_asymmetric(cuda_device):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    n = 512
+    a = torch.eye(n, device=cuda_device, dtype=torch.bfloat16)
+    idx = torch.arange(n, device=cuda_device, dtype=torch.float32)
+    bt = ((idx[:, None] * 3 + idx[None, :] * 0.5) % 64).bfloat16()   # bt[j][k]
+    c = gemm_bf16_tn(a, bt)   # c[i][j] = sum_k I[i][k] bt[j][k] = bt[j][i]
+    assert torch.equal(c, bt.t().contiguous())
+
+
+def test_gemm_exact_integers(cuda_device):
+    M, N, K = 512, 512, 512
+    g = torch.Generator(device=cuda_device)
+    g.manual_seed(9)
+    a = torch.randint(-2, 3, (M, K), device=cuda_device, generator=g).bfloat16()
+    bt = torch.randint(-2, 3, (N, K), device=cuda_device, generator=g).bfloat16()
+    c = gemm_bf16_tn(a, bt)
+    ref = (a.double() @ bt.double().t())
+    # |ref| <= 2048 < 2^8 * 8 -> integers up to 256 exact in bf16; compare in bf16
+    assert torch.equal(c, ref.float().bfloat16())
+
+
+def test_gemm_large_vs_hipblaslt(cuda_device):
+    M = N = K = 4096
+    a = _rand((M, K), cuda_device, 10).bfloat16()
+    bt = _rand((N, K), cuda_device, 11).bfloat16()
+    c = gemm_bf16_tn(a, bt).float()
+    ref = torch.matmul(a, bt.t()).float()
+    rel = ((c - ref).norm() / ref.norm()).item()
+    assert rel <= 1e-2, rel
+
+
+@pytest.mark.parametrize("rows,H", [(1, 4096), (7, 4096), (2048, 4096), (33, 2048), (5, 8192), (3, 128)])
+def test_rmsnorm_fwd_bwd(cuda_device, rows, H):
+    x = _rand((rows, H), cuda_device, 12, 3.0).bfloat16().requires_grad_()
+    w = (1 + 0.1 * _rand((H,), cuda_device, 13)).bfloat16().requires_grad_()
+    y = rmsnorm(x, w, 1e-5)
+    assert (y.float() - rmsnorm_ref(x.detach(), w.detach(), 1e-5).float()).abs().max() < 3e-2
+    dy = _rand((rows, H), cuda_device, 14).bfloat16()
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    yr.backward(dy.float())
+    assert (x.grad.float() - xr.grad).abs().max() <= 2e-2 * xr.grad.abs().max() + 1e-3
+    assert (w.grad.float() - wr.grad).abs().max() <= 2e-2 * wr.grad.abs().max() + 1e-3
+
+
+@pytest.mark.parametrize("rows,F", [(1, 8), (2048, 14336), (3, 1000)])
+def test_swiglu_fwd_bwd(cuda_device, rows, F):
+    gu = _rand((rows, 2 * F), cuda_device, 15, 4.0).bfloat16().requires_grad_()
+    h = swiglu(gu)
+    assert (h.float() - swiglu_ref(gu.detach()).float()).abs().max() <= 0.05
+    dh = _rand((rows, F), cuda_device, 16).bfloat16()
+    h.backward(dh)
+    gr = gu.detach().float().requires_grad_()
+    g, u = gr.chunk(2, -1)
+    (torch.nn.functional.silu(g) * u).backward(dh.float())
+    assert (gu.grad.float() - gr.grad).abs().max() <= 2e-2 * gr.grad.abs().max() + 1e-2
+
+
+@pytest.mark.parametrize("B,S,H,D", [(1, 2048, 32, 128), (2, 17, 8, 128), (1, 5, 3, 64)])
+def test_rope_fwd_bwd(cuda_device, B, S, H, D):
+    cos, sin = rope_tables(S, D, device=cuda_device)
+    x = _rand((B, S, H, D), cuda_device, 17, 2.0).bfloat16().requires_grad_()
+    y = rope(x, cos, sin)
+    assert (y.float() - rope_ref(x.detach(), cos, sin).float()).abs().max() <= 3e-2
+    dy = _rand((B, S, H, D), cuda_device, 18).bfloat16()
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    rope_ref(xr, cos, sin).backward(dy.float())
+    assert (x.grad.float() - xr.grad).abs().max() <= 3e-2
