@@ -18,7 +18,7 @@ BUILD     := build
 
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
              -Inative/kernels
-CXXFLAGS  := -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -Inative/libmxnode
+CXXFLAGS  := -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -Inative/libmxnode -I$(ROCM)/include
 LDLIBS_NODE := -ldl -lpthread
 
 KERNEL_SRCS := native/kernels/gemm_bf16.hip native/kernels/vector_add.hip \
@@ -54,7 +54,11 @@ $(OUT_LIB)/libmxnode.so: $(NODE_OBJS)
 	@mkdir -p $(OUT_LIB)
 	$(CXX) -shared -o $@ $^ $(LDLIBS_NODE)
 
-$(OUT_BIN)/mx-%: native/tools/mx_%.cc $(NODE_OBJS)
+$(OUT_BIN)/mx-gpu-enum: native/tools/mx_gpu_enum.cc $(NODE_OBJS)
+	@mkdir -p $(OUT_BIN)
+	$(CXX) $(CXXFLAGS) -o $@ $< $(NODE_OBJS) $(LDLIBS_NODE)
+
+$(OUT_BIN)/mx-cdi-gen: native/tools/mx_cdi_gen.cc $(NODE_OBJS)
 	@mkdir -p $(OUT_BIN)
 	$(CXX) $(CXXFLAGS) -o $@ $< $(NODE_OBJS) $(LDLIBS_NODE)
 

@@ -1,0 +1,244 @@
+// N02 (event part) + N06-core: amd-smi backed health events and metrics.
+//
+// amd-smi (/opt/rocm/lib/libamd_smi.so) is dlopen'ed at run time, so the
+// library builds and its sysfs parts run on hosts without ROCm; the types come
+// from the installed header.  Replaces the DCGM sampling behind the reference
+// stack's dcgm-exporter [ext, R26f] and the NVML Xid watch [ext, R26d].
+#include <amd_smi/amdsmi.h>
+#include <dlfcn.h>
+
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "mxnode.h"
+#include "util.h"
+
+namespace {
+
+#define MX_SMI_FN(name) decltype(&::name) name = nullptr
+
+struct SmiApi {
+  void* handle = nullptr;
+  MX_SMI_FN(amdsmi_init);
+  MX_SMI_FN(amdsmi_shut_down);
+  MX_SMI_FN(amdsmi_get_socket_handles);
+  MX_SMI_FN(amdsmi_get_processor_handles);
+  MX_SMI_FN(amdsmi_get_processor_type);
+  MX_SMI_FN(amdsmi_get_gpu_bdf_id);
+  MX_SMI_FN(amdsmi_get_gpu_activity);
+  MX_SMI_FN(amdsmi_get_gpu_memory_usage);
+  MX_SMI_FN(amdsmi_get_gpu_memory_total);
+  MX_SMI_FN(amdsmi_get_temp_metric);
+  MX_SMI_FN(amdsmi_get_power_info);
+  MX_SMI_FN(amdsmi_get_clock_info);
+  MX_SMI_FN(amdsmi_get_gpu_total_ecc_count);
+  MX_SMI_FN(amdsmi_get_gpu_process_list);
+  MX_SMI_FN(amdsmi_get_gpu_driver_info);
+  MX_SMI_FN(amdsmi_init_gpu_event_notification);
+  MX_SMI_FN(amdsmi_set_gpu_event_notification_mask);
+  MX_SMI_FN(amdsmi_get_gpu_event_notification);
+  MX_SMI_FN(amdsmi_stop_gpu_event_notification);
+  std::vector<amdsmi_processor_handle> gpus;
+  bool events_on = false;
+  std::string driver_version;
+};
+
+std::mutex g_mu;
+SmiApi* g_api = nullptr;
+
+template <typename F>
+bool bind(void* h, const char* name, F* slot) {
+  *slot = reinterpret_cast<F>(dlsym(h, name));
+  return *slot != nullptr;
+}
+
+void fmt_bdf(uint64_t bdf, char* out, size_t n) {
+  // amd-smi BDF id: domain[63:32] bus[15:8] device[7:3] function[2:0]
+  std::snprintf(out, n, "%04llx:%02llx:%02llx.%llx",
+                static_cast<unsigned long long>((bdf >> 32) & 0xffff),
+                static_cast<unsigned long long>((bdf >> 8) & 0xff),
+                static_cast<unsigned long long>((bdf >> 3) & 0x1f),
+                static_cast<unsigned long long>(bdf & 0x7));
+}
+
+}  // namespace
+
+extern "C" int mx_smi_open(char* err, size_t errlen) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_api) return 1;
+  const char* env = std::getenv("MXK8S_AMDSMI_LIB");
+  const char* candidates[] = {env, "libamd_smi.so", "/opt/rocm/lib/libamd_smi.so"};
+  void* h = nullptr;
+  for (const char* c : candidates) {
+    if (!c || !*c) continue;
+    h = dlopen(c, RTLD_NOW | RTLD_LOCAL);
+    if (h) break;
+  }
+  if (!h) {
+    mx::set_err(err, errlen, std::string("cannot load libamd_smi.so: ") + dlerror());
+    return 0;
+  }
+  auto* api = new SmiApi();
+  api->handle = h;
+  bool ok = true;
+#define B(name) ok &= bind(h, #name, &api->name)
+  B(amdsmi_init); B(amdsmi_shut_down); B(amdsmi_get_socket_handles);
+  B(amdsmi_get_processor_handles); B(amdsmi_get_processor_type); B(amdsmi_get_gpu_bdf_id);
+  B(amdsmi_get_gpu_activity); B(amdsmi_get_gpu_memory_usage); B(amdsmi_get_gpu_memory_total);
+  B(amdsmi_get_temp_metric); B(amdsmi_get_power_info); B(amdsmi_get_clock_info);
+  B(amdsmi_get_gpu_total_ecc_count); B(amdsmi_get_gpu_process_list);
+  B(amdsmi_get_gpu_driver_info);
+#undef B
+  // event API is optional
+  bind(h, "amdsmi_init_gpu_event_notification", &api->amdsmi_init_gpu_event_notification);
+  bind(h, "amdsmi_set_gpu_event_notification_mask", &api->amdsmi_set_gpu_event_notification_mask);
+  bind(h, "amdsmi_get_gpu_event_notification", &api->amdsmi_get_gpu_event_notification);
+  bind(h, "amdsmi_stop_gpu_event_notification", &api->amdsmi_stop_gpu_event_notification);
+  if (!ok) {
+    mx::set_err(err, errlen, "libamd_smi.so lacks required symbols");
+    dlclose(h);
+    delete api;
+    return 0;
+  }
+  amdsmi_status_t st = api->amdsmi_init(AMDSMI_INIT_AMD_GPUS);
+  if (st != AMDSMI_STATUS_SUCCESS) {
+    mx::set_err(err, errlen, "amdsmi_init failed: status " + std::to_string(st));
+    dlclose(h);
+    delete api;
+    return 0;
+  }
+  uint32_t nsock = 0;
+  api->amdsmi_get_socket_handles(&nsock, nullptr);
+  std::vector<amdsmi_socket_handle> socks(nsock);
+  if (nsock) api->amdsmi_get_socket_handles(&nsock, socks.data());
+  for (uint32_t s = 0; s < nsock; ++s) {
+    uint32_t np = 0;
+    api->amdsmi_get_processor_handles(socks[s], &np, nullptr);
+    std::vector<amdsmi_processor_handle> ps(np);
+    if (np) api->amdsmi_get_processor_handles(socks[s], &np, ps.data());
+    for (uint32_t p = 0; p < np; ++p) {
+      processor_type_t t;
+      if (api->amdsmi_get_processor_type(ps[p], &t) == AMDSMI_STATUS_SUCCESS &&
+          t == AMDSMI_PROCESSOR_TYPE_AMD_GPU)
+        api->gpus.push_back(ps[p]);
+    }
+  }
+  if (!api->gpus.empty()) {
+    amdsmi_driver_info_t di;
+    std::memset(&di, 0, sizeof(di));
+    if (api->amdsmi_get_gpu_driver_info(api->gpus[0], &di) == AMDSMI_STATUS_SUCCESS)
+      api->driver_version = di.driver_version;
+  }
+  g_api = api;
+  return 1;
+}
+
+extern "C" void mx_smi_close(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_api) return;
+  if (g_api->events_on && g_api->amdsmi_stop_gpu_event_notification)
+    for (auto h : g_api->gpus) g_api->amdsmi_stop_gpu_event_notification(h);
+  g_api->amdsmi_shut_down();
+  dlclose(g_api->handle);
+  delete g_api;
+  g_api = nullptr;
+}
+
+extern "C" int mx_smi_count(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_api ? static_cast<int>(g_api->gpus.size()) : -1;
+}
+
+extern "C" const char* mx_smi_driver_version(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_api ? g_api->driver_version.c_str() : "";
+}
+
+extern "C" int mx_smi_sample(int i, mx_gpu_sample* o) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  std::memset(o, 0, sizeof(*o));
+  o->index = i;
+  o->temp_edge_mc = o->temp_hotspot_mc = o->temp_mem_mc = INT64_MIN;
+  if (!g_api || i < 0 || i >= static_cast<int>(g_api->gpus.size())) return 0;
+  SmiApi& a = *g_api;
+  amdsmi_processor_handle h = a.gpus[i];
+  uint64_t bdf = 0;
+  if (a.amdsmi_get_gpu_bdf_id(h, &bdf) == AMDSMI_STATUS_SUCCESS) fmt_bdf(bdf, o->bdf, sizeof(o->bdf));
+  amdsmi_engine_usage_t u;
+  std::memset(&u, 0, sizeof(u));
+  if (a.amdsmi_get_gpu_activity(h, &u) == AMDSMI_STATUS_SUCCESS) {
+    o->gfx_activity_pct = u.gfx_activity;
+    o->umc_activity_pct = u.umc_activity;
+  }
+  a.amdsmi_get_gpu_memory_usage(h, AMDSMI_MEM_TYPE_VRAM, &o->vram_used_bytes);
+  a.amdsmi_get_gpu_memory_total(h, AMDSMI_MEM_TYPE_VRAM, &o->vram_total_bytes);
+  int64_t t = 0;
+  if (a.amdsmi_get_temp_metric(h, AMDSMI_TEMPERATURE_TYPE_EDGE, AMDSMI_TEMP_CURRENT, &t) == AMDSMI_STATUS_SUCCESS)
+    o->temp_edge_mc = t * 1000;
+  if (a.amdsmi_get_temp_metric(h, AMDSMI_TEMPERATURE_TYPE_HOTSPOT, AMDSMI_TEMP_CURRENT, &t) == AMDSMI_STATUS_SUCCESS)
+    o->temp_hotspot_mc = t * 1000;
+  if (a.amdsmi_get_temp_metric(h, AMDSMI_TEMPERATURE_TYPE_VRAM, AMDSMI_TEMP_CURRENT, &t) == AMDSMI_STATUS_SUCCESS)
+    o->temp_mem_mc = t * 1000;
+  amdsmi_power_info_t p;
+  std::memset(&p, 0, sizeof(p));
+  if (a.amdsmi_get_power_info(h, &p) == AMDSMI_STATUS_SUCCESS) {
+    o->power_w = p.current_socket_power ? p.current_socket_power
+                                        : (p.socket_power ? p.socket_power : p.average_socket_power);
+    // ROCm 7.2 amd-smi reports power_limit in microwatts on MI355X (1.4e9 = 1400 W)
+    o->power_limit_w = p.power_limit > 100000u ? p.power_limit / 1000000u : p.power_limit;
+  }
+  amdsmi_clk_info_t c;
+  std::memset(&c, 0, sizeof(c));
+  if (a.amdsmi_get_clock_info(h, AMDSMI_CLK_TYPE_SYS, &c) == AMDSMI_STATUS_SUCCESS) o->sclk_mhz = c.clk;
+  std::memset(&c, 0, sizeof(c));
+  if (a.amdsmi_get_clock_info(h, AMDSMI_CLK_TYPE_MEM, &c) == AMDSMI_STATUS_SUCCESS) o->mclk_mhz = c.clk;
+  amdsmi_error_count_t e;
+  std::memset(&e, 0, sizeof(e));
+  if (a.amdsmi_get_gpu_total_ecc_count(h, &e) == AMDSMI_STATUS_SUCCESS) {
+    o->ecc_correctable = e.correctable_count;
+    o->ecc_uncorrectable = e.uncorrectable_count;
+  }
+  uint32_t np = 0;
+  if (a.amdsmi_get_gpu_process_list(h, &np, nullptr) == AMDSMI_STATUS_SUCCESS) o->num_processes = np;
+  o->valid = 1;
+  return 1;
+}
+
+extern "C" int mx_smi_wait_events(int timeout_ms, int* gpu_out, int* event_out, int max) {
+  SmiApi* a;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    a = g_api;
+    if (!a || !a->amdsmi_get_gpu_event_notification) return -1;
+    if (!a->events_on) {
+      const uint64_t mask = (1ull << (AMDSMI_EVT_NOTIF_GPU_PRE_RESET - 1)) |
+                            (1ull << (AMDSMI_EVT_NOTIF_GPU_POST_RESET - 1)) |
+                            (1ull << (AMDSMI_EVT_NOTIF_THERMAL_THROTTLE - 1)) |
+                            (1ull << (AMDSMI_EVT_NOTIF_VMFAULT - 1));
+      for (auto h : a->gpus) {
+        if (a->amdsmi_init_gpu_event_notification(h) != AMDSMI_STATUS_SUCCESS) return -1;
+        a->amdsmi_set_gpu_event_notification_mask(h, mask);
+      }
+      a->events_on = true;
+    }
+  }
+  std::vector<amdsmi_evt_notification_data_t> ev(max > 0 ? max : 1);
+  uint32_t n = static_cast<uint32_t>(ev.size());
+  amdsmi_status_t st = a->amdsmi_get_gpu_event_notification(timeout_ms, &n, ev.data());
+  if (st != AMDSMI_STATUS_SUCCESS) return st == AMDSMI_STATUS_NO_DATA ? 0 : -1;
+  int count = 0;
+  for (uint32_t k = 0; k < n && count < max; ++k) {
+    int gi = -1;
+    for (size_t j = 0; j < a->gpus.size(); ++j)
+      if (a->gpus[j] == ev[k].processor_handle) gi = static_cast<int>(j);
+    gpu_out[count] = gi;
+    event_out[count] = static_cast<int>(ev[k].event);
+    ++count;
+  }
+  return count;
+}
