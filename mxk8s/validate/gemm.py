@@ -1,0 +1,127 @@
+"""Validator config 3: CDNA4 bf16 MFMA GEMM throughput + correctness.
+
+Protocol (BASELINE.md "Measurement protocol"): random uniform [-1, 1) bf16
+operands (never zeros: DVFS clocks higher on zeros), >= 2 s of warm-up
+launches, then the median of >= 50 timed launches with HIP events;
+TFLOPS = 2*M*N*K / t.  Correctness: fp32 reference on a sub-block and
+relative error against hipBLASLt (torch.matmul) on the full output.
+
+Schedules of the 256x256 kernel are A/B-timed in ONE process with rounds
+interleaved (cdna_hip_programming.md §5.4 rule 24) when --variants is given.
+
+    python -m mxk8s.validate.gemm --sizes 4096,8192,16384 [--variants all]
+
+Prints one ``RESULT {json}`` line per (size, kernel).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+import time
+
+import torch
+
+from ..ops import _lib
+from ..ops.gemm import gemm_bf16_tn
+
+
+def _events_time(fn, iters: int) -> list[float]:
+    times = []
+    for _ in range(iters):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        times.append(s.elapsed_time(e) * 1e-3)
+    return times
+
+
+def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None) -> list[dict]:
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    L = _lib.lib()
+    stream = lambda: _lib.stream_ptr(dev)  # noqa: E731
+    results = []
+    for n in sizes:
+        M = N = K = n
+        g = torch.Generator(device=dev)
+        g.manual_seed(n)
+        A = (torch.rand((M, K), device=dev, generator=g) * 2 - 1).bfloat16()
+        Bt = (torch.rand((N, K), device=dev, generator=g) * 2 - 1).bfloat16()
+        C = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        ref = torch.matmul(A, Bt.t())
+        kernels = {}
+        for v in variants:
+            def mk(v=v):
+                st = L.mxk_gemm_bf16_tn_variant(A.data_ptr(), Bt.data_ptr(), C.data_ptr(), M, N, K,
+                                                K, K, N, v, stream())
+                if st:
+                    _lib.check(st, f"gemm variant {v}")
+            kernels[f"mxk_v{v}"] = mk
+        kernels["mxk_default"] = lambda: gemm_bf16_tn(A, Bt, C)
+        kernels["hipblaslt"] = lambda: torch.matmul(A, Bt.t(), out=C)
+        # correctness of every hand-written schedule
+        checks = {}
+        for name, fn in kernels.items():
+            if name == "hipblaslt":
+                continue
+            C.zero_()
+            fn()
+            torch.cuda.synchronize()
+            rel = ((C.float() - ref.float()).norm() / ref.float().norm()).item()
+            sub = (A[:128].float() @ Bt[:128].float().t())
+            sub_err = (C[:128, :128].float() - sub).abs().max().item()
+            checks[name] = (rel, sub_err)
+            if not (rel < 1e-2 and sub_err <= 2 ** -7 * sub.abs().max().item() + 1e-3):
+                raise RuntimeError(f"{name} wrong at {n}: rel {rel}, max sub err {sub_err}")
+        # warm up >= warmup_s on random data (clock settles under load)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < warmup_s:
+            for fn in kernels.values():
+                fn()
+            torch.cuda.synchronize()
+        samples = {k: [] for k in kernels}
+        for _ in range(rounds):
+            for name, fn in kernels.items():
+                samples[name] += _events_time(fn, max(1, iters // rounds))
+        flops = 2.0 * M * N * K
+        for name, ts in samples.items():
+            med = statistics.median(ts)
+            r = {"kernel": name, "M": M, "N": N, "K": K, "dtype": "bf16",
+                 "median_ms": med * 1e3, "min_ms": min(ts) * 1e3,
+                 "tflops_median": flops / med / 1e12, "tflops_best": flops / min(ts) / 1e12,
+                 "samples": len(ts), "data": "uniform[-1,1) random"}
+            if name in checks:
+                r["rel_err_vs_hipblaslt"], r["max_abs_err_subblock_vs_fp32"] = checks[name]
+            results.append(r)
+            print("RESULT " + json.dumps(r), flush=True)
+    return results
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--sizes", default="4096,8192,16384")
+    p.add_argument("--variants", default="", help="'all' or comma list of schedule ids")
+    p.add_argument("--iters", type=int, default=60)
+    p.add_argument("--rounds", type=int, default=6)
+    p.add_argument("--warmup-s", type=float, default=2.0)
+    p.add_argument("--device", type=int, default=None)
+    a = p.parse_args(argv)
+    if a.device is not None:
+        torch.cuda.set_device(a.device)
+    nv = _lib.lib().mxk_gemm_bf16_tn_num_variants()
+    if a.variants == "all":
+        variants = list(range(nv))
+    elif a.variants:
+        variants = [int(x) for x in a.variants.split(",")]
+    else:
+        variants = []
+    run([int(x) for x in a.sizes.split(",")], variants, a.iters, a.warmup_s, a.rounds)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -62,6 +62,14 @@ __device__ __forceinline__ bf16x8_t lds_read_b128(const char* p) {
 
 }  // namespace
 
+// Main-loop schedules (selected at compile time; A/B-benchmarked in one process
+// through mxk_gemm_bf16_tn_variant):
+//   0: per phase {4 B + 4 A ds_reads, 1/4 of the next tile's DMA, 16 MFMA}
+//   1: whole next-tile DMA issued right after the barrier; all 24 fragment
+//      reads of the tile issued up front, then 64 MFMAs (compiler places the
+//      counted lgkmcnt waits)
+//   2: whole next-tile DMA up front; per k-step {12 reads, 32 MFMA}
+template <int V>
 __global__ void __launch_bounds__(NTHREADS, 2)
 mxk_gemm_bf16_tn_256x256(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                          uint16_t* __restrict__ C, int M, int N, int K,
@@ -121,30 +129,77 @@ mxk_gemm_bf16_tn_256x256(const uint16_t* __restrict__ A, const uint16_t* __restr
     const char* As = cur + a_wave;
     const char* Bs = cur + TILE_BYTES + b_wave;
 
-    // Four phases: (ks, m-half).  Each phase prefetches one quarter of the
-    // next K tile (A quarter + B quarter) ahead of its 16 MFMAs.
+    if constexpr (V == 0) {
 #pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {
-      const int ks = ph >> 1;
-      const int mh = ph & 1;
-      const int koff = ks ? off_k1 : off_k0;
-      bf16x8_t a[4], b[4];
+      for (int ph = 0; ph < 4; ++ph) {
+        const int ks = ph >> 1;
+        const int mh = ph & 1;
+        const int koff = ks ? off_k1 : off_k0;
+        bf16x8_t a[4], b[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = lds_read_b128(Bs + j * 2048 + koff);
+        for (int j = 0; j < 4; ++j) b[j] = lds_read_b128(Bs + j * 2048 + koff);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = lds_read_b128(As + (mh * 4 + i) * 2048 + koff);
-      if (more) {
-        stage_quarter(A, lda, m0, kn, nxt, ph, tid);
-        stage_quarter(Bt, ldb, n0, kn, nxt + TILE_BYTES, ph, tid);
+        for (int i = 0; i < 4; ++i) a[i] = lds_read_b128(As + (mh * 4 + i) * 2048 + koff);
+        if (more) {
+          stage_quarter(A, lda, m0, kn, nxt, ph, tid);
+          stage_quarter(Bt, ldb, n0, kn, nxt + TILE_BYTES, ph, tid);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[mh * 4 + i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[mh * 4 + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
       }
-      __builtin_amdgcn_s_setprio(1);
+    } else {
+      // The next tile's buffer was released by the barrier that ended tile
+      // t-1, so its whole DMA can start now and has the full tile to land.
+      if (more) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int q = 0; q < 4; ++q) {
+          stage_quarter(A, lda, m0, kn, nxt, q, tid);
+          stage_quarter(Bt, ldb, n0, kn, nxt + TILE_BYTES, q, tid);
+        }
+      }
+      if constexpr (V == 1) {
+        bf16x8_t a[2][8], b[2][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[mh * 4 + i][j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[mh * 4 + i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
+        for (int ks = 0; ks < 2; ++ks) {
+          const int koff = ks ? off_k1 : off_k0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) b[ks][j] = lds_read_b128(Bs + j * 2048 + koff);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[ks][i] = lds_read_b128(As + i * 2048 + koff);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], a[ks][i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int koff = ks ? off_k1 : off_k0;
+          bf16x8_t a[8], b[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) b[j] = lds_read_b128(Bs + j * 2048 + koff);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[i] = lds_read_b128(As + i * 2048 + koff);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+        }
+      }
     }
     // Retire the next tile's DMA (issued by this wave), then a barrier so every
     // wave's DMA has landed and every wave is done reading `cur` before it is
@@ -240,6 +295,34 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // ---------------------------------------------------------------------------
 // Host launchers (C ABI, stream-ordered, capture-safe: no sync, no malloc).
 // ---------------------------------------------------------------------------
+namespace {
+constexpr int kDefaultVariant = 1;
+constexpr int kNumVariants = 3;
+
+void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
+                int N, int K, int lda, int ldb, int ldc) {
+  auto* a = static_cast<const uint16_t*>(A);
+  auto* b = static_cast<const uint16_t*>(Bt);
+  auto* c = static_cast<uint16_t*>(C);
+  switch (v) {
+    case 0: hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256<0>, dim3(nwg), dim3(NTHREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 1: hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256<1>, dim3(nwg), dim3(NTHREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    default: hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256<2>, dim3(nwg), dim3(NTHREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+  }
+}
+}  // namespace
+
+// Benchmark hook: run schedule `variant` of the 256x256 kernel (fast shapes only).
+MXK_API int mxk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int M, int N, int K,
+                                     int lda, int ldb, int ldc, int variant, hipStream_t stream) {
+  if (M % BM || N % BN || K % BK || variant < 0 || variant >= kNumVariants)
+    return static_cast<int>(hipErrorInvalidValue);
+  launch_256(variant, (M / BM) * (N / BN), stream, A, Bt, C, M, N, K, lda, ldb, ldc);
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+MXK_API int mxk_gemm_bf16_tn_num_variants(void) { return kNumVariants; }
+
 MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,
                              int lda, int ldb, int ldc, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return static_cast<int>(hipErrorInvalidValue);
@@ -250,9 +333,7 @@ MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int 
                     (reinterpret_cast<uintptr_t>(C) % 8 == 0);
   if (fast) {
     const int nwg = (M / BM) * (N / BN);
-    hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256, dim3(nwg), dim3(NTHREADS), 0, stream,
-                       static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
-                       static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
+    launch_256(kDefaultVariant, nwg, stream, A, Bt, C, M, N, K, lda, ldb, ldc);
   } else {
     dim3 grid((N + 63) / 64, (M + 63) / 64);
     hipLaunchKernelGGL(mxk_gemm_bf16_tn_generic, grid, dim3(256), 0, stream,
