@@ -227,6 +227,161 @@ mxk_gemm_bf16_tn_256x256(const uint16_t* __restrict__ A, const uint16_t* __restr
 }
 
 // ---------------------------------------------------------------------------
+// Schedule 3/4: 4 waves (one per SIMD), each owning a 128x128 output block
+// (8x8 tiles of 16x16 -> 256 fp32 accumulators, kept in the AGPR half of the
+// unified 512-entry register file), BK = 32 K-stages in an NS-deep LDS ring.
+//
+// Per 32-deep stage a wave issues 16 ds_read_b128 for 64 MFMAs (half the LDS
+// bytes per FLOP of the 8-wave 128x64 layout); the LDS-DMA for stage s+NS-1
+// is issued NS-2 stages ahead of its use, and the fragments of stage s+1 are
+// read into a second register set while stage s's MFMAs run, so the matrix
+// pipe is fed from registers right after every barrier.
+//
+// Stage s lives in LDS buffer s % NS:   [A 256 rows x 64 B | B 256 rows x 64 B]
+// Row r's 16-B chunk c sits at chunk c ^ h((r >> 2) & 3), h = {0,2,3,1}: every
+// 16-lane ds_read_b128 group then hits 16 distinct 16-B bank slots
+// (tests/test_gemm_swizzle.py).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int W4_BK = 32;
+constexpr int W4_THREADS = 256;
+constexpr int W4_OP_BYTES = 256 * W4_BK * 2;        // 16 KiB per operand per stage
+constexpr int W4_STAGE_BYTES = 2 * W4_OP_BYTES;     // 32 KiB
+
+__device__ __forceinline__ int w4_h(int q) { return (((q ^ (q >> 1)) & 1) << 1) | (q >> 1); }
+
+// One operand stage (256 rows x 32 k) = 4 glds per thread (1 KiB per wave
+// instruction = 16 rows of 64 B).
+__device__ __forceinline__ void w4_stage_operand(const uint16_t* __restrict__ src, int ld, int row0,
+                                                 int k0, char* lds_op, int tid) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = q * 64 + (tid >> 2);
+    const int pc = tid & 3;
+    const int c = pc ^ w4_h((row >> 2) & 3);
+    const uint16_t* g = src + static_cast<size_t>(row0 + row) * ld + k0 + c * 8;
+    char* dst = lds_op + q * 4096 + (tid >> 6) * 1024;
+    __builtin_amdgcn_global_load_lds(g, (lds_void*)dst, 16, 0, 0);
+  }
+}
+}  // namespace
+
+template <int NS>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                    uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[NS * W4_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1;   // 0..1 -> 128 rows
+  const int wn = wave & 1;    // 0..1 -> 128 cols
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int wgid = mxk::xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  const int frow = lane & 15;
+  const int foff = frow * 64 + (((lane >> 4) ^ w4_h((frow >> 2) & 3)) * 16);
+  const int a_off = wm * 128 * 64 + foff;               // + i*1024 for subtile i
+  const int b_off = W4_OP_BYTES + wn * 128 * 64 + foff;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / W4_BK;
+  // prologue: stages 0 .. NS-2 in flight (clamped past the end)
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) {
+    const int kk = (s < ns ? s : ns - 1) * W4_BK;
+    w4_stage_operand(A, lda, m0, kk, smem + s * W4_STAGE_BYTES, tid);
+    w4_stage_operand(Bt, ldb, n0, kk, smem + s * W4_STAGE_BYTES + W4_OP_BYTES, tid);
+  }
+  // stage 0 landed (8 glds per later stage may stay in flight)
+  if constexpr (NS == 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t fa[2][8], fb[2][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa[0][i] = lds_read_b128(smem + a_off + i * 1024);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb[0][j] = lds_read_b128(smem + b_off + j * 1024);
+
+  // Uniform steady state (ns is even: K % 64 == 0 on this path).  Past the
+  // end the DMA re-fetches the last stage into the free buffer and the
+  // fragment reads hit stale LDS: both harmless, and every trip keeps the
+  // same vmcnt bookkeeping (no tail branches inside the loop).
+  for (int s = 0; s < ns; s += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int st = s + u;
+      // (1) own part of stage st+1 landed; the barrier publishes every wave's
+      //     part and certifies all waves finished reading stage st-1.
+      if constexpr (NS == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // (2) DMA for stage st+NS-1 into the buffer stage st-1 used.
+      {
+        const int sn = st + NS - 1;
+        const int kk = (sn < ns ? sn : ns - 1) * W4_BK;
+        char* buf = smem + (sn % NS) * W4_STAGE_BYTES;
+        w4_stage_operand(A, lda, m0, kk, buf, tid);
+        w4_stage_operand(Bt, ldb, n0, kk, buf + W4_OP_BYTES, tid);
+      }
+      // (3) fragments of stage st+1 into the other register set
+      {
+        const char* nb = smem + ((st + 1) % NS) * W4_STAGE_BYTES;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fa[u ^ 1][i] = lds_read_b128(nb + a_off + i * 1024);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fb[u ^ 1][j] = lds_read_b128(nb + b_off + j * 1024);
+      }
+      // (4) 64 MFMAs on stage st straight from registers
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][j], fa[u][i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      // Retire the prefetch reads here (they had the whole MFMA block to
+      // land).  lgkmcnt only counts to 15, so if they were still pending at
+      // the next stage's first MFMA the compiler would have to wait
+      // lgkmcnt(0) on the NEW prefetch as well.  0xC07F = lgkmcnt(0) only.
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + crow;
+    uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 128 + ccol;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4_t v = acc[i][j];
+      uint2 pk;
+      pk.x = mxk::pack2bf(v[0], v[1]);
+      pk.y = mxk::pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generic bounds-checked MFMA GEMM (any M, N, K; K-contiguous operands).
 // 64x64 tile, 256 threads (2x2 waves of 32x32), register-staged through LDS.
 // Used for shapes the 256x256 kernel does not tile exactly.
@@ -297,7 +452,7 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int kDefaultVariant = 1;
-constexpr int kNumVariants = 3;
+constexpr int kNumVariants = 5;
 
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
                 int N, int K, int lda, int ldb, int ldc) {
@@ -307,7 +462,9 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
   switch (v) {
     case 0: hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256<0>, dim3(nwg), dim3(NTHREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 1: hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256<1>, dim3(nwg), dim3(NTHREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    default: hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256<2>, dim3(nwg), dim3(NTHREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 2: hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256<2>, dim3(nwg), dim3(NTHREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 3: hipLaunchKernelGGL(mxk_gemm_bf16_tn_w4<4>, dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    default: hipLaunchKernelGGL(mxk_gemm_bf16_tn_w4<3>, dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
   }
 }
 }  // namespace
