@@ -22,7 +22,7 @@ CXXFLAGS  := -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -Inative/l
 LDLIBS_NODE := -ldl -lpthread
 
 KERNEL_SRCS := native/kernels/gemm_bf16.hip native/kernels/vector_add.hip \
-               native/kernels/fused_ops.hip
+               native/kernels/fused_ops.hip native/kernels/optim.hip
 KERNEL_OBJS := $(patsubst native/kernels/%.hip,$(BUILD)/kernels/%.o,$(KERNEL_SRCS))
 KERNEL_HDRS := $(wildcard native/kernels/*.h)
 
@@ -65,17 +65,25 @@ $(OUT_BIN)/mx-cdi-gen: native/tools/mx_cdi_gen.cc $(NODE_OBJS)
 # ---- validator binaries (HIP / RCCL / rocBLAS) ----
 tools: $(OUT_BIN)/mx-vector-add $(OUT_BIN)/mx-gemm-bench $(OUT_BIN)/mx-allreduce-perf
 
-$(OUT_BIN)/mx-vector-add: native/tools/vector_add_main.hip $(BUILD)/kernels/vector_add.o $(KERNEL_HDRS)
-	@mkdir -p $(OUT_BIN)
-	$(HIPCC) $(HIPFLAGS) -o $@ $< $(BUILD)/kernels/vector_add.o
+$(BUILD)/tools/%.o: native/tools/%.hip $(KERNEL_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OUT_BIN)/mx-gemm-bench: native/tools/gemm_bench_main.hip $(BUILD)/kernels/gemm_bf16.o $(KERNEL_HDRS)
-	@mkdir -p $(OUT_BIN)
-	$(HIPCC) $(HIPFLAGS) -o $@ $< $(BUILD)/kernels/gemm_bf16.o -L$(ROCM)/lib -lrocblas
+$(BUILD)/tools/allreduce_perf.o: native/rccl_bench/allreduce_perf.cc
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(OUT_BIN)/mx-allreduce-perf: native/rccl_bench/allreduce_perf.cc
+$(OUT_BIN)/mx-vector-add: $(BUILD)/tools/vector_add_main.o $(BUILD)/kernels/vector_add.o
 	@mkdir -p $(OUT_BIN)
-	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -L$(ROCM)/lib -lrccl -lpthread
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^
+
+$(OUT_BIN)/mx-gemm-bench: $(BUILD)/tools/gemm_bench_main.o $(BUILD)/kernels/gemm_bf16.o
+	@mkdir -p $(OUT_BIN)
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
+
+$(OUT_BIN)/mx-allreduce-perf: $(BUILD)/tools/allreduce_perf.o
+	@mkdir -p $(OUT_BIN)
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lpthread -Wl,-rpath,$(ROCM)/lib
 
 # ---- host tests (sanitized) ----
 test-native: $(BUILD)/asan/test_mxnode

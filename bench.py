@@ -180,6 +180,7 @@ def main(argv=None) -> int:
     p.add_argument("--seq-len", type=int, default=2048, help="ddp mode")
     p.add_argument("--micro-batch", type=int, default=1, help="ddp mode")
     p.add_argument("--layers", type=int, default=None, help="ddp mode: override (NOT headline)")
+    p.add_argument("--bucket-mb", type=float, default=512.0, help="ddp mode: all-reduce bucket size")
     args = p.parse_args(argv)
 
     world, rank, _ = _dist_env()
@@ -205,7 +206,7 @@ def main(argv=None) -> int:
             args.steps = 10
         if args.warmup is None:
             args.warmup = 3
-        from mxk8s.validate.ddp import run_ddp_bench
+        from mxk8s.train.ddp_llama import run_ddp_bench
         out = run_ddp_bench(args)
 
     if rank == 0:

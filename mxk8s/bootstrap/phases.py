@@ -1,0 +1,313 @@
+"""Idempotent, resumable, phase-gated host bring-up (``mxk8s bootstrap``).
+
+The reference is a manual runbook (/root/reference/README.md:13-335) with a
+reboot in the middle (README.md:70-74), a "do not proceed" gate (:84), a fixed
+``sleep 15`` (:326) and a control-plane taint it never removes.  Here every
+step is a phase with a completion marker in /var/lib/mxk8s/phase, so a rerun
+after the reboot (or after any failure) resumes where it stopped:
+
+  prep          swap off, overlay/br_netfilter, sysctls (+ numa_balancing=0)   README.md:13-56
+  driver-check  amdgpu loaded, /dev/kfd, gfx950 GPUs via libmxnode, iommu=pt   README.md:60-84
+  runtime       containerd, SystemdCgroup=true, CDI enabled                    README.md:88-124,151-155
+  cdi           /etc/cdi/amd.com-gpu.json from mx-cdi-gen (no toolkit/shim)     replaces README.md:126-149
+  k8s-packages  pkgs.k8s.io v1.34 kubelet/kubeadm/kubectl (held)               README.md:159-187
+  cluster       kubeadm init --config, kubeconfig, untaint, Flannel, Ready     README.md:191-243
+  stack         amd-gpu-stack (helm, or kubectl apply of the rendered chart)   README.md:247-286
+  validate      busybox (config 1) + hip-vector-add (config 2), wait + RESULT  README.md:288-335
+
+``--dry-run --root DIR`` writes every file under DIR and records (does not
+run) every command, which is what the CPU test tier checks.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+import shlex
+import shutil
+import subprocess
+import sys
+import time
+from typing import Callable, Optional, Sequence
+
+from . import hostfiles as hf
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+@dataclasses.dataclass
+class Context:
+    root: str = "/"
+    dry_run: bool = False
+    upgrade: bool = False
+    node_name: str = ""
+    advertise_address: str = ""
+    kubeconfig_home: str = os.path.expanduser("~")
+    repo: str = REPO
+    actions: list = dataclasses.field(default_factory=list)
+    out: Callable[[str], None] = lambda s: print(s, file=sys.stderr)
+
+    # ---- filesystem, relative to root ----
+    def path(self, p: str) -> str:
+        if self.root in ("", "/"):
+            return p
+        return os.path.join(self.root, p.lstrip("/"))
+
+    def read(self, p: str) -> Optional[str]:
+        try:
+            with open(self.path(p)) as f:
+                return f.read()
+        except OSError:
+            return None
+
+    def exists(self, p: str) -> bool:
+        return os.path.exists(self.path(p))
+
+    def write(self, p: str, content: str, mode: int = 0o644) -> bool:
+        """Write iff content differs. Returns True if the file changed."""
+        if self.read(p) == content:
+            return False
+        full = self.path(p)
+        os.makedirs(os.path.dirname(full), exist_ok=True)
+        tmp = full + ".mxk8s-tmp"
+        with open(tmp, "w") as f:
+            f.write(content)
+        os.chmod(tmp, mode)
+        os.replace(tmp, full)
+        self.actions.append(("write", p))
+        return True
+
+    # ---- commands ----
+    def run(self, cmd: Sequence[str] | str, check: bool = True, capture: bool = False,
+            env: Optional[dict] = None) -> subprocess.CompletedProcess:
+        argv = shlex.split(cmd) if isinstance(cmd, str) else list(cmd)
+        self.actions.append(("run", argv))
+        if self.dry_run:
+            return subprocess.CompletedProcess(argv, 0, "", "")
+        self.out("+ " + " ".join(shlex.quote(a) for a in argv))
+        return subprocess.run(argv, check=check, text=True,
+                              capture_output=capture, env={**os.environ, **(env or {})})
+
+    def have(self, tool: str) -> bool:
+        return shutil.which(tool) is not None
+
+    def commands(self) -> list[str]:
+        return [" ".join(shlex.quote(a) for a in x[1]) for x in self.actions if x[0] == "run"]
+
+
+class PhaseError(RuntimeError):
+    pass
+
+
+# ---------------------------------------------------------------------------
+# phases
+# ---------------------------------------------------------------------------
+
+def phase_prep(ctx: Context) -> None:
+    if ctx.upgrade:
+        ctx.run("apt-get update")
+        ctx.run("apt-get upgrade -y")
+    ctx.run("swapoff -a")
+    fstab = ctx.read("/etc/fstab")
+    if fstab is not None:
+        ctx.write("/etc/fstab", hf.comment_swap(fstab))
+    ctx.write("/etc/modules-load.d/k8s.conf", hf.modules_load_conf())
+    ctx.run("modprobe overlay")
+    ctx.run("modprobe br_netfilter")
+    ctx.write("/etc/sysctl.d/k8s.conf", hf.sysctl_k8s_conf())
+    ctx.write("/etc/sysctl.d/99-amd-gpu.conf", hf.sysctl_amd_gpu_conf())
+    ctx.run("sysctl --system")
+
+
+def driver_report(ctx: Context) -> dict:
+    """Facts the driver gate decides on (also used by ``mxk8s doctor gpu``)."""
+    from ..native import node
+    rep = {"amdgpu_module": ctx.exists("/sys/module/amdgpu"),
+           "kfd": ctx.exists("/dev/kfd"), "gpus": [], "errors": []}
+    cmdline = ctx.read("/proc/cmdline") or ""
+    rep["iommu_pt"] = "iommu=pt" in cmdline.split()
+    try:
+        gpus = node.enumerate_gpus("" if ctx.root in ("", "/") else ctx.root)
+        rep["gpus"] = [g.to_dict() for g in gpus]
+    except Exception as e:   # no KFD topology
+        rep["errors"].append(str(e))
+    rep["gfx950"] = sum(1 for g in rep["gpus"] if g["arch"] == "gfx950")
+    return rep
+
+
+def phase_driver_check(ctx: Context) -> None:
+    rep = driver_report(ctx)
+    problems = []
+    if not rep["amdgpu_module"]:
+        problems.append("amdgpu kernel module not loaded (install amdgpu-dkms + ROCm 7.x, reboot)")
+    if not rep["kfd"]:
+        problems.append("/dev/kfd missing (KFD not initialised)")
+    if not rep["gpus"]:
+        problems.append("no AMD GPUs in the KFD topology: " + "; ".join(rep["errors"]))
+    if problems:
+        # the reference's "Do not proceed" gate (README.md:84), made machine-checkable
+        raise PhaseError("driver gate failed:\n  - " + "\n  - ".join(problems) +
+                         "\nInstall the host driver, reboot, then re-run `mxk8s bootstrap` "
+                         "(completed phases are skipped).")
+    if not rep["iommu_pt"]:
+        ctx.out("WARNING: kernel cmdline lacks iommu=pt (recommended for MI355X P2P/RCCL)")
+    ctx.out(f"driver gate ok: {len(rep['gpus'])} GPU(s), {rep['gfx950']} gfx950")
+
+
+def phase_runtime(ctx: Context) -> None:
+    if not ctx.have("containerd") or ctx.dry_run:
+        ctx.run("apt-get update")
+        ctx.run("apt-get install -y apt-transport-https ca-certificates curl "
+                "software-properties-common containerd")
+    ctx.run("systemctl enable containerd")
+    ctx.run("systemctl start containerd")
+    ctx.run("containerd --version")
+    current = ctx.read("/etc/containerd/config.toml")
+    if not current:
+        if ctx.dry_run or not ctx.have("containerd"):
+            current = hf.minimal_containerd_config(2)
+        else:
+            current = ctx.run("containerd config default", capture=True).stdout
+    ctx.write("/etc/containerd/config.toml", hf.configure_containerd(current))
+    ctx.run("systemctl restart containerd")
+
+
+def phase_cdi(ctx: Context) -> None:
+    from ..native import node
+    root = "" if ctx.root in ("", "/") else ctx.root
+    spec = node.cdi_spec(root)
+    ctx.write(hf.CDI_SPEC_PATH, json.dumps(spec, indent=2) + "\n")
+    ctx.out(f"CDI spec: {len(spec['devices'])} device entries -> {hf.CDI_SPEC_PATH}")
+
+
+def phase_k8s_packages(ctx: Context) -> None:
+    ctx.run("apt-get update")
+    ctx.run("apt-get install -y apt-transport-https ca-certificates curl gpg")
+    ctx.run("mkdir -p -m 755 /etc/apt/keyrings")
+    ctx.run(["bash", "-c",
+             f"curl -fsSL https://pkgs.k8s.io/core:/stable:/{hf.K8S_MINOR}/deb/Release.key | "
+             "gpg --dearmor -o /etc/apt/keyrings/kubernetes-apt-keyring.gpg"])
+    ctx.write("/etc/apt/sources.list.d/kubernetes.list", hf.kubernetes_apt_source())
+    ctx.run("apt-get update")
+    ctx.run("apt-get install -y kubelet kubeadm kubectl")
+    ctx.run("apt-mark hold kubelet kubeadm kubectl")
+    ctx.run("systemctl enable --now kubelet")
+
+
+def _kubectl(ctx: Context, *args: str, check: bool = True, capture: bool = False):
+    return ctx.run(["kubectl", "--kubeconfig", "/etc/kubernetes/admin.conf", *args],
+                   check=check, capture=capture)
+
+
+def phase_cluster(ctx: Context) -> None:
+    ctx.write("/etc/mxk8s/kubeadm-config.yaml",
+              hf.kubeadm_config(ctx.node_name, ctx.advertise_address))
+    if not ctx.exists("/etc/kubernetes/admin.conf") or ctx.dry_run:
+        ctx.run(["kubeadm", "init", "--config", ctx.path("/etc/mxk8s/kubeadm-config.yaml")])
+    home = ctx.kubeconfig_home
+    ctx.run(["mkdir", "-p", f"{home}/.kube"])
+    ctx.run(["cp", "-f", "/etc/kubernetes/admin.conf", f"{home}/.kube/config"])
+    uid, gid = os.getuid(), os.getgid()
+    ctx.run(["chown", f"{uid}:{gid}", f"{home}/.kube/config"])
+    # single node: remove the control-plane taint (kubeadm config already sets
+    # taints: [], this also fixes clusters initialised without our config)
+    _kubectl(ctx, "taint", "nodes", "--all", "node-role.kubernetes.io/control-plane-", check=False)
+    _kubectl(ctx, "apply", "-f", os.path.join(ctx.repo, "deploy", "cni", "kube-flannel.yaml"))
+    _kubectl(ctx, "-n", "kube-flannel", "rollout", "status", "ds/kube-flannel-ds", "--timeout=300s")
+    _kubectl(ctx, "wait", "node", "--all", "--for=condition=Ready", "--timeout=300s")
+
+
+def phase_stack(ctx: Context) -> None:
+    chart = os.path.join(ctx.repo, "charts", "amd-gpu-stack")
+    if ctx.have("helm") and not ctx.dry_run:
+        ctx.run(["helm", "upgrade", "--install", "amd-gpu-stack", chart, "-n", "amd-gpu",
+                 "--create-namespace", "--set", "driver.enabled=false",
+                 "--kubeconfig", "/etc/kubernetes/admin.conf"])
+    else:
+        _kubectl(ctx, "create", "namespace", "amd-gpu", check=False)
+        _kubectl(ctx, "apply", "-f", os.path.join(ctx.repo, "deploy", "amd-gpu-stack.yaml"))
+    _kubectl(ctx, "-n", "amd-gpu", "rollout", "status", "ds/amd-gpu-stack-device-plugin",
+             "--timeout=300s")
+    # capacity check (README.md:293-296): amd.com/gpu must be allocatable
+    if not ctx.dry_run:
+        deadline = time.time() + 120
+        while True:
+            r = _kubectl(ctx, "get", "nodes", "-o",
+                         "jsonpath={.items[0].status.allocatable.amd\\.com/gpu}",
+                         check=False, capture=True)
+            if r.returncode == 0 and r.stdout.strip() not in ("", "0"):
+                ctx.out(f"allocatable amd.com/gpu: {r.stdout.strip()}")
+                break
+            if time.time() > deadline:
+                raise PhaseError("amd.com/gpu never became allocatable (see `mxk8s doctor gpu`)")
+            time.sleep(3)
+
+
+def phase_validate(ctx: Context) -> None:
+    ex = os.path.join(ctx.repo, "deploy", "examples")
+    for name, manifest in (("busybox-smoke", "busybox-smoke.yaml"),
+                           ("hip-vector-add", "hip-vector-add.yaml")):
+        _kubectl(ctx, "delete", "pod", name, "--ignore-not-found", check=False)
+        _kubectl(ctx, "apply", "-f", os.path.join(ex, manifest))
+        # instead of the reference's fixed `sleep 15` (README.md:326)
+        _kubectl(ctx, "wait", f"pod/{name}", "--for=jsonpath={.status.phase}=Succeeded",
+                 "--timeout=600s")
+        r = _kubectl(ctx, "logs", f"pod/{name}", capture=True, check=False)
+        if not ctx.dry_run and name == "hip-vector-add":
+            lines = [l for l in (r.stdout or "").splitlines() if l.startswith("RESULT ")]
+            if not lines or not json.loads(lines[-1][7:]).get("pass"):
+                raise PhaseError(f"{name}: no passing RESULT line in logs")
+
+
+PHASES: list[tuple[str, Callable[[Context], None]]] = [
+    ("prep", phase_prep),
+    ("driver-check", phase_driver_check),
+    ("runtime", phase_runtime),
+    ("cdi", phase_cdi),
+    ("k8s-packages", phase_k8s_packages),
+    ("cluster", phase_cluster),
+    ("stack", phase_stack),
+    ("validate", phase_validate),
+]
+PHASE_NAMES = [n for n, _ in PHASES]
+
+
+def completed(ctx: Context) -> list[str]:
+    t = ctx.read(hf.PHASE_FILE)
+    if not t:
+        return []
+    try:
+        return list(json.loads(t).get("completed", []))
+    except ValueError:
+        return []
+
+
+def mark(ctx: Context, name: str) -> None:
+    done = completed(ctx)
+    if name not in done:
+        done.append(name)
+    ctx.write(hf.PHASE_FILE, json.dumps({"completed": done, "updated": int(time.time())}) + "\n")
+
+
+def run(ctx: Context, only: Optional[Sequence[str]] = None, resume: bool = True,
+        until: Optional[str] = None) -> list[str]:
+    """Run phases in order.  Returns the phases executed this call."""
+    names = list(only) if only else PHASE_NAMES
+    unknown = [n for n in names if n not in PHASE_NAMES]
+    if unknown:
+        raise ValueError(f"unknown phase(s) {unknown}; choose from {PHASE_NAMES}")
+    done = set(completed(ctx)) if resume and not only else set()
+    ran = []
+    for name, fn in PHASES:
+        if name not in names:
+            continue
+        if name in done:
+            ctx.out(f"[mxk8s] phase {name}: already complete, skipping")
+            continue
+        ctx.out(f"[mxk8s] phase {name}")
+        fn(ctx)
+        mark(ctx, name)
+        ran.append(name)
+        if until and name == until:
+            break
+    return ran

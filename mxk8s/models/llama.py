@@ -1,0 +1,169 @@
+"""Llama-3 architecture (random init) for the DDP validator / training bench.
+
+BASELINE.json config 5: "PyTorch-ROCm DDP pod, Llama-3-8B synthetic training
+step on amd.com/gpu=8".  The reference has no model code at all (SURVEY.md
+§2.5); this is a from-scratch MI355X-first implementation:
+
+* fused projections: one [q|k|v] GEMM per attention block and one [gate|up]
+  GEMM per MLP (fewer, larger hipBLASLt GEMMs);
+* hand-written HIP kernels for the memory-bound glue: RMSNorm fwd/bwd,
+  SwiGLU fwd/bwd, rotary embedding fwd/bwd (``mxk8s.ops.fused``);
+* attention through ``scaled_dot_product_attention`` (causal, GQA) — the
+  ROCm flash backend;
+* bf16 parameters; fp32 master weights and AdamW state live in the optimizer
+  (``mxk8s.parallel.optim.FlatAdamW``).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.fused import rmsnorm, rope, rope_tables, swiglu
+
+
+@dataclasses.dataclass
+class LlamaConfig:
+    dim: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    ffn_dim: int = 14336
+    vocab_size: int = 128256
+    norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    max_seq_len: int = 8192
+
+    @classmethod
+    def llama3_8b(cls) -> "LlamaConfig":
+        return cls()
+
+    @classmethod
+    def tiny(cls) -> "LlamaConfig":
+        return cls(dim=256, n_layers=2, n_heads=8, n_kv_heads=2, ffn_dim=512, vocab_size=1024,
+                   max_seq_len=256)
+
+    @property
+    def head_dim(self) -> int:
+        return self.dim // self.n_heads
+
+    def num_params(self) -> int:
+        d, f, v, L = self.dim, self.ffn_dim, self.vocab_size, self.n_layers
+        kv = self.n_kv_heads * self.head_dim
+        per_layer = d * (d + 2 * kv) + d * d + 3 * d * f + 2 * d
+        return L * per_layer + 2 * v * d + d
+
+    def flops_per_token(self, seq_len: int) -> float:
+        """Training FLOPs/token: 6 * params (matmuls) + attention (causal)."""
+        n = self.num_params() - self.vocab_size * self.dim   # embedding lookup is free
+        attn = 6 * self.n_layers * self.dim * seq_len       # 12*L*d*S, halved by causality
+        return 6.0 * n + attn
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim: int, eps: float):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        return rmsnorm(x, self.weight, self.eps)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        hd = cfg.head_dim
+        self.wqkv = nn.Linear(cfg.dim, (cfg.n_heads + 2 * cfg.n_kv_heads) * hd, bias=False)
+        self.wo = nn.Linear(cfg.n_heads * hd, cfg.dim, bias=False)
+
+    def forward(self, x, cos, sin):
+        B, S, _ = x.shape
+        c = self.cfg
+        hd = c.head_dim
+        qkv = self.wqkv(x)
+        q, k, v = qkv.split([c.n_heads * hd, c.n_kv_heads * hd, c.n_kv_heads * hd], dim=-1)
+        q = rope(q.reshape(B, S, c.n_heads, hd), cos, sin)
+        k = rope(k.reshape(B, S, c.n_kv_heads, hd), cos, sin)
+        v = v.reshape(B, S, c.n_kv_heads, hd)
+        o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
+                                           is_causal=True, enable_gqa=True)
+        return self.wo(o.transpose(1, 2).reshape(B, S, c.n_heads * hd))
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.w13 = nn.Linear(cfg.dim, 2 * cfg.ffn_dim, bias=False)   # [gate | up]
+        self.w2 = nn.Linear(cfg.ffn_dim, cfg.dim, bias=False)
+
+    def forward(self, x):
+        return self.w2(swiglu(self.w13(x)))
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.attn_norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.attn = Attention(cfg)
+        self.mlp_norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.mlp = MLP(cfg)
+
+    def forward(self, x, cos, sin):
+        x = x + self.attn(self.attn_norm(x), cos, sin)
+        return x + self.mlp(self.mlp_norm(x))
+
+
+class Llama(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.embed = nn.Embedding(cfg.vocab_size, cfg.dim)
+        self.layers = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layers)])
+        self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.lm_head = nn.Linear(cfg.dim, cfg.vocab_size, bias=False)
+        self._rope = {}   # device -> (cos, sin) fp32 tables, never cast with the model
+        self.reset_parameters()
+
+    @torch.no_grad()
+    def reset_parameters(self, seed: int = 0) -> None:
+        """Random init (N(0, 0.02), residual projections scaled by 1/sqrt(2L)),
+        generated on the parameters' own device: an 8B model initialises in
+        seconds on the GPU instead of minutes on the host."""
+        gens = {}
+        std = 0.02
+        for name, p in self.named_parameters():
+            if p.dim() == 1:
+                p.fill_(1.0)
+                continue
+            if p.device not in gens:
+                gens[p.device] = torch.Generator(device=p.device).manual_seed(seed)
+            s = std / math.sqrt(2 * self.cfg.n_layers) if name.endswith(("wo.weight", "w2.weight")) else std
+            p.normal_(0.0, s, generator=gens[p.device])
+
+    def rope_tables(self, device) -> tuple[torch.Tensor, torch.Tensor]:
+        key = str(device)
+        if key not in self._rope:
+            self._rope[key] = rope_tables(self.cfg.max_seq_len, self.cfg.head_dim,
+                                          self.cfg.rope_theta, device=device)
+        return self._rope[key]
+
+    def forward(self, tokens: torch.Tensor) -> torch.Tensor:
+        cos, sin = self.rope_tables(tokens.device)
+        x = self.embed(tokens)
+        for layer in self.layers:
+            x = layer(x, cos, sin)
+        return self.lm_head(self.norm(x))
+
+    def loss(self, tokens: torch.Tensor, labels: torch.Tensor | None = None) -> torch.Tensor:
+        """Next-token cross entropy (fp32 softmax)."""
+        if labels is None:
+            inp, labels = tokens[:, :-1], tokens[:, 1:]
+        else:
+            inp = tokens
+        logits = self(inp)
+        return F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), labels.reshape(-1))

@@ -1,0 +1,144 @@
+"""Llama-3 DDP training on synthetic tokens (BASELINE config 5).
+
+One process per GPU (torchrun), RCCL over xGMI, flat bucketed all-reduce
+overlapped with backward (``mxk8s.parallel.ddp.FlatDDP``), fused flat AdamW
+(``mxk8s.parallel.optim.FlatAdamW``), bf16 compute.
+
+    python -m torch.distributed.run --standalone --nproc-per-node 8 \\
+        -m mxk8s.train.ddp_llama --steps 10 --seq-len 2048
+
+``run_ddp_bench`` is what ``bench.py --mode ddp`` calls: W warm-up steps, K
+timed steps bracketed by barrier + synchronize, slowest rank's time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+from ..models.llama import Llama, LlamaConfig
+from ..parallel import dist as mxdist
+from ..parallel.ddp import FlatDDP
+from ..parallel.optim import FlatAdamW
+
+MI355X_BF16_DENSE_PEAK = 2.5e15   # FLOP/s, dense (MI355X_MICROARCH.md)
+
+
+def build(cfg: LlamaConfig, device: torch.device, bucket_mb: float, lr: float = 3e-4):
+    with torch.device(device):
+        model = Llama(cfg)
+    model = model.to(torch.bfloat16)
+    ddp = FlatDDP(model, bucket_mb=bucket_mb)
+    opt = FlatAdamW(ddp.space, lr=lr, grad_scale=ddp.grad_scale)
+    return model, ddp, opt
+
+
+def train_step(model, ddp, opt, tokens) -> torch.Tensor:
+    loss = model.loss(tokens)
+    loss.backward()
+    ddp.finish_grad_sync()
+    opt.step()
+    ddp.zero_grad()
+    return loss.detach()
+
+
+def run_ddp_bench(args) -> dict:
+    world, rank, local = mxdist.world_info()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        backend = "nccl"
+    else:
+        dev = torch.device("cpu")
+        backend = "gloo"
+    mxdist.init_distributed(backend=backend, device=dev if backend == "nccl" else None)
+    cfg = LlamaConfig.llama3_8b()
+    model_name = "Llama-3-8B"
+    if getattr(args, "layers", None):
+        cfg.n_layers = args.layers
+        model_name = f"Llama-3-8B-shape, {args.layers} layers (NOT the headline config)"
+    if getattr(args, "tiny", False):
+        cfg = LlamaConfig.tiny()
+        model_name = "tiny-llama (test)"
+    seq, mb = args.seq_len, args.micro_batch
+    bucket_mb = getattr(args, "bucket_mb", 512.0)
+    model, ddp, opt = build(cfg, dev, bucket_mb)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    nbatches = 4
+    batches = [torch.randint(0, cfg.vocab_size, (mb, seq + 1), device=dev, generator=g)
+               for _ in range(nbatches)]
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for i in range(args.warmup):
+        train_step(model, ddp, opt, batches[i % nbatches])
+    sync()
+    mxdist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    losses = []
+    for i in range(args.steps):
+        losses.append(train_step(model, ddp, opt, batches[i % nbatches]))
+    sync()
+    mxdist.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    dt_max = mxdist.max_over_ranks(dt, dev)
+    tokens = world * mb * seq * args.steps
+    tps = tokens / dt_max
+    flops_tok = cfg.flops_per_token(seq)
+    mfu = flops_tok * tps / (MI355X_BF16_DENSE_PEAK * world)
+    peak_mem = torch.cuda.max_memory_allocated(dev) if dev.type == "cuda" else 0
+    final_loss = float(torch.stack(losses).float().mean().item()) if losses else float("nan")
+    return {
+        "metric": "Llama-3-8B DDP training throughput (tokens/s, whole job)",
+        "value": round(tps, 1),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (uniform random token ids), random-init weights",
+        "config": {"model": model_name, "global_batch": world * mb, "seq_len": seq,
+                   "parallelism": f"dp{world}"},
+        "tokens_per_s_per_gpu": round(tps / world, 1),
+        "mfu": round(mfu, 4),
+        "params": cfg.num_params(),
+        "peak_mem_gib": round(peak_mem / 2 ** 30, 2),
+        "mean_loss": final_loss,
+        "bucket_mb": bucket_mb,
+        "grad_norm_last": float(opt.last_grad_norm.item()),
+    }
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--seq-len", type=int, default=2048)
+    p.add_argument("--micro-batch", type=int, default=1)
+    p.add_argument("--layers", type=int, default=None)
+    p.add_argument("--bucket-mb", type=float, default=512.0)
+    p.add_argument("--tiny", action="store_true")
+    a = p.parse_args(argv)
+    out = run_ddp_bench(a)
+    if mxdist.world_info()[1] == 0:
+        print(json.dumps(out), flush=True)
+    if mxdist.active():
+        torch.distributed.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

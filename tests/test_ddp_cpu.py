@@ -1,0 +1,132 @@
+"""Multi-process data-parallel logic on CPU (gloo, world_size 2): the flat
+bucketed all-reduce must give every rank the SUM of all ranks' gradients,
+identical to a single-process reference, and the flat AdamW must match
+torch.optim.AdamW."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from mxk8s.models.llama import Llama, LlamaConfig
+from mxk8s.parallel.ddp import FlatDDP, FlatParamSpace
+from mxk8s.parallel.optim import FlatAdamW
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batch(rank, cfg):
+    g = torch.Generator().manual_seed(100 + rank)
+    return torch.randint(0, cfg.vocab_size, (2, 17), generator=g)
+
+
+def _worker(rank, world, port, outdir, bucket_mb):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    cfg = LlamaConfig.tiny()
+    model = Llama(cfg)   # fp32 on CPU (the CPU reference path of every fused op)
+    ddp = FlatDDP(model, bucket_mb=bucket_mb)
+    assert (len(ddp.buckets) > 1) == (bucket_mb < 1)
+    loss = model.loss(_batch(rank, cfg))
+    loss.backward()
+    ddp.finish_grad_sync()
+    torch.save({"grad": ddp.space.grad_buf.clone(), "param": ddp.space.param_buf.clone()},
+               os.path.join(outdir, f"r{rank}.pt"))
+    # one optimizer step keeps replicas identical
+    opt = FlatAdamW(ddp.space, lr=1e-3, grad_scale=ddp.grad_scale)
+    opt.step()
+    torch.save({"param_after": ddp.space.param_buf.clone()}, os.path.join(outdir, f"s{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bucket_mb", [0.05, 512.0])
+def test_flat_ddp_gloo_two_ranks(bucket_mb):
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), d, bucket_mb), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"r{i}.pt"), weights_only=True) for i in range(world)]
+        s = [torch.load(os.path.join(d, f"s{i}.pt"), weights_only=True) for i in range(world)]
+    assert torch.equal(r[0]["grad"], r[1]["grad"])
+    assert torch.equal(s[0]["param_after"], s[1]["param_after"])
+    # single-process reference: sum of per-rank gradients
+    cfg = LlamaConfig.tiny()
+    ref_sum = None
+    for rank in range(world):
+        torch.manual_seed(0)
+        model = Llama(cfg)
+        space = FlatParamSpace(model)
+        model.loss(_batch(rank, cfg)).backward()
+        ref_sum = space.grad_buf.clone() if ref_sum is None else ref_sum + space.grad_buf
+    assert torch.allclose(r[0]["grad"], ref_sum, rtol=1e-5, atol=1e-6)
+
+
+def test_flat_space_views_and_grad_accumulation():
+    torch.manual_seed(0)
+    model = Llama(LlamaConfig.tiny())
+    before = {n: p.detach().clone() for n, p in model.named_parameters()}
+    space = FlatParamSpace(model)
+    for n, p in model.named_parameters():
+        assert torch.equal(p.detach(), before[n])
+        assert p.data_ptr() >= space.param_buf.data_ptr()
+        assert p.grad is not None and p.grad.data_ptr() >= space.grad_buf.data_ptr()
+    # 2-D (decay) params first, 1-D (norms) last
+    dims = [p.dim() for p in space.params]
+    assert dims == sorted(dims, reverse=True)
+    assert all(o % 64 == 0 for o in space.offsets)
+    tok = torch.randint(0, 1024, (2, 9))
+    model.loss(tok).backward()
+    g1 = space.grad_buf.clone()
+    model.loss(tok).backward()   # accumulates in place into the flat buffer
+    assert torch.allclose(space.grad_buf, 2 * g1, rtol=1e-5, atol=1e-7)
+    space.zero_grad()
+    assert space.grad_buf.abs().sum() == 0
+
+
+def test_flat_adamw_matches_torch_adamw():
+    torch.manual_seed(1)
+    lin = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.LayerNorm(32))
+    ref = [p.detach().clone().requires_grad_() for p in lin.parameters()]
+    space = FlatParamSpace(lin)
+    opt = FlatAdamW(space, lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
+                    max_grad_norm=0.0)
+    decay = [r for r in ref if r.dim() >= 2]
+    nodecay = [r for r in ref if r.dim() < 2]
+    topt = torch.optim.AdamW([{"params": decay, "weight_decay": 0.1},
+                              {"params": nodecay, "weight_decay": 0.0}],
+                             lr=1e-2, betas=(0.9, 0.95), eps=1e-8)
+    for step in range(3):
+        x = torch.randn(4, 16)
+        lin(x).pow(2).sum().backward()
+        opt.step()
+        space.zero_grad()
+        # same grads for the reference params
+        out = torch.nn.functional.layer_norm(
+            torch.nn.functional.linear(x, ref[0], ref[1]), (32,), ref[2], ref[3])
+        out.pow(2).sum().backward()
+        topt.step()
+        topt.zero_grad()
+    for p, r in zip(lin.parameters(), ref):
+        assert torch.allclose(p.detach(), r.detach(), rtol=1e-4, atol=1e-5)
+
+
+def test_grad_clipping_reference():
+    lin = torch.nn.Linear(8, 8, bias=False)
+    space = FlatParamSpace(lin)
+    opt = FlatAdamW(space, lr=0.0, weight_decay=0.0, max_grad_norm=1.0, grad_scale=0.5)
+    space.grad_buf.fill_(1.0)
+    opt.step()
+    norm = float(opt.last_grad_norm)
+    # the buffer holds the SUM over 2 ranks -> mean grad norm = 0.5 * ||1||
+    assert abs(norm - 0.5 * (64 ** 0.5)) < 1e-4
+    assert abs(float(opt._scale[0]) - 0.5 / (norm + 1e-6)) < 1e-6
