@@ -1,0 +1,41 @@
+"""``python -m mxk8s.deviceplugin`` — the amd.com/gpu device plugin DaemonSet entry point."""
+from __future__ import annotations
+
+import argparse
+import logging
+import sys
+
+from .plugin import PluginConfig, run_forever
+
+
+def _bool(s: str) -> bool:
+    return str(s).lower() in ("1", "true", "yes", "on")
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser(description=__doc__)
+    p.add_argument("--resource-name", default="amd.com/gpu")
+    p.add_argument("--plugin-dir", default="/var/lib/kubelet/device-plugins/")
+    p.add_argument("--socket-name", default="amd-gpu.sock")
+    p.add_argument("--sysfs-root", default="")
+    p.add_argument("--health-interval", type=float, default=5.0)
+    p.add_argument("--event-quarantine", type=float, default=60.0)
+    p.add_argument("--cdi", type=_bool, default=True)
+    p.add_argument("--device-specs", type=_bool, default=True)
+    p.add_argument("--fault-file", default=None)
+    p.add_argument("--no-smi-events", action="store_true")
+    a = p.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    cfg = PluginConfig(resource_name=a.resource_name, plugin_dir=a.plugin_dir,
+                       socket_name=a.socket_name, sysfs_root=a.sysfs_root,
+                       health_interval=a.health_interval, event_quarantine_s=a.event_quarantine,
+                       use_cdi=a.cdi, use_device_specs=a.device_specs,
+                       use_smi_events=not a.no_smi_events)
+    if a.fault_file:
+        cfg.fault_file = a.fault_file
+    run_forever(cfg)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

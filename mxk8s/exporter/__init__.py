@@ -1,0 +1,230 @@
+"""amd-smi Prometheus exporter on :9400 — the DCGM-exporter counterpart.
+
+The reference stack's GPU Operator runs dcgm-exporter (DCGM_FI_DEV_GPU_UTIL,
+_FB_USED, _GPU_TEMP, _POWER_USAGE, ... [ext]).  This exporter
+samples amd-smi through ``libmxnode`` (C++, dlopen'ed amd-smi) on a
+background thread and serves the latest snapshot, so scrapes never touch the
+driver:
+
+  amd_gpu_utilization_percent            amd_gpu_memory_activity_percent
+  amd_gpu_memory_used_bytes              amd_gpu_memory_total_bytes
+  amd_gpu_temperature_celsius{sensor}    amd_gpu_power_watts / _power_limit_watts
+  amd_gpu_clock_mhz{type=sclk|mclk}      amd_gpu_ecc_errors_total{type}
+  amd_gpu_processes                      amd_gpu_xgmi_links
+  amd_gpu_device_healthy                 amd_gpu_info{arch,product,uuid,bdf,...}
+  amd_gpu_stack_component_up{component}  amd_gpu_exporter_sample_seconds
+
+Per-GPU labels: gpu, bdf, uuid and — through the kubelet PodResources API —
+namespace, pod, container of the workload the GPU is allocated to.
+"""
+from __future__ import annotations
+
+import dataclasses
+import http.server
+import logging
+import os
+import threading
+import time
+from typing import Callable, Optional
+
+from ..native import node
+
+log = logging.getLogger("mxk8s.exporter")
+
+
+def _esc(v) -> str:
+    return str(v).replace("\\", "\\\\").replace("\n", "\\n").replace('"', '\\"')
+
+
+class MetricWriter:
+    def __init__(self):
+        self.lines: list[str] = []
+        self._declared = set()
+
+    def add(self, name: str, mtype: str, help_: str, value, labels: Optional[dict] = None):
+        if value is None:
+            return
+        if name not in self._declared:
+            self.lines.append(f"# HELP {name} {help_}")
+            self.lines.append(f"# TYPE {name} {mtype}")
+            self._declared.add(name)
+        lab = ""
+        if labels:
+            lab = "{" + ",".join(f'{k}="{_esc(v)}"' for k, v in labels.items()) + "}"
+        if isinstance(value, float):
+            val = repr(value)
+        else:
+            val = str(int(value)) if isinstance(value, bool) else str(value)
+        self.lines.append(f"{name}{lab} {val}")
+
+    def text(self) -> str:
+        return "\n".join(self.lines) + "\n"
+
+
+class SmiBackend:
+    """Real backend: libmxnode topology + amd-smi samples, matched by BDF."""
+
+    def __init__(self, sysfs_root: str = ""):
+        self.sysfs_root = sysfs_root
+        self.ok, self.err = node.smi_open()
+        self.driver = node.smi_driver_version() if self.ok else ""
+
+    def gpus(self) -> list[node.GpuInfo]:
+        return node.enumerate_gpus(self.sysfs_root)
+
+    def samples(self) -> dict[str, node.GpuSample]:
+        if not self.ok:
+            return {}
+        out = {}
+        for i in range(max(0, node.smi_count())):
+            s = node.smi_sample(i)
+            if s.valid:
+                out[s.bdf] = s
+        return out
+
+    def health(self, index: int) -> int:
+        return node.health_check(index, self.sysfs_root, os.environ.get("MXK8S_FAULT_FILE"))
+
+
+def render_metrics(gpus, samples: dict, health: Callable[[int], int], owners: dict,
+                   driver: str, components: dict, sample_seconds: float) -> str:
+    w = MetricWriter()
+    for g in gpus:
+        base = {"gpu": str(g.index), "bdf": g.bdf, "uuid": g.uuid}
+        own = owners.get(str(g.index))
+        if own:
+            base.update(namespace=own[0], pod=own[1], container=own[2])
+        w.add("amd_gpu_info", "gauge", "Static GPU facts (value is always 1).", 1,
+              {**base, "arch": g.arch, "product": g.product, "device_id": f"0x{g.device_id:04x}",
+               "driver_version": driver, "numa_node": str(g.numa_node)})
+        h = health(g.index)
+        w.add("amd_gpu_device_healthy", "gauge", "1 if the device plugin would report Healthy.",
+              1 if h == 0 else 0, base)
+        w.add("amd_gpu_xgmi_links", "gauge", "xGMI links of the GPU (KFD topology).", g.xgmi_links, base)
+        s = samples.get(g.bdf)
+        if s is None:
+            continue
+        w.add("amd_gpu_utilization_percent", "gauge", "GFX engine activity (%).", s.gfx_activity_pct, base)
+        w.add("amd_gpu_memory_activity_percent", "gauge", "Memory controller activity (%).",
+              s.umc_activity_pct, base)
+        w.add("amd_gpu_memory_used_bytes", "gauge", "VRAM in use (bytes).", s.vram_used_bytes, base)
+        w.add("amd_gpu_memory_total_bytes", "gauge", "VRAM size (bytes).", s.vram_total_bytes, base)
+        for sensor, val in (("edge", s.temp_edge_c), ("hotspot", s.temp_hotspot_c), ("memory", s.temp_mem_c)):
+            if val is not None:
+                w.add("amd_gpu_temperature_celsius", "gauge", "Temperature by sensor (C).",
+                      float(val), {**base, "sensor": sensor})
+        w.add("amd_gpu_power_watts", "gauge", "Socket power (W).", s.power_w, base)
+        w.add("amd_gpu_power_limit_watts", "gauge", "Power cap (W).", s.power_limit_w, base)
+        w.add("amd_gpu_clock_mhz", "gauge", "Current clock (MHz).", s.sclk_mhz, {**base, "type": "sclk"})
+        w.add("amd_gpu_clock_mhz", "gauge", "Current clock (MHz).", s.mclk_mhz, {**base, "type": "mclk"})
+        w.add("amd_gpu_ecc_errors_total", "counter", "Accumulated ECC errors.", s.ecc_correctable,
+              {**base, "type": "correctable"})
+        w.add("amd_gpu_ecc_errors_total", "counter", "Accumulated ECC errors.", s.ecc_uncorrectable,
+              {**base, "type": "uncorrectable"})
+        w.add("amd_gpu_processes", "gauge", "Processes with a KFD context on the GPU.",
+              s.num_processes, base)
+    for comp, up in sorted(components.items()):
+        w.add("amd_gpu_stack_component_up", "gauge", "1 if the stack component is healthy.",
+              1 if up else 0, {"component": comp})
+    w.add("amd_gpu_exporter_sample_seconds", "gauge", "Time the last sample took (s).",
+          float(sample_seconds))
+    return w.text()
+
+
+@dataclasses.dataclass
+class ExporterConfig:
+    port: int = 9400
+    interval: float = 5.0
+    pod_resources_socket: Optional[str] = None
+    plugin_socket: str = "/var/lib/kubelet/device-plugins/amd-gpu.sock"
+    cdi_spec: str = "/etc/cdi/amd.com-gpu.json"
+
+
+class Exporter:
+    def __init__(self, cfg: ExporterConfig, backend=None):
+        self.cfg = cfg
+        self.backend = backend or SmiBackend()
+        self._text = "# no sample yet\n"
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self._httpd: Optional[http.server.ThreadingHTTPServer] = None
+        self.samples_taken = 0
+
+    def components(self) -> dict:
+        c = {"amd_smi": bool(getattr(self.backend, "ok", True))}
+        c["device_plugin"] = os.path.exists(self.cfg.plugin_socket)
+        c["cdi_spec"] = os.path.exists(self.cfg.cdi_spec)
+        return c
+
+    def sample_once(self) -> str:
+        t0 = time.perf_counter()
+        gpus = self.backend.gpus()
+        samples = self.backend.samples()
+        owners = {}
+        if self.cfg.pod_resources_socket and os.path.exists(self.cfg.pod_resources_socket):
+            try:
+                from .podresources import gpu_owners
+                owners = gpu_owners(self.cfg.pod_resources_socket)
+            except Exception as e:   # kubelet busy/old: metrics without pod labels
+                log.debug("pod-resources unavailable: %s", e)
+        text = render_metrics(gpus, samples, self.backend.health, owners,
+                              getattr(self.backend, "driver", ""), self.components(),
+                              time.perf_counter() - t0)
+        with self._lock:
+            self._text = text
+        self.samples_taken += 1
+        return text
+
+    def metrics(self) -> str:
+        with self._lock:
+            return self._text
+
+    def _loop(self):
+        while not self._stop.is_set():
+            try:
+                self.sample_once()
+            except Exception:
+                log.exception("sampling failed")
+            self._stop.wait(self.cfg.interval)
+
+    def start(self) -> "Exporter":
+        self.sample_once()
+        self._thread = threading.Thread(target=self._loop, name="mxk8s-exporter", daemon=True)
+        self._thread.start()
+        exporter = self
+
+        class Handler(http.server.BaseHTTPRequestHandler):
+            def do_GET(self):
+                if self.path.startswith("/metrics"):
+                    body = exporter.metrics().encode()
+                    ctype = "text/plain; version=0.0.4; charset=utf-8"
+                elif self.path.startswith("/healthz"):
+                    body, ctype = b"ok\n", "text/plain"
+                else:
+                    self.send_response(404)
+                    self.end_headers()
+                    return
+                self.send_response(200)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def log_message(self, *a):
+                pass
+
+        self._httpd = http.server.ThreadingHTTPServer(("", self.cfg.port), Handler)
+        threading.Thread(target=self._httpd.serve_forever, name="mxk8s-exporter-http",
+                         daemon=True).start()
+        return self
+
+    @property
+    def port(self) -> int:
+        return self._httpd.server_address[1] if self._httpd else self.cfg.port
+
+    def stop(self):
+        self._stop.set()
+        if self._httpd:
+            self._httpd.shutdown()
+            self._httpd.server_close()

@@ -1,0 +1,32 @@
+"""``python -m mxk8s.exporter --port 9400`` (DaemonSet entry point)."""
+from __future__ import annotations
+
+import argparse
+import logging
+import sys
+import time
+
+from . import Exporter, ExporterConfig
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser(description=__doc__)
+    p.add_argument("--port", type=int, default=9400)
+    p.add_argument("--interval", type=float, default=5.0)
+    p.add_argument("--pod-resources-socket", default=None)
+    p.add_argument("--once", action="store_true", help="print one sample and exit")
+    a = p.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(message)s")
+    ex = Exporter(ExporterConfig(port=a.port, interval=a.interval,
+                                 pod_resources_socket=a.pod_resources_socket))
+    if a.once:
+        sys.stdout.write(ex.sample_once())
+        return 0
+    ex.start()
+    logging.getLogger("mxk8s.exporter").info("serving /metrics on :%d", ex.port)
+    while True:
+        time.sleep(3600)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

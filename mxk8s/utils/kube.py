@@ -1,0 +1,75 @@
+"""Minimal Kubernetes API client (in-cluster service account or kubeconfig
+token), enough for the node labeller and ``mxk8s doctor``: GET and JSON
+merge-PATCH over HTTPS with the cluster CA.  No kubernetes Python package is
+needed (none is installed in the image)."""
+from __future__ import annotations
+
+import json
+import os
+import ssl
+import urllib.error
+import urllib.request
+from typing import Optional
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+class KubeError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"HTTP {status}: {msg}")
+        self.status = status
+
+
+class KubeClient:
+    def __init__(self, server: str, token: Optional[str] = None, ca_file: Optional[str] = None,
+                 insecure: bool = False, timeout: float = 10.0):
+        self.server = server.rstrip("/")
+        self.token = token
+        self.timeout = timeout
+        if self.server.startswith("https"):
+            ctx = ssl.create_default_context(cafile=ca_file) if ca_file else ssl.create_default_context()
+            if insecure:
+                ctx.check_hostname = False
+                ctx.verify_mode = ssl.CERT_NONE
+            self._ctx = ctx
+        else:
+            self._ctx = None
+
+    @classmethod
+    def in_cluster(cls, sa_dir: str = SA_DIR) -> "KubeClient":
+        host = os.environ.get("KUBERNETES_SERVICE_HOST")
+        port = os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+        if not host:
+            raise RuntimeError("not running in a cluster (KUBERNETES_SERVICE_HOST unset)")
+        with open(os.path.join(sa_dir, "token")) as f:
+            token = f.read().strip()
+        if ":" in host and not host.startswith("["):
+            host = f"[{host}]"
+        return cls(f"https://{host}:{port}", token, os.path.join(sa_dir, "ca.crt"))
+
+    def _req(self, method: str, path: str, body=None, content_type="application/json"):
+        data = None if body is None else json.dumps(body).encode()
+        req = urllib.request.Request(self.server + path, data=data, method=method)
+        req.add_header("Accept", "application/json")
+        if data is not None:
+            req.add_header("Content-Type", content_type)
+        if self.token:
+            req.add_header("Authorization", f"Bearer {self.token}")
+        try:
+            with urllib.request.urlopen(req, timeout=self.timeout, context=self._ctx) as r:
+                return json.loads(r.read() or b"{}")
+        except urllib.error.HTTPError as e:
+            raise KubeError(e.code, e.read().decode(errors="replace")[:500]) from None
+
+    def get(self, path: str) -> dict:
+        return self._req("GET", path)
+
+    def merge_patch(self, path: str, patch: dict) -> dict:
+        return self._req("PATCH", path, patch, "application/merge-patch+json")
+
+    def get_node(self, name: str) -> dict:
+        return self.get(f"/api/v1/nodes/{name}")
+
+    def patch_node_labels(self, name: str, labels: dict) -> dict:
+        """labels: value None deletes the label (JSON merge patch)."""
+        return self.merge_patch(f"/api/v1/nodes/{name}", {"metadata": {"labels": labels}})
