@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.fused import rmsnorm, rope, rope_tables, swiglu
+from ..ops.fused import add_rmsnorm, rmsnorm, rope, rope_tables, swiglu
 
 
 @dataclasses.dataclass
@@ -106,6 +106,11 @@ class MLP(nn.Module):
 
 
 class Block(nn.Module):
+    """Pre-norm block.  ``forward(h, y)`` takes the residual stream h and its
+    already-normalised copy y = attn_norm(h) and returns the block's output
+    residual and the MLP delta still to be added, so every residual add is
+    fused into the following RMSNorm (``add_rmsnorm``)."""
+
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.attn_norm = RMSNorm(cfg.dim, cfg.norm_eps)
@@ -113,9 +118,10 @@ class Block(nn.Module):
         self.mlp_norm = RMSNorm(cfg.dim, cfg.norm_eps)
         self.mlp = MLP(cfg)
 
-    def forward(self, x, cos, sin):
-        x = x + self.attn(self.attn_norm(x), cos, sin)
-        return x + self.mlp(self.mlp_norm(x))
+    def forward(self, h, y, cos, sin):
+        a = self.attn(y, cos, sin)
+        h, y2 = add_rmsnorm(h, a, self.mlp_norm.weight, self.mlp_norm.eps)
+        return h, self.mlp(y2)
 
 
 class Llama(nn.Module):
@@ -154,10 +160,13 @@ class Llama(nn.Module):
 
     def forward(self, tokens: torch.Tensor) -> torch.Tensor:
         cos, sin = self.rope_tables(tokens.device)
-        x = self.embed(tokens)
-        for layer in self.layers:
-            x = layer(x, cos, sin)
-        return self.lm_head(self.norm(x))
+        h = self.embed(tokens)
+        y = rmsnorm(h, self.layers[0].attn_norm.weight, self.cfg.norm_eps) if self.layers else h
+        for i, layer in enumerate(self.layers):
+            h, delta = layer(h, y, cos, sin)
+            nxt = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.norm
+            h, y = add_rmsnorm(h, delta, nxt.weight, nxt.eps)
+        return self.lm_head(y)
 
     def loss(self, tokens: torch.Tensor, labels: torch.Tensor | None = None) -> torch.Tensor:
         """Next-token cross entropy (fp32 softmax)."""

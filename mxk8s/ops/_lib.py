@@ -38,7 +38,8 @@ _SIGNATURES = {
     "mxk_error_string": (ctypes.c_char_p, [_i]),
     "mxk_rmsnorm_fwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _f, _vp]),
     "mxk_rmsnorm_bwd_workspace": (_l, [_i, _i]),
-    "mxk_rmsnorm_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
+    "mxk_add_rmsnorm_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _f, _vp]),
+    "mxk_rmsnorm_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
     "mxk_swiglu_fwd": (_i, [_vp, _vp, _l, _i, _vp]),
     "mxk_swiglu_bwd": (_i, [_vp, _vp, _vp, _l, _i, _vp]),
     "mxk_rope": (_i, [_vp, _vp, _vp, _vp, _l, _i, _i, _i, _f, _vp]),

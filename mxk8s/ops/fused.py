@@ -77,10 +77,63 @@ class _RMSNorm(torch.autograd.Function):
         ws = torch.empty(L.mxk_rmsnorm_bwd_workspace(rows, H) // 4, dtype=torch.float32,
                          device=x2.device)
         st = L.mxk_rmsnorm_bwd(dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), rstd.data_ptr(),
-                               dx.data_ptr(), dw.data_ptr(), None, ws.data_ptr(), rows, H,
+                               None, dx.data_ptr(), dw.data_ptr(), None, ws.data_ptr(), rows, H,
                                _lib.stream_ptr(x2.device))
         _lib.check(st, "mxk_rmsnorm_bwd")
         return dx.view(ctx.shape), dw, None
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    """h = x + delta ; y = rmsnorm(h) * w  ->  (h, y).  Backward fuses the
+    residual gradient into the norm's input gradient: dx = ddelta =
+    dh + rmsnorm_bwd(dy)."""
+
+    @staticmethod
+    def forward(ctx, x, delta, w, eps):
+        H = x.shape[-1]
+        x2 = x.contiguous().view(-1, H)
+        d2 = delta.contiguous().view(-1, H)
+        rows = x2.shape[0]
+        h = torch.empty_like(x2)
+        y = torch.empty_like(x2)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        st = _lib.lib().mxk_add_rmsnorm_fwd(x2.data_ptr(), d2.data_ptr(), w.data_ptr(), h.data_ptr(),
+                                            y.data_ptr(), rstd.data_ptr(), rows, H, float(eps),
+                                            _lib.stream_ptr(x.device))
+        _lib.check(st, "mxk_add_rmsnorm_fwd")
+        ctx.save_for_backward(h, w, rstd)
+        ctx.shape = x.shape
+        return h.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        h, w, rstd = ctx.saved_tensors
+        rows, H = h.shape
+        L = _lib.lib()
+        dw = torch.empty_like(w)
+        if dy is None:
+            dy = torch.zeros_like(h)
+        dy2 = dy.contiguous().view(rows, H)
+        dres = None if dh is None else dh.contiguous().view(rows, H)
+        dx = torch.empty_like(h)
+        ws = torch.empty(L.mxk_rmsnorm_bwd_workspace(rows, H) // 4, dtype=torch.float32,
+                         device=h.device)
+        st = L.mxk_rmsnorm_bwd(dy2.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr(),
+                               None if dres is None else dres.data_ptr(), dx.data_ptr(),
+                               dw.data_ptr(), None, ws.data_ptr(), rows, H,
+                               _lib.stream_ptr(h.device))
+        _lib.check(st, "mxk_rmsnorm_bwd")
+        dx = dx.view(ctx.shape)
+        return dx, dx, dw, None
+
+
+def add_rmsnorm(x: torch.Tensor, delta: torch.Tensor, w: torch.Tensor,
+                eps: float = 1e-5) -> tuple[torch.Tensor, torch.Tensor]:
+    """Fused pre-norm residual step: returns (h, rmsnorm(h) * w) with h = x + delta."""
+    if x.device.type == "cpu" or x.dtype != torch.bfloat16:
+        h = x + delta
+        return h, rmsnorm(h, w, eps)
+    return _AddRMSNorm.apply(x, delta, w, eps)
 
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
@@ -167,5 +220,5 @@ def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     return _RoPE.apply(x, cos_s, sin_s)
 
 
-__all__ = ["rmsnorm", "swiglu", "rope", "rope_tables", "rmsnorm_ref", "swiglu_ref",
+__all__ = ["rmsnorm", "add_rmsnorm", "swiglu", "rope", "rope_tables", "rmsnorm_ref", "swiglu_ref",
            "rope_ref"]

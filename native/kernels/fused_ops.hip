@@ -41,25 +41,42 @@ constexpr int kChunk = kRowThreads * 8;   // elements covered per pass over a ro
 // ---------------------------------------------------------------------------
 // RMSNorm:  y = x * rstd * w,  rstd = 1/sqrt(mean(x^2) + eps)   (one row/block)
 // ---------------------------------------------------------------------------
+// With `delta` != nullptr this is the fused residual step of a pre-norm
+// transformer: h = x + delta is written to h_out and normalised in the same
+// pass (saves a separate add kernel and a re-read of h).
 __global__ void __launch_bounds__(kRowThreads)
-mxk_rmsnorm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+mxk_rmsnorm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ delta,
+                       const uint16_t* __restrict__ w, uint16_t* __restrict__ h_out,
                        uint16_t* __restrict__ y, float* __restrict__ rstd_out, int H, float eps) {
   __shared__ float red[4];
   const size_t row = blockIdx.x;
   const uint16_t* xr = x + row * H;
+  const uint16_t* dr = delta ? delta + row * H : nullptr;
+  uint16_t* hr = h_out ? h_out + row * H : nullptr;
   float ss = 0.f;
   for (int c = threadIdx.x * 8; c < H; c += kChunk) {
     float f[8];
     load8(xr + c, f);
+    if (dr) {
+      float d[8];
+      load8(dr + c, d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += d[e];
+      store8(hr + c, f);
+      // normalise the bf16-rounded h, exactly what a separate add would feed
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = mxk::bf2f(mxk::f2bf(f[e]));
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) ss += f[e] * f[e];
   }
   const float rstd = rsqrtf(block_sum256(ss, red) / static_cast<float>(H) + eps);
   if (threadIdx.x == 0 && rstd_out) rstd_out[row] = rstd;
+  const uint16_t* src = dr ? hr : xr;
   uint16_t* yr = y + row * H;
   for (int c = threadIdx.x * 8; c < H; c += kChunk) {
     float f[8], g[8];
-    load8(xr + c, f);   // second read hits L1/L2 (row is 2*H bytes)
+    load8(src + c, f);   // second read hits L1/L2 (row is 2*H bytes)
     load8(w + c, g);
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] = f[e] * rstd * g[e];
@@ -74,8 +91,8 @@ mxk_rmsnorm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restric
 __global__ void __launch_bounds__(kRowThreads)
 mxk_rmsnorm_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                        const uint16_t* __restrict__ w, const float* __restrict__ rstd,
-                       uint16_t* __restrict__ dx, float* __restrict__ dw_part, int rows, int H,
-                       int rows_per_block) {
+                       const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
+                       float* __restrict__ dw_part, int rows, int H, int rows_per_block) {
   __shared__ float red[4];
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
@@ -110,6 +127,12 @@ mxk_rmsnorm_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restri
       for (int e = 0; e < 8; ++e) {
         o[e] = rs * (a[e] * g[e] - b[e] * rs * rs * mean_gx);
       }
+      if (dres) {   // fused residual: gradient flowing around the norm
+        float r[8];
+        load8(dres + off + c, r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += r[e];
+      }
       store8(dx + off + c, o);
 #pragma unroll
       for (int q = 0; q < kMaxPass; ++q)
@@ -132,16 +155,25 @@ mxk_rmsnorm_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restri
   }
 }
 
-// out[c] = sum_b part[b][c]  (fp32 in, bf16 or fp32 out)
+// out[c] = sum_b part[b][c]  (fp32 in, bf16 or fp32 out).  A block owns 64
+// columns; its 4 waves take every 4th slab row (each wave reads 256
+// contiguous bytes per row) and fold through LDS in a fixed order.
 __global__ void __launch_bounds__(256)
 mxk_colsum_kernel(const float* __restrict__ part, int nb, int H, uint16_t* __restrict__ out_bf16,
                   float* __restrict__ out_f32) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= H) return;
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[static_cast<size_t>(b) * H + c];
-  if (out_bf16) out_bf16[c] = mxk::f2bf(s);
-  if (out_f32) out_f32[c] = s;
+  if (c < H)
+    for (int b = g; b < nb; b += 4) s += part[static_cast<size_t>(b) * H + c];
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < H) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (out_bf16) out_bf16[c] = mxk::f2bf(t);
+    if (out_f32) out_f32[c] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -256,31 +288,54 @@ MXK_API int mxk_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, 
   if (H % 8 || !aligned16(x) || !aligned16(w) || !aligned16(y))
     return static_cast<int>(hipErrorInvalidValue);
   hipLaunchKernelGGL(mxk_rmsnorm_fwd_kernel, dim3(rows), dim3(kRowThreads), 0, s,
-                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w),
+                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(nullptr),
+                     static_cast<const uint16_t*>(w), static_cast<uint16_t*>(nullptr),
+                     static_cast<uint16_t*>(y), rstd, H, eps);
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// h = x + delta; y = rmsnorm(h) * w   (one pass)
+MXK_API int mxk_add_rmsnorm_fwd(const void* x, const void* delta, const void* w, void* h, void* y,
+                                float* rstd, int rows, int H, float eps, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (H % 8 || !aligned16(x) || !aligned16(delta) || !aligned16(w) || !aligned16(h) ||
+      !aligned16(y))
+    return static_cast<int>(hipErrorInvalidValue);
+  hipLaunchKernelGGL(mxk_rmsnorm_fwd_kernel, dim3(rows), dim3(kRowThreads), 0, s,
+                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(delta),
+                     static_cast<const uint16_t*>(w), static_cast<uint16_t*>(h),
                      static_cast<uint16_t*>(y), rstd, H, eps);
   MXK_RETURN_LAUNCH_STATUS();
 }
 
 // Workspace size (bytes) the backward needs for its dw slab.
+namespace {
+// one block per CU keeps the dw slab small (256 x H fp32) while every CU works
+constexpr int kBwdBlocks = 256;
+}
+
 MXK_API long mxk_rmsnorm_bwd_workspace(int rows, int H) {
-  const int nb = rows < 512 ? rows : 512;
+  const int nb = rows < kBwdBlocks ? rows : kBwdBlocks;
   return static_cast<long>(nb) * H * 4;
 }
 
+// dx = rmsnorm_bwd(dy) [+ dres].  dres (nullable) is the gradient that flows
+// around the norm through the residual stream (fused add_rmsnorm backward).
 MXK_API int mxk_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
-                            void* dx, void* dw_bf16, float* dw_f32, float* workspace, int rows,
-                            int H, hipStream_t s) {
+                            const void* dres, void* dx, void* dw_bf16, float* dw_f32,
+                            float* workspace, int rows, int H, hipStream_t s) {
   if (rows <= 0) return 0;
-  if (H % 8 || H > 8 * kChunk || !aligned16(dy) || !aligned16(x) || !aligned16(dx))
+  if (H % 8 || H > 8 * kChunk || !aligned16(dy) || !aligned16(x) || !aligned16(dx) ||
+      (dres && !aligned16(dres)))
     return static_cast<int>(hipErrorInvalidValue);
-  const int nb = rows < 512 ? rows : 512;
+  const int nb = rows < kBwdBlocks ? rows : kBwdBlocks;
   const int rpb = (rows + nb - 1) / nb;
   const int nblocks = (rows + rpb - 1) / rpb;
   hipLaunchKernelGGL(mxk_rmsnorm_bwd_kernel, dim3(nblocks), dim3(kRowThreads), 0, s,
                      static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(x),
-                     static_cast<const uint16_t*>(w), rstd, static_cast<uint16_t*>(dx), workspace,
-                     rows, H, rpb);
-  hipLaunchKernelGGL(mxk_colsum_kernel, dim3((H + 255) / 256), dim3(256), 0, s, workspace, nblocks,
+                     static_cast<const uint16_t*>(w), rstd, static_cast<const uint16_t*>(dres),
+                     static_cast<uint16_t*>(dx), workspace, rows, H, rpb);
+  hipLaunchKernelGGL(mxk_colsum_kernel, dim3((H + 63) / 64), dim3(256), 0, s, workspace, nblocks,
                      H, static_cast<uint16_t*>(dw_bf16), dw_f32);
   MXK_RETURN_LAUNCH_STATUS();
 }

@@ -250,6 +250,14 @@ constexpr int W4_STAGE_BYTES = 2 * W4_OP_BYTES;     // 32 KiB
 
 __device__ __forceinline__ int w4_h(int q) { return (((q ^ (q >> 1)) & 1) << 1) | (q >> 1); }
 
+// MFMA with the accumulator pinned to AGPRs ("+a"): with 256 accumulators per
+// wave the compiler's own allocation shuffles them through VGPRs every trip.
+// A chain of MFMAs accumulating into the same registers needs no wait states;
+// the caller pads before the accumulators are read by non-MFMA code.
+__device__ __forceinline__ void mfma_16x16x32_agpr(f32x4_t& acc, bf16x8_t a, bf16x8_t b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
 // One operand stage (256 rows x 32 k) = 4 glds per thread (1 KiB per wave
 // instruction = 16 rows of 64 B).
 __device__ __forceinline__ void w4_stage_operand(const uint16_t* __restrict__ src, int ld, int row0,
@@ -339,22 +347,26 @@ mxk_gemm_bf16_tn_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__
         w4_stage_operand(A, lda, m0, kk, buf, tid);
         w4_stage_operand(Bt, ldb, n0, kk, buf + W4_OP_BYTES, tid);
       }
-      // (3) fragments of stage st+1 into the other register set
+      // (3)+(4) 64 MFMAs on stage st straight from registers, with the 16
+      // fragment reads of stage st+1 (other register set) slotted between
+      // them: one ds_read_b128 after every 4 MFMAs.
       {
         const char* nb = smem + ((st + 1) % NS) * W4_STAGE_BYTES;
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) fa[u ^ 1][i] = lds_read_b128(nb + a_off + i * 1024);
+        for (int i = 0; i < 8; ++i) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) fb[u ^ 1][j] = lds_read_b128(nb + b_off + j * 1024);
+          for (int j = 0; j < 8; ++j) {
+            mfma_16x16x32_agpr(acc[i][j], fb[u][j], fa[u][i]);
+            if ((j & 3) == 3) {
+              const int r = i * 2 + (j >> 2);   // 0..15
+              if (r < 8) fb[u ^ 1][r] = lds_read_b128(nb + b_off + r * 1024);
+              else fa[u ^ 1][r - 8] = lds_read_b128(nb + a_off + (r - 8) * 1024);
+            }
+          }
+        }
+        __builtin_amdgcn_s_setprio(0);
       }
-      // (4) 64 MFMAs on stage st straight from registers
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][j], fa[u][i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
       // Retire the prefetch reads here (they had the whole MFMA block to
       // land).  lgkmcnt only counts to 15, so if they were still pending at
       // the next stage's first MFMA the compiler would have to wait
@@ -362,7 +374,9 @@ mxk_gemm_bf16_tn_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__
       __builtin_amdgcn_s_waitcnt(0xC07F);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // MFMA results -> VALU/accvgpr reads: 16x16x32 is an 8-pass op, pad >= 10
+  // wait states before the epilogue reads the accumulators.
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
   const int crow = lane & 15;
   const int ccol = (lane >> 4) * 4;

@@ -129,3 +129,28 @@ def test_rope_fwd_bwd(cuda_device, B, S, H, D):
     xr = x.detach().float().requires_grad_()
     rope_ref(xr, cos, sin).backward(dy.float())
     assert (x.grad.float() - xr.grad).abs().max() <= 3e-2
+
+
+@pytest.mark.parametrize("rows,H", [(7, 4096), (2048, 4096), (3, 256)])
+def test_add_rmsnorm_fwd_bwd(cuda_device, rows, H):
+    from mxk8s.ops.fused import add_rmsnorm
+    x = _rand((rows, H), cuda_device, 21, 2.0).bfloat16().requires_grad_()
+    d = _rand((rows, H), cuda_device, 22, 2.0).bfloat16().requires_grad_()
+    w = (1 + 0.1 * _rand((H,), cuda_device, 23)).bfloat16().requires_grad_()
+    h, y = add_rmsnorm(x, d, w, 1e-5)
+    href = (x.detach() + d.detach())
+    assert torch.equal(h, href)
+    assert (y.float() - rmsnorm_ref(href, w.detach(), 1e-5).float()).abs().max() < 3e-2
+    dh = _rand((rows, H), cuda_device, 24).bfloat16()
+    dy = _rand((rows, H), cuda_device, 25).bfloat16()
+    torch.autograd.backward([h, y], [dh, dy])
+    xr = x.detach().float().requires_grad_()
+    dr = d.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    hr = xr + dr
+    yr = hr * torch.rsqrt(hr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    torch.autograd.backward([hr, yr], [dh.float(), dy.float()])
+    tol = 2e-2 * xr.grad.abs().max() + 1e-2
+    assert (x.grad.float() - xr.grad).abs().max() <= tol
+    assert (d.grad.float() - dr.grad).abs().max() <= tol
+    assert (w.grad.float() - wr.grad).abs().max() <= 2e-2 * wr.grad.abs().max() + 1e-2
