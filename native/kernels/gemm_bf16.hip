@@ -258,6 +258,15 @@ __device__ __forceinline__ void mfma_16x16x32_agpr(f32x4_t& acc, bf16x8_t a, bf1
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
+// One quarter (64 rows x 32 k) of an operand stage = 1 glds per thread.
+__device__ __forceinline__ void w4_stage_quarter(const uint16_t* __restrict__ src, int ld, int row0,
+                                                 int k0, char* lds_op, int q, int tid) {
+  const int row = q * 64 + (tid >> 2);
+  const int c = (tid & 3) ^ w4_h((row >> 2) & 3);
+  const uint16_t* g = src + static_cast<size_t>(row0 + row) * ld + k0 + c * 8;
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)(lds_op + q * 4096 + (tid >> 6) * 1024), 16, 0, 0);
+}
+
 // One operand stage (256 rows x 32 k) = 4 glds per thread (1 KiB per wave
 // instruction = 16 rows of 64 B).
 __device__ __forceinline__ void w4_stage_operand(const uint16_t* __restrict__ src, int ld, int row0,
@@ -339,19 +348,16 @@ mxk_gemm_bf16_tn_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__
       if constexpr (NS == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      // (2) DMA for stage st+NS-1 into the buffer stage st-1 used.
+      // (2)-(4) 64 MFMAs on stage st straight from registers.  Slotted between
+      // them (so the matrix pipe never waits on issue): the 16 fragment reads
+      // of stage st+1 into the other register set (one ds_read_b128 per 4
+      // MFMAs) and the 8 LDS-DMA pieces of stage st+NS-1 into the buffer stage
+      // st-1 used (one glds per 8 MFMAs).
       {
+        const char* nb = smem + ((st + 1) % NS) * W4_STAGE_BYTES;
         const int sn = st + NS - 1;
         const int kk = (sn < ns ? sn : ns - 1) * W4_BK;
         char* buf = smem + (sn % NS) * W4_STAGE_BYTES;
-        w4_stage_operand(A, lda, m0, kk, buf, tid);
-        w4_stage_operand(Bt, ldb, n0, kk, buf + W4_OP_BYTES, tid);
-      }
-      // (3)+(4) 64 MFMAs on stage st straight from registers, with the 16
-      // fragment reads of stage st+1 (other register set) slotted between
-      // them: one ds_read_b128 after every 4 MFMAs.
-      {
-        const char* nb = smem + ((st + 1) % NS) * W4_STAGE_BYTES;
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -362,6 +368,10 @@ mxk_gemm_bf16_tn_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__
               const int r = i * 2 + (j >> 2);   // 0..15
               if (r < 8) fb[u ^ 1][r] = lds_read_b128(nb + b_off + r * 1024);
               else fa[u ^ 1][r - 8] = lds_read_b128(nb + a_off + (r - 8) * 1024);
+            }
+            if (j == 7) {
+              if (i < 4) w4_stage_quarter(A, lda, m0, kk, buf, i, tid);
+              else w4_stage_quarter(Bt, ldb, n0, kk, buf + W4_OP_BYTES, i - 4, tid);
             }
           }
         }
