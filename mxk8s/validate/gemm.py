@@ -40,7 +40,8 @@ def _events_time(fn, iters: int) -> list[float]:
     return times
 
 
-def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None) -> list[dict]:
+def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
+        ablation_from: int = 1 << 30) -> list[dict]:
     dev = device or torch.device("cuda", torch.cuda.current_device())
     L = _lib.lib()
     stream = lambda: _lib.stream_ptr(dev)  # noqa: E731
@@ -65,8 +66,9 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None) 
         kernels["hipblaslt"] = lambda: torch.matmul(A, Bt.t(), out=C)
         # correctness of every hand-written schedule
         checks = {}
+        ablations = set(f"mxk_v{v}" for v in variants if v >= ablation_from)
         for name, fn in kernels.items():
-            if name == "hipblaslt":
+            if name == "hipblaslt" or name in ablations:
                 continue
             C.zero_()
             fn()
@@ -119,7 +121,8 @@ def main(argv=None) -> int:
         variants = [int(x) for x in a.variants.split(",")]
     else:
         variants = []
-    run([int(x) for x in a.sizes.split(",")], variants, a.iters, a.warmup_s, a.rounds)
+    run([int(x) for x in a.sizes.split(",")], variants, a.iters, a.warmup_s, a.rounds,
+        ablation_from=_lib.lib().mxk_gemm_bf16_tn_first_ablation())
     return 0
 
 

@@ -258,6 +258,38 @@ __device__ __forceinline__ void mfma_16x16x32_agpr(f32x4_t& acc, bf16x8_t a, bf1
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
+// LDS-DMA stream of one operand as `buffer_load_dwordx4 ... offen lds`: the
+// operand panel (row0 .. row0+255) is a buffer resource in SGPRs, each lane's
+// row/chunk offset is ONE VGPR computed once, and the piece / k offset is a
+// scalar soffset — so a piece costs one VMEM instruction plus one `s_add m0`
+// (no per-piece 64-bit VALU address math, no v_readfirstlane for M0; the
+// hipBLASLt MT256x256x64 kernel issues its pieces the same way).
+struct DmaStream {
+  __amdgpu_buffer_rsrc_t rsrc;   // uniform: panel base, 256 rows * ld * 2 bytes
+  uint32_t lane_off;             // per lane: (row-in-piece * ld + swizzled chunk * 8) * 2
+  uint32_t piece_stride;         // uniform: rows-per-piece * ld * 2
+  __device__ __forceinline__ void issue(char* lds_op, int piece, int piece_bytes, int k_bytes,
+                                        int wave_s) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rsrc, (lds_void*)(lds_op + piece * piece_bytes + wave_s * 1024), 16, lane_off,
+        k_bytes + piece * piece_stride, 0, 0);
+  }
+};
+
+// rows_per_piece = threads / 4 (64 B rows, 4 lanes per row)
+__device__ __forceinline__ DmaStream make_dma(const uint16_t* src, int ld, int row0, int tid,
+                                              int rows_per_piece) {
+  DmaStream d;
+  const uint16_t* base = src + static_cast<size_t>(row0) * ld;
+  d.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, 256 * ld * 2,
+                                             0x00020000);
+  const int row = tid >> 2;                        // row within a piece
+  const int c = (tid & 3) ^ w4_h((row >> 2) & 3);  // (row>>2)&3 is piece-invariant
+  d.lane_off = static_cast<uint32_t>((row * ld + c * 8) * 2);
+  d.piece_stride = static_cast<uint32_t>(rows_per_piece * ld * 2);
+  return d;
+}
+
 // One quarter (64 rows x 32 k) of an operand stage = 1 glds per thread.
 __device__ __forceinline__ void w4_stage_quarter(const uint16_t* __restrict__ src, int ld, int row0,
                                                  int k0, char* lds_op, int q, int tid) {
@@ -283,7 +315,9 @@ __device__ __forceinline__ void w4_stage_operand(const uint16_t* __restrict__ sr
 }
 }  // namespace
 
-template <int NS>
+// ABL (ablation, timing-only builds; outputs are wrong): 1 = skip the
+// steady-state LDS-DMA, 2 = skip the fragment prefetch reads.
+template <int NS, int ABL = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -308,6 +342,9 @@ mxk_gemm_bf16_tn_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__
   const int foff = frow * 64 + (((lane >> 4) ^ w4_h((frow >> 2) & 3)) * 16);
   const int a_off = wm * 128 * 64 + foff;               // + i*1024 for subtile i
   const int b_off = W4_OP_BYTES + wn * 128 * 64 + foff;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const DmaStream dma_a = make_dma(A, lda, m0, tid, 64);
+  const DmaStream dma_b = make_dma(Bt, ldb, n0, tid, 64);
 
   f32x4_t acc[8][8];
 #pragma unroll
@@ -320,8 +357,11 @@ mxk_gemm_bf16_tn_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s) {
     const int kk = (s < ns ? s : ns - 1) * W4_BK;
-    w4_stage_operand(A, lda, m0, kk, smem + s * W4_STAGE_BYTES, tid);
-    w4_stage_operand(Bt, ldb, n0, kk, smem + s * W4_STAGE_BYTES + W4_OP_BYTES, tid);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      dma_a.issue(smem + s * W4_STAGE_BYTES, q, 4096, kk * 2, wave_s);
+      dma_b.issue(smem + s * W4_STAGE_BYTES + W4_OP_BYTES, q, 4096, kk * 2, wave_s);
+    }
   }
   // stage 0 landed (8 glds per later stage may stay in flight)
   if constexpr (NS == 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -364,14 +404,14 @@ mxk_gemm_bf16_tn_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             mfma_16x16x32_agpr(acc[i][j], fb[u][j], fa[u][i]);
-            if ((j & 3) == 3) {
+            if ((j & 3) == 3 && ABL != 2) {
               const int r = i * 2 + (j >> 2);   // 0..15
               if (r < 8) fb[u ^ 1][r] = lds_read_b128(nb + b_off + r * 1024);
               else fa[u ^ 1][r - 8] = lds_read_b128(nb + a_off + (r - 8) * 1024);
             }
-            if (j == 7) {
-              if (i < 4) w4_stage_quarter(A, lda, m0, kk, buf, i, tid);
-              else w4_stage_quarter(Bt, ldb, n0, kk, buf + W4_OP_BYTES, i - 4, tid);
+            if (j == 7 && ABL != 1) {
+              if (i < 4) dma_a.issue(buf, i, 4096, kk * 2, wave_s);
+              else dma_b.issue(buf + W4_OP_BYTES, i - 4, 4096, kk * 2, wave_s);
             }
           }
         }
@@ -386,6 +426,312 @@ mxk_gemm_bf16_tn_w4(const uint16_t* __restrict__ A, const uint16_t* __restrict__
   }
   // MFMA results -> VALU/accvgpr reads: 16x16x32 is an 8-pass op, pad >= 10
   // wait states before the epilogue reads the accumulators.
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + crow;
+    uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 128 + ccol;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4_t v = acc[i][j];
+      uint2 pk;
+      pk.x = mxk::pack2bf(v[0], v[1]);
+      pk.y = mxk::pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Schedule 4: 8 waves (two per SIMD), each owning a 128x64 output block
+// (8x4 tiles of 16x16 -> 128 fp32 accumulators pinned to AGPRs), on the same
+// BK = 32, 4-deep LDS ring as schedule 3.  Two waves per SIMD let one wave's
+// LDS-DMA issue (~60 cycles per piece among MFMAs, MI355X_MICROARCH.md
+// cycle constants) hide under its partner's MFMAs, which a single wave per
+// SIMD cannot do.  Per 32-deep stage a wave issues 32 MFMAs, 12 fragment
+// reads for the next stage and 4 LDS-DMA pieces (2 per operand).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int W8_THREADS = 512;
+
+// One half (128 rows x 32 k) of an operand stage = 1 glds per thread.
+__device__ __forceinline__ void w8_stage_half(const uint16_t* __restrict__ src, int ld, int row0,
+                                              int k0, char* lds_op, int q, int tid) {
+  const int row = q * 128 + (tid >> 2);
+  const int c = (tid & 3) ^ w4_h((row >> 2) & 3);
+  const uint16_t* g = src + static_cast<size_t>(row0 + row) * ld + k0 + c * 8;
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)(lds_op + q * 8192 + (tid >> 6) * 1024), 16, 0, 0);
+}
+}  // namespace
+
+template <int NS>
+__global__ void __launch_bounds__(W8_THREADS, 2)
+mxk_gemm_bf16_tn_w8(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                    uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[NS * W4_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2;   // 0..1 -> 128 rows
+  const int wn = wave & 3;    // 0..3 -> 64 cols
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int wgid = mxk::xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  const int frow = lane & 15;
+  const int foff = frow * 64 + (((lane >> 4) ^ w4_h((frow >> 2) & 3)) * 16);
+  const int a_off = wm * 128 * 64 + foff;               // + i*1024 for subtile i
+  const int b_off = W4_OP_BYTES + wn * 64 * 64 + foff;  // + j*1024
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const DmaStream dma_a = make_dma(A, lda, m0, tid, 128);
+  const DmaStream dma_b = make_dma(Bt, ldb, n0, tid, 128);
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / W4_BK;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) {
+    const int kk = (s < ns ? s : ns - 1) * W4_BK;
+    char* buf = smem + s * W4_STAGE_BYTES;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      dma_a.issue(buf, q, 8192, kk * 2, wave_s);
+      dma_b.issue(buf + W4_OP_BYTES, q, 8192, kk * 2, wave_s);
+    }
+  }
+  // stage 0 landed: 4 glds per later stage may stay in flight
+  if constexpr (NS == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t fa[2][8], fb[2][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa[0][i] = lds_read_b128(smem + a_off + i * 1024);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[0][j] = lds_read_b128(smem + b_off + j * 1024);
+
+  for (int s = 0; s < ns; s += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int st = s + u;
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // this wave's prefetch reads done
+      if constexpr (NS == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      {
+        const char* nb = smem + ((st + 1) % NS) * W4_STAGE_BYTES;
+        const int sn = st + NS - 1;
+        const int kk = (sn < ns ? sn : ns - 1) * W4_BK;
+        char* buf = smem + (sn % NS) * W4_STAGE_BYTES;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            mfma_16x16x32_agpr(acc[i][j], fb[u][j], fa[u][i]);
+            const int t = i * 4 + j;          // MFMA index 0..31
+            if ((t & 1) == 1 && t < 24) {      // 12 reads, one per 2 MFMAs
+              const int r = t >> 1;
+              if (r < 4) fb[u ^ 1][r] = lds_read_b128(nb + b_off + r * 1024);
+              else fa[u ^ 1][r - 4] = lds_read_b128(nb + a_off + (r - 4) * 1024);
+            }
+            if ((t & 7) == 4) {               // 4 DMA pieces, one per 8 MFMAs
+              const int q = t >> 3;
+              if (q < 2) dma_a.issue(buf, q, 8192, kk * 2, wave_s);
+              else dma_b.issue(buf + W4_OP_BYTES, q - 2, 8192, kk * 2, wave_s);
+            }
+          }
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + crow;
+    uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 64 + ccol;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4_t v = acc[i][j];
+      uint2 pk;
+      pk.x = mxk::pack2bf(v[0], v[1]);
+      pk.y = mxk::pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Schedule 5: 4 waves (one per SIMD), 128x128 AGPR accumulators per wave,
+// BK = 64 stages of full 128-byte rows in a 2-stage LDS ring (128 KiB).
+//
+// Staging 64-k rows means every LDS-DMA piece (1 KiB per wave instruction =
+// 8 rows x 128 B) fetches whole 128-B cache lines: the 32-k stages of
+// schedule 3 split every line over two pieces issued a stage apart.
+// Timeline per stage s (two 32-deep k-steps, 64 MFMAs each):
+//   k-step s.0 : MFMAs from register set 0 (frags of s.0); prefetch set 1 <-
+//                frags of s.1 (same buffer).
+//   wait own DMA of stage s+1, ONE barrier: stage s+1 visible to all waves,
+//                and every wave is done reading buffer s.
+//   k-step s.1 : MFMAs from set 1; prefetch set 0 <- frags of (s+1).0 and
+//                issue the 16 DMA pieces of stage s+2 into buffer s.
+// So a stage's DMA has two k-steps (128 MFMAs) to land and there is one
+// barrier per 128 MFMAs.  LDS swizzle: 16-B chunk c of row r at c ^ ((r>>1)&7)
+// (tests/test_gemm_swizzle.py, BK=64 layout).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int W4B_OP_BYTES = 256 * 128;            // 32 KiB per operand per stage
+constexpr int W4B_STAGE_BYTES = 2 * W4B_OP_BYTES;  // 64 KiB
+
+struct DmaStream64 {
+  __amdgpu_buffer_rsrc_t rsrc;   // uniform: 256-row panel
+  uint32_t lane_off;             // per lane: row-in-piece * ld * 2 + swizzled chunk * 16
+  uint32_t piece_stride;         // uniform: 8 rows * ld * 2
+  // global piece g = p*4 + wave (rows 8g .. 8g+7) -> LDS bytes [g*1024, +1024)
+  __device__ __forceinline__ void issue(char* lds_op, int p, int k_bytes, int wave_s) const {
+    const int g = p * 4 + wave_s;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_op + g * 1024), 16, lane_off,
+                                             k_bytes + g * piece_stride, 0, 0);
+  }
+};
+
+__device__ __forceinline__ DmaStream64 make_dma64(const uint16_t* src, int ld, int row0, int lane,
+                                                  int wave) {
+  DmaStream64 d;
+  const uint16_t* base = src + static_cast<size_t>(row0) * ld;
+  d.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, 256 * ld * 2,
+                                             0x00020000);
+  const int r = lane >> 3;                                   // row within the piece
+  // row = 8g + r with g = 4p + wave: (row >> 1) & 7 = (4 (wave & 1) + (r >> 1)) & 7
+  const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & 7);
+  d.lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
+  d.piece_stride = static_cast<uint32_t>(8 * ld * 2);
+  return d;
+}
+}  // namespace
+
+template <int ABL = 0>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave >> 1;
+  const int wn = wave & 1;
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int wgid = mxk::xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  const DmaStream64 dma_a = make_dma64(A, lda, m0, lane, wave_s);
+  const DmaStream64 dma_b = make_dma64(Bt, ldb, n0, lane, wave_s);
+
+  // fragment offsets: lane reads row (l & 15) of a 16-row subtile, logical
+  // chunk ks*4 + (l >> 4) stored at chunk ^ ((l & 15) >> 1)
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  const int a_base = wm * 128 * 128;
+  const int b_base = W4B_OP_BYTES + wn * 128 * 128;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / BK;   // 64-deep stages
+  // prologue: stages 0 and 1
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int kb = (s < ns ? s : ns - 1) * BK * 2;
+    char* buf = smem + s * W4B_STAGE_BYTES;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      dma_a.issue(buf, p, kb, wave_s);
+      dma_b.issue(buf + W4B_OP_BYTES, p, kb, wave_s);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // stage 0 (own pieces) landed
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * 2048 + off_k0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * 2048 + off_k0);
+
+  for (int s = 0; s < ns; ++s) {
+    const char* cur = smem + (s & 1) * W4B_STAGE_BYTES;
+    char* nxt = smem + ((s + 1) & 1) * W4B_STAGE_BYTES;
+    // ---- k-step s.0: MFMAs on set 0, prefetch set 1 (s.1) from `cur`
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
+        if ((j & 3) == 3 && ABL != 2) {
+          const int r = i * 2 + (j >> 2);
+          if (r < 8) f1b[r] = lds_read_b128(cur + b_base + r * 2048 + off_k1);
+          else f1a[r - 8] = lds_read_b128(cur + a_base + (r - 8) * 2048 + off_k1);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (ABL != 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of stage s+1 landed
+    __builtin_amdgcn_s_barrier();
+    // ---- k-step s.1: MFMAs on set 1, prefetch set 0 ((s+1).0) from `nxt`,
+    //      DMA of stage s+2 into `cur` (fully consumed: certified by the barrier)
+    const int kb = (s + 2 < ns ? s + 2 : ns - 1) * BK * 2;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
+        if ((j & 3) == 1 && ABL != 2) {
+          const int r = i * 2 + (j >> 2);
+          if (r < 8) f0b[r] = lds_read_b128(nxt + b_base + r * 2048 + off_k0);
+          else f0a[r - 8] = lds_read_b128(nxt + a_base + (r - 8) * 2048 + off_k0);
+        }
+        if ((j & 3) == 3 && ABL != 1) {
+          const int p = i * 2 + (j >> 2);   // 0..15
+          if (p < 8) dma_a.issue(const_cast<char*>(cur), p, kb, wave_s);
+          else dma_b.issue(const_cast<char*>(cur) + W4B_OP_BYTES, p - 8, kb, wave_s);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
   const int crow = lane & 15;
@@ -476,7 +822,8 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int kDefaultVariant = 1;
-constexpr int kNumVariants = 5;
+constexpr int kNumVariants = 9;
+constexpr int kFirstAblation = 6;   // variants >= this produce wrong outputs (timing only)
 
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
                 int N, int K, int lda, int ldb, int ldc) {
@@ -487,8 +834,12 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 0: hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256<0>, dim3(nwg), dim3(NTHREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 1: hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256<1>, dim3(nwg), dim3(NTHREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 2: hipLaunchKernelGGL(mxk_gemm_bf16_tn_256x256<2>, dim3(nwg), dim3(NTHREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 3: hipLaunchKernelGGL(mxk_gemm_bf16_tn_w4<4>, dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    default: hipLaunchKernelGGL(mxk_gemm_bf16_tn_w4<3>, dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 3: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4<4, 0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 4: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8<4>), dim3(nwg), dim3(W8_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 5: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 6: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 7: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<2>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    default: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<3>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
   }
 }
 }  // namespace
@@ -503,6 +854,7 @@ MXK_API int mxk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int
 }
 
 MXK_API int mxk_gemm_bf16_tn_num_variants(void) { return kNumVariants; }
+MXK_API int mxk_gemm_bf16_tn_first_ablation(void) { return kFirstAblation; }
 
 MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,
                              int lda, int ldb, int ldc, hipStream_t stream) {

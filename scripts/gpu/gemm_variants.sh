@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-timeout -k 10 400 python3 -m mxk8s.validate.gemm --sizes ${SIZES:-4096,8192} --variants all \
+timeout -k 10 400 python3 -m mxk8s.validate.gemm --sizes ${SIZES:-8192,4096} --variants all \
     --iters 60 --rounds 6 > gpurun_out/gemm_variants.log 2>&1
 rc=$?; echo "gemm rc=$rc"; grep RESULT gpurun_out/gemm_variants.log | python3 -c "
 import sys, json
