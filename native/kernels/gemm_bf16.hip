@@ -578,55 +578,79 @@ mxk_gemm_bf16_tn_w8(const uint16_t* __restrict__ A, const uint16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// Schedule 5: 4 waves (one per SIMD), 128x128 AGPR accumulators per wave,
-// BK = 64 stages of full 128-byte rows in a 2-stage LDS ring (128 KiB).
+// Schedules 5/6: 4 waves (one per SIMD), 128x128 AGPR accumulators per wave,
+// BK = 64 stages in a 2-stage LDS ring (128 KiB), two 32-deep k-steps of 64
+// MFMAs per stage.  Register set 0 holds the fragments of k-step s.0, set 1
+// those of s.1; each k-step prefetches the other set while its MFMAs run.
 //
-// Staging 64-k rows means every LDS-DMA piece (1 KiB per wave instruction =
-// 8 rows x 128 B) fetches whole 128-B cache lines: the 32-k stages of
-// schedule 3 split every line over two pieces issued a stage apart.
-// Timeline per stage s (two 32-deep k-steps, 64 MFMAs each):
-//   k-step s.0 : MFMAs from register set 0 (frags of s.0); prefetch set 1 <-
-//                frags of s.1 (same buffer).
-//   wait own DMA of stage s+1, ONE barrier: stage s+1 visible to all waves,
-//                and every wave is done reading buffer s.
-//   k-step s.1 : MFMAs from set 1; prefetch set 0 <- frags of (s+1).0 and
-//                issue the 16 DMA pieces of stage s+2 into buffer s.
-// So a stage's DMA has two k-steps (128 MFMAs) to land and there is one
-// barrier per 128 MFMAs.  LDS swizzle: 16-B chunk c of row r at c ^ ((r>>1)&7)
-// (tests/test_gemm_swizzle.py, BK=64 layout).
+// HALF = false (schedule 5): DMA pieces are 8 rows x 128 B (whole cache
+//   lines).  k-step s.1 issues all 16 pieces of stage s+2 into buffer s;
+//   ONE barrier per stage (between s.0 and s.1).  Swizzle: chunk c of row r
+//   at c ^ ((r>>1)&7).
+// HALF = true (schedule 6): pieces are 16 rows x 64 B of one k-half, so each
+//   k-step issues 8 pieces (one per 8 MFMAs instead of one per 4 in every
+//   other k-step): s.0 issues the k-half 1 of stage s+1, s.1 the k-half 0 of
+//   stage s+2.  A 16-row subtile is two 1-KiB blocks (k-half 0, k-half 1) of
+//   64-B rows with chunk c of row r at c ^ h((r>>2)&3), h = {0,2,3,1}; two
+//   barriers per stage.
+// (A 64-B pad per 1-KiB piece, hipBLASLt-style, measured within noise of the
+// dense layout: the DMA landing banks are not the limiter.)
+// Layouts are conflict-free for the 16x16x32 fragment reads and the DMA
+// source swizzle inverts the read one (tests/test_gemm_swizzle.py).
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int W4B_OP_BYTES = 256 * 128;            // 32 KiB per operand per stage
 constexpr int W4B_STAGE_BYTES = 2 * W4B_OP_BYTES;  // 64 KiB
 
+__device__ __forceinline__ int w4b_h(int q) { return (((q ^ (q >> 1)) & 1) << 1) | (q >> 1); }
+
+template <bool HALF>
 struct DmaStream64 {
   __amdgpu_buffer_rsrc_t rsrc;   // uniform: 256-row panel
   uint32_t lane_off;             // per lane: row-in-piece * ld * 2 + swizzled chunk * 16
-  uint32_t piece_stride;         // uniform: 8 rows * ld * 2
-  // global piece g = p*4 + wave (rows 8g .. 8g+7) -> LDS bytes [g*1024, +1024)
-  __device__ __forceinline__ void issue(char* lds_op, int p, int k_bytes, int wave_s) const {
+  uint32_t piece_stride;         // uniform: rows per piece * ld * 2
+  // whole-line pieces: g = p*4 + wave (rows 8g .. 8g+7) -> LDS [g*1024, +1024)
+  // half pieces:       q = p*4 + wave (rows 16q .. 16q+15), k-half kh ->
+  //                    LDS [q*2048 + kh*1024, +1024)
+  __device__ __forceinline__ void issue(char* lds_op, int p, int k_bytes, int wave_s,
+                                        int kh = 0) const {
     const int g = p * 4 + wave_s;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_op + g * 1024), 16, lane_off,
-                                             k_bytes + g * piece_stride, 0, 0);
+    const int dst = HALF ? g * 2048 + kh * 1024 : g * 1024;
+    const int soff = HALF ? k_bytes + kh * 64 + g * piece_stride : k_bytes + g * piece_stride;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_op + dst), 16, lane_off, soff,
+                                             0, 0);
   }
 };
 
-__device__ __forceinline__ DmaStream64 make_dma64(const uint16_t* src, int ld, int row0, int lane,
-                                                  int wave) {
-  DmaStream64 d;
+template <bool HALF>
+__device__ __forceinline__ DmaStream64<HALF> make_dma64(const uint16_t* src, int ld, int row0,
+                                                        int lane, int wave) {
+  DmaStream64<HALF> d;
   const uint16_t* base = src + static_cast<size_t>(row0) * ld;
   d.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, 256 * ld * 2,
                                              0x00020000);
-  const int r = lane >> 3;                                   // row within the piece
-  // row = 8g + r with g = 4p + wave: (row >> 1) & 7 = (4 (wave & 1) + (r >> 1)) & 7
-  const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & 7);
-  d.lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
-  d.piece_stride = static_cast<uint32_t>(8 * ld * 2);
+  if (HALF) {
+    const int r = lane >> 2;                      // row within the 16-row piece
+    const int c = (lane & 3) ^ w4b_h((r >> 2) & 3);
+    d.lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
+    d.piece_stride = static_cast<uint32_t>(16 * ld * 2);
+  } else {
+    const int r = lane >> 3;                      // row within the 8-row piece
+    // row = 8g + r with g = 4p + wave: (row >> 1) & 7 = (4 (wave & 1) + (r >> 1)) & 7
+    const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & 7);
+    d.lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
+    d.piece_stride = static_cast<uint32_t>(8 * ld * 2);
+  }
   return d;
 }
 }  // namespace
 
-template <int ABL = 0>
+// ABL (timing ablations, wrong results): 1 = no DMA, 2 = no fragment reads,
+// 3 = no vmcnt before the barrier.  ORD (whole-line mode) places k-step s.1's
+// 16 DMA pieces and 16 prefetch reads: 0 = interleaved (one of each per 4
+// MFMAs), 1 = DMA over the first 32 MFMAs then reads over the last 32,
+// 2 = reads first, then DMA.
+template <int ABL = 0, bool HALF = false, int ORD = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -648,17 +672,24 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   const int m0 = (first_m + in_group % gsize) * BM;
   const int n0 = (in_group / gsize) * BN;
 
-  const DmaStream64 dma_a = make_dma64(A, lda, m0, lane, wave_s);
-  const DmaStream64 dma_b = make_dma64(Bt, ldb, n0, lane, wave_s);
+  const DmaStream64<HALF> dma_a = make_dma64<HALF>(A, lda, m0, lane, wave_s);
+  const DmaStream64<HALF> dma_b = make_dma64<HALF>(Bt, ldb, n0, lane, wave_s);
 
-  // fragment offsets: lane reads row (l & 15) of a 16-row subtile, logical
-  // chunk ks*4 + (l >> 4) stored at chunk ^ ((l & 15) >> 1)
+  // fragment offsets: lane reads row x = (l & 15) of a 16-row subtile,
+  // logical chunk ks*4 + (l >> 4)
   const int frow = lane & 15;
-  const int fch = (lane >> 4) ^ (frow >> 1);
-  const int off_k0 = frow * 128 + fch * 16;
-  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
-  const int a_base = wm * 128 * 128;
-  const int b_base = W4B_OP_BYTES + wn * 128 * 128;
+  int off_k0, off_k1;
+  if (HALF) {
+    off_k0 = frow * 64 + (((lane >> 4) ^ w4b_h(frow >> 2)) * 16);
+    off_k1 = off_k0 + 1024;
+  } else {
+    const int fch = (lane >> 4) ^ (frow >> 1);
+    off_k0 = frow * 128 + fch * 16;
+    off_k1 = frow * 128 + (fch ^ 4) * 16;
+  }
+  constexpr int SUB = 2048;                      // bytes per 16-row subtile
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
 
   f32x4_t acc[8][8];
 #pragma unroll
@@ -667,30 +698,37 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int ns = K / BK;   // 64-deep stages
-  // prologue: stages 0 and 1
+  auto kbytes = [&](int st) { return (st < ns ? st : ns - 1) * BK * 2; };
+  // prologue: stage 0 whole, stage 1 whole (HALF: only its k-half 0)
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const int kb = (s < ns ? s : ns - 1) * BK * 2;
     char* buf = smem + s * W4B_STAGE_BYTES;
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      dma_a.issue(buf, p, kb, wave_s);
-      dma_b.issue(buf + W4B_OP_BYTES, p, kb, wave_s);
+    for (int p = 0; p < (HALF ? 4 : 8); ++p) {
+#pragma unroll
+      for (int kh = 0; kh < (HALF ? 2 : 1); ++kh) {
+        if (HALF && s == 1 && kh == 1) continue;
+        dma_a.issue(buf, p, kbytes(s), wave_s, kh);
+        dma_b.issue(buf + W4B_OP_BYTES, p, kbytes(s), wave_s, kh);
+      }
     }
   }
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // stage 0 (own pieces) landed
+  if constexpr (HALF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // stage 0 (own pieces) landed
   __builtin_amdgcn_s_barrier();
 
   bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * 2048 + off_k0);
+  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * 2048 + off_k0);
+  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
 
   for (int s = 0; s < ns; ++s) {
-    const char* cur = smem + (s & 1) * W4B_STAGE_BYTES;
+    char* cur = smem + (s & 1) * W4B_STAGE_BYTES;
     char* nxt = smem + ((s + 1) & 1) * W4B_STAGE_BYTES;
     // ---- k-step s.0: MFMAs on set 0, prefetch set 1 (s.1) from `cur`
+    //      (HALF: DMA k-half 1 of stage s+1 into `nxt`; buffer s-1's k-half 1
+    //      was consumed in (s-1).0)
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -700,37 +738,79 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
         mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
         if ((j & 3) == 3 && ABL != 2) {
           const int r = i * 2 + (j >> 2);
-          if (r < 8) f1b[r] = lds_read_b128(cur + b_base + r * 2048 + off_k1);
-          else f1a[r - 8] = lds_read_b128(cur + a_base + (r - 8) * 2048 + off_k1);
+          if (r < 8) f1b[r] = lds_read_b128(cur + b_base + r * SUB + off_k1);
+          else f1a[r - 8] = lds_read_b128(cur + a_base + (r - 8) * SUB + off_k1);
+        }
+        if (HALF && (j & 3) == 1 && ABL != 1) {
+          const int p = i * 2 + (j >> 2);   // 0..15
+          if (p < 4) dma_a.issue(nxt, p, kbytes(s + 1), wave_s, 1);
+          else if (p < 8) dma_b.issue(nxt + W4B_OP_BYTES, p - 4, kbytes(s + 1), wave_s, 1);
         }
       }
     }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    if (ABL != 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of stage s+1 landed
+    // own pieces of stage s+1's first k-half landed (HALF: 8 younger pieces
+    // of k-half 1 stay in flight)
+    if (ABL != 3) {
+      if constexpr (HALF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     // ---- k-step s.1: MFMAs on set 1, prefetch set 0 ((s+1).0) from `nxt`,
-    //      DMA of stage s+2 into `cur` (fully consumed: certified by the barrier)
-    const int kb = (s + 2 < ns ? s + 2 : ns - 1) * BK * 2;
+    //      DMA of stage s+2 (HALF: its k-half 0) into `cur`, fully consumed:
+    //      certified by the barrier
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
+        if (ORD != 0 && !HALF) {
+          // halves of the k-step: slot t = (i & 3) * 4 + (j >> 1) on odd j
+          const bool first = i < 4;
+          if ((j & 1) == 1) {
+            const int t = (i & 3) * 4 + (j >> 1);
+            if (first == (ORD == 2)) {
+              if (ABL != 2) {
+                if (t < 8) f0b[t] = lds_read_b128(nxt + b_base + t * SUB + off_k0);
+                else f0a[t - 8] = lds_read_b128(nxt + a_base + (t - 8) * SUB + off_k0);
+              }
+            } else if (ABL != 1) {
+              if (t < 8) dma_a.issue(cur, t, kbytes(s + 2), wave_s);
+              else dma_b.issue(cur + W4B_OP_BYTES, t - 8, kbytes(s + 2), wave_s);
+            }
+          }
+          continue;
+        }
         if ((j & 3) == 1 && ABL != 2) {
           const int r = i * 2 + (j >> 2);
-          if (r < 8) f0b[r] = lds_read_b128(nxt + b_base + r * 2048 + off_k0);
-          else f0a[r - 8] = lds_read_b128(nxt + a_base + (r - 8) * 2048 + off_k0);
+          if (r < 8) f0b[r] = lds_read_b128(nxt + b_base + r * SUB + off_k0);
+          else f0a[r - 8] = lds_read_b128(nxt + a_base + (r - 8) * SUB + off_k0);
         }
-        if ((j & 3) == 3 && ABL != 1) {
-          const int p = i * 2 + (j >> 2);   // 0..15
-          if (p < 8) dma_a.issue(const_cast<char*>(cur), p, kb, wave_s);
-          else dma_b.issue(const_cast<char*>(cur) + W4B_OP_BYTES, p - 8, kb, wave_s);
+        if (ABL != 1) {
+          if (HALF) {
+            if ((j & 3) == 3) {
+              const int p = i * 2 + (j >> 2);
+              if (p < 4) dma_a.issue(cur, p, kbytes(s + 2), wave_s, 0);
+              else if (p < 8) dma_b.issue(cur + W4B_OP_BYTES, p - 4, kbytes(s + 2), wave_s, 0);
+            }
+          } else if ((j & 3) == 3) {
+            const int p = i * 2 + (j >> 2);   // 0..15
+            if (p < 8) dma_a.issue(cur, p, kbytes(s + 2), wave_s);
+            else dma_b.issue(cur + W4B_OP_BYTES, p - 8, kbytes(s + 2), wave_s);
+          }
         }
       }
     }
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (HALF) {
+      // k-half 1 of stage s+1 (issued in s.0) must be visible before (s+1).0
+      // prefetches it; the 8 pieces just issued stay in flight
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      if (ABL != 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
@@ -821,9 +901,9 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // Host launchers (C ABI, stream-ordered, capture-safe: no sync, no malloc).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kDefaultVariant = 1;
-constexpr int kNumVariants = 9;
-constexpr int kFirstAblation = 6;   // variants >= this produce wrong outputs (timing only)
+constexpr int kDefaultVariant = 5;
+constexpr int kNumVariants = 12;
+constexpr int kFirstAblation = 9;   // variants >= this produce wrong outputs (timing only)
 
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
                 int N, int K, int lda, int ldb, int ldc) {
@@ -837,8 +917,11 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 3: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4<4, 0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 4: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8<4>), dim3(nwg), dim3(W8_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 5: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 6: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 7: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<2>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 6: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, true>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 7: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 8: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 2>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 9: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 10: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<2>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     default: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<3>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
   }
 }

@@ -82,3 +82,33 @@ def test_staging_is_inverse_of_read_swizzle():
     for row in range(256):
         for c in range(4):
             assert image[addr64(row, c)] == (row, c)
+
+
+# ---- 4-wave BK=64 kernel (w4b), HALF mode: a 16-row subtile is two 1-KiB
+# blocks (k-half 0, k-half 1) of 64-B rows; each DMA piece is one block.
+def addr_half(row, chunk):
+    kh, c = chunk >> 2, chunk & 3
+    return (row >> 4) * 2048 + kh * 1024 + (row & 15) * 64 + (c ^ h(((row & 15) >> 2) & 3)) * 16
+
+
+def test_w4b_half_reads_conflict_free():
+    for base in range(0, 256, 16):
+        for ks in range(2):
+            for g in GROUPS:
+                slots = {slot(addr_half(base + (l & 15), ks * 4 + (l >> 4))) for l in g}
+                assert len(slots) == 16, (base, ks, g)
+
+
+def test_w4b_half_dma_source_swizzle_matches_reads():
+    # piece (q, kh): lane l writes LDS q*2048 + kh*1024 + l*16 from row
+    # 16q + (l>>2), logical chunk 4*kh + ((l&3) ^ h((l>>4)&3)).
+    image = {}
+    for q in range(16):
+        for kh in range(2):
+            for l in range(64):
+                r = l >> 2
+                c = (l & 3) ^ h((r >> 2) & 3)
+                image[q * 2048 + kh * 1024 + l * 16] = (16 * q + r, 4 * kh + c)
+    for row in range(256):
+        for c in range(8):
+            assert image[addr_half(row, c)] == (row, c)
