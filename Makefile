@@ -5,6 +5,7 @@
 #   make node       C++ node library    mxk8s/_lib/libmxnode.so (+ CLIs in bin/)
 #   make tools      validator binaries  bin/mx-vector-add bin/mx-gemm-bench bin/mx-allreduce-perf
 #   make test-native  host unit tests of libmxnode (ASan+UBSan build)
+#   make test-native-tsan  libmxnode re-entrancy test under ThreadSanitizer
 #
 # Everything lands inside the repo so `gpurun` snapshots carry it to the box.
 
@@ -30,7 +31,7 @@ NODE_SRCS := $(wildcard native/libmxnode/*.cc)
 NODE_OBJS := $(patsubst native/libmxnode/%.cc,$(BUILD)/node/%.o,$(NODE_SRCS))
 NODE_HDRS := $(wildcard native/libmxnode/*.h)
 
-.PHONY: all kernels node tools clean test-native
+.PHONY: all kernels node tools clean test-native test-native-tsan
 all: kernels node tools
 
 kernels: $(OUT_LIB)/libmxkernels.so
@@ -79,11 +80,11 @@ $(OUT_BIN)/mx-vector-add: $(BUILD)/tools/vector_add_main.o $(BUILD)/kernels/vect
 
 $(OUT_BIN)/mx-gemm-bench: $(BUILD)/tools/gemm_bench_main.o $(BUILD)/kernels/gemm_bf16.o
 	@mkdir -p $(OUT_BIN)
-	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrocblas -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
 
 $(OUT_BIN)/mx-allreduce-perf: $(BUILD)/tools/allreduce_perf.o
 	@mkdir -p $(OUT_BIN)
-	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lpthread -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lrocprofiler-sdk-roctx -lpthread -Wl,-rpath,$(ROCM)/lib
 
 # ---- host tests (sanitized) ----
 test-native: $(BUILD)/asan/test_mxnode
@@ -93,6 +94,14 @@ $(BUILD)/asan/test_mxnode: native/libmxnode/tests/test_mxnode.cc $(NODE_SRCS) $(
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -g -fsanitize=address,undefined -fno-omit-frame-pointer -o $@ \
 	    native/libmxnode/tests/test_mxnode.cc $(NODE_SRCS) $(LDLIBS_NODE)
+
+test-native-tsan: $(BUILD)/tsan/test_mxnode_threads
+	TSAN_OPTIONS=halt_on_error=1 $(BUILD)/tsan/test_mxnode_threads tests/fixtures/sysfs
+
+$(BUILD)/tsan/test_mxnode_threads: native/libmxnode/tests/test_mxnode_threads.cc $(NODE_SRCS) $(NODE_HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -g -fsanitize=thread -o $@ \
+	    native/libmxnode/tests/test_mxnode_threads.cc $(NODE_SRCS) $(LDLIBS_NODE)
 
 clean:
 	rm -rf $(BUILD) $(OUT_LIB)/*.so $(OUT_BIN)

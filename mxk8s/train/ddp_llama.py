@@ -24,6 +24,7 @@ from ..models.llama import Llama, LlamaConfig
 from ..parallel import dist as mxdist
 from ..parallel.ddp import FlatDDP
 from ..parallel.optim import FlatAdamW
+from ..utils import roctx
 
 MI355X_BF16_DENSE_PEAK = 2.5e15   # FLOP/s, dense (MI355X_MICROARCH.md)
 
@@ -38,11 +39,15 @@ def build(cfg: LlamaConfig, device: torch.device, bucket_mb: float, lr: float = 
 
 
 def train_step(model, ddp, opt, tokens) -> torch.Tensor:
-    loss = model.loss(tokens)
-    loss.backward()
-    ddp.finish_grad_sync()
-    opt.step()
-    ddp.zero_grad()
+    # roctx ranges: host-side phases on rocprofv3 --marker-trace timelines
+    with roctx.range("step.forward"):
+        loss = model.loss(tokens)
+    with roctx.range("step.backward+allreduce"):
+        loss.backward()
+        ddp.finish_grad_sync()
+    with roctx.range("step.adamw"):
+        opt.step()
+        ddp.zero_grad()
     return loss.detach()
 
 

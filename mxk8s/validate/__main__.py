@@ -11,6 +11,13 @@ lines; the process exits non-zero if any test fails.
   gemm       CDNA4 bf16 MFMA GEMM TFLOPS vs rocBLAS (bin/mx-gemm-bench) config 3
   rccl       RCCL all-reduce sweep over xGMI (bin/mx-allreduce-perf)  config 4
   ddp        Llama-3-8B DDP synthetic training step (bench.py --mode ddp) config 5
+
+  --profile  adds a rocprofv3 counter pass of the GEMM (separate processes,
+             one counter group each): MFMA busy, LDS bank conflicts, clock,
+             L2 hit rate as RESULT lines (mxk8s.validate.profile)
+  --debug    runs every GPU step with AMD_SERIALIZE_KERNEL=3 and
+             HIP_LAUNCH_BLOCKING=1, so a faulting kernel is reported at its
+             own launch instead of at a later synchronisation
 """
 from __future__ import annotations
 
@@ -24,6 +31,8 @@ import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 BIN = os.environ.get("MXK8S_BIN", os.path.join(REPO, "bin"))
+DEBUG_ENV = {"AMD_SERIALIZE_KERNEL": "3", "HIP_LAUNCH_BLOCKING": "1"}
+_extra_env: dict = {}
 
 
 def emit(d: dict) -> None:
@@ -33,7 +42,7 @@ def emit(d: dict) -> None:
 def _run(cmd, timeout=None, env=None) -> tuple[int, str]:
     print("+ " + " ".join(cmd), file=sys.stderr, flush=True)
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
-                       env={**os.environ, **(env or {})})
+                       env={**os.environ, **_extra_env, **(env or {})})
     sys.stderr.write(p.stderr[-4000:])
     return p.returncode, p.stdout
 
@@ -86,17 +95,34 @@ def test_gemm(sizes: str, gpus: int) -> bool:
     return rc == 0 and bool(rs)
 
 
-def test_rccl(gpus: int, minb: int, maxb: int, scaling: str) -> bool:
+def test_gemm_profile(sizes: str, out_dir: str) -> bool:
+    from . import profile
+    try:
+        summary = profile.profile_gemm(sizes.split(",")[0], out_dir)
+    except (RuntimeError, OSError, subprocess.TimeoutExpired) as e:
+        emit({"test": "gemm_profile", "pass": False, "error": str(e)[-500:]})
+        return False
+    for k, v in summary.items():
+        emit({"test": "gemm_profile", "kernel": k[:120], "pass": True, **v["derived"]})
+    return bool(summary)
+
+
+def test_rccl(gpus: int, minb: int, maxb: int, scaling: str, ops: str = "allreduce") -> bool:
     sc = scaling or str(gpus)
     rc, out = _run([os.path.join(BIN, "mx-allreduce-perf"), "-b", str(minb), "-e", str(maxb),
-                    "-f", "2", "--scaling", sc], timeout=3600)
+                    "-f", "2", "--scaling", sc, "--op", ops], timeout=3600)
     rs = results_from(out)
     for r in rs:
-        if r.get("test") == "allreduce_summary" or r.get("bytes") in (minb, maxb) \
+        if str(r.get("test", "")).endswith("_summary") or r.get("bytes") in (minb, maxb) \
                 or not r.get("pass", True):
             emit(r)
-    curve = {str(r["ngpus"]): r["peak_busbw_GBps"] for r in rs if r.get("test") == "allreduce_summary"}
-    emit({"test": "rccl_summary", "peak_busbw_GBps_by_ngpus": curve, "pass": rc == 0})
+    curves = {}
+    for r in rs:
+        t = str(r.get("test", ""))
+        if t.endswith("_summary"):
+            curves.setdefault(t[:-len("_summary")], {})[str(r["ngpus"])] = r["peak_busbw_GBps"]
+    emit({"test": "rccl_summary", "peak_busbw_GBps_by_ngpus": curves.get("allreduce", {}),
+          "peak_busbw_GBps_by_op": curves, "pass": rc == 0})
     return rc == 0 and bool(rs)
 
 
@@ -127,10 +153,18 @@ def main(argv=None) -> int:
     p.add_argument("--rccl-min-bytes", type=int, default=8)
     p.add_argument("--rccl-max-bytes", type=int, default=1 << 33)
     p.add_argument("--rccl-scaling", default="")
+    p.add_argument("--rccl-ops", default="allreduce",
+                   help="comma list of allreduce,reducescatter,allgather,alltoall or 'all'")
     p.add_argument("--ddp", action="store_true")
     p.add_argument("--ddp-seq-len", type=int, default=2048)
     p.add_argument("--ddp-steps", type=int, default=10)
+    p.add_argument("--profile", action="store_true", help="rocprofv3 counter pass of the GEMM")
+    p.add_argument("--profile-dir", default=os.environ.get("MXK8S_PROFILE_DIR", "/tmp/mxk8s-pmc"))
+    p.add_argument("--debug", action="store_true",
+                   help="serialise kernels (AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING=1)")
     a = p.parse_args(argv)
+    if a.debug:
+        _extra_env.update(DEBUG_ENV)
     tests = [t for t in a.tests.split(",") if t]
     if a.ddp and "ddp" not in tests:
         tests.append("ddp")
@@ -143,8 +177,11 @@ def main(argv=None) -> int:
             status[t] = test_vectoradd()
         elif t == "gemm":
             status[t] = test_gemm(a.gemm_sizes, a.gpus)
+            if a.profile:
+                status["gemm_profile"] = test_gemm_profile(a.gemm_sizes, a.profile_dir)
         elif t == "rccl":
-            status[t] = test_rccl(a.gpus, a.rccl_min_bytes, a.rccl_max_bytes, a.rccl_scaling)
+            status[t] = test_rccl(a.gpus, a.rccl_min_bytes, a.rccl_max_bytes, a.rccl_scaling,
+                                  a.rccl_ops)
         elif t == "ddp":
             status[t] = test_ddp(a.gpus, a.ddp_seq_len, a.ddp_steps)
         else:

@@ -25,6 +25,7 @@ import torch
 
 from ..ops import _lib
 from ..ops.gemm import gemm_bf16_tn
+from ..utils import roctx
 
 
 def _events_time(fn, iters: int) -> list[float]:
@@ -81,14 +82,16 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
                 raise RuntimeError(f"{name} wrong at {n}: rel {rel}, max sub err {sub_err}")
         # warm up >= warmup_s on random data (clock settles under load)
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < warmup_s:
-            for fn in kernels.values():
-                fn()
-            torch.cuda.synchronize()
+        with roctx.range(f"gemm.warmup.{n}"):
+            while time.perf_counter() - t0 < warmup_s:
+                for fn in kernels.values():
+                    fn()
+                torch.cuda.synchronize()
         samples = {k: [] for k in kernels}
         for _ in range(rounds):
             for name, fn in kernels.items():
-                samples[name] += _events_time(fn, max(1, iters // rounds))
+                with roctx.range(f"gemm.timed.{name}.{n}"):
+                    samples[name] += _events_time(fn, max(1, iters // rounds))
         flops = 2.0 * M * N * K
         for name, ts in samples.items():
             med = statistics.median(ts)

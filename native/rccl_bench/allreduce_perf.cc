@@ -1,20 +1,31 @@
-// mx-allreduce-perf: RCCL all-reduce bus-bandwidth sweep over xGMI (BASELINE config 4).
+// mx-allreduce-perf: RCCL collective bus-bandwidth sweeps over xGMI (BASELINE
+// config 4).
 //
 // No rccl-tests binary ships in the image, so this is a from-scratch
-// equivalent of `all_reduce_perf -b 8 -e 8G -f 2 -g N`:
+// equivalent of `all_reduce_perf -b 8 -e 8G -f 2 -g N` (and of the
+// reduce_scatter / all_gather / alltoall variants the DP/TP/SP/EP paths use):
 //   * single process, N GPUs (ncclCommInitAll over the allocated devices),
-//     one ncclGroupStart/End per iteration, out-of-place sum;
+//     one ncclGroupStart/End per iteration, out-of-place;
 //   * or one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK from torchrun;
 //     the ncclUniqueId travels through --id-file);
 //   * --scaling 1,2,4,8 repeats the sweep on the first n GPUs for each n
 //     (the 1/2/4/8 curve of the north star).
-// algbw = bytes / t; busbw = algbw * 2 (n-1) / n (n = 1: busbw = 0 by definition).
-// Each rank sends (rank+1); the result must be n(n+1)/2 everywhere sampled.
+//
+// Sizes follow the nccl-tests convention: S = bytes of the LARGER per-rank
+// buffer (all-reduce: the buffer; reduce-scatter: the input; all-gather: the
+// output; all-to-all: the whole send buffer).  algbw = S / t;
+//   busbw = algbw * 2 (n-1)/n   (all-reduce)
+//   busbw = algbw * (n-1)/n     (reduce-scatter, all-gather, all-to-all)
+// (n = 1: busbw = 0 by definition; the RESULT keeps algbw.)
+// Correctness: rank r contributes (r+1) everywhere; sums must equal
+// n(n+1)/2, gathered / exchanged chunk j must equal j+1.
 //
 //   mx-allreduce-perf [-b 8] [-e 8G] [-f 2] [-g N] [--scaling 1,2,4,8]
+//                     [--op allreduce|reducescatter|allgather|alltoall|all]
 //                     [--dtype float|bf16] [--iters 20] [--warmup 5] [--id-file F]
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
@@ -48,6 +59,22 @@ namespace {
     }                                                                             \
   } while (0)
 
+enum class Op { AllReduce, ReduceScatter, AllGather, AllToAll };
+
+const char* op_name(Op op) {
+  switch (op) {
+    case Op::AllReduce: return "allreduce";
+    case Op::ReduceScatter: return "reducescatter";
+    case Op::AllGather: return "allgather";
+    default: return "alltoall";
+  }
+}
+
+double bus_factor(Op op, int n) {
+  if (n <= 1) return 0.0;
+  return op == Op::AllReduce ? 2.0 * (n - 1) / n : double(n - 1) / n;
+}
+
 size_t parse_size(const char* s) {
   char* end = nullptr;
   double v = std::strtod(s, &end);
@@ -80,9 +107,12 @@ struct Opts {
   int factor = 2;
   int ngpus = -1;
   std::vector<int> scaling;
+  std::vector<Op> ops{Op::AllReduce};
   bool bf16 = false;
   int iters = 20, warmup = 5;
   std::string id_file;
+  size_t esz() const { return bf16 ? 2 : 4; }
+  ncclDataType_t dt() const { return bf16 ? ncclBfloat16 : ncclFloat; }
 };
 
 float read_elem(const void* dptr, size_t idx, bool bf16) {
@@ -106,16 +136,67 @@ int iters_for(size_t bytes, int base) {
   return base;
 }
 
+// Element counts of one sweep point: `chunk` = per-peer block, send/recv =
+// per-rank buffer elements; `count` is what the RCCL call takes.
+struct Shape {
+  size_t count, send, recv;
+};
+
+Shape shape_for(Op op, size_t bytes, size_t esz, int n) {
+  size_t elems = std::max<size_t>(1, bytes / esz);
+  if (op == Op::AllReduce) return {elems, elems, elems};
+  const size_t chunk = std::max<size_t>(1, elems / n);
+  switch (op) {
+    case Op::ReduceScatter: return {chunk, chunk * n, chunk};
+    case Op::AllGather: return {chunk, chunk, chunk * n};
+    default: return {chunk, chunk * n, chunk * n};   // all-to-all: count per pair
+  }
+}
+
+void issue(Op op, const void* sb, void* rb, const Shape& s, ncclDataType_t dt, ncclComm_t comm,
+           hipStream_t st) {
+  switch (op) {
+    case Op::AllReduce: CHECK_NCCL(ncclAllReduce(sb, rb, s.count, dt, ncclSum, comm, st)); break;
+    case Op::ReduceScatter: CHECK_NCCL(ncclReduceScatter(sb, rb, s.count, dt, ncclSum, comm, st)); break;
+    case Op::AllGather: CHECK_NCCL(ncclAllGather(sb, rb, s.count, dt, comm, st)); break;
+    default: CHECK_NCCL(ncclAllToAll(sb, rb, s.count, dt, comm, st)); break;
+  }
+}
+
+// Sampled correctness check of one rank's receive buffer.
+bool check_recv(Op op, const void* rb, const Shape& s, int n, bool bf16) {
+  const float sum = n * (n + 1) / 2.0f;
+  if (op == Op::AllReduce || op == Op::ReduceScatter)
+    return read_elem(rb, 0, bf16) == sum && read_elem(rb, s.recv - 1, bf16) == sum;
+  for (int j = 0; j < n; ++j) {   // chunk j came from rank j, which sent (j+1)
+    if (read_elem(rb, j * s.count, bf16) != float(j + 1)) return false;
+    if (read_elem(rb, j * s.count + s.count - 1, bf16) != float(j + 1)) return false;
+  }
+  return true;
+}
+
+void print_point(Op op, int n, const char* mode, size_t bytes, const Opts& o, double t, bool good) {
+  const double algbw = double(bytes) / t / 1e9;
+  const double busbw = algbw * bus_factor(op, n);
+  std::printf("  %-13s n=%d %14zu %8s %12.2f %12.2f %12.2f %6s\n", op_name(op), n, bytes,
+              o.bf16 ? "bf16" : "float", t * 1e6, algbw, busbw, good ? "ok" : "FAIL");
+  std::printf("RESULT {\"test\":\"%s\",\"ngpus\":%d,\"mode\":\"%s\",\"bytes\":%zu,\"dtype\":\"%s\","
+              "\"op\":\"%s\",\"time_us\":%.3f,\"algbw_GBps\":%.3f,\"busbw_GBps\":%.3f,\"pass\":%s}\n",
+              op_name(op), n, mode, bytes, o.bf16 ? "bf16" : "float",
+              op == Op::AllToAll || op == Op::AllGather ? "copy" : "sum", t * 1e6, algbw, busbw,
+              good ? "true" : "false");
+  std::fflush(stdout);
+}
+
 // -------------------------------------------------------------------------
 // single process, n GPUs
 // -------------------------------------------------------------------------
-bool sweep_single(const Opts& o, int n, double* peak_busbw) {
+bool sweep_single(const Opts& o, Op op, int n, double* peak_busbw) {
   std::vector<int> devs(n);
   for (int i = 0; i < n; ++i) devs[i] = i;
   std::vector<ncclComm_t> comms(n);
   CHECK_NCCL(ncclCommInitAll(comms.data(), n, devs.data()));
-  const size_t esz = o.bf16 ? 2 : 4;
-  const ncclDataType_t dt = o.bf16 ? ncclBfloat16 : ncclFloat;
+  const size_t esz = o.esz();
   std::vector<void*> sb(n), rb(n);
   std::vector<hipStream_t> st(n);
   for (int g = 0; g < n; ++g) {
@@ -127,16 +208,15 @@ bool sweep_single(const Opts& o, int n, double* peak_busbw) {
                        float(g + 1), int(o.bf16));
   }
   for (int g = 0; g < n; ++g) { CHECK_HIP(hipSetDevice(g)); CHECK_HIP(hipStreamSynchronize(st[g])); }
-  const float expect = n * (n + 1) / 2.0f;
   bool ok = true;
-  std::printf("# n=%d  %14s %12s %8s %12s %12s %12s %6s\n", n, "bytes", "count", "type",
+  std::printf("# %s n=%d  %14s %8s %12s %12s %12s %6s\n", op_name(op), n, "bytes", "type",
               "time(us)", "algbw(GB/s)", "busbw(GB/s)", "check");
   for (size_t bytes = o.minb; bytes <= o.maxb; bytes *= o.factor) {
-    const size_t count = std::max<size_t>(1, bytes / esz);
+    const Shape s = shape_for(op, bytes, esz, n);
+    if (std::max(s.send, s.recv) * esz > o.maxb) continue;   // tiny sizes x many ranks
     auto launch = [&]() {
       CHECK_NCCL(ncclGroupStart());
-      for (int g = 0; g < n; ++g)
-        CHECK_NCCL(ncclAllReduce(sb[g], rb[g], count, dt, ncclSum, comms[g], st[g]));
+      for (int g = 0; g < n; ++g) issue(op, sb[g], rb[g], s, o.dt(), comms[g], st[g]);
       CHECK_NCCL(ncclGroupEnd());
     };
     auto sync = [&]() {
@@ -145,26 +225,21 @@ bool sweep_single(const Opts& o, int n, double* peak_busbw) {
     for (int w = 0; w < o.warmup; ++w) launch();
     sync();
     const int it = iters_for(bytes, o.iters);
+    roctxRangePushA(op_name(op));
     auto t0 = std::chrono::steady_clock::now();
     for (int i = 0; i < it; ++i) launch();
     sync();
     const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / it;
-    const double algbw = double(count * esz) / t / 1e9;
-    const double busbw = n > 1 ? algbw * 2.0 * (n - 1) / n : 0.0;
+    roctxRangePop();
     bool good = true;
     for (int g = 0; g < n; ++g) {
       CHECK_HIP(hipSetDevice(g));
-      good &= read_elem(rb[g], 0, o.bf16) == expect && read_elem(rb[g], count - 1, o.bf16) == expect;
+      good &= check_recv(op, rb[g], s, n, o.bf16);
     }
     ok &= good;
-    *peak_busbw = std::max(*peak_busbw, busbw);
-    std::printf("  n=%d  %14zu %12zu %8s %12.2f %12.2f %12.2f %6s\n", n, count * esz, count,
-                o.bf16 ? "bf16" : "float", t * 1e6, algbw, busbw, good ? "ok" : "FAIL");
-    std::printf("RESULT {\"test\":\"allreduce\",\"ngpus\":%d,\"bytes\":%zu,\"dtype\":\"%s\","
-                "\"op\":\"sum\",\"time_us\":%.3f,\"algbw_GBps\":%.3f,\"busbw_GBps\":%.3f,\"pass\":%s}\n",
-                n, count * esz, o.bf16 ? "bf16" : "float", t * 1e6, algbw, busbw,
-                good ? "true" : "false");
-    std::fflush(stdout);
+    const size_t sbytes = std::max(s.send, s.recv) * esz;
+    *peak_busbw = std::max(*peak_busbw, double(sbytes) / t / 1e9 * bus_factor(op, n));
+    print_point(op, n, "single", sbytes, o, t, good);
     if (bytes > o.maxb / o.factor) break;
   }
   for (int g = 0; g < n; ++g) {
@@ -202,8 +277,7 @@ bool sweep_multiproc(const Opts& o, int rank, int world, int local) {
   CHECK_HIP(hipSetDevice(local));
   ncclComm_t comm;
   CHECK_NCCL(ncclCommInitRank(&comm, world, id, rank));
-  const size_t esz = o.bf16 ? 2 : 4;
-  const ncclDataType_t dt = o.bf16 ? ncclBfloat16 : ncclFloat;
+  const size_t esz = o.esz();
   void *sb, *rb;
   hipStream_t st;
   CHECK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -212,35 +286,54 @@ bool sweep_multiproc(const Opts& o, int rank, int world, int local) {
   hipLaunchKernelGGL(fill_value, dim3(2048), dim3(256), 0, st, sb, o.maxb / esz, float(rank + 1),
                      int(o.bf16));
   CHECK_HIP(hipStreamSynchronize(st));
-  const float expect = world * (world + 1) / 2.0f;
   bool ok = true;
-  for (size_t bytes = o.minb; bytes <= o.maxb; bytes *= o.factor) {
-    const size_t count = std::max<size_t>(1, bytes / esz);
-    for (int w = 0; w < o.warmup; ++w) CHECK_NCCL(ncclAllReduce(sb, rb, count, dt, ncclSum, comm, st));
-    CHECK_HIP(hipStreamSynchronize(st));
-    const int it = iters_for(bytes, o.iters);
-    auto t0 = std::chrono::steady_clock::now();
-    for (int i = 0; i < it; ++i) CHECK_NCCL(ncclAllReduce(sb, rb, count, dt, ncclSum, comm, st));
-    CHECK_HIP(hipStreamSynchronize(st));
-    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / it;
-    const bool good = read_elem(rb, 0, o.bf16) == expect && read_elem(rb, count - 1, o.bf16) == expect;
-    ok &= good;
-    if (rank == 0) {
-      const double algbw = double(count * esz) / t / 1e9;
-      const double busbw = world > 1 ? algbw * 2.0 * (world - 1) / world : 0.0;
-      std::printf("RESULT {\"test\":\"allreduce\",\"ngpus\":%d,\"mode\":\"multiproc\",\"bytes\":%zu,"
-                  "\"dtype\":\"%s\",\"op\":\"sum\",\"time_us\":%.3f,\"algbw_GBps\":%.3f,"
-                  "\"busbw_GBps\":%.3f,\"pass\":%s}\n",
-                  world, count * esz, o.bf16 ? "bf16" : "float", t * 1e6, algbw, busbw,
-                  good ? "true" : "false");
-      std::fflush(stdout);
+  for (Op op : o.ops) {
+    double peak = 0;
+    for (size_t bytes = o.minb; bytes <= o.maxb; bytes *= o.factor) {
+      const Shape s = shape_for(op, bytes, esz, world);
+      if (std::max(s.send, s.recv) * esz > o.maxb) continue;
+      for (int w = 0; w < o.warmup; ++w) issue(op, sb, rb, s, o.dt(), comm, st);
+      CHECK_HIP(hipStreamSynchronize(st));
+      const int it = iters_for(bytes, o.iters);
+      roctxRangePushA(op_name(op));
+      auto t0 = std::chrono::steady_clock::now();
+      for (int i = 0; i < it; ++i) issue(op, sb, rb, s, o.dt(), comm, st);
+      CHECK_HIP(hipStreamSynchronize(st));
+      const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / it;
+      roctxRangePop();
+      const bool good = check_recv(op, rb, s, world, o.bf16);
+      ok &= good;
+      const size_t sbytes = std::max(s.send, s.recv) * esz;
+      peak = std::max(peak, double(sbytes) / t / 1e9 * bus_factor(op, world));
+      if (rank == 0) print_point(op, world, "multiproc", sbytes, o, t, good);
+      if (bytes > o.maxb / o.factor) break;
     }
-    if (bytes > o.maxb / o.factor) break;
+    if (rank == 0)
+      std::printf("RESULT {\"test\":\"%s_summary\",\"ngpus\":%d,\"peak_busbw_GBps\":%.3f}\n",
+                  op_name(op), world, peak);
   }
   CHECK_HIP(hipFree(sb));
   CHECK_HIP(hipFree(rb));
   CHECK_NCCL(ncclCommDestroy(comm));
   return ok;
+}
+
+bool parse_ops(const char* s, std::vector<Op>* out) {
+  out->clear();
+  std::stringstream ss(s);
+  std::string x;
+  while (std::getline(ss, x, ',')) {
+    if (x == "all") {
+      *out = {Op::AllReduce, Op::ReduceScatter, Op::AllGather, Op::AllToAll};
+      return true;
+    }
+    if (x == "allreduce") out->push_back(Op::AllReduce);
+    else if (x == "reducescatter") out->push_back(Op::ReduceScatter);
+    else if (x == "allgather") out->push_back(Op::AllGather);
+    else if (x == "alltoall") out->push_back(Op::AllToAll);
+    else return false;
+  }
+  return !out->empty();
 }
 
 }  // namespace
@@ -257,7 +350,9 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[i], "--iters") && i + 1 < argc) o.iters = std::max(1, std::atoi(argv[++i]));
     else if (!std::strcmp(argv[i], "--warmup") && i + 1 < argc) o.warmup = std::max(0, std::atoi(argv[++i]));
     else if (!std::strcmp(argv[i], "--id-file") && i + 1 < argc) o.id_file = argv[++i];
-    else { std::fprintf(stderr, "unknown argument %s\n", argv[i]); return 2; }
+    else if (!std::strcmp(argv[i], "--op") && i + 1 < argc) {
+      if (!parse_ops(argv[++i], &o.ops)) { std::fprintf(stderr, "bad --op %s\n", argv[i]); return 2; }
+    } else { std::fprintf(stderr, "unknown argument %s\n", argv[i]); return 2; }
   }
   if (o.minb < 1 || o.maxb < o.minb) { std::fprintf(stderr, "bad size range\n"); return 2; }
   const char* ws = std::getenv("WORLD_SIZE");
@@ -275,15 +370,18 @@ int main(int argc, char** argv) {
   }
   if (o.scaling.empty()) o.scaling.push_back(o.ngpus > 0 ? o.ngpus : count);
   bool ok = true;
-  for (int n : o.scaling) {
-    if (n < 1 || n > count) {
-      std::printf("RESULT {\"test\":\"allreduce\",\"ngpus\":%d,\"pass\":false,\"skipped\":true,"
-                  "\"error\":\"only %d GPU(s) visible\"}\n", n, count);
-      continue;
+  for (Op op : o.ops) {
+    for (int n : o.scaling) {
+      if (n < 1 || n > count) {
+        std::printf("RESULT {\"test\":\"%s\",\"ngpus\":%d,\"pass\":false,\"skipped\":true,"
+                    "\"error\":\"only %d GPU(s) visible\"}\n", op_name(op), n, count);
+        continue;
+      }
+      double peak = 0;
+      ok &= sweep_single(o, op, n, &peak);
+      std::printf("RESULT {\"test\":\"%s_summary\",\"ngpus\":%d,\"peak_busbw_GBps\":%.3f}\n",
+                  op_name(op), n, peak);
     }
-    double peak = 0;
-    ok &= sweep_single(o, n, &peak);
-    std::printf("RESULT {\"test\":\"allreduce_summary\",\"ngpus\":%d,\"peak_busbw_GBps\":%.3f}\n", n, peak);
   }
   return ok ? 0 : 1;
 }

@@ -11,6 +11,7 @@
 //                 [--devices all|0,1] [--no-ref]
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <atomic>
@@ -118,6 +119,7 @@ bool run_device(int dev, const Opts& o) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     float spent = 0;
+    roctxRangePushA("gemm.warmup");
     while (spent < o.warmup_ms) {
       CK(hipEventRecord(e0, st));
       for (int i = 0; i < 10; ++i) mxk_gemm_bf16_tn(A, B, C, n, n, n, n, n, n, st);
@@ -127,7 +129,9 @@ bool run_device(int dev, const Opts& o) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       spent += ms;
     }
+    roctxRangePop();
     std::vector<float> t(o.iters);
+    roctxRangePushA("gemm.timed");
     for (int i = 0; i < o.iters; ++i) {
       CK(hipEventRecord(e0, st));
       mxk_gemm_bf16_tn(A, B, C, n, n, n, n, n, n, st);
@@ -135,6 +139,7 @@ bool run_device(int dev, const Opts& o) {
       CK(hipEventSynchronize(e1));
       CK(hipEventElapsedTime(&t[i], e0, e1));
     }
+    roctxRangePop();
     std::sort(t.begin(), t.end());
     const double med = t[t.size() / 2] * 1e-3;
     const double tflops = 2.0 * n * double(n) * n / med / 1e12;

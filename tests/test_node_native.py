@@ -118,3 +118,10 @@ def test_native_unit_tests_under_asan():
     r = subprocess.run(["make", "-C", REPO, "-s", "test-native"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "libmxnode tests passed" in r.stdout
+
+
+def test_native_thread_safety_under_tsan():
+    """libmxnode entry points are re-entrant (ThreadSanitizer build, 8 threads)."""
+    r = subprocess.run(["make", "-C", REPO, "-s", "test-native-tsan"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "thread-safety test: ok" in r.stdout
