@@ -46,6 +46,8 @@ _SIGNATURES = {
     "mxk_rope": (_i, [_vp, _vp, _vp, _vp, _l, _i, _i, _i, _f, _vp]),
     "mxk_sumsq_partials": (_i, [_l]),
     "mxk_grad_clip_scale": (_i, [_vp, _l, _vp, _f, _f, _vp, _vp]),
+    "mxk_grad_sumsq": (_i, [_vp, _l, _vp, _vp, _vp]),
+    "mxk_clip_scale_from_sumsq": (_i, [_vp, _f, _f, _vp, _vp]),
     "mxk_adamw_bf16": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _f, _f, _f, _f, _f, _i, _vp, _vp]),
 }
 

@@ -16,7 +16,15 @@ Design (MI355X-first rather than a copy of torch DDP's call pattern):
   MI355X), ring collectives are per-link bound and want few, large messages;
   16 GB of Llama-3-8B bf16 gradients = ~32 buckets;
 * the 1/world average and gradient clipping are folded into the fused
-  optimizer kernel (``mxk8s.parallel.optim``), not applied as separate passes.
+  optimizer kernel (``mxk8s.parallel.optim``), not applied as separate passes;
+* ``shard_optimizer=True`` (ZeRO-1): buckets are padded to world*64 elements,
+  each bucket is REDUCE-SCATTERED instead of all-reduced (rank r keeps chunk
+  r), the fp32 master/moments exist only for the rank's shard (12 B/param /
+  world), AdamW updates only that shard and an all-gather per bucket puts the
+  new bf16 parameters back on every rank.  Same bytes on the wire as the
+  all-reduce (RS + AG = AR), 1/world of the optimizer's HBM traffic and
+  memory — the AdamW pass is HBM-bound (28 B/param), so at 8 GPUs it drops
+  from ~38 ms to ~5 ms per Llama-3-8B step.
 
 Works with any backend: ``nccl`` (= RCCL) on GPUs, ``gloo`` on CPU (tests).
 """
@@ -35,12 +43,21 @@ ALIGN = 64   # elements: keeps every slot 16-B (bf16) and 32-B (fp32) aligned
 
 
 class FlatParamSpace:
-    """Contiguous bf16 (or any dtype) storage for all parameters and grads."""
+    """Contiguous bf16 (or any dtype) storage for all parameters and grads.
 
-    def __init__(self, module: nn.Module, dtype: Optional[torch.dtype] = None):
+    ``bucket_elems`` groups consecutive parameters into buckets of at most that
+    many elements (a parameter larger than the cap gets its own bucket);
+    every bucket's end is padded to a multiple of ``pad`` elements so a
+    sharded optimizer can split each bucket evenly over the ranks.
+    """
+
+    def __init__(self, module: nn.Module, dtype: Optional[torch.dtype] = None,
+                 bucket_elems: Optional[int] = None, pad: int = ALIGN):
         params = [p for p in module.parameters() if p.requires_grad]
         if not params:
             raise ValueError("module has no trainable parameters")
+        if pad % ALIGN:
+            raise ValueError(f"pad must be a multiple of {ALIGN}")
         dev = params[0].device
         self.dtype = dtype or params[0].dtype
         # backward order ~ reverse registration order; 1-D (no-decay) last
@@ -48,13 +65,24 @@ class FlatParamSpace:
                 [p for p in reversed(params) if p.dim() < 2]
         self.params = order
         self.offsets = []
+        self.buckets: list[tuple[int, int, list]] = []   # (start, end, params)
+        cap = bucket_elems or (1 << 62)
         off = 0
         n_decay = 0
+        b_start, b_params = 0, []
         for p in order:
+            n = (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+            if b_params and off + n - b_start > cap:
+                off = (off + pad - 1) // pad * pad
+                self.buckets.append((b_start, off, b_params))
+                b_start, b_params = off, []
             self.offsets.append(off)
-            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+            b_params.append(p)
+            off += n
             if p.dim() >= 2:
                 n_decay = off
+        off = (off + pad - 1) // pad * pad
+        self.buckets.append((b_start, off, b_params))
         self.numel = off
         self.n_decay = n_decay
         self.param_buf = torch.zeros(self.numel, dtype=self.dtype, device=dev)
@@ -74,40 +102,53 @@ class FlatParamSpace:
 
 
 class Bucket:
-    __slots__ = ("start", "end", "params", "pending", "handle", "launched")
+    __slots__ = ("start", "end", "params", "pending", "handle", "launched", "shard_off")
 
-    def __init__(self, start: int):
+    def __init__(self, start: int, end: int = 0, params=None):
         self.start = start
-        self.end = start
-        self.params: list = []
+        self.end = end or start
+        self.params: list = list(params or [])
         self.pending = 0
         self.handle = None
         self.launched = False
+        self.shard_off = 0      # offset of this bucket's chunk in the rank's shard
+
+    def chunk(self, world: int) -> int:
+        return (self.end - self.start) // world
 
 
 class FlatDDP:
     """Wraps a module whose parameters were flattened by :class:`FlatParamSpace`."""
 
     def __init__(self, module: nn.Module, bucket_mb: float = 512.0,
-                 process_group=None, broadcast_from: Optional[int] = 0):
+                 process_group=None, broadcast_from: Optional[int] = 0,
+                 shard_optimizer: bool = False):
         self.module = module
-        self.space = FlatParamSpace(module)
         self.group = process_group
         self.world = dist.get_world_size(process_group) if mxdist.active() else 1
-        esz = self.space.param_buf.element_size()
+        self.rank = dist.get_rank(process_group) if mxdist.active() else 0
+        # ZeRO-1: gradients are reduce-scattered (each rank keeps 1/world of
+        # every bucket) and the optimizer state is sharded the same way
+        self.sharded = shard_optimizer and self.world > 1
+        esz = next(p for p in module.parameters() if p.requires_grad).element_size()
         cap = max(1, int(bucket_mb * 2 ** 20 / esz))
+        self.space = FlatParamSpace(module, bucket_elems=cap,
+                                    pad=ALIGN * (self.world if self.sharded else 1))
         self.buckets: list[Bucket] = []
-        cur = Bucket(0)
         self._bucket_of = {}
-        for p, o in zip(self.space.params, self.space.offsets):
-            n = (p.numel() + ALIGN - 1) // ALIGN * ALIGN
-            if cur.params and (o + n - cur.start) > cap:
-                self.buckets.append(cur)
-                cur = Bucket(o)
-            cur.params.append(p)
-            cur.end = o + n
-            self._bucket_of[id(p)] = cur
-        self.buckets.append(cur)
+        shard_off = 0
+        for start, end, params in self.space.buckets:
+            b = Bucket(start, end, params)
+            b.shard_off = shard_off
+            shard_off += b.chunk(self.world) if self.sharded else 0
+            self.buckets.append(b)
+            for p in params:
+                self._bucket_of[id(p)] = b
+        self.shard_numel = shard_off
+        # reduce-scattered gradient shard (bf16, what the sharded AdamW reads)
+        self.grad_shard = (torch.zeros(shard_off, dtype=self.space.dtype,
+                                       device=self.space.grad_buf.device)
+                           if self.sharded else None)
         self._sync_enabled = True
         self._hooks = []
         if self.world > 1:
@@ -116,6 +157,12 @@ class FlatDDP:
             for p in self.space.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
         self._reset_buckets()
+
+    def shard_range(self, b: Bucket) -> tuple[int, int]:
+        """Flat [lo, hi) of this rank's chunk of bucket ``b``."""
+        c = b.chunk(self.world)
+        lo = b.start + self.rank * c
+        return lo, lo + c
 
     # ------------------------------------------------------------------
     def _reset_buckets(self) -> None:
@@ -128,8 +175,14 @@ class FlatDDP:
         if b.launched:
             return
         b.launched = True
-        b.handle = dist.all_reduce(self.space.grad_buf[b.start:b.end], op=dist.ReduceOp.SUM,
-                                   group=self.group, async_op=True)
+        g = self.space.grad_buf[b.start:b.end]
+        if self.sharded:
+            c = b.chunk(self.world)
+            b.handle = dist.reduce_scatter_tensor(self.grad_shard[b.shard_off:b.shard_off + c], g,
+                                                  op=dist.ReduceOp.SUM, group=self.group,
+                                                  async_op=True)
+        else:
+            b.handle = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def _on_grad(self, p) -> None:
         if not self._sync_enabled:

@@ -91,3 +91,126 @@ class FlatAdamW:
             denom = v.sqrt() / (bc2 ** 0.5) + self.eps
             p.addcdiv_(m, denom, value=-self.lr / bc1)
         sp.param_buf.copy_(self.master.to(sp.param_buf.dtype))
+
+
+class ShardedFlatAdamW:
+    """ZeRO-1 AdamW for a :class:`~mxk8s.parallel.ddp.FlatDDP` built with
+    ``shard_optimizer=True``.
+
+    State per rank: fp32 master / exp_avg / exp_avg_sq for the rank's chunk
+    of every bucket only (shard-local layout = the chunks in bucket order, the
+    same layout as ``ddp.grad_shard``).  A step:
+
+      1. sum of squares of the local gradient shard -> all-reduce of ONE fp32
+         -> clip scale (device scalar, folds in 1/world; no host sync);
+      2. per bucket: fused AdamW over the rank's chunk (split where the chunk
+         crosses the no-weight-decay boundary), writing the bf16 parameters
+         in place into the rank's chunk of ``param_buf``, then an async
+         in-place all-gather of that bucket — the all-gather of bucket b runs
+         on the RCCL stream while AdamW of bucket b+1 runs;
+      3. the compute stream waits on every all-gather (no host sync).
+    """
+
+    def __init__(self, ddp, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
+                 weight_decay: float = 0.1, max_grad_norm: float = 1.0):
+        if not ddp.sharded:
+            raise ValueError("ShardedFlatAdamW needs FlatDDP(shard_optimizer=True) with world > 1")
+        import torch.distributed as dist
+        self._dist = dist
+        self.ddp = ddp
+        sp = ddp.space
+        self.lr, self.b1, self.b2, self.eps = lr, betas[0], betas[1], eps
+        self.wd = weight_decay
+        self.max_grad_norm = max_grad_norm
+        self.step_count = 0
+        dev = sp.param_buf.device
+        # shard-local segments (shard_lo, flat_lo, n, wd): chunks split at n_decay
+        self.segments = []
+        for b in ddp.buckets:
+            lo, hi = ddp.shard_range(b)
+            cuts = [lo] + ([sp.n_decay] if lo < sp.n_decay < hi else []) + [hi]
+            for a, z in zip(cuts[:-1], cuts[1:]):
+                self.segments.append((b, b.shard_off + (a - lo), a, z - a,
+                                      self.wd if a < sp.n_decay else 0.0))
+        self.master = torch.empty(ddp.shard_numel, dtype=torch.float32, device=dev)
+        for b in ddp.buckets:
+            lo, hi = ddp.shard_range(b)
+            self.master[b.shard_off:b.shard_off + hi - lo].copy_(sp.param_buf[lo:hi].float())
+        self.exp_avg = torch.zeros_like(self.master)
+        self.exp_avg_sq = torch.zeros_like(self.master)
+        self._scale = torch.ones(2, dtype=torch.float32, device=dev)   # [scale, grad norm]
+        self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        if dev.type == "cuda":
+            n_part = _lib.lib().mxk_sumsq_partials(ddp.shard_numel)
+            self._partials = torch.zeros(n_part, dtype=torch.float32, device=dev)
+
+    @property
+    def last_grad_norm(self) -> torch.Tensor:
+        return self._scale[1]
+
+    def _clip(self) -> None:
+        ddp = self.ddp
+        g = ddp.grad_shard
+        if g.device.type == "cuda":
+            L = _lib.lib()
+            s = _lib.stream_ptr(g.device)
+            _lib.check(L.mxk_grad_sumsq(g.data_ptr(), g.numel(), self._partials.data_ptr(),
+                                        self._sumsq.data_ptr(), s), "mxk_grad_sumsq")
+            self._dist.all_reduce(self._sumsq, op=self._dist.ReduceOp.SUM, group=ddp.group)
+            _lib.check(L.mxk_clip_scale_from_sumsq(self._sumsq.data_ptr(), 1.0 / ddp.world,
+                                                   float(self.max_grad_norm),
+                                                   self._scale.data_ptr(), s),
+                       "mxk_clip_scale_from_sumsq")
+            return
+        self._sumsq[0] = g.float().pow(2).sum()
+        self._dist.all_reduce(self._sumsq, op=self._dist.ReduceOp.SUM, group=ddp.group)
+        norm = self._sumsq[0].sqrt() / ddp.world
+        clip = 1.0
+        if self.max_grad_norm > 0 and norm > self.max_grad_norm:
+            clip = self.max_grad_norm / (norm + 1e-6)
+        self._scale[0] = clip / ddp.world
+        self._scale[1] = norm
+
+    def _adamw_segment(self, so: int, flat_lo: int, n: int, wd: float) -> None:
+        sp, ddp = self.ddp.space, self.ddp
+        if sp.param_buf.device.type == "cuda":
+            L = _lib.lib()
+            esz, fsz = sp.param_buf.element_size(), 4
+            st = L.mxk_adamw_bf16(sp.param_buf.data_ptr() + flat_lo * esz,
+                                  self.master.data_ptr() + so * fsz,
+                                  self.exp_avg.data_ptr() + so * fsz,
+                                  self.exp_avg_sq.data_ptr() + so * fsz,
+                                  ddp.grad_shard.data_ptr() + so * esz, n, float(self.lr),
+                                  float(self.b1), float(self.b2), float(self.eps), float(wd),
+                                  self.step_count, self._scale.data_ptr(),
+                                  _lib.stream_ptr(sp.param_buf.device))
+            _lib.check(st, "mxk_adamw_bf16")
+            return
+        bc1 = 1 - self.b1 ** self.step_count
+        bc2 = 1 - self.b2 ** self.step_count
+        g = ddp.grad_shard[so:so + n].float() * self._scale[0]
+        p, m, v = self.master[so:so + n], self.exp_avg[so:so + n], self.exp_avg_sq[so:so + n]
+        p.mul_(1 - self.lr * wd)
+        m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+        v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+        p.addcdiv_(m, v.sqrt() / (bc2 ** 0.5) + self.eps, value=-self.lr / bc1)
+        sp.param_buf[flat_lo:flat_lo + n].copy_(p.to(sp.param_buf.dtype))
+
+    @torch.no_grad()
+    def step(self) -> None:
+        self.step_count += 1
+        ddp, sp = self.ddp, self.ddp.space
+        self._clip()
+        handles = []
+        seg_i = 0
+        for b in ddp.buckets:
+            while seg_i < len(self.segments) and self.segments[seg_i][0] is b:
+                _, so, lo, n, wd = self.segments[seg_i]
+                self._adamw_segment(so, lo, n, wd)
+                seg_i += 1
+            lo, hi = ddp.shard_range(b)
+            handles.append(self._dist.all_gather_into_tensor(
+                sp.param_buf[b.start:b.end], sp.param_buf[lo:hi], group=ddp.group,
+                async_op=True))
+        for h in handles:
+            h.wait()

@@ -23,18 +23,25 @@ import torch
 from ..models.llama import Llama, LlamaConfig
 from ..parallel import dist as mxdist
 from ..parallel.ddp import FlatDDP
-from ..parallel.optim import FlatAdamW
+from ..parallel.optim import FlatAdamW, ShardedFlatAdamW
 from ..utils import roctx
 
 MI355X_BF16_DENSE_PEAK = 2.5e15   # FLOP/s, dense (MI355X_MICROARCH.md)
 
 
-def build(cfg: LlamaConfig, device: torch.device, bucket_mb: float, lr: float = 3e-4):
+def build(cfg: LlamaConfig, device: torch.device, bucket_mb: float, lr: float = 3e-4,
+          zero: bool = True):
+    """Model + DDP + optimizer.  ``zero`` shards the AdamW state and step over
+    the ranks (ZeRO-1, reduce-scatter + all-gather); it only applies with
+    more than one rank."""
     with torch.device(device):
         model = Llama(cfg)
     model = model.to(torch.bfloat16)
-    ddp = FlatDDP(model, bucket_mb=bucket_mb)
-    opt = FlatAdamW(ddp.space, lr=lr, grad_scale=ddp.grad_scale)
+    ddp = FlatDDP(model, bucket_mb=bucket_mb, shard_optimizer=zero)
+    if ddp.sharded:
+        opt = ShardedFlatAdamW(ddp, lr=lr)
+    else:
+        opt = FlatAdamW(ddp.space, lr=lr, grad_scale=ddp.grad_scale)
     return model, ddp, opt
 
 
@@ -71,7 +78,8 @@ def run_ddp_bench(args) -> dict:
         model_name = "tiny-llama (test)"
     seq, mb = args.seq_len, args.micro_batch
     bucket_mb = getattr(args, "bucket_mb", 512.0)
-    model, ddp, opt = build(cfg, dev, bucket_mb)
+    zero = not getattr(args, "no_zero", False)
+    model, ddp, opt = build(cfg, dev, bucket_mb, zero=zero)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     nbatches = 4
@@ -116,7 +124,7 @@ def run_ddp_bench(args) -> dict:
         "dtype": "bf16",
         "data": "synthetic (uniform random token ids), random-init weights",
         "config": {"model": model_name, "global_batch": world * mb, "seq_len": seq,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}" + ("+zero1" if ddp.sharded else "")},
         "tokens_per_s_per_gpu": round(tps / world, 1),
         "mfu": round(mfu, 4),
         "params": cfg.num_params(),
@@ -136,6 +144,8 @@ def main(argv=None) -> int:
     p.add_argument("--layers", type=int, default=None)
     p.add_argument("--bucket-mb", type=float, default=512.0)
     p.add_argument("--tiny", action="store_true")
+    p.add_argument("--no-zero", action="store_true",
+                   help="replicate the optimizer (all-reduce) instead of ZeRO-1 sharding")
     a = p.parse_args(argv)
     out = run_ddp_bench(a)
     if mxdist.world_info()[1] == 0:

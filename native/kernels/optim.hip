@@ -66,6 +66,29 @@ mxk_clip_scale_kernel(const float* __restrict__ partial, int nb, float inv_world
   }
 }
 
+// Sharded optimizer (ZeRO-1): each rank folds the sum of squares of ITS
+// gradient shard into out[0]; the trainer all-reduces that scalar and
+// mxk_scale_from_sumsq_kernel turns the global sum into [scale, norm].
+__global__ void __launch_bounds__(kThreads)
+mxk_fold_sum_kernel(const float* __restrict__ partial, int nb, float* __restrict__ out) {
+  __shared__ float red[kThreads / 64];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += kThreads) s += partial[i];
+  float f = mxk::wave_sum(static_cast<float>(s));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void mxk_scale_from_sumsq_kernel(const float* __restrict__ sumsq, float inv_world,
+                                            float max_norm, float* __restrict__ out) {
+  const float norm = sqrtf(sumsq[0]) * inv_world;
+  float clip = 1.f;
+  if (max_norm > 0.f && norm > max_norm) clip = max_norm / (norm + 1e-6f);
+  out[0] = inv_world * clip;
+  out[1] = norm;
+}
+
 __global__ void __launch_bounds__(kThreads)
 mxk_adamw_bf16_kernel(uint16_t* __restrict__ param, float* __restrict__ master,
                       float* __restrict__ m, float* __restrict__ v,
@@ -139,6 +162,25 @@ MXK_API int mxk_grad_clip_scale(const void* grad, long n, float* partial_ws, flo
                      static_cast<const uint16_t*>(grad), n, partial_ws);
   hipLaunchKernelGGL(mxk_clip_scale_kernel, dim3(1), dim3(kThreads), 0, s, partial_ws, nb,
                      inv_world, max_norm, out2);
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// out_sumsq[0] = sum of g^2 over this (shard of the) gradient.
+MXK_API int mxk_grad_sumsq(const void* grad, long n, float* partial_ws, float* out_sumsq,
+                           hipStream_t s) {
+  if (n <= 0 || !a16(grad)) return static_cast<int>(hipErrorInvalidValue);
+  const int nb = grid_for(n / 8);
+  hipLaunchKernelGGL(mxk_sumsq_bf16_kernel, dim3(nb), dim3(kThreads), 0, s,
+                     static_cast<const uint16_t*>(grad), n, partial_ws);
+  hipLaunchKernelGGL(mxk_fold_sum_kernel, dim3(1), dim3(kThreads), 0, s, partial_ws, nb, out_sumsq);
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// out2 = [inv_world * clip, norm] from the GLOBAL sum of squares.
+MXK_API int mxk_clip_scale_from_sumsq(const float* sumsq, float inv_world, float max_norm,
+                                      float* out2, hipStream_t s) {
+  hipLaunchKernelGGL(mxk_scale_from_sumsq_kernel, dim3(1), dim3(1), 0, s, sumsq, inv_world,
+                     max_norm, out2);
   MXK_RETURN_LAUNCH_STATUS();
 }
 

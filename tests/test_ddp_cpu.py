@@ -130,3 +130,49 @@ def test_grad_clipping_reference():
     # the buffer holds the SUM over 2 ranks -> mean grad norm = 0.5 * ||1||
     assert abs(norm - 0.5 * (64 ** 0.5)) < 1e-4
     assert abs(float(opt._scale[0]) - 0.5 / (norm + 1e-6)) < 1e-6
+
+
+def _zero_worker(rank, world, port, outdir, bucket_mb):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from mxk8s.parallel.optim import ShardedFlatAdamW
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = LlamaConfig.tiny()
+    out = {}
+    for sharded in (False, True):
+        torch.manual_seed(0)
+        model = Llama(cfg)
+        ddp = FlatDDP(model, bucket_mb=bucket_mb, shard_optimizer=sharded)
+        if sharded:
+            assert ddp.sharded and ddp.shard_numel * world == ddp.space.numel
+            assert all((b.end - b.start) % (64 * world) == 0 for b in ddp.buckets)
+            opt = ShardedFlatAdamW(ddp, lr=1e-3, max_grad_norm=0.5)
+        else:
+            opt = FlatAdamW(ddp.space, lr=1e-3, grad_scale=ddp.grad_scale, max_grad_norm=0.5)
+        for step in range(3):
+            model.loss(_batch(rank * 10 + step, cfg)).backward()
+            ddp.finish_grad_sync()
+            opt.step()
+            ddp.zero_grad()
+        out[sharded] = {n: p.detach().clone() for n, p in model.named_parameters()}
+        out[f"norm{sharded}"] = opt.last_grad_norm.clone()
+    torch.save({"plain": out[False], "zero": out[True], "n0": out["normFalse"],
+                "n1": out["normTrue"]}, os.path.join(outdir, f"z{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bucket_mb", [0.05, 512.0])
+def test_zero1_sharded_optimizer_matches_replicated(bucket_mb):
+    """ZeRO-1 (reduce-scatter + sharded AdamW + all-gather) must produce the
+    same parameters as the replicated all-reduce + AdamW path, on every rank."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_zero_worker, args=(world, _free_port(), d, bucket_mb), nprocs=world, join=True)
+        z = [torch.load(os.path.join(d, f"z{i}.pt"), weights_only=True) for i in range(world)]
+    for r in range(world):
+        assert torch.allclose(z[r]["n0"], z[r]["n1"], rtol=1e-3)
+        for n, p in z[r]["plain"].items():
+            assert torch.allclose(z[r]["zero"][n], p, rtol=1e-4, atol=1e-5), n
+    for n in z[0]["zero"]:
+        assert torch.equal(z[0]["zero"][n], z[1]["zero"][n]), n

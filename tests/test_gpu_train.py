@@ -65,3 +65,26 @@ def test_ddp_bench_tiny_single_gpu(cuda_device):
     out = run_ddp_bench(a)
     assert out["n_gpus"] == 1 and out["value"] > 0
     assert out["mean_loss"] == out["mean_loss"]   # not NaN
+
+
+def test_sharded_clip_kernels_vs_torch(cuda_device):
+    """ZeRO-1 clip path: per-shard sum of squares + scale from the global sum."""
+    from mxk8s.ops import _lib
+    L = _lib.lib()
+    g = torch.Generator(device=cuda_device).manual_seed(5)
+    for n in (8, 1000, 3 * 2 ** 20 + 24):
+        grad = (torch.randn(n, device=cuda_device, generator=g) * 0.7).bfloat16()
+        parts = torch.zeros(L.mxk_sumsq_partials(n), device=cuda_device)
+        sumsq = torch.zeros(1, device=cuda_device)
+        _lib.check(L.mxk_grad_sumsq(grad.data_ptr(), n, parts.data_ptr(), sumsq.data_ptr(),
+                                    _lib.stream_ptr(cuda_device)), "sumsq")
+        ref = grad.float().pow(2).sum()
+        assert torch.allclose(sumsq[0], ref, rtol=1e-4)
+        out = torch.zeros(2, device=cuda_device)
+        world, max_norm = 4, 1.0
+        _lib.check(L.mxk_clip_scale_from_sumsq(sumsq.data_ptr(), 1.0 / world, max_norm,
+                                               out.data_ptr(), _lib.stream_ptr(cuda_device)), "clip")
+        norm = ref.sqrt().item() / world
+        clip = max_norm / (norm + 1e-6) if norm > max_norm else 1.0
+        assert abs(out[1].item() - norm) <= 1e-4 * norm
+        assert abs(out[0].item() - clip / world) <= 1e-4 * clip / world
