@@ -48,6 +48,7 @@ _SIGNATURES = {
     "mxk_grad_clip_scale": (_i, [_vp, _l, _vp, _f, _f, _vp, _vp]),
     "mxk_grad_sumsq": (_i, [_vp, _l, _vp, _vp, _vp]),
     "mxk_clip_scale_from_sumsq": (_i, [_vp, _f, _f, _vp, _vp]),
+    "mxk_attn_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _l, _l, _l, _f, _i, _vp]),
     "mxk_adamw_bf16": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _f, _f, _f, _f, _f, _i, _vp, _vp]),
 }
 

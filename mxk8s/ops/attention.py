@@ -1,0 +1,66 @@
+"""Flash attention on the hand-written gfx950 kernels
+(``native/kernels/attention.hip``).
+
+``flash_attention(q, k, v, causal=True)`` takes q [B, S, Hq, 128] and k/v
+[B, S, Hkv, 128] bf16 tensors whose last two dims are contiguous (token
+strides are free, so q/k/v may be views of a fused QKV projection) and
+returns o [B, S, Hq, 128] — the layout the output projection consumes, no
+transposes.  GQA: Hq % Hkv == 0.  The forward also produces the per-row
+log-sum-exp that the backward kernel uses to recompute P.
+
+``attention_ref`` is the fp32 PyTorch reference the tests compare against.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+
+HEAD_DIM = 128
+BLOCK_Q = 128
+
+
+def supported(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> bool:
+    """Shapes/layouts the HIP kernels handle (others use the reference path)."""
+    if q.device.type != "cuda" or q.dtype != torch.bfloat16:
+        return False
+    B, S, Hq, D = q.shape
+    if D != HEAD_DIM or S % BLOCK_Q or k.shape[2] == 0 or Hq % k.shape[2]:
+        return False
+    for t in (q, k, v):
+        if t.stride(-1) != 1 or t.stride(-2) != D or t.stride(0) != S * t.stride(1) \
+                or t.stride(1) % 8 or t.data_ptr() % 16:
+            return False
+    return True
+
+
+def attention_ref(q, k, v, causal: bool = True, scale: float | None = None) -> torch.Tensor:
+    """fp32 reference: q [B,S,Hq,D], k/v [B,S,Hkv,D] -> [B,S,Hq,D] (q.dtype)."""
+    B, S, Hq, D = q.shape
+    Hkv = k.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    qf = q.float().transpose(1, 2)
+    kf = k.float().transpose(1, 2).repeat_interleave(Hq // Hkv, dim=1)
+    vf = v.float().transpose(1, 2).repeat_interleave(Hq // Hkv, dim=1)
+    s = qf @ kf.transpose(-1, -2) * scale
+    if causal:
+        mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    o = torch.softmax(s, dim=-1) @ vf
+    return o.transpose(1, 2).to(q.dtype)
+
+
+def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None):
+    """HIP forward: returns (o [B,S,Hq,D] bf16, lse [B,Hq,S] fp32)."""
+    B, S, Hq, D = q.shape
+    Hkv = k.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    o = torch.empty((B, S, Hq, D), dtype=q.dtype, device=q.device)
+    lse = torch.empty((B, Hq, S), dtype=torch.float32, device=q.device)
+    st = _lib.lib().mxk_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                 lse.data_ptr(), B, S, Hq, Hkv, D, q.stride(1), k.stride(1),
+                                 v.stride(1), float(scale), int(causal), _lib.stream_ptr(q.device))
+    _lib.check(st, "mxk_attn_fwd")
+    return o, lse

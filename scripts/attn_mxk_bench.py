@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Time the hand-written flash attention (fwd, and fwd+bwd once available)
+against torch SDPA on the Llama-3-8B shape: B=1, Hq=32, Hkv=8, S=2048,
+D=128, causal, bf16, random data.  Prints one RESULT json line per kernel."""
+import json
+import os
+import statistics
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mxk8s.ops import attention as A  # noqa: E402
+
+
+def bench(fn, iters=30):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    return statistics.median(ts)
+
+
+def main():
+    dev = torch.device("cuda")
+    B, Hq, Hk, S, D = 1, 32, 8, int(os.environ.get("SEQ", 2048)), 128
+    g = torch.Generator(device=dev).manual_seed(0)
+    q = torch.randn(B, S, Hq, D, device=dev, generator=g).bfloat16()
+    k = torch.randn(B, S, Hk, D, device=dev, generator=g).bfloat16()
+    v = torch.randn(B, S, Hk, D, device=dev, generator=g).bfloat16()
+    flops_fwd = 4 * B * Hq * S * S * D / 2
+    res = {}
+    res["mxk_fwd"] = bench(lambda: A.attn_fwd(q, k, v, causal=True))
+    qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
+    with torch.no_grad():
+        res["sdpa_fwd"] = bench(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=True,
+                                                                      enable_gqa=True))
+    for name, ms in res.items():
+        print("RESULT " + json.dumps({"kernel": name, "ms": round(ms, 4), "S": S,
+                                      "tflops": round(flops_fwd / ms / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
