@@ -8,8 +8,10 @@ step on amd.com/gpu=8".  The reference has no model code at all (SURVEY.md
   GEMM per MLP (fewer, larger hipBLASLt GEMMs);
 * hand-written HIP kernels for the memory-bound glue: RMSNorm fwd/bwd,
   SwiGLU fwd/bwd, rotary embedding fwd/bwd (``mxk8s.ops.fused``);
-* attention through ``scaled_dot_product_attention`` (causal, GQA) — the
-  ROCm flash backend;
+* causal GQA attention through the hand-written gfx950 flash-attention
+  kernels (``mxk8s.ops.attention``: forward + LSE, dQ and dK/dV passes) on
+  q/k/v in their [B, S, H, D] projection layout (v stays a view of the fused
+  QKV output); shapes those kernels do not tile fall back to SDPA;
 * bf16 parameters; fp32 master weights and AdamW state live in the optimizer
   (``mxk8s.parallel.optim.FlatAdamW``).
 """
@@ -22,6 +24,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.attention import flash_attention, supported as flash_supported
 from ..ops.fused import add_rmsnorm, rmsnorm, rope, rope_tables, swiglu
 
 
@@ -43,8 +46,9 @@ class LlamaConfig:
 
     @classmethod
     def tiny(cls) -> "LlamaConfig":
-        return cls(dim=256, n_layers=2, n_heads=8, n_kv_heads=2, ffn_dim=512, vocab_size=1024,
-                   max_seq_len=256)
+        # head_dim 128 like Llama-3, so the GPU tests run the HIP attention
+        return cls(dim=512, n_layers=2, n_heads=4, n_kv_heads=2, ffn_dim=1024, vocab_size=1024,
+                   max_seq_len=512)
 
     @property
     def head_dim(self) -> int:
@@ -89,7 +93,11 @@ class Attention(nn.Module):
         q, k, v = qkv.split([c.n_heads * hd, c.n_kv_heads * hd, c.n_kv_heads * hd], dim=-1)
         q = rope(q.reshape(B, S, c.n_heads, hd), cos, sin)
         k = rope(k.reshape(B, S, c.n_kv_heads, hd), cos, sin)
-        v = v.reshape(B, S, c.n_kv_heads, hd)
+        v = v.reshape(B, S, c.n_kv_heads, hd)   # view into qkv: token stride (Hq+2Hkv)*hd
+        if flash_supported(q, k, v):
+            # hand-written gfx950 flash attention: [B,S,H,D] in and out, no transposes
+            o = flash_attention(q, k, v, causal=True)
+            return self.wo(o.reshape(B, S, c.n_heads * hd))
         o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
                                            is_causal=True, enable_gqa=True)
         return self.wo(o.transpose(1, 2).reshape(B, S, c.n_heads * hd))

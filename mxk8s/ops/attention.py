@@ -64,3 +64,56 @@ def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None):
                                  v.stride(1), float(scale), int(causal), _lib.stream_ptr(q.device))
     _lib.check(st, "mxk_attn_fwd")
     return o, lse
+
+
+def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = None,
+             dk=None, dv=None):
+    """HIP backward: returns (dq [B,S,Hq,D], dk [B,S,Hkv,D], dv [B,S,Hkv,D]).
+
+    ``dk``/``dv`` may be preallocated views (e.g. slices of a fused dQKV
+    buffer) with a token stride; by default they are fresh contiguous tensors."""
+    B, S, Hq, D = q.shape
+    Hkv = k.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    dout = dout.contiguous()
+    dq = torch.empty((B, S, Hq, D), dtype=q.dtype, device=q.device)
+    if dk is None:
+        dk = torch.empty((B, S, Hkv, D), dtype=k.dtype, device=k.device)
+    if dv is None:
+        dv = torch.empty((B, S, Hkv, D), dtype=v.dtype, device=v.device)
+    L = _lib.lib()
+    ws = torch.empty(L.mxk_attn_bwd_workspace(B, S, Hq) // 4, dtype=torch.float32, device=q.device)
+    st = L.mxk_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
+                        lse.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), ws.data_ptr(),
+                        B, S, Hq, Hkv, D, q.stride(1), k.stride(1), v.stride(1), dk.stride(1),
+                        dv.stride(1), float(scale), int(causal), _lib.stream_ptr(q.device))
+    _lib.check(st, "mxk_attn_bwd")
+    return dq, dk, dv
+
+
+class _FlashAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        o, lse = attn_fwd(q, k, v, causal=causal, scale=scale)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = attn_bwd(q, k, v, o, lse, dout, causal=ctx.causal, scale=ctx.scale)
+        return dq, dk, dv, None, None
+
+
+def flash_attention(q, k, v, causal: bool = True, scale: float | None = None) -> torch.Tensor:
+    """Attention o [B,S,Hq,D] for q [B,S,Hq,D], k/v [B,S,Hkv,D] (GQA).
+
+    Runs the HIP kernels for supported CUDA bf16 inputs (``supported``);
+    CPU / other dtypes take the fp32 reference (used by the CPU tests)."""
+    if supported(q, k, v):
+        return _FlashAttention.apply(q, k, v, causal, scale)
+    if q.device.type == "cuda":
+        raise RuntimeError(f"flash_attention: unsupported shape/layout on GPU: q {tuple(q.shape)} "
+                           f"strides {q.stride()} (need head_dim 128, S % 128 == 0)")
+    return attention_ref(q, k, v, causal=causal, scale=scale)

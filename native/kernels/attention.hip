@@ -293,3 +293,446 @@ MXK_API int mxk_attn_fwd(const void* q, const void* k, const void* v, void* o, f
                        q_tok, k_tok, v_tok, scale);
   MXK_RETURN_LAUNCH_STATUS();
 }
+
+// ===========================================================================
+// Backward.  Three passes, no atomics (deterministic):
+//   1. delta[b][hq][q] = sum_d dO . O                       (mxk_attn_bwd_delta)
+//   2. dQ, query-parallel, structured like the forward: per 64-key block
+//      S^T = K.Q^T and dP^T = V.dO^T with the query on the lane, P^T from the
+//      saved LSE (no max/sum), dS^T = P^T (dP^T - delta), dQ^T += K^T.dS^T
+//      (K^T by ds_read_b64_tr_b16 from the same swizzled image).
+//   3. dK/dV, key-parallel: one workgroup = 4 waves x 32 keys of one
+//      (batch, q-head), sweeping 64-query slices: S = Q.K^T and dP = dO.V^T
+//      with the KEY on the lane, so P and dS are already the B operands of
+//      dV^T += dO^T.P and dK^T += Q^T.dS (dO^T, Q^T by transposed reads);
+//      the accumulator init carries -LSE/scale and -delta, so
+//      p = exp2(c * acc) and dS = p * acc' need no extra subtraction.
+//      Per-q-head partial dK/dV (fp32) are summed over each GQA group by
+//      mxk_attn_bwd_gqa_reduce.
+// Recomputing S and dP in both passes costs 7 instead of 5 MFMA products
+// per tile but removes the dQ atomics (1.3 TB/s chip-wide would bound the
+// pass) and keeps every kernel deterministic.
+// ===========================================================================
+namespace {
+constexpr int BQB = 64;   // queries per slice in the dK/dV kernel
+
+__device__ __forceinline__ void zero16(f32x16_t& x) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) x[r] = 0.f;
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256)
+mxk_attn_bwd_delta_kernel(const uint16_t* __restrict__ o, const uint16_t* __restrict__ dout,
+                          float* __restrict__ delta, int S, int Hq, long rows) {
+  // one 16-lane group per (b, q, hq) row of 128 dims: 8 bf16 per lane
+  const long row = (static_cast<long>(blockIdx.x) * 256 + threadIdx.x) >> 4;
+  const int sub = threadIdx.x & 15;
+  if (row >= rows) return;
+  const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(o + row * D + sub * 8);
+  const bf16x8_t g = *reinterpret_cast<const bf16x8_t*>(dout + row * D + sub * 8);
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    s += mxk::bf2f(static_cast<uint16_t>(a[e])) * mxk::bf2f(static_cast<uint16_t>(g[e]));
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
+  if (sub == 0) {
+    // row = (b * S + q) * Hq + hq  ->  delta[b][hq][q]
+    const long bq = row / Hq;
+    const int hq = static_cast<int>(row % Hq);
+    const long b = bq / S, qi = bq % S;
+    delta[(b * Hq + hq) * S + qi] = s;
+  }
+}
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(NT, 2)
+mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                       const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
+                       const float* __restrict__ lse, const float* __restrict__ delta,
+                       uint16_t* __restrict__ dq, int S, int Hq, int Hkv, long q_tok, long k_tok,
+                       long v_tok, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2 * TILE_BYTES];   // [buf][K | V]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  const int nqb = S / BQ;
+  int bh, qb;
+  map_block(blockIdx.x, gridDim.x / nqb, nqb, CAUSAL, &bh, &qb);
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hkv = hq / (Hq / Hkv);
+  const int q0 = qb * BQ;
+  const int qw0 = q0 + wave * 32;
+  const int myq = qw0 + r32;
+
+  const uint16_t* qb_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
+  const uint16_t* dob_ptr = dout + static_cast<long>(b) * S * Hq * D + static_cast<long>(hq) * D;
+  const uint16_t* kb_ptr = k + static_cast<long>(b) * S * k_tok + static_cast<long>(hkv) * D;
+  const uint16_t* vb_ptr = v + static_cast<long>(b) * S * v_tok + static_cast<long>(hkv) * D;
+
+  bf16x8_t qf[8], dof[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    qf[s] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + static_cast<long>(myq) * q_tok + 16 * s + 8 * h);
+    dof[s] = *reinterpret_cast<const bf16x8_t*>(dob_ptr + static_cast<long>(myq) * Hq * D + 16 * s + 8 * h);
+  }
+  const float c = scale * 1.4426950408889634f;
+  const long lrow = (static_cast<long>(b) * Hq + hq) * S + myq;
+  const float lse2 = lse[lrow] * 1.4426950408889634f;
+  const float dlt = delta[lrow];
+
+  const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
+  const int nkv = kv_end / BKV;
+  const int ld_row = tid >> 4, ld_ch = tid & 15;
+  bf16x8_t kst[4], vst[4];
+  auto load_tile = [&](int j) {
+    const long r0 = static_cast<long>(j) * BKV + ld_row;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      kst[i] = *reinterpret_cast<const bf16x8_t*>(kb_ptr + (r0 + 16 * i) * k_tok + ld_ch * 8);
+      vst[i] = *reinterpret_cast<const bf16x8_t*>(vb_ptr + (r0 + 16 * i) * v_tok + ld_ch * 8);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int off = swz(ld_row + 16 * i, ld_ch);
+      *reinterpret_cast<bf16x8_t*>(smem[buf] + off) = kst[i];
+      *reinterpret_cast<bf16x8_t*>(smem[buf] + TILE_BYTES + off) = vst[i];
+    }
+  };
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  f32x16_t acc[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) zero16(acc[db]);
+  const int G = lane >> 4, i16 = lane & 15;
+  const int tr_key = 4 * h + (i16 >> 2);
+  const int tr_ch = 2 * (G & 1) + ((i16 & 3) >> 1);
+  const int tr_byte = 8 * (i16 & 1);
+
+  for (int j = 0; j < nkv; ++j) {
+    const int buf = j & 1;
+    if (j + 1 < nkv) load_tile(j + 1);
+    const int kv0 = j * BKV;
+    if (!CAUSAL || kv0 <= qw0 + 31) {
+      const char* kt = smem[buf];
+      const char* vt = smem[buf] + TILE_BYTES;
+      const bool diag = CAUSAL && kv0 + BKV - 1 > qw0;
+      // one 32-key half at a time keeps S^T / dP^T to 32 registers
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        f32x16_t s0, p0;
+        zero16(s0);
+        zero16(p0);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8_t kf = lds_b128(kt + swz(32 * kh + r32, 2 * s + h));
+          const bf16x8_t vf = lds_b128(vt + swz(32 * kh + r32, 2 * s + h));
+          s0 = mfma32(kf, qf[s], s0);
+          p0 = mfma32(vf, dof[s], p0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float e0 = exp2f(fmaf(s0[r], c, -lse2));
+          if (diag && kv0 + 32 * kh + crow(r, h) > myq) e0 = 0.f;
+          s0[r] = e0 * (p0[r] - dlt);   // dS^T
+        }
+        bf16x8_t df[2];
+        df[0] = pack8(s0, 0);
+        df[1] = pack8(s0, 8);
+        // dQ^T += K^T . dS^T  (K^T by transposed reads of the K image)
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const int key = 32 * kh + 16 * kk + tr_key;
+            const int ch = 4 * db + tr_ch;
+            const bf16x4_t lo = lds_tr_b64(kt + swz(key, ch) + tr_byte);
+            const bf16x4_t hi = lds_tr_b64(kt + swz(key + 8, ch) + tr_byte);
+            bf16x8_t a;
+            a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+            a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+            acc[db] = mfma32(a, df[kk], acc[db]);
+          }
+        }
+      }
+    }
+    if (j + 1 < nkv) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+  uint16_t* row = dq + (static_cast<long>(b) * S + myq) * Hq * D + static_cast<long>(hq) * D;
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * db + 8 * g + 4 * h;
+      uint2 pk;
+      pk.x = mxk::pack2bf(acc[db][4 * g] * scale, acc[db][4 * g + 1] * scale);
+      pk.y = mxk::pack2bf(acc[db][4 * g + 2] * scale, acc[db][4 * g + 3] * scale);
+      *reinterpret_cast<uint2*>(row + d) = pk;
+    }
+  }
+}
+
+// dK/dV for 128 keys of one (batch, q-head); partials dk_p/dv_p are fp32
+// [B, S, Hq, 128] (summed over the GQA group afterwards).
+template <bool CAUSAL>
+__global__ void __launch_bounds__(NT, 1)
+mxk_attn_bwd_dkdv_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                         const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
+                         const float* __restrict__ lse, const float* __restrict__ delta,
+                         float* __restrict__ dk_p, float* __restrict__ dv_p, int S, int Hq,
+                         int Hkv, long q_tok, long k_tok, long v_tok, float scale) {
+  // [buf][Q tile 64x128 | dO tile 64x128] + lse/delta slices
+  __shared__ __attribute__((aligned(16))) char smem[2][2 * BQB * 256];
+  __shared__ __attribute__((aligned(16))) float srow[2][2][BQB];   // [buf][lse*log2e/c | delta]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  const int nkb = S / BQ;   // 128-key blocks
+  int bh, kb;
+  {
+    // key block kb has (nkb - kb) query blocks of work: heaviest = kb 0
+    int qbi;
+    map_block(blockIdx.x, gridDim.x / nkb, nkb, CAUSAL, &bh, &qbi);
+    kb = CAUSAL ? nkb - 1 - qbi : qbi;
+  }
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hkv = hq / (Hq / Hkv);
+  const int k0 = kb * BQ;
+  const int kw0 = k0 + wave * 32;
+  const int mykey = kw0 + r32;
+
+  const uint16_t* qb_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
+  const uint16_t* dob_ptr = dout + static_cast<long>(b) * S * Hq * D + static_cast<long>(hq) * D;
+  const uint16_t* kb_ptr = k + static_cast<long>(b) * S * k_tok + static_cast<long>(hkv) * D;
+  const uint16_t* vb_ptr = v + static_cast<long>(b) * S * v_tok + static_cast<long>(hkv) * D;
+  const float* lse_b = lse + (static_cast<long>(b) * Hq + hq) * S;
+  const float* dl_b = delta + (static_cast<long>(b) * Hq + hq) * S;
+
+  // K^T / V^T fragments (B operands of S = Q.K^T and dP = dO.V^T)
+  bf16x8_t kf[8], vf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8_t*>(kb_ptr + static_cast<long>(mykey) * k_tok + 16 * s + 8 * h);
+    vf[s] = *reinterpret_cast<const bf16x8_t*>(vb_ptr + static_cast<long>(mykey) * v_tok + 16 * s + 8 * h);
+  }
+  const float c = scale * 1.4426950408889634f;
+  const float inv_c = 1.f / c;
+
+  const int q_begin = CAUSAL ? k0 : 0;
+  const int nsl = (S - q_begin) / BQB;
+  const int ld_row = tid >> 4, ld_ch = tid & 15;
+  bf16x8_t qst[4], dst[4];
+  float rst = 0.f;
+  auto load_slice = [&](int t) {
+    const long r0 = q_begin + static_cast<long>(t) * BQB + ld_row;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      qst[i] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + (r0 + 16 * i) * q_tok + ld_ch * 8);
+      dst[i] = *reinterpret_cast<const bf16x8_t*>(dob_ptr + (r0 + 16 * i) * Hq * D + ld_ch * 8);
+    }
+    if (tid < 2 * BQB) {
+      const long qi = q_begin + static_cast<long>(t) * BQB + (tid & (BQB - 1));
+      rst = tid < BQB ? -lse_b[qi] * 1.4426950408889634f * inv_c : -dl_b[qi];
+    }
+  };
+  auto store_slice = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int off = swz(ld_row + 16 * i, ld_ch);
+      *reinterpret_cast<bf16x8_t*>(smem[buf] + off) = qst[i];
+      *reinterpret_cast<bf16x8_t*>(smem[buf] + BQB * 256 + off) = dst[i];
+    }
+    if (tid < 2 * BQB) srow[buf][tid / BQB][tid & (BQB - 1)] = rst;
+  };
+  load_slice(0);
+  store_slice(0);
+  __syncthreads();
+
+  f32x16_t dka[4], dva[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) { zero16(dka[db]); zero16(dva[db]); }
+  const int G = lane >> 4, i16 = lane & 15;
+  const int tr_row = 4 * h + (i16 >> 2);
+  const int tr_ch = 2 * (G & 1) + ((i16 & 3) >> 1);
+  const int tr_byte = 8 * (i16 & 1);
+
+  for (int t = 0; t < nsl; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nsl) load_slice(t + 1);
+    const int qs0 = q_begin + t * BQB;
+    if (!CAUSAL || qs0 + BQB - 1 >= kw0) {
+      const char* qt = smem[buf];
+      const char* dt = smem[buf] + BQB * 256;
+      // accumulator init: -LSE/scale (S) and -delta (dP) per query row
+      f32x16_t s0, s1, p0, p1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int qr = 8 * g + 4 * h;
+        const float4 l0 = *reinterpret_cast<const float4*>(&srow[buf][0][qr]);
+        const float4 l1 = *reinterpret_cast<const float4*>(&srow[buf][0][32 + qr]);
+        const float4 d0 = *reinterpret_cast<const float4*>(&srow[buf][1][qr]);
+        const float4 d1 = *reinterpret_cast<const float4*>(&srow[buf][1][32 + qr]);
+        s0[4 * g] = l0.x; s0[4 * g + 1] = l0.y; s0[4 * g + 2] = l0.z; s0[4 * g + 3] = l0.w;
+        s1[4 * g] = l1.x; s1[4 * g + 1] = l1.y; s1[4 * g + 2] = l1.z; s1[4 * g + 3] = l1.w;
+        p0[4 * g] = d0.x; p0[4 * g + 1] = d0.y; p0[4 * g + 2] = d0.z; p0[4 * g + 3] = d0.w;
+        p1[4 * g] = d1.x; p1[4 * g + 1] = d1.y; p1[4 * g + 2] = d1.z; p1[4 * g + 3] = d1.w;
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const bf16x8_t q0f = lds_b128(qt + swz(r32, 2 * s + h));
+        const bf16x8_t q1f = lds_b128(qt + swz(32 + r32, 2 * s + h));
+        const bf16x8_t o0f = lds_b128(dt + swz(r32, 2 * s + h));
+        const bf16x8_t o1f = lds_b128(dt + swz(32 + r32, 2 * s + h));
+        s0 = mfma32(q0f, kf[s], s0);
+        s1 = mfma32(q1f, kf[s], s1);
+        p0 = mfma32(o0f, vf[s], p0);
+        p1 = mfma32(o1f, vf[s], p1);
+      }
+      const bool diag = CAUSAL && qs0 < kw0 + 31;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = qs0 + crow(r, h);
+        float e0 = exp2f(s0[r] * c);
+        float e1 = exp2f(s1[r] * c);
+        if (diag && mykey > qi) e0 = 0.f;
+        if (diag && mykey > qi + 32) e1 = 0.f;
+        s0[r] = e0;                 // P
+        s1[r] = e1;
+        p0[r] = e0 * p0[r];         // dS = P (dP - delta)
+        p1[r] = e1 * p1[r];
+      }
+      bf16x8_t pf[4], sf[4];
+      pf[0] = pack8(s0, 0); pf[1] = pack8(s0, 8); pf[2] = pack8(s1, 0); pf[3] = pack8(s1, 8);
+      sf[0] = pack8(p0, 0); sf[1] = pack8(p0, 8); sf[2] = pack8(p1, 0); sf[3] = pack8(p1, 8);
+      // dV^T += dO^T . P ; dK^T += Q^T . dS   (transposed reads of dO / Q)
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int row = 16 * ks + tr_row;
+          const int ch = 4 * db + tr_ch;
+          const bf16x4_t olo = lds_tr_b64(dt + swz(row, ch) + tr_byte);
+          const bf16x4_t ohi = lds_tr_b64(dt + swz(row + 8, ch) + tr_byte);
+          const bf16x4_t qlo = lds_tr_b64(qt + swz(row, ch) + tr_byte);
+          const bf16x4_t qhi = lds_tr_b64(qt + swz(row + 8, ch) + tr_byte);
+          bf16x8_t ao, aq;
+          ao[0] = olo[0]; ao[1] = olo[1]; ao[2] = olo[2]; ao[3] = olo[3];
+          ao[4] = ohi[0]; ao[5] = ohi[1]; ao[6] = ohi[2]; ao[7] = ohi[3];
+          aq[0] = qlo[0]; aq[1] = qlo[1]; aq[2] = qlo[2]; aq[3] = qlo[3];
+          aq[4] = qhi[0]; aq[5] = qhi[1]; aq[6] = qhi[2]; aq[7] = qhi[3];
+          dva[db] = mfma32(ao, pf[ks], dva[db]);
+          dka[db] = mfma32(aq, sf[ks], dka[db]);
+        }
+      }
+    }
+    if (t + 1 < nsl) store_slice(buf ^ 1);
+    __syncthreads();
+  }
+  // partials: lane = key, registers = dims
+  const long prow = ((static_cast<long>(b) * S + mykey) * Hq + hq) * D;
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * db + 8 * g + 4 * h;
+      *reinterpret_cast<float4*>(dk_p + prow + d) =
+          make_float4(dka[db][4 * g] * scale, dka[db][4 * g + 1] * scale,
+                      dka[db][4 * g + 2] * scale, dka[db][4 * g + 3] * scale);
+      *reinterpret_cast<float4*>(dv_p + prow + d) =
+          make_float4(dva[db][4 * g], dva[db][4 * g + 1], dva[db][4 * g + 2], dva[db][4 * g + 3]);
+    }
+  }
+}
+
+// dk[b][s][hkv][:] = sum over the group's q-heads of dk_p[b][s][hq][:] (bf16 out)
+__global__ void __launch_bounds__(256)
+mxk_attn_bwd_gqa_reduce_kernel(const float* __restrict__ dk_p, const float* __restrict__ dv_p,
+                               uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, long n_out,
+                               int Hq, int Hkv, long dk_tok, long dv_tok) {
+  const long i = (static_cast<long>(blockIdx.x) * 256 + threadIdx.x) * 4;   // 4 dims per thread
+  if (i >= n_out) return;
+  const int grp = Hq / Hkv;
+  const int d = static_cast<int>(i % D);
+  const long t = i / D;               // (b*S + s)*Hkv + hkv
+  const int hkv = static_cast<int>(t % Hkv);
+  const long bs = t / Hkv;
+  float4 ak = make_float4(0.f, 0.f, 0.f, 0.f), av = ak;
+  for (int gq = 0; gq < grp; ++gq) {
+    const long src = (bs * Hq + hkv * grp + gq) * D + d;
+    const float4 x = *reinterpret_cast<const float4*>(dk_p + src);
+    const float4 y = *reinterpret_cast<const float4*>(dv_p + src);
+    ak.x += x.x; ak.y += x.y; ak.z += x.z; ak.w += x.w;
+    av.x += y.x; av.y += y.y; av.z += y.z; av.w += y.w;
+  }
+  uint2 pk;
+  pk.x = mxk::pack2bf(ak.x, ak.y);
+  pk.y = mxk::pack2bf(ak.z, ak.w);
+  *reinterpret_cast<uint2*>(dk + bs * dk_tok + hkv * D + d) = pk;
+  pk.x = mxk::pack2bf(av.x, av.y);
+  pk.y = mxk::pack2bf(av.z, av.w);
+  *reinterpret_cast<uint2*>(dv + bs * dv_tok + hkv * D + d) = pk;
+}
+
+// Workspace: delta [B*Hq*S] fp32 + dk/dv partials 2 x [B*S*Hq*128] fp32.
+MXK_API long mxk_attn_bwd_workspace(int B, int S, int Hq) {
+  const long rows = static_cast<long>(B) * Hq * S;
+  return rows * 4 + 2 * rows * D * 4;
+}
+
+// dout, o, dq: [B, S, Hq, 128] contiguous; dk/dv written at token strides
+// dk_tok/dv_tok (they may be views into one fused dQKV buffer).
+MXK_API int mxk_attn_bwd(const void* q, const void* k, const void* v, const void* o,
+                         const void* dout, const float* lse, void* dq, void* dk, void* dv,
+                         void* workspace, int B, int S, int Hq, int Hkv, int head_dim, long q_tok,
+                         long k_tok, long v_tok, long dk_tok, long dv_tok, float scale, int causal,
+                         hipStream_t stream) {
+  if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv || q_tok % 8 ||
+      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 ||
+      (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
+       reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
+       reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
+       reinterpret_cast<uintptr_t>(workspace)) % 16 ||
+      (reinterpret_cast<uintptr_t>(dk) | reinterpret_cast<uintptr_t>(dv)) % 8)
+    return static_cast<int>(hipErrorInvalidValue);
+  const long rows = static_cast<long>(B) * Hq * S;
+  float* delta = static_cast<float*>(workspace);
+  float* dk_p = delta + rows;
+  float* dv_p = dk_p + rows * D;
+  const auto* Q = static_cast<const uint16_t*>(q);
+  const auto* K = static_cast<const uint16_t*>(k);
+  const auto* V = static_cast<const uint16_t*>(v);
+  const auto* dO = static_cast<const uint16_t*>(dout);
+  hipLaunchKernelGGL(mxk_attn_bwd_delta_kernel, dim3((rows * 16 + 255) / 256), dim3(256), 0,
+                     stream, static_cast<const uint16_t*>(o), dO, delta, S, Hq, rows);
+  const int nwg = B * Hq * (S / BQ);
+  if (causal) {
+    hipLaunchKernelGGL(mxk_attn_bwd_dkdv_kernel<true>, dim3(nwg), dim3(NT), 0, stream, Q, K, V,
+                       dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    hipLaunchKernelGGL(mxk_attn_bwd_dq_kernel<true>, dim3(nwg), dim3(NT), 0, stream, Q, K, V, dO,
+                       lse, delta, static_cast<uint16_t*>(dq), S, Hq, Hkv, q_tok, k_tok, v_tok,
+                       scale);
+  } else {
+    hipLaunchKernelGGL(mxk_attn_bwd_dkdv_kernel<false>, dim3(nwg), dim3(NT), 0, stream, Q, K, V,
+                       dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    hipLaunchKernelGGL(mxk_attn_bwd_dq_kernel<false>, dim3(nwg), dim3(NT), 0, stream, Q, K, V,
+                       dO, lse, delta, static_cast<uint16_t*>(dq), S, Hq, Hkv, q_tok, k_tok,
+                       v_tok, scale);
+  }
+  const long n_out = static_cast<long>(B) * S * Hkv * D;
+  hipLaunchKernelGGL(mxk_attn_bwd_gqa_reduce_kernel, dim3((n_out / 4 + 255) / 256), dim3(256), 0,
+                     stream, dk_p, dv_p, static_cast<uint16_t*>(dk), static_cast<uint16_t*>(dv),
+                     n_out, Hq, Hkv, dk_tok, dv_tok);
+  MXK_RETURN_LAUNCH_STATUS();
+}

@@ -44,9 +44,23 @@ def main():
     with torch.no_grad():
         res["sdpa_fwd"] = bench(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=True,
                                                                       enable_gqa=True))
+    o, lse = A.attn_fwd(q, k, v, causal=True)
+    do = torch.randn_like(o)
+    res["mxk_bwd"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True))
+    qg, kg, vg = (t.detach().transpose(1, 2).requires_grad_() for t in (q, k, v))
+    dot = do.transpose(1, 2)
+
+    def sdpa_fb():
+        out = F.scaled_dot_product_attention(qg, kg, vg, is_causal=True, enable_gqa=True)
+        out.backward(dot)
+    res["sdpa_fwd_bwd"] = bench(sdpa_fb)
+    res["mxk_fwd_bwd"] = res["mxk_fwd"] + res["mxk_bwd"]
+    # useful FLOPs: fwd 2 products, bwd 5 products (causal halves all)
+    mult = {"mxk_fwd": 1.0, "sdpa_fwd": 1.0, "mxk_bwd": 2.5, "sdpa_fwd_bwd": 3.5, "mxk_fwd_bwd": 3.5}
     for name, ms in res.items():
         print("RESULT " + json.dumps({"kernel": name, "ms": round(ms, 4), "S": S,
-                                      "tflops": round(flops_fwd / ms / 1e9, 1)}), flush=True)
+                                      "tflops": round(mult[name] * flops_fwd / ms / 1e9, 1)}),
+              flush=True)
 
 
 if __name__ == "__main__":

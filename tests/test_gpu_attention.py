@@ -42,3 +42,26 @@ def test_attn_fwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
     if causal:
         s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=cuda_device).triu(1), float("-inf"))
     assert torch.allclose(lse, torch.logsumexp(s, dim=-1), atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal,fused", [
+    (1, 128, 2, 1, True, False),
+    (2, 256, 4, 2, True, True),
+    (1, 512, 8, 2, True, False),
+    (1, 256, 4, 4, False, False),
+])
+def test_attn_bwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
+    q, k, v = _qkv(B, S, Hq, Hkv, cuda_device, seed=1, fused=fused)
+    g = torch.Generator(device=cuda_device).manual_seed(7)
+    dout = torch.randn(B, S, Hq, 128, device=cuda_device, generator=g).bfloat16()
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    ref = A.attention_ref(qr, kr, vr, causal=causal)
+    ref.backward(dout.float())
+    qh, kh, vh = (t.detach().clone().requires_grad_() for t in (q, k, v))
+    out = A.flash_attention(qh, kh, vh, causal=causal)
+    out.backward(dout)
+    for name, got, want in (("dq", qh.grad, qr.grad), ("dk", kh.grad, kr.grad),
+                            ("dv", vh.grad, vr.grad)):
+        err = (got.float() - want).abs().max().item()
+        tol = 3e-2 * max(1.0, want.abs().max().item())
+        assert err < tol, (name, err, tol)
