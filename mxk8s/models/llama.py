@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.attention import flash_attention, supported as flash_supported
+from ..ops.linear import Linear
 from ..ops.fused import add_rmsnorm, rmsnorm, rope, rope_tables, swiglu
 
 
@@ -82,8 +83,8 @@ class Attention(nn.Module):
         super().__init__()
         self.cfg = cfg
         hd = cfg.head_dim
-        self.wqkv = nn.Linear(cfg.dim, (cfg.n_heads + 2 * cfg.n_kv_heads) * hd, bias=False)
-        self.wo = nn.Linear(cfg.n_heads * hd, cfg.dim, bias=False)
+        self.wqkv = Linear(cfg.dim, (cfg.n_heads + 2 * cfg.n_kv_heads) * hd)
+        self.wo = Linear(cfg.n_heads * hd, cfg.dim)
 
     def forward(self, x, cos, sin):
         B, S, _ = x.shape
@@ -106,8 +107,8 @@ class Attention(nn.Module):
 class MLP(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
-        self.w13 = nn.Linear(cfg.dim, 2 * cfg.ffn_dim, bias=False)   # [gate | up]
-        self.w2 = nn.Linear(cfg.ffn_dim, cfg.dim, bias=False)
+        self.w13 = Linear(cfg.dim, 2 * cfg.ffn_dim)   # [gate | up]
+        self.w2 = Linear(cfg.ffn_dim, cfg.dim)
 
     def forward(self, x):
         return self.w2(swiglu(self.w13(x)))
@@ -139,7 +140,7 @@ class Llama(nn.Module):
         self.embed = nn.Embedding(cfg.vocab_size, cfg.dim)
         self.layers = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layers)])
         self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
-        self.lm_head = nn.Linear(cfg.dim, cfg.vocab_size, bias=False)
+        self.lm_head = Linear(cfg.dim, cfg.vocab_size)
         self._rope = {}   # device -> (cos, sin) fp32 tables, never cast with the model
         self.reset_parameters()
 

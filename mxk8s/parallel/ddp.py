@@ -93,12 +93,41 @@ class FlatParamSpace:
                 view.copy_(p.detach().to(self.dtype))
                 p.data = view
                 p.grad = self.grad_buf[o:o + p.numel()].view_as(p)
+                # direct-gradient params (mxk8s.ops.linear.Linear) write dW
+                # into main_grad themselves: overwrite while fresh, then add
+                p.main_grad = p.grad
+                p._mxk_grad_fresh = True
+        # zero_grad memsets only the ranges autograd ACCUMULATES into
+        # (embedding, norms); direct-gradient weights just get marked fresh
+        self._accum_ranges = self._merge(
+            [(o, o + p.numel()) for p, o in zip(order, self.offsets)
+             if not getattr(p, "_mxk_direct_grad", False)])
+        self.grad_buf.zero_()
+
+    @staticmethod
+    def _merge(ranges):
+        out = []
+        for a, b in sorted(ranges):
+            if out and a <= (out[-1][1] + ALIGN - 1) // ALIGN * ALIGN:
+                out[-1] = (out[-1][0], max(out[-1][1], b))
+            else:
+                out.append((a, b))
+        return out
 
     def zero_grad(self) -> None:
-        self.grad_buf.zero_()
-        for p, o in zip(self.params, self.offsets):   # re-attach if someone set None
+        for a, b in self._accum_ranges:
+            self.grad_buf[a:b].zero_()
+        for p, o in zip(self.params, self.offsets):
+            p._mxk_grad_fresh = True
             if p.grad is None or p.grad.data_ptr() != self.grad_buf[o:].data_ptr():
-                p.grad = self.grad_buf[o:o + p.numel()].view_as(p)
+                p.grad = self.grad_buf[o:o + p.numel()].view_as(p)   # re-attach if set to None
+
+    def zero_stale_direct(self) -> None:
+        """Zero direct-gradient weights that received no gradient this step."""
+        for p in self.params:
+            if getattr(p, "_mxk_direct_grad", False) and p._mxk_grad_fresh:
+                p.main_grad.zero_()
+                p._mxk_grad_fresh = False
 
 
 class Bucket:
@@ -155,7 +184,10 @@ class FlatDDP:
             if broadcast_from is not None:
                 dist.broadcast(self.space.param_buf, src=broadcast_from, group=process_group)
             for p in self.space.params:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                if getattr(p, "_mxk_direct_grad", False):
+                    p._mxk_grad_ready = (lambda p=p: self._on_grad(p))
+                else:
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
         self._reset_buckets()
 
     def shard_range(self, b: Bucket) -> tuple[int, int]:
@@ -203,6 +235,7 @@ class FlatDDP:
 
     def finish_grad_sync(self) -> None:
         """Launch any bucket that did not complete (unused params) and wait."""
+        self.space.zero_stale_direct()
         if self.world > 1:
             for b in self.buckets:
                 if not b.launched:

@@ -90,7 +90,13 @@ def test_flat_space_views_and_grad_accumulation():
     model.loss(tok).backward()   # accumulates in place into the flat buffer
     assert torch.allclose(space.grad_buf, 2 * g1, rtol=1e-5, atol=1e-7)
     space.zero_grad()
-    assert space.grad_buf.abs().sum() == 0
+    # accumulated ranges (embedding, norms) are zeroed; direct-gradient
+    # weights (mxk8s.ops.linear.Linear) are marked fresh instead of memset
+    for a, b in space._accum_ranges:
+        assert space.grad_buf[a:b].abs().sum() == 0
+    assert all(p._mxk_grad_fresh for p in space.params)
+    model.loss(tok).backward()   # fresh -> overwrite, not accumulate
+    assert torch.allclose(space.grad_buf, g1, rtol=1e-5, atol=1e-7)
 
 
 def test_flat_adamw_matches_torch_adamw():
