@@ -126,7 +126,7 @@ def minimal_containerd_config(version: int = 2) -> str:
 # --------------------------------------------------------------------------
 
 def kubeadm_config(node_name: str = "", advertise_address: str = "",
-                   k8s_version: str = K8S_VERSION) -> str:
+                   k8s_version: str = K8S_VERSION, pod_cidr: str = POD_CIDR) -> str:
     init = {"apiVersion": "kubeadm.k8s.io/v1beta4", "kind": "InitConfiguration",
             "nodeRegistration": {"criSocket": CRI_SOCKET,
                                  # untaint up front: single-node cluster (the
@@ -138,12 +138,17 @@ def kubeadm_config(node_name: str = "", advertise_address: str = "",
         init["localAPIEndpoint"] = {"advertiseAddress": advertise_address, "bindPort": 6443}
     cluster = {"apiVersion": "kubeadm.k8s.io/v1beta4", "kind": "ClusterConfiguration",
                "kubernetesVersion": k8s_version,
-               "networking": {"podSubnet": POD_CIDR, "serviceSubnet": "10.96.0.0/12"}}
+               "networking": {"podSubnet": pod_cidr, "serviceSubnet": "10.96.0.0/12"}}
     kubelet = {"apiVersion": "kubelet.config.k8s.io/v1beta1", "kind": "KubeletConfiguration",
                "cgroupDriver": "systemd",
                # Topology Manager uses the NUMA nodes our device plugin reports
                "topologyManagerPolicy": "best-effort"}
     return "---\n".join(yaml.safe_dump(d, sort_keys=False) for d in (init, cluster, kubelet))
+
+
+def k8s_minor(version: str) -> str:
+    """v1.34.1 -> v1.34 (the pkgs.k8s.io repository path)."""
+    return ".".join(version.split(".")[:2])
 
 
 def kubernetes_apt_source(minor: str = K8S_MINOR) -> str:

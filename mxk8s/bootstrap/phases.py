@@ -42,6 +42,8 @@ class Context:
     upgrade: bool = False
     node_name: str = ""
     advertise_address: str = ""
+    pod_cidr: str = hf.POD_CIDR
+    kubernetes_version: str = hf.K8S_VERSION
     kubeconfig_home: str = os.path.expanduser("~")
     repo: str = REPO
     actions: list = dataclasses.field(default_factory=list)
@@ -185,9 +187,9 @@ def phase_k8s_packages(ctx: Context) -> None:
     ctx.run("apt-get install -y apt-transport-https ca-certificates curl gpg")
     ctx.run("mkdir -p -m 755 /etc/apt/keyrings")
     ctx.run(["bash", "-c",
-             f"curl -fsSL https://pkgs.k8s.io/core:/stable:/{hf.K8S_MINOR}/deb/Release.key | "
+             f"curl -fsSL https://pkgs.k8s.io/core:/stable:/{hf.k8s_minor(ctx.kubernetes_version)}/deb/Release.key | "
              "gpg --dearmor -o /etc/apt/keyrings/kubernetes-apt-keyring.gpg"])
-    ctx.write("/etc/apt/sources.list.d/kubernetes.list", hf.kubernetes_apt_source())
+    ctx.write("/etc/apt/sources.list.d/kubernetes.list", hf.kubernetes_apt_source(hf.k8s_minor(ctx.kubernetes_version)))
     ctx.run("apt-get update")
     ctx.run("apt-get install -y kubelet kubeadm kubectl")
     ctx.run("apt-mark hold kubelet kubeadm kubectl")
@@ -201,7 +203,8 @@ def _kubectl(ctx: Context, *args: str, check: bool = True, capture: bool = False
 
 def phase_cluster(ctx: Context) -> None:
     ctx.write("/etc/mxk8s/kubeadm-config.yaml",
-              hf.kubeadm_config(ctx.node_name, ctx.advertise_address))
+              hf.kubeadm_config(ctx.node_name, ctx.advertise_address, ctx.kubernetes_version,
+                                ctx.pod_cidr))
     if not ctx.exists("/etc/kubernetes/admin.conf") or ctx.dry_run:
         ctx.run(["kubeadm", "init", "--config", ctx.path("/etc/mxk8s/kubeadm-config.yaml")])
     home = ctx.kubeconfig_home
@@ -212,7 +215,14 @@ def phase_cluster(ctx: Context) -> None:
     # single node: remove the control-plane taint (kubeadm config already sets
     # taints: [], this also fixes clusters initialised without our config)
     _kubectl(ctx, "taint", "nodes", "--all", "node-role.kubernetes.io/control-plane-", check=False)
-    _kubectl(ctx, "apply", "-f", os.path.join(ctx.repo, "deploy", "cni", "kube-flannel.yaml"))
+    flannel = os.path.join(ctx.repo, "deploy", "cni", "kube-flannel.yaml")
+    if ctx.pod_cidr != hf.POD_CIDR:
+        # Flannel's net-conf must carry the same pod CIDR as kubeadm
+        with open(flannel) as f:
+            text = f.read().replace(f'"Network": "{hf.POD_CIDR}"', f'"Network": "{ctx.pod_cidr}"')
+        ctx.write("/etc/mxk8s/kube-flannel.yaml", text)
+        flannel = ctx.path("/etc/mxk8s/kube-flannel.yaml")
+    _kubectl(ctx, "apply", "-f", flannel)
     _kubectl(ctx, "-n", "kube-flannel", "rollout", "status", "ds/kube-flannel-ds", "--timeout=300s")
     _kubectl(ctx, "wait", "node", "--all", "--for=condition=Ready", "--timeout=300s")
 

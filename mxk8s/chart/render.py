@@ -39,9 +39,24 @@ def _parse_scalar(v: str) -> Any:
         return v
 
 
+def _split_top(expr: str) -> list[str]:
+    """Split on commas outside ``{...}`` (Helm list syntax ``k={a,b}``)."""
+    out, depth, cur = [], 0, ""
+    for ch in expr:
+        if ch == "," and depth == 0:
+            out.append(cur)
+            cur = ""
+            continue
+        depth += ch == "{"
+        depth -= ch == "}"
+        cur += ch
+    out.append(cur)
+    return out
+
+
 def apply_set(values: dict, expr: str) -> None:
-    """Helm ``--set a.b.c=v`` (comma-separated list allowed)."""
-    for item in expr.split(","):
+    """Helm ``--set a.b.c=v`` (comma-separated assignments, ``{x,y}`` lists)."""
+    for item in _split_top(expr):
         if not item:
             continue
         key, _, val = item.partition("=")
@@ -52,7 +67,7 @@ def apply_set(values: dict, expr: str) -> None:
                 d[p] = {}
             d = d[p]
         if val.startswith("{") and val.endswith("}"):
-            d[parts[-1]] = [_parse_scalar(x) for x in val[1:-1].split(";") if x]
+            d[parts[-1]] = [_parse_scalar(x) for x in val[1:-1].split(",") if x]
         else:
             d[parts[-1]] = _parse_scalar(val)
 

@@ -1,6 +1,6 @@
 """``mxk8s`` command line.
 
-  mxk8s bootstrap [--phase P ...] [--all] [--dry-run] [--root DIR] [--upgrade]
+  mxk8s bootstrap [--config mxk8s.toml] [--phase P ...] [--all] [--dry-run] [--root DIR] [--upgrade]
   mxk8s doctor {gpu,node,pod NAME [-n NS]} [--root DIR]
   mxk8s render [--set k=v] [-f values.yaml] [-n NS] [-o FILE]     (offline helm template)
   mxk8s cdi [--root DIR] [--output FILE]                           (ROCm CDI spec)
@@ -14,13 +14,24 @@ from __future__ import annotations
 import argparse
 import dataclasses
 import json
+import os
 import sys
 
 
 def _bootstrap(a) -> int:
+    from . import config
     from .bootstrap import phases
-    ctx = phases.Context(root=a.root, dry_run=a.dry_run, upgrade=a.upgrade,
-                         node_name=a.node_name, advertise_address=a.advertise_address)
+    try:
+        cfg = config.load_bootstrap(a.config, overrides={
+            "root": a.root, "dry_run": a.dry_run or None, "upgrade": a.upgrade or None,
+            "node_name": a.node_name, "advertise_address": a.advertise_address,
+            "pod_cidr": a.pod_cidr, "kubernetes_version": a.kubernetes_version})
+    except (ValueError, OSError) as e:
+        print(f"bootstrap config: {e}", file=sys.stderr)
+        return 2
+    ctx = phases.Context(root=cfg["root"], dry_run=cfg["dry_run"], upgrade=cfg["upgrade"],
+                         node_name=cfg["node_name"], advertise_address=cfg["advertise_address"],
+                         pod_cidr=cfg["pod_cidr"], kubernetes_version=cfg["kubernetes_version"])
     only = a.phase or None
     try:
         ran = phases.run(ctx, only=only, resume=not a.no_resume, until=a.until)
@@ -52,8 +63,14 @@ def _doctor(a) -> int:
 def _render(a) -> int:
     from .chart import render
     from .chart.gotpl import FailError
+    from . import config
     try:
         values = render.load_values(a.chart, a.values, a.set)
+        errs = config.validate_values(values)
+        if errs:
+            print("Error: values don't meet the specifications of the schema(s):\n- "
+                  + "\n- ".join(errs), file=sys.stderr)
+            return 1
         text = render.to_stream(render.render(values, a.namespace, a.release, a.chart))
     except FailError as e:
         print(f"Error: execution error: {e}", file=sys.stderr)
@@ -104,12 +121,16 @@ def main(argv=None) -> int:
     b.add_argument("--phase", action="append", help="run only these phases")
     b.add_argument("--all", action="store_true", help="run every phase (default)")
     b.add_argument("--until", default=None, help="stop after this phase")
+    b.add_argument("--config", default=os.environ.get("MXK8S_CONFIG"),
+                   help="mxk8s.toml with a [bootstrap] table (see mxk8s.config)")
     b.add_argument("--dry-run", action="store_true")
-    b.add_argument("--root", default="/")
+    b.add_argument("--root", default=None)
     b.add_argument("--upgrade", action="store_true")
     b.add_argument("--no-resume", action="store_true")
-    b.add_argument("--node-name", default="")
-    b.add_argument("--advertise-address", default="")
+    b.add_argument("--node-name", default=None)
+    b.add_argument("--advertise-address", default=None)
+    b.add_argument("--pod-cidr", default=None)
+    b.add_argument("--kubernetes-version", default=None)
     d = sub.add_parser("doctor", help="troubleshooting decision trees")
     d.add_argument("what", choices=["gpu", "node", "pod"])
     d.add_argument("name", nargs="?")
