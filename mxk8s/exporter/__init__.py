@@ -11,6 +11,7 @@ driver:
   amd_gpu_temperature_celsius{sensor}    amd_gpu_power_watts / _power_limit_watts
   amd_gpu_clock_mhz{type=sclk|mclk}      amd_gpu_ecc_errors_total{type}
   amd_gpu_processes                      amd_gpu_xgmi_links
+  amd_gpu_link_up{peer,type=xgmi|pcie}   amd_gpu_link_max_bandwidth_bytes{peer,type}
   amd_gpu_device_healthy                 amd_gpu_info{arch,product,uuid,bdf,...}
   amd_gpu_stack_component_up{component}  amd_gpu_exporter_sample_seconds
 
@@ -85,10 +86,17 @@ class SmiBackend:
     def health(self, index: int) -> int:
         return node.health_check(index, self.sysfs_root, os.environ.get("MXK8S_FAULT_FILE"))
 
+    def links(self) -> list:
+        return node.links(self.sysfs_root)
+
 
 def render_metrics(gpus, samples: dict, health: Callable[[int], int], owners: dict,
-                   driver: str, components: dict, sample_seconds: float) -> str:
+                   driver: str, components: dict, sample_seconds: float,
+                   links: Optional[list] = None) -> str:
     w = MetricWriter()
+    by_gpu: dict = {}
+    for l in links or []:
+        by_gpu.setdefault(l.from_index, []).append(l)
     for g in gpus:
         base = {"gpu": str(g.index), "bdf": g.bdf, "uuid": g.uuid}
         own = owners.get(str(g.index))
@@ -101,6 +109,16 @@ def render_metrics(gpus, samples: dict, health: Callable[[int], int], owners: di
         w.add("amd_gpu_device_healthy", "gauge", "1 if the device plugin would report Healthy.",
               1 if h == 0 else 0, base)
         w.add("amd_gpu_xgmi_links", "gauge", "xGMI links of the GPU (KFD topology).", g.xgmi_links, base)
+        for l in by_gpu.get(g.index, []):
+            kind = "xgmi" if l.is_xgmi else "pcie" if l.type == node.LINK_PCIE else str(l.type)
+            peer = str(l.to_index) if l.to_index >= 0 else "cpu"
+            lab = {**base, "peer": peer, "type": kind}
+            # a link listed in the KFD topology is trained and usable
+            w.add("amd_gpu_link_up", "gauge", "1 for every GPU link in the KFD topology.", 1, lab)
+            if l.max_bandwidth_mbps:
+                w.add("amd_gpu_link_max_bandwidth_bytes", "gauge",
+                      "Link bandwidth advertised by KFD (bytes/s).",
+                      int(l.max_bandwidth_mbps) * 125000, lab)
         s = samples.get(g.bdf)
         if s is None:
             continue
@@ -168,9 +186,11 @@ class Exporter:
                 owners = gpu_owners(self.cfg.pod_resources_socket)
             except Exception as e:   # kubelet busy/old: metrics without pod labels
                 log.debug("pod-resources unavailable: %s", e)
+        links_fn = getattr(self.backend, "links", None)
+        links = links_fn() if links_fn else []
         text = render_metrics(gpus, samples, self.backend.health, owners,
                               getattr(self.backend, "driver", ""), self.components(),
-                              time.perf_counter() - t0)
+                              time.perf_counter() - t0, links)
         with self._lock:
             self._text = text
         self.samples_taken += 1

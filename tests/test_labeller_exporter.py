@@ -154,3 +154,14 @@ def test_exporter_http_and_pod_resources():
             ex.stop()
     finally:
         srv.stop(0)
+
+
+def test_link_metrics_from_kfd_topology():
+    root = os.path.join(FX, "mi355x_8gpu")
+    g = node.enumerate_gpus(root)
+    text = render_metrics(g, {}, lambda i: 0, {}, "", {}, 0.0, node.links(root))
+    up = [l for l in text.splitlines() if l.startswith("amd_gpu_link_up{")]
+    assert len([l for l in up if 'type="xgmi"' in l]) == 56          # 8 GPUs x 7 peers
+    assert len([l for l in up if 'type="pcie"' in l]) == 8
+    assert 'amd_gpu_link_up{gpu="0",bdf="0000:05:00.0",uuid="GPU-f4071d07e8ac5500",peer="7",type="xgmi"} 1' in text
+    assert "# TYPE amd_gpu_link_max_bandwidth_bytes gauge" in text
