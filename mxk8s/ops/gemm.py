@@ -55,3 +55,28 @@ def is_fast_shape(M: int, N: int, K: int) -> bool:
 
 def gemm_flops(M: int, N: int, K: int) -> float:
     return 2.0 * M * N * K
+
+
+def gemm_bf16_ex(a: torch.Tensor, b: torch.Tensor, a_kmajor: bool, b_kmajor: bool,
+                 out: torch.Tensor) -> bool:
+    """``out[M][N] = A . B`` on the layout-generic MFMA kernel
+    (``native/kernels/gemm_bf16_layouts.hip``).
+
+    ``a`` is [M, K] if ``a_kmajor`` else [K, M]; ``b`` is [N, K] if
+    ``b_kmajor`` else [K, N]; all row-major with unit inner stride, bf16.
+    Returns False (nothing launched) when the shape does not tile exactly
+    (M, N multiples of 256, K of 64) so the caller can use the library GEMM."""
+    if a.dim() != 2 or b.dim() != 2 or a.stride(1) != 1 or b.stride(1) != 1 or \
+            out.stride(1) != 1 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        return False
+    M, K = (a.shape if a_kmajor else (a.shape[1], a.shape[0]))
+    N, K2 = (b.shape if b_kmajor else (b.shape[1], b.shape[0]))
+    if K != K2 or tuple(out.shape) != (M, N) or not is_fast_shape(M, N, K):
+        return False
+    st = _lib.lib().mxk_gemm_bf16_ex(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K,
+                                     a.stride(0), b.stride(0), out.stride(0), int(a_kmajor),
+                                     int(b_kmajor), _lib.stream_ptr(a.device))
+    if st == 1:   # hipErrorInvalidValue: layout/stride limits -> library GEMM
+        return False
+    _lib.check(st, "mxk_gemm_bf16_ex")
+    return True

@@ -12,8 +12,24 @@ post-accumulate-grad hook plays for other parameters).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
+
+from .gemm import gemm_bf16_ex
+
+# dW = dy^T x has both operands token-major ("NT"): the hand-written
+# layout-generic MFMA kernel beats hipBLASLt there (profiles/r1_gemm_layouts:
+# +10-29 % on the Llama-3-8B wo/w13/w2 shapes); MXK_WGRAD=0 selects hipBLASLt.
+_USE_MXK_WGRAD = os.environ.get("MXK_WGRAD", "1") != "0"
+
+
+def _wgrad_into(sink: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
+    if _USE_MXK_WGRAD and sink.is_cuda and dy2.is_contiguous() and x2.is_contiguous() and \
+            gemm_bf16_ex(dy2, x2, False, False, sink):
+        return
+    torch.matmul(dy2.t(), x2, out=sink)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -34,7 +50,7 @@ class _LinearFn(torch.autograd.Function):
         if sink is None:
             return dx, torch.matmul(dy2.t(), x2)
         if weight._mxk_grad_fresh:
-            torch.matmul(dy2.t(), x2, out=sink)
+            _wgrad_into(sink, dy2, x2)
             weight._mxk_grad_fresh = False
         else:
             sink.addmm_(dy2.t(), x2)

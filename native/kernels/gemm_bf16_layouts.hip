@@ -1,0 +1,299 @@
+// CDNA4 bf16 MFMA GEMM for every operand layout of a linear layer's training
+// step:  C[M][N] (bf16) = sum_k A(m, k) B(k, n), fp32 accumulation.
+//
+//   forward  y  = x  W^T : A = x  [M][K] (K-major), B = W  [N][K] (K-major)
+//   dgrad    dx = dy W   : A = dy [M][K] (K-major), B = W  [K][N] (N-major)
+//   wgrad    dW = dy^T x : A = dy [K][M] (M-major), B = x  [K][N] (N-major)
+//
+// hipBLASLt runs the N-major ("NT"/"NN") layouts of the Llama-3-8B step at
+// 970-1280 TF/s against ~1590 for the K-major forward GEMMs (profiles/r1_ddp),
+// so the backward GEMMs get the same 4-wave BK=64 LDS-DMA schedule as
+// gemm_bf16.hip's w4b kernel with an operand-layout template:
+//
+// * K-major operand: LDS-DMA pieces of 8 rows x 128 B, 16-B chunk c of row r
+//   at c ^ ((r>>1)&7), fragments by ds_read_b128 (as w4b).
+// * N/M-major operand: the stage is 64 k-rows x 256 columns (512 B per row);
+//   a DMA piece is 2 k-rows, rows grouped by 8 with a 128-B pad per group
+//   (group stride 4224 B) and chunk c of row k at c ^ 2(k&3).  Fragments are
+//   the transposed reads ds_read_b64_tr_b16 (two per 16x16x32 operand), which
+//   deliver 8 consecutive k of one column exactly like a ds_read_b128 of a
+//   K-major row - so both kinds mix in one MFMA.  The pad puts the two 16-lane
+//   groups of each half-wave (rows k and k+8) on disjoint bank halves and the
+//   XOR separates the four rows of a group: conflict-free
+//   (tests/test_gemm_layouts.py).
+// LDS: 2 stages x (A + B) <= 132 KiB, one 4-wave workgroup per CU, 128x128
+// AGPR accumulators per wave, one barrier per 64-deep stage.
+#include "mx_common.h"
+
+namespace {
+constexpr int XT = 256;          // threads (4 waves)
+constexpr int XBM = 256;         // macro tile M = N = 256
+constexpr int XBK = 64;          // k per stage
+constexpr int XGROUP_M = 8;
+constexpr int TGROUP = 4224;     // bytes per 8 k-rows (4096 + 128 pad)
+constexpr int KSTEP_T = 4 * TGROUP;   // 32 k-rows
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void xmfma(f32x4_t& acc, bf16x8_t a, bf16x8_t b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// LDS-DMA piece (16 B per lane, `buffer_load_dwordx4 ... offen lds`) issued
+// through inline asm: the compiler then sees no pending LDS write, so it does
+// not put an `s_waitcnt vmcnt(0)` in front of every ds_read_b64_tr_b16 (it
+// cannot prove the transposed reads do not alias the DMA and serialises
+// them, 2-4x slower).  Ordering is ours: counted vmcnt + s_barrier below.
+// M0 is compiler-owned: saved and restored around the load.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 make_rsrc(const void* base, unsigned bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  u32x4 r;
+  r[0] = static_cast<unsigned>(a);
+  r[1] = static_cast<unsigned>(a >> 32);   // stride 0
+  r[2] = bytes;                            // num_records
+  r[3] = 0x00020000u;
+  return r;
+}
+__device__ __forceinline__ void dma16(const u32x4& rsrc, const char* lds, uint32_t voff,
+                                      uint32_t soff) {
+  const uint32_t m = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds)));
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(m), "v"(voff), "s"(rsrc), "s"(soff)
+      : "memory");
+}
+
+__device__ __forceinline__ bf16x4_t tr_b64(const char* p) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s4*)(reinterpret_cast<uintptr_t>(p)));
+}
+
+template <bool NMAJOR>
+struct XOp;
+
+// K-major operand [rows][K]: identical to the w4b kernel's operand.
+template <>
+struct XOp<false> {
+  static constexpr int BYTES = 256 * 128;
+  u32x4 rsrc;
+  uint32_t lane_off, piece_stride;
+  int off0, off1;
+  __device__ __forceinline__ void init(const uint16_t* src, int ld, int row0, int K, int lane,
+                                       int wave) {
+    rsrc = make_rsrc(src + static_cast<size_t>(row0) * ld, 256u * ld * 2u);
+    const int r = lane >> 3;
+    const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & 7);
+    lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
+    piece_stride = static_cast<uint32_t>(8 * ld * 2);
+    const int frow = lane & 15;
+    const int fch = (lane >> 4) ^ (frow >> 1);
+    off0 = frow * 128 + fch * 16;
+    off1 = frow * 128 + (fch ^ 4) * 16;
+    (void)K;
+  }
+  __device__ __forceinline__ void issue(char* lds, int p, int kstage, int wave) const {
+    const int g = p * 4 + wave;
+    dma16(rsrc, lds + g * 1024, lane_off, kstage * (XBK * 2) + g * piece_stride);
+  }
+  // fragment of 16-row subtile i (i = 0..15 over the 256 rows), k-step ks
+  __device__ __forceinline__ bf16x8_t frag(const char* lds, int i, int ks) const {
+    return *reinterpret_cast<const bf16x8_t*>(lds + i * 2048 + (ks ? off1 : off0));
+  }
+};
+
+// N/M-major operand [K][cols]: 64 k-rows x 256 columns per stage.
+template <>
+struct XOp<true> {
+  static constexpr int BYTES = 8 * TGROUP;
+  u32x4 rsrc;
+  uint32_t lane_off, piece_stride, kstride;
+  int base_off, qx;
+  __device__ __forceinline__ void init(const uint16_t* src, int ld, int col0, int K, int lane,
+                                       int wave) {
+    rsrc = make_rsrc(src + col0, static_cast<unsigned>(K) * ld * 2u);
+    // piece g = 4p + wave holds k-rows 8p + 2 wave + h (h = lane >> 5)
+    const int h = lane >> 5, slot = lane & 31;
+    const int c = slot ^ (2 * ((2 * wave + h) & 3));
+    lane_off = static_cast<uint32_t>(h * ld * 2 + c * 16);
+    piece_stride = static_cast<uint32_t>(2 * ld * 2);
+    kstride = static_cast<uint32_t>(XBK * ld * 2);
+    // transposed-read lane constants: group G, row q, column pair b, half-chunk
+    const int G = lane >> 4, i16 = lane & 15, q = i16 >> 2;
+    base_off = G * TGROUP + q * 512 + ((i16 & 3) >> 1) * 16 + 8 * (i16 & 1);
+    qx = 32 * q;
+  }
+  __device__ __forceinline__ void issue(char* lds, int p, int kstage, int wave) const {
+    const int g = p * 4 + wave;
+    dma16(rsrc, lds + p * TGROUP + wave * 1024, lane_off, kstage * kstride + g * piece_stride);
+  }
+  __device__ __forceinline__ bf16x8_t frag(const char* lds, int i, int ks) const {
+    const char* p = lds + base_off + ks * KSTEP_T + ((32 * i) ^ qx);
+    const bf16x4_t lo = tr_b64(p);
+    const bf16x4_t hi = tr_b64(p + 2048);
+    bf16x8_t a;
+    a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+    a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+    return a;
+  }
+};
+}  // namespace
+
+template <bool AN, bool BN>
+__global__ void __launch_bounds__(XT, 1)
+mxk_gemm_bf16_x_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                       uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  constexpr int A_BYTES = XOp<AN>::BYTES;
+  constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1;
+  const int wn = wave & 1;
+
+  const int tiles_m = M / XBM, tiles_n = N / XBM;
+  const int wgid = mxk::xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = XGROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * XGROUP_M;
+  const int gsize = min(tiles_m - first_m, XGROUP_M);
+  const int in_group = wgid - group * per_group;
+  const int m0 = (first_m + in_group % gsize) * XBM;
+  const int n0 = (in_group / gsize) * XBM;
+
+  XOp<AN> oa;
+  XOp<BN> ob;
+  oa.init(A, lda, m0, K, lane, wave);
+  ob.init(B, ldb, n0, K, lane, wave);
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / XBK;
+  auto kst = [&](int st) { return st < ns ? st : ns - 1; };
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    char* buf = smem + s * STAGE;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      oa.issue(buf, p, kst(s), wave);
+      ob.issue(buf + A_BYTES, p, kst(s), wave);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // own pieces of stage 0 landed
+  __builtin_amdgcn_s_barrier();
+
+  // wave (wm, wn) owns subtiles wm*8 .. wm*8+7 of A and wn*8 .. of B
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f0a[i] = oa.frag(smem, wm * 8 + i, 0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f0b[j] = ob.frag(smem + A_BYTES, wn * 8 + j, 0);
+
+  for (int s = 0; s < ns; ++s) {
+    char* cur = smem + (s & 1) * STAGE;
+    char* nxt = smem + ((s + 1) & 1) * STAGE;
+    // ---- k-step s.0: MFMAs on set 0, prefetch set 1 from `cur`
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xmfma(acc[i][j], f0b[j], f0a[i]);
+        if ((j & 3) == 3) {
+          const int r = i * 2 + (j >> 2);
+          if (r < 8) f1b[r] = ob.frag(cur + A_BYTES, wn * 8 + r, 1);
+          else f1a[r - 8] = oa.frag(cur, wm * 8 + r - 8, 1);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of stage s+1 landed
+    __builtin_amdgcn_s_barrier();
+    // ---- k-step s.1: MFMAs on set 1, prefetch set 0 of stage s+1 from
+    //      `nxt`, DMA stage s+2 into `cur` (consumed: certified by the barrier)
+    const int k2 = kst(s + 2);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xmfma(acc[i][j], f1b[j], f1a[i]);
+        if ((j & 3) == 1) {
+          const int r = i * 2 + (j >> 2);
+          if (r < 8) f0b[r] = ob.frag(nxt + A_BYTES, wn * 8 + r, 0);
+          else f0a[r - 8] = oa.frag(nxt, wm * 8 + r - 8, 0);
+        }
+        if ((j & 3) == 3) {
+          const int p = i * 2 + (j >> 2);
+          if (p < 8) oa.issue(cur, p, k2, wave);
+          else ob.issue(cur + A_BYTES, p - 8, k2, wave);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + crow;
+    uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 128 + ccol;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4_t v = acc[i][j];
+      uint2 pk;
+      pk.x = mxk::pack2bf(v[0], v[1]);
+      pk.y = mxk::pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+    }
+  }
+}
+
+// a_kmajor: A stored [M][K] (1) or [K][M] (0); b_kmajor: B stored [N][K] (1)
+// or [K][N] (0).  Row strides lda/ldb/ldc in elements.  Tiles exactly:
+// M % 256, N % 256, K % 64; returns hipErrorInvalidValue otherwise (callers
+// keep the library GEMM for other shapes).
+MXK_API int mxk_gemm_bf16_ex(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                             int ldb, int ldc, int a_kmajor, int b_kmajor, hipStream_t stream) {
+  const auto bytes = [](long rows, long ld) { return rows * ld * 2; };
+  const bool ok = M > 0 && N > 0 && K > 0 && M % XBM == 0 && N % XBM == 0 && K % XBK == 0 &&
+                  lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 &&
+                  (a_kmajor ? lda >= K : lda >= M) && (b_kmajor ? ldb >= K : ldb >= N) &&
+                  ldc >= N && (a_kmajor || bytes(K, lda) < (1L << 32)) &&
+                  (b_kmajor || bytes(K, ldb) < (1L << 32)) &&
+                  reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(C) % 8 == 0;
+  if (!ok) return static_cast<int>(hipErrorInvalidValue);
+  const int nwg = (M / XBM) * (N / XBM);
+  auto a = static_cast<const uint16_t*>(A);
+  auto b = static_cast<const uint16_t*>(B);
+  auto c = static_cast<uint16_t*>(C);
+  if (a_kmajor && b_kmajor)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<false, false>), dim3(nwg), dim3(XT), 0, stream, a,
+                       b, c, M, N, K, lda, ldb, ldc);
+  else if (a_kmajor)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<false, true>), dim3(nwg), dim3(XT), 0, stream, a,
+                       b, c, M, N, K, lda, ldb, ldc);
+  else if (b_kmajor)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<true, false>), dim3(nwg), dim3(XT), 0, stream, a,
+                       b, c, M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<true, true>), dim3(nwg), dim3(XT), 0, stream, a,
+                       b, c, M, N, K, lda, ldb, ldc);
+  MXK_RETURN_LAUNCH_STATUS();
+}

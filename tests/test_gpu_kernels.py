@@ -154,3 +154,27 @@ def test_add_rmsnorm_fwd_bwd(cuda_device, rows, H):
     assert (x.grad.float() - xr.grad).abs().max() <= tol
     assert (d.grad.float() - dr.grad).abs().max() <= tol
     assert (w.grad.float() - wr.grad).abs().max() <= 2e-2 * wr.grad.abs().max() + 1e-2
+
+
+@pytest.mark.parametrize("layout", ["tn", "nn", "nt_wgrad"])
+def test_gemm_layouts_vs_fp32(cuda_device, layout):
+    """Layout-generic MFMA GEMM (K-major / N-major operands, tr_b16 reads)."""
+    from mxk8s.ops.gemm import gemm_bf16_ex
+    g = torch.Generator(device=cuda_device).manual_seed(11)
+    M, N, K = 512, 768, 320
+    r = lambda *s: (torch.rand(*s, device=cuda_device, generator=g) * 2 - 1).bfloat16()  # noqa: E731
+    if layout == "tn":
+        a, b, ak, bk = r(M, K), r(N, K), True, True
+        ref = a.float() @ b.float().t()
+    elif layout == "nn":
+        a, b, ak, bk = r(M, K), r(K, N), True, False
+        ref = a.float() @ b.float()
+    else:
+        a, b, ak, bk = r(K, M), r(K, N), False, False
+        ref = a.float().t() @ b.float()
+    out = torch.empty(M, N, device=cuda_device, dtype=torch.bfloat16)
+    assert gemm_bf16_ex(a, b, ak, bk, out)
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 2 ** -7 * ref.abs().max().item() + 1e-3, err
+    # shapes that do not tile fall back (nothing launched)
+    assert not gemm_bf16_ex(a[:, :-64] if ak else a[:-64], b, ak, bk, out)
