@@ -182,6 +182,7 @@ def main(argv=None) -> int:
     p.add_argument("--layers", type=int, default=None, help="ddp mode: override (NOT headline)")
     p.add_argument("--bucket-mb", type=float, default=512.0, help="ddp mode: all-reduce bucket size")
     p.add_argument("--no-zero", action="store_true", help="ddp mode: replicated optimizer (no ZeRO-1)")
+    p.add_argument("--no-tuned-gemms", action="store_true", help="ddp mode: default hipBLASLt picks")
     args = p.parse_args(argv)
 
     world, rank, _ = _dist_env()

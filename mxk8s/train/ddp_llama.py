@@ -27,6 +27,24 @@ from ..parallel.optim import FlatAdamW, ShardedFlatAdamW
 from ..utils import roctx
 
 MI355X_BF16_DENSE_PEAK = 2.5e15   # FLOP/s, dense (MI355X_MICROARCH.md)
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning",
+                           "tunableop_mi355x_llama3_8b.csv")
+
+
+def use_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
+    """Load the PyTorch TunableOp table of the Llama-3-8B step's hipBLASLt /
+    rocBLAS GEMMs (fastest solution per shape, found once with
+    scripts/gpu/tune_gemms.sh on MI355X) read-only: no tuning at run time.
+    TunableOp ignores the table if the torch / hipBLASLt / rocBLAS versions
+    or the GPU arch recorded in it differ."""
+    if not (torch.cuda.is_available() and os.path.exists(path)):
+        return False
+    import torch.cuda.tunable as tunable
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.record_untuned_enable(False)
+    tunable.set_filename(path, insert_device_ordinal=False)
+    return bool(tunable.read_file(path))
 
 
 def build(cfg: LlamaConfig, device: torch.device, bucket_mb: float, lr: float = 3e-4,
@@ -78,6 +96,7 @@ def run_ddp_bench(args) -> dict:
         model_name = "tiny-llama (test)"
     seq, mb = args.seq_len, args.micro_batch
     bucket_mb = getattr(args, "bucket_mb", 512.0)
+    tuned = False if getattr(args, "no_tuned_gemms", False) else use_tuned_gemms()
     zero = not getattr(args, "no_zero", False)
     model, ddp, opt = build(cfg, dev, bucket_mb, zero=zero)
     g = torch.Generator(device=dev)
@@ -131,6 +150,7 @@ def run_ddp_bench(args) -> dict:
         "peak_mem_gib": round(peak_mem / 2 ** 30, 2),
         "mean_loss": final_loss,
         "bucket_mb": bucket_mb,
+        "tuned_gemms": tuned,
         "grad_norm_last": float(opt.last_grad_norm.item()),
     }
 
@@ -144,6 +164,8 @@ def main(argv=None) -> int:
     p.add_argument("--layers", type=int, default=None)
     p.add_argument("--bucket-mb", type=float, default=512.0)
     p.add_argument("--tiny", action="store_true")
+    p.add_argument("--no-tuned-gemms", action="store_true",
+                   help="do not load the TunableOp GEMM table")
     p.add_argument("--no-zero", action="store_true",
                    help="replicate the optimizer (all-reduce) instead of ZeRO-1 sharding")
     a = p.parse_args(argv)
