@@ -21,6 +21,7 @@ import yaml
 K8S_MINOR = "v1.34"
 K8S_VERSION = "v1.34.1"
 POD_CIDR = "10.244.0.0/16"
+HELM_VERSION = "v3.19.0"
 CRI_SOCKET = "unix:///run/containerd/containerd.sock"
 CDI_DIRS = ["/etc/cdi", "/var/run/cdi"]
 CDI_SPEC_PATH = "/etc/cdi/amd.com-gpu.json"

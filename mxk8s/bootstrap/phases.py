@@ -6,12 +6,14 @@ reboot in the middle (README.md:70-74), a "do not proceed" gate (:84), a fixed
 step is a phase with a completion marker in /var/lib/mxk8s/phase, so a rerun
 after the reboot (or after any failure) resumes where it stopped:
 
+  preflight     root, Ubuntu release, CPU/memory/disk, offline-capable          README.md:5-9
   prep          swap off, overlay/br_netfilter, sysctls (+ numa_balancing=0)   README.md:13-56
   driver-check  amdgpu loaded, /dev/kfd, gfx950 GPUs via libmxnode, iommu=pt   README.md:60-84
   runtime       containerd, SystemdCgroup=true, CDI enabled                    README.md:88-124,151-155
   cdi           /etc/cdi/amd.com-gpu.json from mx-cdi-gen (no toolkit/shim)     replaces README.md:126-149
   k8s-packages  pkgs.k8s.io v1.34 kubelet/kubeadm/kubectl (held)               README.md:159-187
   cluster       kubeadm init --config, kubeconfig, untaint, Flannel, Ready     README.md:191-243
+  helm          pinned helm v3 release, sha256-verified (skipped if present)    README.md:249-255
   stack         amd-gpu-stack (helm, or kubectl apply of the rendered chart)   README.md:247-286
   validate      busybox (config 1) + hip-vector-add (config 2), wait + RESULT  README.md:288-335
 
@@ -104,6 +106,47 @@ class PhaseError(RuntimeError):
 # ---------------------------------------------------------------------------
 # phases
 # ---------------------------------------------------------------------------
+
+SUPPORTED_UBUNTU = ("22.04", "24.04", "24.10", "25.04", "25.10")
+
+
+def preflight_report(ctx: Context) -> dict:
+    """Host facts the preflight phase decides on (R00: the reference only
+    states 'Ubuntu 25, NVIDIA GPU, root, internet' in prose, README.md:5-9)."""
+    osr = {}
+    for line in (ctx.read("/etc/os-release") or "").splitlines():
+        k, _, v = line.partition("=")
+        osr[k] = v.strip().strip('"')
+    mem_kb = 0
+    for line in (ctx.read("/proc/meminfo") or "").splitlines():
+        if line.startswith("MemTotal:"):
+            mem_kb = int(line.split()[1])
+    try:
+        st = os.statvfs(ctx.path("/var/lib") if ctx.exists("/var/lib") else ctx.path("/"))
+        free_gb = st.f_bavail * st.f_frsize / 2 ** 30
+    except OSError:
+        free_gb = 0.0
+    return {"os_id": osr.get("ID", ""), "os_version": osr.get("VERSION_ID", ""),
+            "root": os.geteuid() == 0, "cpus": os.cpu_count() or 0,
+            "mem_gib": round(mem_kb / 2 ** 20, 1), "free_disk_gib": round(free_gb, 1)}
+
+
+def phase_preflight(ctx: Context) -> None:
+    rep = preflight_report(ctx)
+    if not rep["root"] and not ctx.dry_run:
+        raise PhaseError("bootstrap needs root (sudo python3 -m mxk8s bootstrap); "
+                         "use --dry-run --root DIR to inspect the plan")
+    if rep["os_id"] != "ubuntu":
+        ctx.out(f"WARNING: tested on Ubuntu {'/'.join(SUPPORTED_UBUNTU)}; found {rep['os_id'] or '?'}")
+    elif rep["os_version"] not in SUPPORTED_UBUNTU:
+        ctx.out(f"WARNING: Ubuntu {rep['os_version']} is untested "
+                f"(tested: {', '.join(SUPPORTED_UBUNTU)})")
+    if rep["mem_gib"] and rep["mem_gib"] < 64:
+        ctx.out(f"WARNING: {rep['mem_gib']} GiB RAM; kubelet + an 8-GPU training pod want >= 64")
+    if rep["free_disk_gib"] and rep["free_disk_gib"] < 50:
+        ctx.out(f"WARNING: {rep['free_disk_gib']} GiB free under /var/lib (images need ~50)")
+    ctx.out("preflight: " + json.dumps(rep))
+
 
 def phase_prep(ctx: Context) -> None:
     if ctx.upgrade:
@@ -227,6 +270,38 @@ def phase_cluster(ctx: Context) -> None:
     _kubectl(ctx, "wait", "node", "--all", "--for=condition=Ready", "--timeout=300s")
 
 
+def phase_helm(ctx: Context) -> None:
+    """Install the pinned helm release (the reference pipes get-helm-3 into
+    bash, README.md:251-255).  The tarball is verified against the sha256 the
+    release publishes next to it (or MXK8S_HELM_SHA256); offline hosts can
+    point MXK8S_HELM_TARBALL at a copied tarball.  Without helm the stack phase
+    applies the pre-rendered manifests instead, so a failure here only warns."""
+    if ctx.have("helm") and not ctx.dry_run:
+        ctx.out("helm already installed")
+        return
+    ver = hf.HELM_VERSION
+    tgz = os.environ.get("MXK8S_HELM_TARBALL", f"/tmp/helm-{ver}-linux-amd64.tar.gz")
+    url = f"https://get.helm.sh/helm-{ver}-linux-amd64.tar.gz"
+    want = os.environ.get("MXK8S_HELM_SHA256", "")
+    try:
+        if not os.path.exists(tgz) or ctx.dry_run:
+            ctx.run(["curl", "-fsSL", "-o", tgz, url])
+        if not want:
+            r = ctx.run(["curl", "-fsSL", url + ".sha256sum"], capture=True)
+            want = (r.stdout or "").split()[0] if (r.stdout or "").strip() else ""
+        if not ctx.dry_run:
+            import hashlib
+            with open(tgz, "rb") as f:
+                got = hashlib.sha256(f.read()).hexdigest()
+            if not want or got != want:
+                raise PhaseError(f"helm tarball checksum mismatch: {got} != {want or '?'}")
+        ctx.run(["tar", "-xzf", tgz, "-C", "/tmp", "linux-amd64/helm"])
+        ctx.run(["install", "-m", "0755", "/tmp/linux-amd64/helm", "/usr/local/bin/helm"])
+    except (subprocess.CalledProcessError, OSError, PhaseError) as e:
+        ctx.out(f"WARNING: helm not installed ({e}); the stack phase will kubectl-apply "
+                "deploy/amd-gpu-stack.yaml")
+
+
 def phase_stack(ctx: Context) -> None:
     chart = os.path.join(ctx.repo, "charts", "amd-gpu-stack")
     if ctx.have("helm") and not ctx.dry_run:
@@ -270,12 +345,14 @@ def phase_validate(ctx: Context) -> None:
 
 
 PHASES: list[tuple[str, Callable[[Context], None]]] = [
+    ("preflight", phase_preflight),
     ("prep", phase_prep),
     ("driver-check", phase_driver_check),
     ("runtime", phase_runtime),
     ("cdi", phase_cdi),
     ("k8s-packages", phase_k8s_packages),
     ("cluster", phase_cluster),
+    ("helm", phase_helm),
     ("stack", phase_stack),
     ("validate", phase_validate),
 ]

@@ -210,7 +210,7 @@ def test_bootstrap_driver_gate_blocks(tmp_path):
     ctx = phases.Context(root=str(root), dry_run=True, out=lambda s: None)
     with pytest.raises(phases.PhaseError, match="driver gate failed"):
         phases.run(ctx, until="driver-check")
-    assert phases.completed(ctx) == ["prep"]   # resumes at driver-check after the reboot
+    assert phases.completed(ctx) == ["preflight", "prep"]   # resumes at driver-check after the reboot
 
 
 def test_cli_bootstrap_and_render(tmp_path):
@@ -292,3 +292,23 @@ def test_doctor_node(tmp_path):
         {"metadata": {"name": "coredns"}, "status": {"phase": "Running"}}]}))
     checks = doctor.check_node(h)
     assert all(c.status != "fail" for c in checks), [(c.name, c.detail) for c in checks]
+
+
+def test_preflight_and_helm_phases_dry_run(tmp_path):
+    root = tmp_path / "host"
+    (root / "etc").mkdir(parents=True)
+    (root / "etc/os-release").write_text('ID=ubuntu\nVERSION_ID="24.04"\n')
+    (root / "proc").mkdir()
+    (root / "proc/meminfo").write_text("MemTotal:       3170000000 kB\n")
+    out = []
+    ctx = phases.Context(root=str(root), dry_run=True, out=out.append)
+    phases.phase_preflight(ctx)
+    rep = json.loads(out[-1].split("preflight: ", 1)[1])
+    assert rep["os_id"] == "ubuntu" and rep["os_version"] == "24.04" and rep["mem_gib"] > 3000
+    assert not any("WARNING" in o for o in out)
+    phases.phase_helm(ctx)
+    cmds = ctx.commands()
+    assert any("get.helm.sh/helm-v3" in c and c.startswith("curl") for c in cmds)
+    assert any(c.endswith(".sha256sum") for c in cmds)       # checksum fetched, not trusted blindly
+    assert any("/usr/local/bin/helm" in c for c in cmds)
+    assert phases.PHASE_NAMES[0] == "preflight" and "helm" in phases.PHASE_NAMES
