@@ -68,6 +68,15 @@ __device__ __forceinline__ float half_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// v_exp_f32 directly: inputs are <= 0 (or -inf for masked keys), where the
+// libm exp2f's denormal range fix-up (cmp/cndmask/ldexp) is dead weight.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// 8-element MFMA operand from two transposed 4-element reads
+__device__ __forceinline__ bf16x8_t cat8(bf16x4_t lo, bf16x4_t hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // row of a 32x32 accumulator register r (0..15) for lane half h
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -212,21 +221,23 @@ mxk_attn_fwd_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s1[r]);
       mx = half_max(mx);
       const float m_new = fmaxf(m, mx);
-      const float alpha = exp2f((m - m_new) * c);
+      const float alpha = fexp2((m - m_new) * c);
       m = m_new;
       const float mc = m_new * c;
       float ls = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        s0[r] = exp2f(fmaf(s0[r], c, -mc));
-        s1[r] = exp2f(fmaf(s1[r], c, -mc));
+        s0[r] = fexp2(fmaf(s0[r], c, -mc));
+        s1[r] = fexp2(fmaf(s1[r], c, -mc));
         ls += s0[r] + s1[r];
       }
       l = l * alpha + ls;
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {   // wave-uniform: some row max moved
 #pragma unroll
-      for (int db = 0; db < 4; ++db)
+        for (int db = 0; db < 4; ++db)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[db][r] *= alpha;
+          for (int r = 0; r < 16; ++r) acc[db][r] *= alpha;
+      }
       // P^T fragments for the 4 16-key k-steps
       bf16x8_t pf[4];
       pf[0] = pack8(s0, 0);
@@ -242,9 +253,7 @@ mxk_attn_fwd_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__
           const int ch = 4 * db + tr_ch;
           const bf16x4_t lo = lds_tr_b64(vt + swz(key, ch) + tr_byte);
           const bf16x4_t hi = lds_tr_b64(vt + swz(key + 8, ch) + tr_byte);
-          bf16x8_t a;
-          a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
-          a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+          const bf16x8_t a = cat8(lo, hi);
           acc[db] = mfma32(a, pf[ks], acc[db]);
         }
       }
@@ -440,7 +449,7 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float e0 = exp2f(fmaf(s0[r], c, -lse2));
+          float e0 = fexp2(fmaf(s0[r], c, -lse2));
           if (diag && kv0 + 32 * kh + crow(r, h) > myq) e0 = 0.f;
           s0[r] = e0 * (p0[r] - dlt);   // dS^T
         }
@@ -456,9 +465,7 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
             const int ch = 4 * db + tr_ch;
             const bf16x4_t lo = lds_tr_b64(kt + swz(key, ch) + tr_byte);
             const bf16x4_t hi = lds_tr_b64(kt + swz(key + 8, ch) + tr_byte);
-            bf16x8_t a;
-            a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
-            a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+            const bf16x8_t a = cat8(lo, hi);
             acc[db] = mfma32(a, df[kk], acc[db]);
           }
         }
@@ -604,8 +611,8 @@ mxk_attn_bwd_dkdv_kernel(const uint16_t* __restrict__ q, const uint16_t* __restr
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = qs0 + crow(r, h);
-        float e0 = exp2f(s0[r] * c);
-        float e1 = exp2f(s1[r] * c);
+        float e0 = fexp2(s0[r] * c);
+        float e1 = fexp2(s1[r] * c);
         if (diag && mykey > qi) e0 = 0.f;
         if (diag && mykey > qi + 32) e1 = 0.f;
         s0[r] = e0;                 // P
@@ -627,11 +634,8 @@ mxk_attn_bwd_dkdv_kernel(const uint16_t* __restrict__ q, const uint16_t* __restr
           const bf16x4_t ohi = lds_tr_b64(dt + swz(row + 8, ch) + tr_byte);
           const bf16x4_t qlo = lds_tr_b64(qt + swz(row, ch) + tr_byte);
           const bf16x4_t qhi = lds_tr_b64(qt + swz(row + 8, ch) + tr_byte);
-          bf16x8_t ao, aq;
-          ao[0] = olo[0]; ao[1] = olo[1]; ao[2] = olo[2]; ao[3] = olo[3];
-          ao[4] = ohi[0]; ao[5] = ohi[1]; ao[6] = ohi[2]; ao[7] = ohi[3];
-          aq[0] = qlo[0]; aq[1] = qlo[1]; aq[2] = qlo[2]; aq[3] = qlo[3];
-          aq[4] = qhi[0]; aq[5] = qhi[1]; aq[6] = qhi[2]; aq[7] = qhi[3];
+          const bf16x8_t ao = cat8(olo, ohi);
+          const bf16x8_t aq = cat8(qlo, qhi);
           dva[db] = mfma32(ao, pf[ks], dva[db]);
           dka[db] = mfma32(aq, sf[ks], dka[db]);
         }
