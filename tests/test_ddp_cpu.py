@@ -184,3 +184,24 @@ def test_zero1_sharded_optimizer_matches_replicated(bucket_mb):
             assert torch.allclose(z[r]["zero"][n], p, rtol=1e-4, atol=1e-4), n
     for n in z[0]["zero"]:
         assert torch.equal(z[0]["zero"][n], z[1]["zero"][n]), n
+
+
+def test_ddp_trainer_torchrun_two_ranks_cpu():
+    """The trainer entry point under torch.distributed.run (gloo, 2 ranks, CPU):
+    ZeRO-1 path end to end, one JSON result line from rank 0."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "mxk8s.train.ddp_llama", "--tiny", "--steps", "2", "--warmup", "1",
+           "--seq-len", "64", "--micro-batch", "1", "--bucket-mb", "0.5"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                       env={**os.environ, "PYTHONPATH": repo, "OMP_NUM_THREADS": "2"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2+zero1"
+    assert d["value"] > 0 and d["steps"] == 2
