@@ -604,7 +604,9 @@ constexpr int W4B_STAGE_BYTES = 2 * W4B_OP_BYTES;  // 64 KiB
 
 __device__ __forceinline__ int w4b_h(int q) { return (((q ^ (q >> 1)) & 1) << 1) | (q >> 1); }
 
-template <bool HALF>
+// CP: cache-policy bits of the LDS-DMA loads (aux operand: 1 = sc0, 2 = nt,
+// 16 = sc1).  hipBLASLt's MT256x256x64 kernels issue theirs with sc1.
+template <bool HALF, int CP = 0>
 struct DmaStream64 {
   __amdgpu_buffer_rsrc_t rsrc;   // uniform: 256-row panel
   uint32_t lane_off;             // per lane: row-in-piece * ld * 2 + swizzled chunk * 16
@@ -618,14 +620,14 @@ struct DmaStream64 {
     const int dst = HALF ? g * 2048 + kh * 1024 : g * 1024;
     const int soff = HALF ? k_bytes + kh * 64 + g * piece_stride : k_bytes + g * piece_stride;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_op + dst), 16, lane_off, soff,
-                                             0, 0);
+                                             0, CP);
   }
 };
 
-template <bool HALF>
-__device__ __forceinline__ DmaStream64<HALF> make_dma64(const uint16_t* src, int ld, int row0,
+template <bool HALF, int CP = 0>
+__device__ __forceinline__ DmaStream64<HALF, CP> make_dma64(const uint16_t* src, int ld, int row0,
                                                         int lane, int wave) {
-  DmaStream64<HALF> d;
+  DmaStream64<HALF, CP> d;
   const uint16_t* base = src + static_cast<size_t>(row0) * ld;
   d.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, 256 * ld * 2,
                                              0x00020000);
@@ -650,7 +652,7 @@ __device__ __forceinline__ DmaStream64<HALF> make_dma64(const uint16_t* src, int
 // 16 DMA pieces and 16 prefetch reads: 0 = interleaved (one of each per 4
 // MFMAs), 1 = DMA over the first 32 MFMAs then reads over the last 32,
 // 2 = reads first, then DMA.
-template <int ABL = 0, bool HALF = false, int ORD = 0>
+template <int ABL = 0, bool HALF = false, int ORD = 0, int CP = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -672,8 +674,8 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   const int m0 = (first_m + in_group % gsize) * BM;
   const int n0 = (in_group / gsize) * BN;
 
-  const DmaStream64<HALF> dma_a = make_dma64<HALF>(A, lda, m0, lane, wave_s);
-  const DmaStream64<HALF> dma_b = make_dma64<HALF>(Bt, ldb, n0, lane, wave_s);
+  const DmaStream64<HALF, CP> dma_a = make_dma64<HALF, CP>(A, lda, m0, lane, wave_s);
+  const DmaStream64<HALF, CP> dma_b = make_dma64<HALF, CP>(Bt, ldb, n0, lane, wave_s);
 
   // fragment offsets: lane reads row x = (l & 15) of a 16-row subtile,
   // logical chunk ks*4 + (l >> 4)
@@ -832,6 +834,139 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// Schedule 7: the w4b pipeline with 8 waves (2 per SIMD), each owning a
+// 128 x 64 block (8 x 4 AGPR tiles).  Every wave issues half the LDS-DMA
+// pieces of w4b (8 per stage) and while one wave of a SIMD is held up by a
+// DMA issue or an LDS read the other keeps the matrix core busy; the price is
+// 1.5x the LDS fragment traffic (each A fragment is read by 4 waves).
+// ---------------------------------------------------------------------------
+constexpr int W8B_THREADS = 512;
+
+template <int CP>
+__device__ __forceinline__ void w8b_issue(const DmaStream64<false, CP>& d, char* lds_op, int p,
+                                          int k_bytes, int wave_s) {
+  const int g = p * 8 + wave_s;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(d.rsrc, (lds_void*)(lds_op + g * 1024), 16, d.lane_off,
+                                           k_bytes + g * d.piece_stride, 0, CP);
+}
+
+template <int CP = 0>
+__global__ void __launch_bounds__(W8B_THREADS, 1)
+mxk_gemm_bf16_tn_w8b(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 2;   // 0..1: 128-row half
+  const int wn = wave_s & 3;    // 0..3: 64-column quarter
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int wgid = mxk::xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  // DMA pieces g = p*8 + wave (p = 0..3), rows 8g .. 8g+7 -> LDS g*1024;
+  // (row >> 1) & 7 = (4 (wave & 1) + (r >> 1)) & 7, so w4b's lane offsets hold
+  const DmaStream64<false, CP> dma_a = make_dma64<false, CP>(A, lda, m0, lane, wave_s);
+  const DmaStream64<false, CP> dma_b = make_dma64<false, CP>(Bt, ldb, n0, lane, wave_s);
+
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 4 * SUB;
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / BK;
+  auto kbytes = [&](int st) { return (st < ns ? st : ns - 1) * BK * 2; };
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    char* buf = smem + s * W4B_STAGE_BYTES;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      w8b_issue<CP>(dma_a, buf, p, kbytes(s), wave_s);
+      w8b_issue<CP>(dma_b, buf + W4B_OP_BYTES, p, kbytes(s), wave_s);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // own pieces of stage 0 landed
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t f0a[8], f0b[4], f1a[8], f1b[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
+
+  for (int s = 0; s < ns; ++s) {
+    char* cur = smem + (s & 1) * W4B_STAGE_BYTES;
+    char* nxt = smem + ((s + 1) & 1) * W4B_STAGE_BYTES;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
+      }
+      if (i < 4) {   // 12 prefetch reads over the first 16 MFMAs of the k-step
+        f1b[i] = lds_read_b128(cur + b_base + i * SUB + off_k1);
+        f1a[2 * i] = lds_read_b128(cur + a_base + (2 * i) * SUB + off_k1);
+        f1a[2 * i + 1] = lds_read_b128(cur + a_base + (2 * i + 1) * SUB + off_k1);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int kb = kbytes(s + 2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
+        if (j == 1) {   // 8 DMA pieces over the k-step: one per 4 MFMAs
+          if (i < 4) w8b_issue<CP>(dma_a, cur, i, kb, wave_s);
+          else w8b_issue<CP>(dma_b, cur + W4B_OP_BYTES, i - 4, kb, wave_s);
+        }
+      }
+      if (i < 4) {
+        f0b[i] = lds_read_b128(nxt + b_base + i * SUB + off_k0);
+        f0a[2 * i] = lds_read_b128(nxt + a_base + (2 * i) * SUB + off_k0);
+        f0a[2 * i + 1] = lds_read_b128(nxt + a_base + (2 * i + 1) * SUB + off_k0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + crow;
+    uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 64 + ccol;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4_t v = acc[i][j];
+      uint2 pk;
+      pk.x = mxk::pack2bf(v[0], v[1]);
+      pk.y = mxk::pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generic bounds-checked MFMA GEMM (any M, N, K; K-contiguous operands).
 // 64x64 tile, 256 threads (2x2 waves of 32x32), register-staged through LDS.
 // Used for shapes the 256x256 kernel does not tile exactly.
@@ -917,9 +1052,9 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 3: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4<4, 0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 4: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8<4>), dim3(nwg), dim3(W8_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 5: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 6: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, true>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 7: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 8: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 2>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 6: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 0, 16>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 7: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8b<0>), dim3(nwg), dim3(W8B_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 8: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8b<16>), dim3(nwg), dim3(W8B_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 9: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 10: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<2>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     default: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<3>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
