@@ -608,9 +608,17 @@ __device__ __forceinline__ int w4b_h(int q) { return (((q ^ (q >> 1)) & 1) << 1)
 // 16 = sc1).  hipBLASLt's MT256x256x64 kernels issue theirs with sc1.
 template <bool HALF, int CP = 0>
 struct DmaStream64 {
+  // CP & 32 ("VOFF" addressing, hipBLASLt-style): one precomputed VGPR offset
+  // per piece, soffset 0 and the k step folded into a per-stage descriptor
+  // base; otherwise one lane VGPR + a per-piece SGPR soffset.
+  static constexpr bool VOFF = (CP & 32) != 0;
+  static constexpr int AUX = CP & 31;
   __amdgpu_buffer_rsrc_t rsrc;   // uniform: 256-row panel
   uint32_t lane_off;             // per lane: row-in-piece * ld * 2 + swizzled chunk * 16
   uint32_t piece_stride;         // uniform: rows per piece * ld * 2
+  const char* base;              // VOFF: panel base
+  uint32_t bytes;                // VOFF: panel bytes
+  uint32_t voff[8];              // VOFF: lane_off + (p*4 + wave) * piece_stride
   // whole-line pieces: g = p*4 + wave (rows 8g .. 8g+7) -> LDS [g*1024, +1024)
   // half pieces:       q = p*4 + wave (rows 16q .. 16q+15), k-half kh ->
   //                    LDS [q*2048 + kh*1024, +1024)
@@ -618,9 +626,16 @@ struct DmaStream64 {
                                         int kh = 0) const {
     const int g = p * 4 + wave_s;
     const int dst = HALF ? g * 2048 + kh * 1024 : g * 1024;
-    const int soff = HALF ? k_bytes + kh * 64 + g * piece_stride : k_bytes + g * piece_stride;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_op + dst), 16, lane_off, soff,
-                                             0, CP);
+    if constexpr (VOFF && !HALF) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<char*>(base + k_bytes), 0, static_cast<int>(bytes), 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(lds_op + dst), 16, voff[p], 0, 0,
+                                               AUX);
+    } else {
+      const int soff = HALF ? k_bytes + kh * 64 + g * piece_stride : k_bytes + g * piece_stride;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_op + dst), 16, lane_off, soff,
+                                               0, AUX);
+    }
   }
 };
 
@@ -643,6 +658,10 @@ __device__ __forceinline__ DmaStream64<HALF, CP> make_dma64(const uint16_t* src,
     d.lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
     d.piece_stride = static_cast<uint32_t>(8 * ld * 2);
   }
+  d.base = reinterpret_cast<const char*>(base);
+  d.bytes = static_cast<uint32_t>(256 * ld * 2);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) d.voff[p] = d.lane_off + (p * 4 + wave) * d.piece_stride;
   return d;
 }
 }  // namespace
@@ -738,6 +757,7 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
+        if (ORD == 3 && i == 3 && j == 7) __builtin_amdgcn_s_barrier();   // lockstep waves
         if ((j & 3) == 3 && ABL != 2) {
           const int r = i * 2 + (j >> 2);
           if (r < 8) f1b[r] = lds_read_b128(cur + b_base + r * SUB + off_k1);
@@ -768,7 +788,8 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
-        if (ORD != 0 && !HALF) {
+        if (ORD == 3 && i == 3 && j == 7) __builtin_amdgcn_s_barrier();
+        if ((ORD == 1 || ORD == 2) && !HALF) {
           // halves of the k-step: slot t = (i & 3) * 4 + (j >> 1) on odd j
           const bool first = i < 4;
           if ((j & 1) == 1) {
@@ -1036,7 +1057,7 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // Host launchers (C ABI, stream-ordered, capture-safe: no sync, no malloc).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kDefaultVariant = 5;
+constexpr int kDefaultVariant = 6;
 constexpr int kNumVariants = 12;
 constexpr int kFirstAblation = 9;   // variants >= this produce wrong outputs (timing only)
 
@@ -1052,9 +1073,9 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 3: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4<4, 0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 4: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8<4>), dim3(nwg), dim3(W8_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 5: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 6: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 0, 16>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 7: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8b<0>), dim3(nwg), dim3(W8B_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 8: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8b<16>), dim3(nwg), dim3(W8B_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 6: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 0, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 7: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 3, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 8: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 0, 48>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 9: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 10: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<2>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     default: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<3>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
