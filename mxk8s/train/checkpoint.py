@@ -1,0 +1,96 @@
+"""Checkpoint / resume of the flat-buffer trainer (SURVEY.md §5
+"Checkpoint / resume": the reference has none; its only resumable sequence is
+the manual reboot gate, /root/reference/README.md:70-84).
+
+Everything the trainer owns lives in a handful of flat buffers
+(:class:`~mxk8s.parallel.ddp.FlatParamSpace`, the AdamW master / moment
+buffers), so a checkpoint is a few large contiguous tensors — no per-parameter
+state dicts, no pickles:
+
+  <dir>/params.safetensors        bf16 parameters (rank 0; identical on all ranks)
+  <dir>/optim-rank<r>.safetensors fp32 master / exp_avg / exp_avg_sq of rank r
+                                  (its ZeRO-1 shard, or the full buffers when
+                                  the optimizer is replicated — then rank 0 only)
+  <dir>/meta.json                 step, world size, layout fingerprint, sharding
+
+Loading checks the layout fingerprint (parameter shapes, offsets, bucket
+padding) and, for sharded state, the world size, and refuses mismatches.
+Files are written to a temporary name and renamed, so a crash mid-save never
+leaves a truncated checkpoint in place.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+from typing import Optional
+
+import torch
+from safetensors.torch import load_file, save_file
+
+from ..parallel import dist as mxdist
+
+
+def layout_fingerprint(space) -> str:
+    h = hashlib.sha256()
+    for p, o in zip(space.params, space.offsets):
+        h.update(f"{tuple(p.shape)}@{o};".encode())
+    h.update(f"numel={space.numel};dtype={space.dtype}".encode())
+    return h.hexdigest()[:16]
+
+
+def _atomic_save(tensors: dict, path: str, meta: Optional[dict] = None) -> None:
+    tmp = path + ".tmp"
+    save_file({k: v.detach().contiguous().cpu() for k, v in tensors.items()}, tmp,
+              metadata={k: str(v) for k, v in (meta or {}).items()})
+    os.replace(tmp, path)
+
+
+def save(ckpt_dir: str, ddp, opt, step: int) -> None:
+    """Collective: every rank calls it (rank 0 writes params + meta)."""
+    world, rank, _ = mxdist.world_info()
+    sharded = bool(getattr(ddp, "sharded", False))
+    os.makedirs(ckpt_dir, exist_ok=True)
+    fp = layout_fingerprint(ddp.space)
+    if sharded or rank == 0:
+        _atomic_save({"master": opt.master, "exp_avg": opt.exp_avg, "exp_avg_sq": opt.exp_avg_sq},
+                      os.path.join(ckpt_dir, f"optim-rank{rank if sharded else 0}.safetensors"),
+                      {"step_count": opt.step_count, "layout": fp})
+    if rank == 0:
+        _atomic_save({"params": ddp.space.param_buf}, os.path.join(ckpt_dir, "params.safetensors"),
+                     {"layout": fp})
+        meta = {"step": step, "optimizer_step": opt.step_count, "world_size": world,
+                "sharded": sharded, "layout": fp, "numel": ddp.space.numel,
+                "format": "mxk8s-flat-v1"}
+        tmp = os.path.join(ckpt_dir, "meta.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(meta, f, indent=1)
+        os.replace(tmp, os.path.join(ckpt_dir, "meta.json"))
+    mxdist.barrier()
+
+
+def load(ckpt_dir: str, ddp, opt) -> int:
+    """Restore parameters and optimizer state; returns the saved step."""
+    world, rank, _ = mxdist.world_info()
+    with open(os.path.join(ckpt_dir, "meta.json")) as f:
+        meta = json.load(f)
+    if meta.get("format") != "mxk8s-flat-v1":
+        raise ValueError(f"{ckpt_dir}: not an mxk8s flat checkpoint")
+    fp = layout_fingerprint(ddp.space)
+    if meta["layout"] != fp:
+        raise ValueError(f"{ckpt_dir}: parameter layout {meta['layout']} != model layout {fp}")
+    sharded = bool(getattr(ddp, "sharded", False))
+    if meta["sharded"] != sharded or (sharded and meta["world_size"] != world):
+        raise ValueError(f"{ckpt_dir}: saved with world_size={meta['world_size']} "
+                         f"sharded={meta['sharded']}, running world_size={world} sharded={sharded}")
+    dev = ddp.space.param_buf.device
+    params = load_file(os.path.join(ckpt_dir, "params.safetensors"))["params"]
+    with torch.no_grad():
+        ddp.space.param_buf.copy_(params.to(dev))
+        st = load_file(os.path.join(ckpt_dir, f"optim-rank{rank if sharded else 0}.safetensors"))
+        opt.master.copy_(st["master"].to(dev))
+        opt.exp_avg.copy_(st["exp_avg"].to(dev))
+        opt.exp_avg_sq.copy_(st["exp_avg_sq"].to(dev))
+    opt.step_count = int(meta["optimizer_step"])
+    mxdist.barrier()
+    return int(meta["step"])

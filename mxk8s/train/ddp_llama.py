@@ -109,6 +109,10 @@ def run_ddp_bench(args) -> dict:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    start_step = 0
+    if getattr(args, "resume", None):
+        from . import checkpoint
+        start_step = checkpoint.load(args.resume, ddp, opt)
     for i in range(args.warmup):
         train_step(model, ddp, opt, batches[i % nbatches])
     sync()
@@ -123,6 +127,10 @@ def run_ddp_bench(args) -> dict:
     sync()
     dt = time.perf_counter() - t0
     dt_max = mxdist.max_over_ranks(dt, dev)
+    if getattr(args, "save_checkpoint", None):   # outside the timed region
+        from . import checkpoint
+        checkpoint.save(args.save_checkpoint, ddp, opt,
+                        step=start_step + args.warmup + args.steps)
     tokens = world * mb * seq * args.steps
     tps = tokens / dt_max
     flops_tok = cfg.flops_per_token(seq)
@@ -164,6 +172,9 @@ def main(argv=None) -> int:
     p.add_argument("--layers", type=int, default=None)
     p.add_argument("--bucket-mb", type=float, default=512.0)
     p.add_argument("--tiny", action="store_true")
+    p.add_argument("--save-checkpoint", default=None, metavar="DIR",
+                   help="write params + optimizer state after the run (mxk8s.train.checkpoint)")
+    p.add_argument("--resume", default=None, metavar="DIR", help="restore a checkpoint first")
     p.add_argument("--no-tuned-gemms", action="store_true",
                    help="do not load the TunableOp GEMM table")
     p.add_argument("--no-zero", action="store_true",

@@ -186,17 +186,20 @@ def test_zero1_sharded_optimizer_matches_replicated(bucket_mb):
         assert torch.equal(z[0]["zero"][n], z[1]["zero"][n]), n
 
 
-def test_ddp_trainer_torchrun_two_ranks_cpu():
+def test_ddp_trainer_torchrun_two_ranks_cpu(tmp_path):
     """The trainer entry point under torch.distributed.run (gloo, 2 ranks, CPU):
-    ZeRO-1 path end to end, one JSON result line from rank 0."""
+    ZeRO-1 path end to end, one JSON result line from rank 0, a sharded
+    checkpoint written after the timed steps."""
     import json
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ck = str(tmp_path / "ck")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            "-m", "mxk8s.train.ddp_llama", "--tiny", "--steps", "2", "--warmup", "1",
-           "--seq-len", "64", "--micro-batch", "1", "--bucket-mb", "0.5"]
+           "--seq-len", "64", "--micro-batch", "1", "--bucket-mb", "0.5",
+           "--save-checkpoint", ck]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
                        env={**os.environ, "PYTHONPATH": repo, "OMP_NUM_THREADS": "2"})
     assert r.returncode == 0, r.stderr[-3000:]
@@ -205,3 +208,73 @@ def test_ddp_trainer_torchrun_two_ranks_cpu():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2+zero1"
     assert d["value"] > 0 and d["steps"] == 2
+    assert sorted(os.listdir(ck)) == ["meta.json", "optim-rank0.safetensors",
+                                      "optim-rank1.safetensors", "params.safetensors"]
+    assert json.load(open(os.path.join(ck, "meta.json")))["step"] == 3
+
+
+def _ckpt_worker(rank, world, port, outdir, sharded):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from mxk8s.parallel.optim import ShardedFlatAdamW
+    from mxk8s.train import checkpoint
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = LlamaConfig.tiny()
+
+    def build():
+        torch.manual_seed(0)
+        model = Llama(cfg)
+        ddp = FlatDDP(model, bucket_mb=0.05, shard_optimizer=sharded)
+        opt = ShardedFlatAdamW(ddp, lr=1e-3) if sharded else \
+            FlatAdamW(ddp.space, lr=1e-3, grad_scale=ddp.grad_scale)
+        return model, ddp, opt
+
+    def steps(model, ddp, opt, lo, hi):
+        for s in range(lo, hi):
+            model.loss(_batch(rank * 100 + s, cfg)).backward()
+            ddp.finish_grad_sync()
+            opt.step()
+            ddp.zero_grad()
+
+    m1, d1, o1 = build()
+    steps(m1, d1, o1, 0, 4)                       # uninterrupted run
+    m2, d2, o2 = build()
+    steps(m2, d2, o2, 0, 2)
+    checkpoint.save(os.path.join(outdir, "ck"), d2, o2, step=2)
+    m3, d3, o3 = build()                           # "restarted job"
+    assert checkpoint.load(os.path.join(outdir, "ck"), d3, o3) == 2
+    steps(m3, d3, o3, 2, 4)
+    torch.save({"a": d1.space.param_buf.clone(), "b": d3.space.param_buf.clone(),
+                "ma": o1.master.clone(), "mb": o3.master.clone()},
+               os.path.join(outdir, f"c{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_checkpoint_resume_matches_uninterrupted(sharded):
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ckpt_worker, args=(world, _free_port(), d, sharded), nprocs=world, join=True)
+        files = sorted(os.listdir(os.path.join(d, "ck")))
+        assert "meta.json" in files and "params.safetensors" in files
+        assert ("optim-rank1.safetensors" in files) == sharded
+        for r in range(world):
+            c = torch.load(os.path.join(d, f"c{r}.pt"), weights_only=True)
+            assert torch.equal(c["a"], c["b"])
+            assert torch.equal(c["ma"], c["mb"])
+
+
+def test_checkpoint_rejects_layout_mismatch(tmp_path):
+    from mxk8s.train import checkpoint
+    torch.manual_seed(0)
+    model = Llama(LlamaConfig.tiny())
+    ddp = FlatDDP(model)
+    opt = FlatAdamW(ddp.space)
+    checkpoint.save(str(tmp_path / "ck"), ddp, opt, step=5)
+    cfg2 = LlamaConfig.tiny()
+    cfg2.n_layers = 1
+    m2 = Llama(cfg2)
+    d2 = FlatDDP(m2)
+    with pytest.raises(ValueError, match="layout"):
+        checkpoint.load(str(tmp_path / "ck"), d2, FlatAdamW(d2.space))
