@@ -671,6 +671,20 @@ __device__ __forceinline__ DmaStream64<HALF, CP> make_dma64(const uint16_t* src,
 // 16 DMA pieces and 16 prefetch reads: 0 = interleaved (one of each per 4
 // MFMAs), 1 = DMA over the first 32 MFMAs then reads over the last 32,
 // 2 = reads first, then DMA.
+// Diagnostic build only (ABL == 5): s_memtime stamps split every k-iteration
+// into k-step 0 / wait + barrier / k-step 1; per-segment cycle sums of all
+// waves land in g_w4b_stamps (read by mxk_gemm_bf16_stamps).  The stamps'
+// fences forbid overlaps the real kernel has: read the SHARES, not the time.
+__device__ unsigned long long g_w4b_stamps[4];
+
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
 template <int ABL = 0, bool HALF = false, int ORD = 0, int CP = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
@@ -744,6 +758,7 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 #pragma unroll
   for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
 
+  unsigned long long seg0 = 0, seg1 = 0, seg2 = 0, t0 = 0;
   for (int s = 0; s < ns; ++s) {
     char* cur = smem + (s & 1) * W4B_STAGE_BYTES;
     char* nxt = smem + ((s + 1) & 1) * W4B_STAGE_BYTES;
@@ -751,6 +766,7 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
     //      (HALF: DMA k-half 1 of stage s+1 into `nxt`; buffer s-1's k-half 1
     //      was consumed in (s-1).0)
     __builtin_amdgcn_s_waitcnt(0xC07F);
+    if constexpr (ABL == 5) t0 = stamp();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -771,6 +787,8 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
       }
     }
     __builtin_amdgcn_s_setprio(0);
+    unsigned long long t1 = 0;
+    if constexpr (ABL == 5) t1 = stamp();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     // own pieces of stage s+1's first k-half landed (HALF: 8 younger pieces
     // of k-half 1 stay in flight)
@@ -779,6 +797,12 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
+    unsigned long long t2 = 0;
+    if constexpr (ABL == 5) {
+      t2 = stamp();
+      seg0 += t1 - t0;
+      seg1 += t2 - t1;
+    }
     // ---- k-step s.1: MFMAs on set 1, prefetch set 0 ((s+1).0) from `nxt`,
     //      DMA of stage s+2 (HALF: its k-half 0) into `cur`, fully consumed:
     //      certified by the barrier
@@ -827,12 +851,156 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
       }
     }
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (ABL == 5) seg2 += stamp() - t2;
     if constexpr (HALF) {
       // k-half 1 of stage s+1 (issued in s.0) must be visible before (s+1).0
       // prefetches it; the 8 pieces just issued stay in flight
       __builtin_amdgcn_s_waitcnt(0xC07F);
       if (ABL != 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  if constexpr (ABL == 5) {
+    if (lane == 0) {
+      atomicAdd(&g_w4b_stamps[0], seg0);
+      atomicAdd(&g_w4b_stamps[1], seg1);
+      atomicAdd(&g_w4b_stamps[2], seg2);
+      atomicAdd(&g_w4b_stamps[3], 1ull);
+    }
+  } else {
+    (void)seg0; (void)seg1; (void)seg2; (void)t0;
+  }
+
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + crow;
+    uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 128 + ccol;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4_t v = acc[i][j];
+      uint2 pk;
+      pk.x = mxk::pack2bf(v[0], v[1]);
+      pk.y = mxk::pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Schedule 8 ("early reads"): the w4b tile and LDS image, but each k-step
+// issues ALL 16 fragment reads of the next k-step at its start (LDS-bound
+// bursts the matrix core hides) instead of one per 4 MFMAs.  k-step 0's
+// reads retire after 16 MFMAs; a barrier there certifies that every wave is
+// done with the stage's buffer, so the 16 LDS-DMA pieces of stage s+2 are
+// spread over BOTH k-steps (8 each) instead of all landing in k-step 1, where
+// the diagnostic stamps (variant 12) put +300 cycles.  Stage s+1 is waited
+// for with vmcnt(8) (its pieces were issued 1.5-2 k-steps earlier).
+// ---------------------------------------------------------------------------
+template <int CP = 32>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4e(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int wgid = mxk::xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  const DmaStream64<false, CP> dma_a = make_dma64<false, CP>(A, lda, m0, lane, wave_s);
+  const DmaStream64<false, CP> dma_b = make_dma64<false, CP>(Bt, ldb, n0, lane, wave_s);
+
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / BK;
+  auto kbytes = [&](int st) { return (st < ns ? st : ns - 1) * BK * 2; };
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    char* buf = smem + s * W4B_STAGE_BYTES;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      dma_a.issue(buf, p, kbytes(s), wave_s);
+      dma_b.issue(buf + W4B_OP_BYTES, p, kbytes(s), wave_s);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
+
+  for (int s = 0; s < ns; ++s) {
+    char* cur = smem + (s & 1) * W4B_STAGE_BYTES;
+    char* nxt = smem + ((s + 1) & 1) * W4B_STAGE_BYTES;
+    const int kb = kbytes(s + 2);
+    // ---- k-step s.0
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // set 0 in registers
+#pragma unroll
+    for (int r = 0; r < 8; ++r) f1b[r] = lds_read_b128(cur + b_base + r * SUB + off_k1);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) f1a[r] = lds_read_b128(cur + a_base + r * SUB + off_k1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
+        if (i == 1 && j == 7) {
+          // every wave's reads of `cur` retired -> stage s+2 may land there
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_s_barrier();
+        }
+        if (i >= 2 && i < 6 && (j & 3) == 3) {
+          const int p = (i - 2) * 2 + (j >> 2);   // 0..7: A pieces
+          dma_a.issue(cur, p, kb, wave_s);
+        }
+      }
+    }
+    // stage s+1 (issued 1.5-2 k-steps ago) landed; the 8 newest stay in flight
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // ---- k-step s.1
+#pragma unroll
+    for (int r = 0; r < 8; ++r) f0b[r] = lds_read_b128(nxt + b_base + r * SUB + off_k0);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) f0a[r] = lds_read_b128(nxt + a_base + r * SUB + off_k0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
+        if (i < 4 && (j & 3) == 3) {
+          const int p = i * 2 + (j >> 2);         // 0..7: B pieces
+          dma_b.issue(cur + W4B_OP_BYTES, p, kb, wave_s);
+        }
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -1058,7 +1226,7 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int kDefaultVariant = 6;
-constexpr int kNumVariants = 12;
+constexpr int kNumVariants = 13;
 constexpr int kFirstAblation = 9;   // variants >= this produce wrong outputs (timing only)
 
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
@@ -1074,11 +1242,12 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 4: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8<4>), dim3(nwg), dim3(W8_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 5: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 6: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 0, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 7: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 3, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 8: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 0, 48>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 7: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8b<0>), dim3(nwg), dim3(W8B_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 8: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4e<32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 9: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 10: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<2>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    default: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<3>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 11: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<3>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    default: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<5, false, 0, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
   }
 }
 }  // namespace
@@ -1093,6 +1262,18 @@ MXK_API int mxk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int
 }
 
 MXK_API int mxk_gemm_bf16_tn_num_variants(void) { return kNumVariants; }
+
+// Diagnostic stamps of variant 12: out[0..2] = summed cycles of k-step 0,
+// wait + barrier, k-step 1 over all waves; out[3] = waves.  reset != 0
+// clears them.
+MXK_API int mxk_gemm_bf16_stamps(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4b_stamps), sizeof(unsigned long long) * 4);
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_w4b_stamps), z, sizeof(z));
+  }
+  return static_cast<int>(e);
+}
 MXK_API int mxk_gemm_bf16_tn_first_ablation(void) { return kFirstAblation; }
 
 MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,
