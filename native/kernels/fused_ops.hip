@@ -155,6 +155,78 @@ mxk_rmsnorm_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restri
   }
 }
 
+// Wave-per-row backward for H = 512 * NC (Llama-3-8B: H 4096, NC 8): a wave
+// keeps its row of dy / x (/ dres) in registers, so every byte is read once
+// (the block-per-row kernel above reads dy and x twice and pays a block-wide
+// __syncthreads reduction per row); the row dot product is a wave reduction.
+// Lane l owns columns 8l + 512c (c < NC) and accumulates dw for them over
+// the wave's rows; the block's 4 waves fold their dw partials through LDS
+// into one fp32 slab row per block (then mxk_colsum_kernel as before).
+template <int NC>
+__global__ void __launch_bounds__(256)
+mxk_rmsnorm_bwd_wave_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                            const uint16_t* __restrict__ w, const float* __restrict__ rstd,
+                            const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
+                            float* __restrict__ dw_part, int rows) {
+  constexpr int H = 512 * NC;
+  __shared__ float fold[4][H];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int gw = blockIdx.x * 4 + wave;
+  const int nw = gridDim.x * 4;
+  float wf[NC][8], dwacc[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    load8(w + 512 * c + 8 * lane, wf[c]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dwacc[c][e] = 0.f;
+  }
+  for (int r = gw; r < rows; r += nw) {
+    const size_t off = static_cast<size_t>(r) * H + 8 * lane;
+    const float rs = rstd[r];
+    bf16x8_t gy[NC], gx[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      gy[c] = *reinterpret_cast<const bf16x8_t*>(dy + off + 512 * c);
+      gx[c] = *reinterpret_cast<const bf16x8_t*>(x + off + 512 * c);
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        dot += mxk::bf2f(static_cast<uint16_t>(gy[c][e])) * wf[c][e] *
+               mxk::bf2f(static_cast<uint16_t>(gx[c][e]));
+    const float k = mxk::wave_sum(dot) * (rs * rs / static_cast<float>(H));
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float a = mxk::bf2f(static_cast<uint16_t>(gy[c][e]));
+        const float b = mxk::bf2f(static_cast<uint16_t>(gx[c][e]));
+        o[e] = rs * (a * wf[c][e] - b * k);
+        dwacc[c][e] += a * b * rs;
+      }
+      if (dres) {
+        float rr[8];
+        load8(dres + off + 512 * c, rr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += rr[e];
+      }
+      store8(dx + off + 512 * c, o);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) fold[wave][512 * c + 8 * lane + e] = dwacc[c][e];
+  __syncthreads();
+  float* slab = dw_part + static_cast<size_t>(blockIdx.x) * H;
+  for (int i = threadIdx.x; i < H; i += 256)
+    slab[i] = (fold[0][i] + fold[1][i]) + (fold[2][i] + fold[3][i]);
+}
+
 // out[c] = sum_b part[b][c]  (fp32 in, bf16 or fp32 out).  A block owns 64
 // columns; its 4 waves take every 4th slab row (each wave reads 256
 // contiguous bytes per row) and fold through LDS in a fixed order.
@@ -329,6 +401,22 @@ MXK_API int mxk_rmsnorm_bwd(const void* dy, const void* x, const void* w, const 
       (dres && !aligned16(dres)))
     return static_cast<int>(hipErrorInvalidValue);
   const int nb = rows < kBwdBlocks ? rows : kBwdBlocks;
+  if ((H == 2048 || H == 4096 || H == 8192) && aligned16(w) && rows >= 4 * nb) {
+    auto* a = static_cast<const uint16_t*>(dy);
+    auto* b = static_cast<const uint16_t*>(x);
+    auto* g = static_cast<const uint16_t*>(w);
+    auto* d = static_cast<const uint16_t*>(dres);
+    auto* o = static_cast<uint16_t*>(dx);
+    if (H == 2048)
+      hipLaunchKernelGGL(mxk_rmsnorm_bwd_wave_kernel<4>, dim3(nb), dim3(256), 0, s, a, b, g, rstd, d, o, workspace, rows);
+    else if (H == 4096)
+      hipLaunchKernelGGL(mxk_rmsnorm_bwd_wave_kernel<8>, dim3(nb), dim3(256), 0, s, a, b, g, rstd, d, o, workspace, rows);
+    else
+      hipLaunchKernelGGL(mxk_rmsnorm_bwd_wave_kernel<16>, dim3(nb), dim3(256), 0, s, a, b, g, rstd, d, o, workspace, rows);
+    hipLaunchKernelGGL(mxk_colsum_kernel, dim3((H + 63) / 64), dim3(256), 0, s, workspace, nb, H,
+                       static_cast<uint16_t*>(dw_bf16), dw_f32);
+    MXK_RETURN_LAUNCH_STATUS();
+  }
   const int rpb = (rows + nb - 1) / nb;
   const int nblocks = (rows + rpb - 1) / rpb;
   hipLaunchKernelGGL(mxk_rmsnorm_bwd_kernel, dim3(nblocks), dim3(kRowThreads), 0, s,

@@ -89,7 +89,8 @@ def test_gemm_large_vs_hipblaslt(cuda_device):
     assert rel <= 1e-2, rel
 
 
-@pytest.mark.parametrize("rows,H", [(1, 4096), (7, 4096), (2048, 4096), (33, 2048), (5, 8192), (3, 128)])
+@pytest.mark.parametrize("rows,H", [(1, 4096), (7, 4096), (2048, 4096), (33, 2048), (5, 8192), (3, 128),
+                                    (4096, 2048), (1024, 8192), (3000, 4096)])
 def test_rmsnorm_fwd_bwd(cuda_device, rows, H):
     x = _rand((rows, H), cuda_device, 12, 3.0).bfloat16().requires_grad_()
     w = (1 + 0.1 * _rand((H,), cuda_device, 13)).bfloat16().requires_grad_()
