@@ -24,7 +24,7 @@ LDLIBS_NODE := -ldl -lpthread
 
 KERNEL_SRCS := native/kernels/gemm_bf16.hip native/kernels/vector_add.hip \
                native/kernels/fused_ops.hip native/kernels/optim.hip native/kernels/attention.hip \
-               native/kernels/gemm_bf16_layouts.hip
+               native/kernels/gemm_bf16_layouts.hip native/kernels/xent.hip
 KERNEL_OBJS := $(patsubst native/kernels/%.hip,$(BUILD)/kernels/%.o,$(KERNEL_SRCS))
 KERNEL_HDRS := $(wildcard native/kernels/*.h)
 

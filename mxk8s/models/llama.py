@@ -26,6 +26,7 @@ import torch.nn.functional as F
 
 from ..ops.attention import flash_attention, supported as flash_supported
 from ..ops.linear import Linear
+from ..ops.xent import cross_entropy
 from ..ops.fused import add_rmsnorm, rmsnorm, rope, rope_tables, swiglu
 
 
@@ -184,4 +185,5 @@ class Llama(nn.Module):
         else:
             inp = tokens
         logits = self(inp)
-        return F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), labels.reshape(-1))
+        # fused bf16 softmax cross-entropy on GPU (no fp32 logits copy)
+        return cross_entropy(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1))

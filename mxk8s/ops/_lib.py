@@ -53,6 +53,8 @@ _SIGNATURES = {
     "mxk_attn_bwd_workspace": (_l, [_i, _i, _i]),
     "mxk_attn_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i,
                           _l, _l, _l, _l, _l, _f, _i, _vp]),
+    "mxk_xent_fwd": (_i, [_vp, _vp, _vp, _vp, _l, _i, _l, _vp]),
+    "mxk_xent_bwd": (_i, [_vp, _vp, _vp, _vp, _l, _i, _l, _vp]),
     "mxk_adamw_bf16": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _f, _f, _f, _f, _f, _i, _vp, _vp]),
 }
 

@@ -179,3 +179,22 @@ def test_gemm_layouts_vs_fp32(cuda_device, layout):
     assert err <= 2 ** -7 * ref.abs().max().item() + 1e-3, err
     # shapes that do not tile fall back (nothing launched)
     assert not gemm_bf16_ex(a[:, :-64] if ak else a[:-64], b, ak, bk, out)
+
+
+@pytest.mark.parametrize("T,V", [(4, 128256), (300, 1000), (7, 8)])
+def test_fused_cross_entropy_vs_fp32(cuda_device, T, V):
+    from mxk8s.ops.xent import cross_entropy
+    g = torch.Generator(device=cuda_device).manual_seed(21)
+    logits = (torch.randn(T, V, device=cuda_device, generator=g) * 3).bfloat16()
+    labels = torch.randint(0, V, (T,), device=cuda_device, generator=g)
+    if T > 4:
+        labels[1] = -100          # ignore_index row: no loss, no gradient
+    ref_in = logits.float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(ref_in, labels, ignore_index=-100)
+    ref.backward()
+    x = logits.clone().requires_grad_()
+    loss = cross_entropy(x, labels)
+    assert abs(loss.item() - ref.item()) <= 1e-3 * max(1.0, abs(ref.item()))
+    loss.backward()
+    err = (x.grad.float() - ref_in.grad).abs().max().item()
+    assert err <= 2 ** -8 * ref_in.grad.abs().max().item() + 1e-6, err
