@@ -178,7 +178,7 @@ def main(argv=None) -> int:
     p.add_argument("--no-reference", action="store_true")
     p.add_argument("--no-allreduce", action="store_true")
     p.add_argument("--seq-len", type=int, default=2048, help="ddp mode")
-    p.add_argument("--micro-batch", type=int, default=4, help="ddp mode: sequences per GPU per step (4 x 2048 tokens: 168 GiB peak of 288)")
+    p.add_argument("--micro-batch", type=int, default=8, help="ddp mode: sequences per GPU per step (8 x 2048 tokens: 197 GiB peak of 288 at 1 GPU)")
     p.add_argument("--layers", type=int, default=None, help="ddp mode: override (NOT headline)")
     p.add_argument("--bucket-mb", type=float, default=512.0, help="ddp mode: all-reduce bucket size")
     p.add_argument("--no-zero", action="store_true", help="ddp mode: replicated optimizer (no ZeRO-1)")

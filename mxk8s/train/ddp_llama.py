@@ -168,7 +168,7 @@ def main(argv=None) -> int:
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--seq-len", type=int, default=2048)
-    p.add_argument("--micro-batch", type=int, default=4)
+    p.add_argument("--micro-batch", type=int, default=8)
     p.add_argument("--layers", type=int, default=None)
     p.add_argument("--bucket-mb", type=float, default=512.0)
     p.add_argument("--tiny", action="store_true")
