@@ -660,6 +660,191 @@ mxk_attn_bwd_dkdv_kernel(const uint16_t* __restrict__ q, const uint16_t* __restr
   }
 }
 
+// dK/dV with 16x16x32 MFMAs: one workgroup = 8 waves x 16 keys (128 keys of
+// one (batch, q-head)), so a wave holds dK^T / dV^T of its keys in 64
+// registers (32x32 tiles need 128) and two waves share each SIMD - the
+// 32-key kernel above runs one wave per SIMD and leaves the matrix core idle
+// through its exp / pack / LDS phases.  Per 32-query k-step:
+//   S  = Q.K^T, dP = dO.V^T    (A: Q / dO rows, ds_read_b128; B: K / V in registers)
+//   P  = exp2(c S'), dS = P dP' (accumulators pre-loaded with -LSE/scale, -delta)
+//   dV^T += dO^T.P, dK^T += Q^T.dS  (A: transposed reads of the same images;
+//   B: two 16x16 accumulator tiles = 8 consecutive-by-4 queries per lane)
+// Q / dO image: 256-B rows, chunk c of row r at c ^ 2(r & 7) - conflict-free
+// for the 16x16x32 row reads and the transposed reads (tests/test_attention_layout.py).
+namespace {
+__device__ __forceinline__ int swz16(int row, int ch) {
+  return row * 256 + ((ch ^ (2 * (row & 7))) << 4);
+}
+__device__ __forceinline__ f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8_t pack2x4(const f32x4_t& lo, const f32x4_t& hi) {
+  bf16x8_t o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = static_cast<short>(mxk::f2bf(lo[j]));
+    o[4 + j] = static_cast<short>(mxk::f2bf(hi[j]));
+  }
+  return o;
+}
+constexpr int NT16 = 512;
+}  // namespace
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(NT16, 1)
+mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                           const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
+                           const float* __restrict__ lse, const float* __restrict__ delta,
+                           float* __restrict__ dk_p, float* __restrict__ dv_p, int S, int Hq,
+                           int Hkv, long q_tok, long k_tok, long v_tok, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2 * BQB * 256];   // [buf][Q | dO]
+  __shared__ __attribute__((aligned(16))) float srow[2][2][BQB];       // [buf][-lse/scale | -delta]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c16 = lane & 15;
+  const int G = lane >> 4;
+
+  const int nkb = S / BQ;
+  int bh, kb;
+  {
+    int qbi;
+    map_block(blockIdx.x, gridDim.x / nkb, nkb, CAUSAL, &bh, &qbi);
+    kb = CAUSAL ? nkb - 1 - qbi : qbi;
+  }
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hkv = hq / (Hq / Hkv);
+  const int k0 = kb * BQ;
+  const int kw0 = k0 + wave * 16;
+  const int mykey = kw0 + c16;
+
+  const uint16_t* qb_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
+  const uint16_t* dob_ptr = dout + static_cast<long>(b) * S * Hq * D + static_cast<long>(hq) * D;
+  const uint16_t* kb_ptr = k + static_cast<long>(b) * S * k_tok + static_cast<long>(hkv) * D;
+  const uint16_t* vb_ptr = v + static_cast<long>(b) * S * v_tok + static_cast<long>(hkv) * D;
+  const float* lse_b = lse + (static_cast<long>(b) * Hq + hq) * S;
+  const float* dl_b = delta + (static_cast<long>(b) * Hq + hq) * S;
+
+  // B operands of S / dP: lane holds K[mykey][32 s + 8 G .. +7]
+  bf16x8_t kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8_t*>(kb_ptr + static_cast<long>(mykey) * k_tok + 32 * s + 8 * G);
+    vf[s] = *reinterpret_cast<const bf16x8_t*>(vb_ptr + static_cast<long>(mykey) * v_tok + 32 * s + 8 * G);
+  }
+  const float c = scale * 1.4426950408889634f;
+  const float inv_c = 1.f / c;
+
+  const int q_begin = CAUSAL ? k0 : 0;
+  const int nsl = (S - q_begin) / BQB;
+  // loader: 512 threads x 2 chunks per tile (64 rows x 16 chunks)
+  const int ld_row = tid >> 4, ld_ch = tid & 15;
+  bf16x8_t qst[2], dst[2];
+  float rst = 0.f;
+  auto load_slice = [&](int t) {
+    const long r0 = q_begin + static_cast<long>(t) * BQB + ld_row;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      qst[i] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + (r0 + 32 * i) * q_tok + ld_ch * 8);
+      dst[i] = *reinterpret_cast<const bf16x8_t*>(dob_ptr + (r0 + 32 * i) * Hq * D + ld_ch * 8);
+    }
+    if (tid < 2 * BQB) {
+      const long qi = q_begin + static_cast<long>(t) * BQB + (tid & (BQB - 1));
+      rst = tid < BQB ? -lse_b[qi] * 1.4426950408889634f * inv_c : -dl_b[qi];
+    }
+  };
+  auto store_slice = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int off = swz16(ld_row + 32 * i, ld_ch);
+      *reinterpret_cast<bf16x8_t*>(smem[buf] + off) = qst[i];
+      *reinterpret_cast<bf16x8_t*>(smem[buf] + BQB * 256 + off) = dst[i];
+    }
+    if (tid < 2 * BQB) srow[buf][tid / BQB][tid & (BQB - 1)] = rst;
+  };
+  load_slice(0);
+  store_slice(0);
+  __syncthreads();
+
+  f32x4_t dka[8], dva[8];
+#pragma unroll
+  for (int db = 0; db < 8; ++db) {
+    dka[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    dva[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  // transposed-read lane constants: row 4G + (i >> 2), column block 4 (i & 3)
+  const int tr_row = 4 * G + (c16 >> 2);
+  const int tr_chb = (c16 & 3) >> 1;
+  const int tr_byte = 8 * (c16 & 1);
+
+  for (int t = 0; t < nsl; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nsl) load_slice(t + 1);
+    const int qs0 = q_begin + t * BQB;
+    if (!CAUSAL || qs0 + BQB - 1 >= kw0) {
+      const char* qt = smem[buf];
+      const char* dt = smem[buf] + BQB * 256;
+      const bool diag = CAUSAL && qs0 < kw0 + 15;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        f32x4_t st[2], pt[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int qr = 32 * ks + 16 * h + 4 * G;
+          const float4 l4 = *reinterpret_cast<const float4*>(&srow[buf][0][qr]);
+          const float4 d4 = *reinterpret_cast<const float4*>(&srow[buf][1][qr]);
+          st[h] = f32x4_t{l4.x, l4.y, l4.z, l4.w};
+          pt[h] = f32x4_t{d4.x, d4.y, d4.z, d4.w};
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = 32 * ks + 16 * h + c16;
+            st[h] = mfma16(*reinterpret_cast<const bf16x8_t*>(qt + swz16(row, 4 * s + G)), kf[s], st[h]);
+            pt[h] = mfma16(*reinterpret_cast<const bf16x8_t*>(dt + swz16(row, 4 * s + G)), vf[s], pt[h]);
+          }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float e = fexp2(st[h][r] * c);
+            if (diag && mykey > qs0 + 32 * ks + 16 * h + 4 * G + r) e = 0.f;
+            st[h][r] = e;                  // P
+            pt[h][r] = e * pt[h][r];       // dS
+          }
+        }
+        const bf16x8_t pf = pack2x4(st[0], st[1]);
+        const bf16x8_t sf = pack2x4(pt[0], pt[1]);
+#pragma unroll
+        for (int db = 0; db < 8; ++db) {
+          const int row = 32 * ks + tr_row;
+          const int ch = 2 * db + tr_chb;
+          const bf16x8_t ao = cat8(lds_tr_b64(dt + swz16(row, ch) + tr_byte),
+                                   lds_tr_b64(dt + swz16(row + 16, ch) + tr_byte));
+          const bf16x8_t aq = cat8(lds_tr_b64(qt + swz16(row, ch) + tr_byte),
+                                   lds_tr_b64(qt + swz16(row + 16, ch) + tr_byte));
+          dva[db] = mfma16(ao, pf, dva[db]);
+          dka[db] = mfma16(aq, sf, dka[db]);
+        }
+      }
+    }
+    if (t + 1 < nsl) store_slice(buf ^ 1);
+    __syncthreads();
+  }
+  // lane = key, registers r: d = 16 db + 4 G + r
+  const long prow = ((static_cast<long>(b) * S + mykey) * Hq + hq) * D;
+#pragma unroll
+  for (int db = 0; db < 8; ++db) {
+    const int d = 16 * db + 4 * G;
+    *reinterpret_cast<float4*>(dk_p + prow + d) =
+        make_float4(dka[db][0] * scale, dka[db][1] * scale, dka[db][2] * scale, dka[db][3] * scale);
+    *reinterpret_cast<float4*>(dv_p + prow + d) =
+        make_float4(dva[db][0], dva[db][1], dva[db][2], dva[db][3]);
+  }
+}
+
 // dk[b][s][hkv][:] = sum over the group's q-heads of dk_p[b][s][hq][:] (bf16 out)
 __global__ void __launch_bounds__(256)
 mxk_attn_bwd_gqa_reduce_kernel(const float* __restrict__ dk_p, const float* __restrict__ dv_p,
@@ -722,13 +907,13 @@ MXK_API int mxk_attn_bwd(const void* q, const void* k, const void* v, const void
                      stream, static_cast<const uint16_t*>(o), dO, delta, S, Hq, rows);
   const int nwg = B * Hq * (S / BQ);
   if (causal) {
-    hipLaunchKernelGGL(mxk_attn_bwd_dkdv_kernel<true>, dim3(nwg), dim3(NT), 0, stream, Q, K, V,
+    hipLaunchKernelGGL(mxk_attn_bwd_dkdv16_kernel<true>, dim3(nwg), dim3(NT16), 0, stream, Q, K, V,
                        dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
     hipLaunchKernelGGL(mxk_attn_bwd_dq_kernel<true>, dim3(nwg), dim3(NT), 0, stream, Q, K, V, dO,
                        lse, delta, static_cast<uint16_t*>(dq), S, Hq, Hkv, q_tok, k_tok, v_tok,
                        scale);
   } else {
-    hipLaunchKernelGGL(mxk_attn_bwd_dkdv_kernel<false>, dim3(nwg), dim3(NT), 0, stream, Q, K, V,
+    hipLaunchKernelGGL(mxk_attn_bwd_dkdv16_kernel<false>, dim3(nwg), dim3(NT16), 0, stream, Q, K, V,
                        dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
     hipLaunchKernelGGL(mxk_attn_bwd_dq_kernel<false>, dim3(nwg), dim3(NT), 0, stream, Q, K, V,
                        dO, lse, delta, static_cast<uint16_t*>(dq), S, Hq, Hkv, q_tok, k_tok,

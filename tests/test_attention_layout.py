@@ -75,3 +75,55 @@ def test_v_transposed_read_semantics():
             for j in range(8):
                 want = (16 * ks + 8 * (j >> 2) + 4 * h + (j & 3), 32 * db + (l & 31))
                 assert frag[l][j] == want, (db, ks, l, j, frag[l][j], want)
+
+
+# ---- dK/dV kernel (16x16x32 MFMAs): Q / dO image, chunk c of row r at c ^ 2(r&7)
+def swz16(row, ch):
+    return row * 256 + ((ch ^ (2 * (row & 7))) << 4)
+
+
+def test_dkdv16_row_reads_conflict_free():
+    # A operand of S = Q.K^T: lane l reads row 16t + (l&15), chunk 4s + (l>>4)
+    for t in range(4):
+        for s in range(4):
+            for g in B128_GROUPS:
+                used = []
+                for l in g:
+                    used += list(banks(swz16(16 * t + (l & 15), 4 * s + (l >> 4)), 16))
+                assert len(used) == len(set(used)) == 64, (t, s)
+
+
+def tr16_addr(lane, ks, jh, db):
+    G, i = lane >> 4, lane & 15
+    row = 32 * ks + 16 * jh + 4 * G + (i >> 2)
+    ch = 2 * db + ((i & 3) >> 1)
+    return swz16(row, ch) + 8 * (i & 1)
+
+
+def test_dkdv16_transposed_reads_conflict_free_and_exact():
+    image = {}
+    for q in range(64):
+        for d in range(128):
+            image[swz16(q, d // 8) + 2 * (d % 8)] = (q, d)
+    for ks, db in itertools.product(range(2), range(8)):
+        for jh in range(2):
+            for half in (range(0, 32), range(32, 64)):
+                used = []
+                for l in half:
+                    used += list(banks(tr16_addr(l, ks, jh, db), 8))
+                assert len(used) == len(set(used)) == 64, (ks, jh, db)
+        # semantics: lane l element j = dO[q(j)][d = 16 db + (l & 15)] with the
+        # P-fragment query order q(j) = 32 ks + 16 (j >> 2) + 4 (l >> 4) + (j & 3)
+        frag = {l: [None] * 8 for l in range(64)}
+        for jh in range(2):
+            for g in range(4):
+                lanes = list(range(16 * g, 16 * g + 16))
+                rows = [[image[tr16_addr(lanes[4 * qq + p], ks, jh, db) + 2 * e]
+                         for p in range(4) for e in range(4)] for qq in range(4)]
+                for x, l in enumerate(lanes):
+                    for qq in range(4):
+                        frag[l][4 * jh + qq] = rows[qq][x]
+        for l in range(64):
+            for j in range(8):
+                want = (32 * ks + 16 * (j >> 2) + 4 * (l >> 4) + (j & 3), 16 * db + (l & 15))
+                assert frag[l][j] == want
