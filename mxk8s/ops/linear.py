@@ -25,9 +25,16 @@ from .gemm import gemm_bf16_ex
 _USE_MXK_WGRAD = os.environ.get("MXK_WGRAD", "1") != "0"
 
 
+def _tail_heavy(M: int, N: int, cus: int = 256) -> bool:
+    """Few 256x256 tiles with a half-empty last round (e.g. 384 tiles on 256
+    CUs): hipBLASLt's stream-K kernels balance that tail, ours do not."""
+    tiles = (M // 256) * (N // 256)
+    return tiles < 2 * cus and 0 < tiles % cus <= cus // 2
+
+
 def _wgrad_into(sink: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
     if _USE_MXK_WGRAD and sink.is_cuda and dy2.is_contiguous() and x2.is_contiguous() and \
-            gemm_bf16_ex(dy2, x2, False, False, sink):
+            not _tail_heavy(*sink.shape) and gemm_bf16_ex(dy2, x2, False, False, sink):
         return
     torch.matmul(dy2.t(), x2, out=sink)
 

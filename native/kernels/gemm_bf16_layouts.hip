@@ -83,14 +83,21 @@ struct XOp<false> {
   static constexpr int BYTES = 256 * 128;
   u32x4 rsrc;
   uint32_t lane_off, piece_stride;
+  uint32_t voff[8];              // lane_off + (p*4 + wave) * piece_stride
+  const char* base;
+  unsigned bytes;
   int off0, off1;
   __device__ __forceinline__ void init(const uint16_t* src, int ld, int row0, int K, int lane,
                                        int wave) {
     rsrc = make_rsrc(src + static_cast<size_t>(row0) * ld, 256u * ld * 2u);
+    base = reinterpret_cast<const char*>(src + static_cast<size_t>(row0) * ld);
+    bytes = 256u * ld * 2u;
     const int r = lane >> 3;
     const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & 7);
     lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
     piece_stride = static_cast<uint32_t>(8 * ld * 2);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) voff[p] = lane_off + (p * 4 + wave) * piece_stride;
     const int frow = lane & 15;
     const int fch = (lane >> 4) ^ (frow >> 1);
     off0 = frow * 128 + fch * 16;
@@ -99,7 +106,8 @@ struct XOp<false> {
   }
   __device__ __forceinline__ void issue(char* lds, int p, int kstage, int wave) const {
     const int g = p * 4 + wave;
-    dma16(rsrc, lds + g * 1024, lane_off, kstage * (XBK * 2) + g * piece_stride);
+    // hipBLASLt-style addressing: per-piece VGPR offset, k folded into the base
+    dma16(make_rsrc(base + kstage * (XBK * 2), bytes), lds + g * 1024, voff[p], 0);
   }
   // fragment of 16-row subtile i (i = 0..15 over the 256 rows), k-step ks
   __device__ __forceinline__ bf16x8_t frag(const char* lds, int i, int ks) const {
@@ -113,24 +121,31 @@ struct XOp<true> {
   static constexpr int BYTES = 8 * TGROUP;
   u32x4 rsrc;
   uint32_t lane_off, piece_stride, kstride;
+  uint32_t voff[8];
+  const char* base;
+  unsigned bytes;
   int base_off, qx;
   __device__ __forceinline__ void init(const uint16_t* src, int ld, int col0, int K, int lane,
                                        int wave) {
     rsrc = make_rsrc(src + col0, static_cast<unsigned>(K) * ld * 2u);
+    base = reinterpret_cast<const char*>(src + col0);
+    bytes = static_cast<unsigned>(K) * ld * 2u;
     // piece g = 4p + wave holds k-rows 8p + 2 wave + h (h = lane >> 5)
     const int h = lane >> 5, slot = lane & 31;
     const int c = slot ^ (2 * ((2 * wave + h) & 3));
     lane_off = static_cast<uint32_t>(h * ld * 2 + c * 16);
     piece_stride = static_cast<uint32_t>(2 * ld * 2);
     kstride = static_cast<uint32_t>(XBK * ld * 2);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) voff[p] = lane_off + (p * 4 + wave) * piece_stride;
     // transposed-read lane constants: group G, row q, column pair b, half-chunk
     const int G = lane >> 4, i16 = lane & 15, q = i16 >> 2;
     base_off = G * TGROUP + q * 512 + ((i16 & 3) >> 1) * 16 + 8 * (i16 & 1);
     qx = 32 * q;
   }
   __device__ __forceinline__ void issue(char* lds, int p, int kstage, int wave) const {
-    const int g = p * 4 + wave;
-    dma16(rsrc, lds + p * TGROUP + wave * 1024, lane_off, kstage * kstride + g * piece_stride);
+    const uint32_t k_off = kstage * kstride;
+    dma16(make_rsrc(base + k_off, bytes - k_off), lds + p * TGROUP + wave * 1024, voff[p], 0);
   }
   __device__ __forceinline__ bf16x8_t frag(const char* lds, int i, int ks) const {
     const char* p = lds + base_off + ks * KSTEP_T + ((32 * i) ^ qx);
