@@ -16,7 +16,8 @@ import os
 import threading
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
-KERNEL_LIB_PATH = os.path.join(_LIB_DIR, "libmxkernels.so")
+# MXK_KERNELS_LIB points at an alternative build (A/B runs of a kernel change).
+KERNEL_LIB_PATH = os.environ.get("MXK_KERNELS_LIB") or os.path.join(_LIB_DIR, "libmxkernels.so")
 
 _lock = threading.Lock()
 _lib = None
@@ -34,7 +35,7 @@ _SIGNATURES = {
     "mxk_gemm_bf16_ex": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_tn_variant": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_tn_num_variants": (_i, []),
-    "mxk_gemm_bf16_tn_first_ablation": (_i, []),
+    "mxk_gemm_bf16_tn_is_ablation": (_i, [_i]),
     "mxk_vector_add_f32": (_i, [_vp, _vp, _vp, _l, _vp]),
     "mxk_vector_add_bf16": (_i, [_vp, _vp, _vp, _l, _vp]),
     "mxk_error_string": (ctypes.c_char_p, [_i]),

@@ -42,7 +42,7 @@ def _events_time(fn, iters: int) -> list[float]:
 
 
 def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
-        ablation_from: int = 1 << 30) -> list[dict]:
+        is_ablation=lambda v: False) -> list[dict]:
     dev = device or torch.device("cuda", torch.cuda.current_device())
     L = _lib.lib()
     stream = lambda: _lib.stream_ptr(dev)  # noqa: E731
@@ -67,7 +67,7 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
         kernels["hipblaslt"] = lambda: torch.matmul(A, Bt.t(), out=C)
         # correctness of every hand-written schedule
         checks = {}
-        ablations = set(f"mxk_v{v}" for v in variants if v >= ablation_from)
+        ablations = set(f"mxk_v{v}" for v in variants if is_ablation(v))
         for name, fn in kernels.items():
             if name == "hipblaslt" or name in ablations:
                 continue
@@ -125,7 +125,7 @@ def main(argv=None) -> int:
     else:
         variants = []
     run([int(x) for x in a.sizes.split(",")], variants, a.iters, a.warmup_s, a.rounds,
-        ablation_from=_lib.lib().mxk_gemm_bf16_tn_first_ablation())
+        is_ablation=lambda v: bool(_lib.lib().mxk_gemm_bf16_tn_is_ablation(v)))
     return 0
 
 

@@ -583,16 +583,14 @@ mxk_gemm_bf16_tn_w8(const uint16_t* __restrict__ A, const uint16_t* __restrict__
 // MFMAs per stage.  Register set 0 holds the fragments of k-step s.0, set 1
 // those of s.1; each k-step prefetches the other set while its MFMAs run.
 //
-// HALF = false (schedule 5): DMA pieces are 8 rows x 128 B (whole cache
-//   lines).  k-step s.1 issues all 16 pieces of stage s+2 into buffer s;
-//   ONE barrier per stage (between s.0 and s.1).  Swizzle: chunk c of row r
-//   at c ^ ((r>>1)&7).
-// HALF = true (schedule 6): pieces are 16 rows x 64 B of one k-half, so each
-//   k-step issues 8 pieces (one per 8 MFMAs instead of one per 4 in every
-//   other k-step): s.0 issues the k-half 1 of stage s+1, s.1 the k-half 0 of
-//   stage s+2.  A 16-row subtile is two 1-KiB blocks (k-half 0, k-half 1) of
-//   64-B rows with chunk c of row r at c ^ h((r>>2)&3), h = {0,2,3,1}; two
-//   barriers per stage.
+// DMA pieces are 8 rows x 128 B (whole cache lines).  k-step s.1 issues all
+// 16 pieces of stage s+2 into buffer s; ONE barrier per stage (between s.0
+// and s.1).  Swizzle: chunk c of row r at c ^ ((r>>1)&7).  Schedule 5
+// addresses the DMA with one lane VGPR + a per-piece SGPR offset, 6 and 13
+// with a VGPR offset per piece (hipBLASLt-style, +2.8%); 13 (the default)
+// also has exact LDS waits (ORD 4 below).
+// (Half-line pieces, 16 rows x 64 B, spread the DMA evenly over both
+// k-steps but double the cache-line requests: slower here and in w4q.)
 // (A 64-B pad per 1-KiB piece, hipBLASLt-style, measured within noise of the
 // dense layout: the DMA landing banks are not the limiter.)
 // Layouts are conflict-free for the 16x16x32 fragment reads and the DMA
@@ -606,7 +604,7 @@ __device__ __forceinline__ int w4b_h(int q) { return (((q ^ (q >> 1)) & 1) << 1)
 
 // CP: cache-policy bits of the LDS-DMA loads (aux operand: 1 = sc0, 2 = nt,
 // 16 = sc1).  hipBLASLt's MT256x256x64 kernels issue theirs with sc1.
-template <bool HALF, int CP = 0>
+template <int CP = 0>
 struct DmaStream64 {
   // CP & 32 ("VOFF" addressing, hipBLASLt-style): one precomputed VGPR offset
   // per piece, soffset 0 and the k step folded into a per-stage descriptor
@@ -619,45 +617,35 @@ struct DmaStream64 {
   const char* base;              // VOFF: panel base
   uint32_t bytes;                // VOFF: panel bytes
   uint32_t voff[8];              // VOFF: lane_off + (p*4 + wave) * piece_stride
-  // whole-line pieces: g = p*4 + wave (rows 8g .. 8g+7) -> LDS [g*1024, +1024)
-  // half pieces:       q = p*4 + wave (rows 16q .. 16q+15), k-half kh ->
-  //                    LDS [q*2048 + kh*1024, +1024)
-  __device__ __forceinline__ void issue(char* lds_op, int p, int k_bytes, int wave_s,
-                                        int kh = 0) const {
+  // piece g = p*4 + wave (rows 8g .. 8g+7) -> LDS [g*1024, +1024)
+  __device__ __forceinline__ void issue(char* lds_op, int p, int k_bytes, int wave_s) const {
     const int g = p * 4 + wave_s;
-    const int dst = HALF ? g * 2048 + kh * 1024 : g * 1024;
-    if constexpr (VOFF && !HALF) {
+    const int dst = g * 1024;
+    if constexpr (VOFF) {
       const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<char*>(base + k_bytes), 0, static_cast<int>(bytes), 0x00020000);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(lds_op + dst), 16, voff[p], 0, 0,
                                                AUX);
     } else {
-      const int soff = HALF ? k_bytes + kh * 64 + g * piece_stride : k_bytes + g * piece_stride;
+      const int soff = k_bytes + g * piece_stride;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_op + dst), 16, lane_off, soff,
                                                0, AUX);
     }
   }
 };
 
-template <bool HALF, int CP = 0>
-__device__ __forceinline__ DmaStream64<HALF, CP> make_dma64(const uint16_t* src, int ld, int row0,
+template <int CP = 0>
+__device__ __forceinline__ DmaStream64<CP> make_dma64(const uint16_t* src, int ld, int row0,
                                                         int lane, int wave) {
-  DmaStream64<HALF, CP> d;
+  DmaStream64<CP> d;
   const uint16_t* base = src + static_cast<size_t>(row0) * ld;
   d.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, 256 * ld * 2,
                                              0x00020000);
-  if (HALF) {
-    const int r = lane >> 2;                      // row within the 16-row piece
-    const int c = (lane & 3) ^ w4b_h((r >> 2) & 3);
-    d.lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
-    d.piece_stride = static_cast<uint32_t>(16 * ld * 2);
-  } else {
-    const int r = lane >> 3;                      // row within the 8-row piece
-    // row = 8g + r with g = 4p + wave: (row >> 1) & 7 = (4 (wave & 1) + (r >> 1)) & 7
-    const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & 7);
-    d.lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
-    d.piece_stride = static_cast<uint32_t>(8 * ld * 2);
-  }
+  const int r = lane >> 3;                      // row within the 8-row piece
+  // row = 8g + r with g = 4p + wave: (row >> 1) & 7 = (4 (wave & 1) + (r >> 1)) & 7
+  const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & 7);
+  d.lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
+  d.piece_stride = static_cast<uint32_t>(8 * ld * 2);
   d.base = reinterpret_cast<const char*>(base);
   d.bytes = static_cast<uint32_t>(256 * ld * 2);
 #pragma unroll
@@ -670,7 +658,12 @@ __device__ __forceinline__ DmaStream64<HALF, CP> make_dma64(const uint16_t* src,
 // 3 = no vmcnt before the barrier.  ORD (whole-line mode) places k-step s.1's
 // 16 DMA pieces and 16 prefetch reads: 0 = interleaved (one of each per 4
 // MFMAs), 1 = DMA over the first 32 MFMAs then reads over the last 32,
-// 2 = reads first, then DMA.
+// 2 = reads first, then DMA, 3 = a mid-k-step barrier (lockstep waves).
+// ORD >= 4 drops the lgkmcnt(0) at the top of k-step s.0: the scalar loads
+// are drained before the loop so the compiler's per-operand LDS waits are
+// exact counts, and the MFMAs start while the last prefetch reads of s.1 are
+// still in flight.  ORD 4 also spreads s.0's reads one per 3 MFMAs, so the
+// barrier's lgkmcnt(0) finds them long retired; ORD 5 keeps s.0's placement.
 // Diagnostic build only (ABL == 5): s_memtime stamps split every k-iteration
 // into k-step 0 / wait + barrier / k-step 1; per-segment cycle sums of all
 // waves land in g_w4b_stamps (read by mxk_gemm_bf16_stamps).  The stamps'
@@ -685,7 +678,7 @@ __device__ __forceinline__ unsigned long long stamp() {
   return t;
 }
 
-template <int ABL = 0, bool HALF = false, int ORD = 0, int CP = 0>
+template <int ABL = 0, int ORD = 0, int CP = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -707,21 +700,15 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   const int m0 = (first_m + in_group % gsize) * BM;
   const int n0 = (in_group / gsize) * BN;
 
-  const DmaStream64<HALF, CP> dma_a = make_dma64<HALF, CP>(A, lda, m0, lane, wave_s);
-  const DmaStream64<HALF, CP> dma_b = make_dma64<HALF, CP>(Bt, ldb, n0, lane, wave_s);
+  const DmaStream64<CP> dma_a = make_dma64<CP>(A, lda, m0, lane, wave_s);
+  const DmaStream64<CP> dma_b = make_dma64<CP>(Bt, ldb, n0, lane, wave_s);
 
   // fragment offsets: lane reads row x = (l & 15) of a 16-row subtile,
   // logical chunk ks*4 + (l >> 4)
   const int frow = lane & 15;
-  int off_k0, off_k1;
-  if (HALF) {
-    off_k0 = frow * 64 + (((lane >> 4) ^ w4b_h(frow >> 2)) * 16);
-    off_k1 = off_k0 + 1024;
-  } else {
-    const int fch = (lane >> 4) ^ (frow >> 1);
-    off_k0 = frow * 128 + fch * 16;
-    off_k1 = frow * 128 + (fch ^ 4) * 16;
-  }
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
   constexpr int SUB = 2048;                      // bytes per 16-row subtile
   const int a_base = wm * 8 * SUB;
   const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
@@ -734,22 +721,17 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 
   const int ns = K / BK;   // 64-deep stages
   auto kbytes = [&](int st) { return (st < ns ? st : ns - 1) * BK * 2; };
-  // prologue: stage 0 whole, stage 1 whole (HALF: only its k-half 0)
+  // prologue: stages 0 and 1
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     char* buf = smem + s * W4B_STAGE_BYTES;
 #pragma unroll
-    for (int p = 0; p < (HALF ? 4 : 8); ++p) {
-#pragma unroll
-      for (int kh = 0; kh < (HALF ? 2 : 1); ++kh) {
-        if (HALF && s == 1 && kh == 1) continue;
-        dma_a.issue(buf, p, kbytes(s), wave_s, kh);
-        dma_b.issue(buf + W4B_OP_BYTES, p, kbytes(s), wave_s, kh);
-      }
+    for (int p = 0; p < 8; ++p) {
+      dma_a.issue(buf, p, kbytes(s), wave_s);
+      dma_b.issue(buf + W4B_OP_BYTES, p, kbytes(s), wave_s);
     }
   }
-  if constexpr (HALF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // stage 0 (own pieces) landed
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // stage 0 (own pieces) landed
   __builtin_amdgcn_s_barrier();
 
   bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
@@ -759,13 +741,14 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
 
   unsigned long long seg0 = 0, seg1 = 0, seg2 = 0, t0 = 0;
+  // ORD 4: drain everything (incl. kernel-argument scalar loads) here, so the
+  // compiler's per-register LDS waits inside the loop are exact counts
+  if constexpr (ORD >= 4) __builtin_amdgcn_s_waitcnt(0xC07F);
   for (int s = 0; s < ns; ++s) {
     char* cur = smem + (s & 1) * W4B_STAGE_BYTES;
     char* nxt = smem + ((s + 1) & 1) * W4B_STAGE_BYTES;
     // ---- k-step s.0: MFMAs on set 0, prefetch set 1 (s.1) from `cur`
-    //      (HALF: DMA k-half 1 of stage s+1 into `nxt`; buffer s-1's k-half 1
-    //      was consumed in (s-1).0)
-    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if constexpr (ORD < 4) __builtin_amdgcn_s_waitcnt(0xC07F);
     if constexpr (ABL == 5) t0 = stamp();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -774,15 +757,19 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
       for (int j = 0; j < 8; ++j) {
         mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
         if (ORD == 3 && i == 3 && j == 7) __builtin_amdgcn_s_barrier();   // lockstep waves
-        if ((j & 3) == 3 && ABL != 2) {
+        if (ORD == 4) {
+          // one read per 3 MFMAs: the last lands 17 MFMAs before the
+          // barrier's lgkmcnt(0) instead of right at it
+          const int m = i * 8 + j;
+          if (m % 3 == 1 && m / 3 < 16 && ABL != 2) {
+            const int r = m / 3;
+            if (r < 8) f1b[r] = lds_read_b128(cur + b_base + r * SUB + off_k1);
+            else f1a[r - 8] = lds_read_b128(cur + a_base + (r - 8) * SUB + off_k1);
+          }
+        } else if ((j & 3) == 3 && ABL != 2) {
           const int r = i * 2 + (j >> 2);
           if (r < 8) f1b[r] = lds_read_b128(cur + b_base + r * SUB + off_k1);
           else f1a[r - 8] = lds_read_b128(cur + a_base + (r - 8) * SUB + off_k1);
-        }
-        if (HALF && (j & 3) == 1 && ABL != 1) {
-          const int p = i * 2 + (j >> 2);   // 0..15
-          if (p < 4) dma_a.issue(nxt, p, kbytes(s + 1), wave_s, 1);
-          else if (p < 8) dma_b.issue(nxt + W4B_OP_BYTES, p - 4, kbytes(s + 1), wave_s, 1);
         }
       }
     }
@@ -790,12 +777,8 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
     unsigned long long t1 = 0;
     if constexpr (ABL == 5) t1 = stamp();
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    // own pieces of stage s+1's first k-half landed (HALF: 8 younger pieces
-    // of k-half 1 stay in flight)
-    if (ABL != 3) {
-      if constexpr (HALF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // own pieces of stage s+1 landed
+    if (ABL != 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     unsigned long long t2 = 0;
     if constexpr (ABL == 5) {
@@ -804,7 +787,7 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
       seg1 += t2 - t1;
     }
     // ---- k-step s.1: MFMAs on set 1, prefetch set 0 ((s+1).0) from `nxt`,
-    //      DMA of stage s+2 (HALF: its k-half 0) into `cur`, fully consumed:
+    //      DMA of stage s+2 into `cur`, fully consumed:
     //      certified by the barrier
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -813,7 +796,7 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
       for (int j = 0; j < 8; ++j) {
         mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
         if (ORD == 3 && i == 3 && j == 7) __builtin_amdgcn_s_barrier();
-        if ((ORD == 1 || ORD == 2) && !HALF) {
+        if (ORD == 1 || ORD == 2) {
           // halves of the k-step: slot t = (i & 3) * 4 + (j >> 1) on odd j
           const bool first = i < 4;
           if ((j & 1) == 1) {
@@ -835,30 +818,15 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
           if (r < 8) f0b[r] = lds_read_b128(nxt + b_base + r * SUB + off_k0);
           else f0a[r - 8] = lds_read_b128(nxt + a_base + (r - 8) * SUB + off_k0);
         }
-        if (ABL != 1) {
-          if (HALF) {
-            if ((j & 3) == 3) {
-              const int p = i * 2 + (j >> 2);
-              if (p < 4) dma_a.issue(cur, p, kbytes(s + 2), wave_s, 0);
-              else if (p < 8) dma_b.issue(cur + W4B_OP_BYTES, p - 4, kbytes(s + 2), wave_s, 0);
-            }
-          } else if ((j & 3) == 3) {
-            const int p = i * 2 + (j >> 2);   // 0..15
-            if (p < 8) dma_a.issue(cur, p, kbytes(s + 2), wave_s);
-            else dma_b.issue(cur + W4B_OP_BYTES, p - 8, kbytes(s + 2), wave_s);
-          }
+        if (ABL != 1 && (j & 3) == 3) {
+          const int p = i * 2 + (j >> 2);   // 0..15
+          if (p < 8) dma_a.issue(cur, p, kbytes(s + 2), wave_s);
+          else dma_b.issue(cur + W4B_OP_BYTES, p - 8, kbytes(s + 2), wave_s);
         }
       }
     }
     __builtin_amdgcn_s_setprio(0);
     if constexpr (ABL == 5) seg2 += stamp() - t2;
-    if constexpr (HALF) {
-      // k-half 1 of stage s+1 (issued in s.0) must be visible before (s+1).0
-      // prefetches it; the 8 pieces just issued stay in flight
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      if (ABL != 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   if constexpr (ABL == 5) {
@@ -871,6 +839,180 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   } else {
     (void)seg0; (void)seg1; (void)seg2; (void)t0;
   }
+
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + crow;
+    uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 128 + ccol;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4_t v = acc[i][j];
+      uint2 pk;
+      pk.x = mxk::pack2bf(v[0], v[1]);
+      pk.y = mxk::pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Schedule 16 ("w4q"): the w4b tile and MFMA stream on a 4-deep ring of
+// 32-deep k-steps (4 x 32 KiB LDS) instead of 2 x 64-deep stages.  Every
+// k-step issues 8 LDS-DMA pieces per wave (one per 8 MFMAs) for the stage 4
+// k-steps ahead, so
+//   * the texture path sees a uniform 8 pieces per k-step instead of 16
+//     every other k-step (the diagnostic stamps put +300 cycles on the
+//     DMA-carrying k-step of w4b), and
+//   * a piece has ~2.5 k-steps to land instead of ~1.5;
+// at the price of one barrier per k-step (the waves run in near lockstep).
+// Stage image: 16-row x 64-B pieces, chunk c of row r at c ^ h((r >> 2) & 3)
+// (conflict-free b128 reads: tests/test_gemm_swizzle.py::test_w4b_half_*).
+namespace {
+constexpr int W4Q_OP_BYTES = 256 * 64;               // 16 KiB per operand per k-step
+constexpr int W4Q_STAGE_BYTES = 2 * W4Q_OP_BYTES;    // 32 KiB
+constexpr int W4Q_RING = 4;
+
+template <int CP>
+struct DmaRing32 {
+  static constexpr int AUX = CP & 31;
+  const char* base;
+  uint32_t bytes;
+  uint32_t voff[4];   // piece g = 4p + wave: rows 16g .. 16g+15
+  __device__ __forceinline__ void issue(char* lds_op, int p, int k_bytes, int wave_s) const {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(base + k_bytes), 0, static_cast<int>(bytes), 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(lds_op + (p * 4 + wave_s) * 1024), 16,
+                                             voff[p], 0, 0, AUX);
+  }
+};
+
+template <int CP>
+__device__ __forceinline__ DmaRing32<CP> make_ring32(const uint16_t* src, int ld, int row0, int lane,
+                                                     int wave) {
+  DmaRing32<CP> d;
+  const uint16_t* base = src + static_cast<size_t>(row0) * ld;
+  const int r = lane >> 2;                        // row within the 16-row piece
+  const int c = (lane & 3) ^ w4b_h((r >> 2) & 3);
+  const uint32_t lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
+  d.base = reinterpret_cast<const char*>(base);
+  d.bytes = static_cast<uint32_t>(256 * ld * 2);
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+    d.voff[p] = lane_off + static_cast<uint32_t>((p * 4 + wave) * 16 * ld * 2);
+  return d;
+}
+
+// One k-step: 64 MFMAs on (fa, fb); 16 reads of the next k-step's fragments
+// (one per 3 MFMAs, all retired well before the closing lgkmcnt(0)); 8 DMA
+// pieces of the stage 4 k-steps ahead into `dma_dst` (one per 8 MFMAs).
+template <int ABL, int CP>
+__device__ __forceinline__ void w4q_kstep(f32x4_t (&acc)[8][8], const bf16x8_t (&fa)[8],
+                                          const bf16x8_t (&fb)[8], bf16x8_t (&na)[8],
+                                          bf16x8_t (&nb)[8], const char* nxt, int a_base,
+                                          int b_base, int off, const DmaRing32<CP>& da,
+                                          const DmaRing32<CP>& db, char* dma_dst, int dma_k,
+                                          int wave_s) {
+  constexpr int SUB = 1024;
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mfma_16x16x32_agpr(acc[i][j], fb[j], fa[i]);
+      const int m = i * 8 + j;
+      if (ABL != 2 && m % 3 == 1 && m / 3 < 16) {
+        const int r = m / 3;
+        if (r < 8) nb[r] = lds_read_b128(nxt + b_base + r * SUB + off);
+        else na[r - 8] = lds_read_b128(nxt + a_base + (r - 8) * SUB + off);
+      }
+      if (ABL != 1 && m % 8 == 5) {
+        const int p = m / 8;
+        if (p < 4) da.issue(dma_dst, p, dma_k, wave_s);
+        else db.issue(dma_dst + W4Q_OP_BYTES, p - 4, dma_k, wave_s);
+      }
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+  // the next k-step DMAs into the buffer just read: every wave's reads must
+  // have retired; the stage read by the next k-step (issued two k-steps ago)
+  // must have landed
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  if (ABL != 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+}  // namespace
+
+template <int ABL = 0, int CP = 32>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4q(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[W4Q_RING * W4Q_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave >> 1;
+  const int wn = wave & 1;
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int wgid = mxk::xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  const DmaRing32<CP> da = make_ring32<CP>(A, lda, m0, lane, wave_s);
+  const DmaRing32<CP> db = make_ring32<CP>(Bt, ldb, n0, lane, wave_s);
+
+  const int frow = lane & 15;
+  const int off = frow * 64 + (((lane >> 4) ^ w4b_h(frow >> 2)) * 16);
+  constexpr int SUB = 1024;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4Q_OP_BYTES + wn * 8 * SUB;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / 32;   // even: K % 64 == 0
+  // past the end the DMA re-reads the last k-step into a consumed buffer, so
+  // every k-step issues the same number of pieces (uniform vmcnt arithmetic)
+  auto kbytes = [&](int t) { return (t < nk ? t : nk - 1) * 64; };
+  auto stage = [&](int t) { return smem + (t & (W4Q_RING - 1)) * W4Q_STAGE_BYTES; };
+#pragma unroll
+  for (int t = 0; t < W4Q_RING; ++t) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      da.issue(stage(t), p, kbytes(t), wave_s);
+      db.issue(stage(t) + W4Q_OP_BYTES, p, kbytes(t), wave_s);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // k-steps 0 and 1 landed
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off);
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // incl. scalar loads: exact LDS waits in the loop
+
+  for (int t = 0; t < nk; t += 2) {
+    // k-step t: buffer t % 4 was read during k-step t-1 (barrier-certified),
+    // so it takes the DMA of k-step t + 4
+    w4q_kstep<ABL, CP>(acc, f0a, f0b, f1a, f1b, stage(t + 1), a_base, b_base, off, da, db,
+                       stage(t), kbytes(t + 4), wave_s);
+    w4q_kstep<ABL, CP>(acc, f1a, f1b, f0a, f0b, stage(t + 2), a_base, b_base, off, da, db,
+                       stage(t + 1), kbytes(t + 5), wave_s);
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
   const int crow = lane & 15;
   const int ccol = (lane >> 4) * 4;
@@ -920,8 +1062,8 @@ mxk_gemm_bf16_tn_w4e(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   const int m0 = (first_m + in_group % gsize) * BM;
   const int n0 = (in_group / gsize) * BN;
 
-  const DmaStream64<false, CP> dma_a = make_dma64<false, CP>(A, lda, m0, lane, wave_s);
-  const DmaStream64<false, CP> dma_b = make_dma64<false, CP>(Bt, ldb, n0, lane, wave_s);
+  const DmaStream64<CP> dma_a = make_dma64<CP>(A, lda, m0, lane, wave_s);
+  const DmaStream64<CP> dma_b = make_dma64<CP>(Bt, ldb, n0, lane, wave_s);
 
   const int frow = lane & 15;
   const int fch = (lane >> 4) ^ (frow >> 1);
@@ -1032,7 +1174,7 @@ mxk_gemm_bf16_tn_w4e(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 constexpr int W8B_THREADS = 512;
 
 template <int CP>
-__device__ __forceinline__ void w8b_issue(const DmaStream64<false, CP>& d, char* lds_op, int p,
+__device__ __forceinline__ void w8b_issue(const DmaStream64<CP>& d, char* lds_op, int p,
                                           int k_bytes, int wave_s) {
   const int g = p * 8 + wave_s;
   __builtin_amdgcn_raw_ptr_buffer_load_lds(d.rsrc, (lds_void*)(lds_op + g * 1024), 16, d.lane_off,
@@ -1062,8 +1204,8 @@ mxk_gemm_bf16_tn_w8b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 
   // DMA pieces g = p*8 + wave (p = 0..3), rows 8g .. 8g+7 -> LDS g*1024;
   // (row >> 1) & 7 = (4 (wave & 1) + (r >> 1)) & 7, so w4b's lane offsets hold
-  const DmaStream64<false, CP> dma_a = make_dma64<false, CP>(A, lda, m0, lane, wave_s);
-  const DmaStream64<false, CP> dma_b = make_dma64<false, CP>(Bt, ldb, n0, lane, wave_s);
+  const DmaStream64<CP> dma_a = make_dma64<CP>(A, lda, m0, lane, wave_s);
+  const DmaStream64<CP> dma_b = make_dma64<CP>(Bt, ldb, n0, lane, wave_s);
 
   const int frow = lane & 15;
   const int fch = (lane >> 4) ^ (frow >> 1);
@@ -1225,9 +1367,12 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // Host launchers (C ABI, stream-ordered, capture-safe: no sync, no malloc).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kDefaultVariant = 6;
-constexpr int kNumVariants = 13;
-constexpr int kFirstAblation = 9;   // variants >= this produce wrong outputs (timing only)
+constexpr int kDefaultVariant = 13;
+constexpr int kNumVariants = 18;
+// timing ablations and stamp builds: wrong outputs or perturbed schedules
+__host__ __device__ constexpr bool is_ablation(int v) {
+  return (v >= 9 && v <= 12) || v == 14 || v == 17;
+}
 
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
                 int N, int K, int lda, int ldb, int ldc) {
@@ -1241,13 +1386,18 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 3: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4<4, 0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 4: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8<4>), dim3(nwg), dim3(W8_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 5: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 6: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, false, 0, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 6: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, 0, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 7: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w8b<0>), dim3(nwg), dim3(W8B_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 8: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4e<32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 9: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 10: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<2>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 11: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<3>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    default: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<5, false, 0, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 12: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<5, 0, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 13: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, 4, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 14: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<5, 4, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 15: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, 5, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 16: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4q<0, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 17: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4q<1, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
   }
 }
 }  // namespace
@@ -1274,7 +1424,7 @@ MXK_API int mxk_gemm_bf16_stamps(unsigned long long* out, int reset) {
   }
   return static_cast<int>(e);
 }
-MXK_API int mxk_gemm_bf16_tn_first_ablation(void) { return kFirstAblation; }
+MXK_API int mxk_gemm_bf16_tn_is_ablation(int variant) { return is_ablation(variant) ? 1 : 0; }
 
 MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,
                              int lda, int ldb, int ldc, hipStream_t stream) {

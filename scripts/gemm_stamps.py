@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Share of each k-iteration segment of the default GEMM schedule (diagnostic
-build = variant 12 with s_memtime stamps): k-step 0, wait + barrier, k-step 1."""
+build = variant 12 with s_memtime stamps; STAMP_VARIANT=14 stamps schedule 13): k-step 0, wait + barrier, k-step 1."""
 import ctypes
 import json
 import os
@@ -14,6 +14,7 @@ from mxk8s.ops import _lib  # noqa: E402
 
 def main():
     n = int(os.environ.get("SIZE", 8192))
+    variant = int(os.environ.get("STAMP_VARIANT", 12))
     dev = torch.device("cuda")
     L = _lib.lib()
     L.mxk_gemm_bf16_stamps.restype = ctypes.c_int
@@ -24,13 +25,13 @@ def main():
     C = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
     out = (ctypes.c_ulonglong * 4)()
     for _ in range(20):
-        L.mxk_gemm_bf16_tn_variant(A.data_ptr(), B.data_ptr(), C.data_ptr(), n, n, n, n, n, n, 12,
+        L.mxk_gemm_bf16_tn_variant(A.data_ptr(), B.data_ptr(), C.data_ptr(), n, n, n, n, n, n, variant,
                                    _lib.stream_ptr(dev))
     torch.cuda.synchronize()
     _lib.check(L.mxk_gemm_bf16_stamps(out, 1), "stamps reset")
     iters = 50
     for _ in range(iters):
-        L.mxk_gemm_bf16_tn_variant(A.data_ptr(), B.data_ptr(), C.data_ptr(), n, n, n, n, n, n, 12,
+        L.mxk_gemm_bf16_tn_variant(A.data_ptr(), B.data_ptr(), C.data_ptr(), n, n, n, n, n, n, variant,
                                    _lib.stream_ptr(dev))
     torch.cuda.synchronize()
     _lib.check(L.mxk_gemm_bf16_stamps(out, 0), "stamps read")
@@ -39,7 +40,7 @@ def main():
     waves = out[3]
     ksteps = waves * (n // 64)
     print("RESULT " + json.dumps({
-        "size": n, "waves": waves,
+        "size": n, "variant": variant, "waves": waves,
         "share_kstep0": round(seg[0] / tot, 4), "share_wait_barrier": round(seg[1] / tot, 4),
         "share_kstep1": round(seg[2] / tot, 4),
         "cycles_per_kiter": {"kstep0": round(seg[0] / ksteps, 1), "wait_barrier": round(seg[1] / ksteps, 1),
