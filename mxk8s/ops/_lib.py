@@ -51,6 +51,8 @@ _SIGNATURES = {
     "mxk_grad_sumsq": (_i, [_vp, _l, _vp, _vp, _vp]),
     "mxk_clip_scale_from_sumsq": (_i, [_vp, _f, _f, _vp, _vp]),
     "mxk_attn_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _l, _l, _l, _f, _i, _vp]),
+    "mxk_attn_fwd_variant": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _l, _l, _l, _f, _i, _i,
+                                  _vp]),
     "mxk_attn_bwd_workspace": (_l, [_i, _i, _i]),
     "mxk_attn_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i,
                           _l, _l, _l, _l, _l, _f, _i, _vp]),

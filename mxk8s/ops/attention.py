@@ -52,16 +52,20 @@ def attention_ref(q, k, v, causal: bool = True, scale: float | None = None) -> t
     return o.transpose(1, 2).to(q.dtype)
 
 
-def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None):
-    """HIP forward: returns (o [B,S,Hq,D] bf16, lse [B,Hq,S] fp32)."""
+def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None, variant: int = 2):
+    """HIP forward: returns (o [B,S,Hq,D] bf16, lse [B,Hq,S] fp32).
+
+    ``variant`` 2 (default) feeds K/V by LDS-DMA, 1 is the same with the
+    loop unrolled by two, 0 stages K/V through registers (A/B runs)."""
     B, S, Hq, D = q.shape
     Hkv = k.shape[2]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     o = torch.empty((B, S, Hq, D), dtype=q.dtype, device=q.device)
     lse = torch.empty((B, Hq, S), dtype=torch.float32, device=q.device)
-    st = _lib.lib().mxk_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
-                                 lse.data_ptr(), B, S, Hq, Hkv, D, q.stride(1), k.stride(1),
-                                 v.stride(1), float(scale), int(causal), _lib.stream_ptr(q.device))
+    st = _lib.lib().mxk_attn_fwd_variant(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                         lse.data_ptr(), B, S, Hq, Hkv, D, q.stride(1),
+                                         k.stride(1), v.stride(1), float(scale), int(causal),
+                                         int(variant), _lib.stream_ptr(q.device))
     _lib.check(st, "mxk_attn_fwd")
     return o, lse
 

@@ -27,6 +27,8 @@
 // strides (so q/k/v can be views of the fused QKV projection), o
 // [B, S, Hq, 128] contiguous, lse [B, Hq, S] fp32 (natural log of the row's
 // sum of exp(scale * s)) for the backward pass.
+#include <type_traits>
+
 #include "mx_common.h"
 
 namespace {
@@ -281,26 +283,272 @@ mxk_attn_fwd_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-MXK_API int mxk_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B,
-                         int S, int Hq, int Hkv, int head_dim, long q_tok, long k_tok, long v_tok,
-                         float scale, int causal, hipStream_t stream) {
+// Forward, DMA-fed (the default): the same math and LDS image, but
+//   * K/V tiles land in LDS by LDS-DMA (`buffer_load ... lds`, swizzle applied
+//     on the source address) issued at the top of the iteration for the next
+//     tile: no staging VGPRs, no ds_writes, and no 64-bit address arithmetic
+//     per tile (one SGPR offset);
+//   * the per-lane LDS read offsets of K (8) and V (8) are loop invariants;
+//   * scale-and-shift and the row sum use packed fp32 (v_pk_fma_f32,
+//     v_pk_add_f32), halving the softmax's full-rate VALU work.
+// Requires S * token_stride * 2 < 2^32 for K and V (buffer offsets).
+namespace {
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+}
+
+template <bool CAUSAL, bool UNROLL>
+__global__ void __launch_bounds__(NT, 2)
+mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                        const uint16_t* __restrict__ v, uint16_t* __restrict__ o,
+                        float* __restrict__ lse, int S, int Hq, int Hkv, long q_tok, long k_tok,
+                        long v_tok, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2 * TILE_BYTES];   // [buf][K | V]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  const int nqb = S / BQ;
+  int bh, qb;
+  map_block(blockIdx.x, gridDim.x / nqb, nqb, CAUSAL, &bh, &qb);
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hkv = hq / (Hq / Hkv);
+  const int q0 = qb * BQ;
+  const int qw0 = q0 + wave * 32;
+  const int myq = qw0 + r32;
+
+  const uint16_t* qb_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
+  const uint16_t* kb_ptr = k + static_cast<long>(b) * S * k_tok + static_cast<long>(hkv) * D;
+  const uint16_t* vb_ptr = v + static_cast<long>(b) * S * v_tok + static_cast<long>(hkv) * D;
+
+  bf16x8_t qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    qf[s] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + static_cast<long>(myq) * q_tok + 16 * s + 8 * h);
+
+  const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
+  const int nkv = kv_end / BKV;
+
+  // DMA: wave w moves the 1-KiB pieces g = 4w + p (rows 4g .. 4g+3) of K and
+  // V; lane i lands at row 4g + (i >> 4), slot i & 15, so it fetches chunk
+  // (i & 15) ^ f(row) with f(row) = (row & 3) << 2 | (row >> 2) & 3
+  // = (i >> 4) << 2 | p.
+  const mxk::u32x4 rk = mxk::make_rsrc(kb_ptr, static_cast<unsigned>(S * k_tok * 2));
+  const mxk::u32x4 rv = mxk::make_rsrc(vb_ptr, static_cast<unsigned>(S * v_tok * 2));
+  const int prow = lane >> 4, pslot = lane & 15;
+  uint32_t kvo[4], vvo[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int row = 4 * (4 * wave + p) + prow;
+    const int ch = pslot ^ ((prow << 2) | p);
+    kvo[p] = static_cast<uint32_t>(row * k_tok * 2 + ch * 16);
+    vvo[p] = static_cast<uint32_t>(row * v_tok * 2 + ch * 16);
+  }
+  const uint32_t k_step = static_cast<uint32_t>(BKV * k_tok * 2);
+  const uint32_t v_step = static_cast<uint32_t>(BKV * v_tok * 2);
+  auto issue = [&](int j, int buf) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      mxk::dma16(rk, smem[buf] + (4 * wave + p) * 1024, kvo[p], j * k_step);
+      mxk::dma16(rv, smem[buf] + TILE_BYTES + (4 * wave + p) * 1024, vvo[p], j * v_step);
+    }
+  };
+  issue(0, 0);
+
+  // loop-invariant LDS read offsets: K rows r32 (+32 rows = +8 KiB), chunk
+  // 2s + h; V transposed reads at keys tr_key (+8), chunk 4db + tr_ch, with
+  // +16 keys = +4 KiB per k-step
+  int koff[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) koff[s] = swz(r32, 2 * s + h);
+  const int G = lane >> 4, i16 = lane & 15;
+  const int tr_key = 4 * h + (i16 >> 2);
+  const int tr_ch = 2 * (G & 1) + ((i16 & 3) >> 1);
+  const int tr_byte = 8 * (i16 & 1);
+  int voff[4][2];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    voff[db][0] = swz(tr_key, 4 * db + tr_ch) + tr_byte;
+    voff[db][1] = swz(tr_key + 8, 4 * db + tr_ch) + tr_byte;
+  }
+
+  const float c = scale * 1.4426950408889634f;   // scores -> log2 domain
+  const f32x2_t cc = {c, c};
+  float m = -INFINITY, l = 0.f;
+  f32x16_t acc[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[db][r] = 0.f;
+
+  // Consume the Q fragments here: the compiler then waits for their loads
+  // before the loop instead of placing vmcnt waits inside it, where they
+  // would also wait for the next tile's (untracked) DMA.
+#pragma unroll
+  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile 0
+  __syncthreads();
+
+  // the loop body; UNROLL makes the LDS buffer a compile-time constant (read
+  // addresses are then loop-invariant VGPRs + immediate offsets)
+  auto step = [&](int j, int buf) {
+    // buffer buf^1 was last read in iteration j-1 (barrier-certified)
+    if (j + 1 < nkv) issue(j + 1, buf ^ 1);
+    const int kv0 = j * BKV;
+    const bool active = !CAUSAL || kv0 <= qw0 + 31;
+    if (active) {
+      const char* kt = smem[buf];
+      const char* vt = smem[buf] + TILE_BYTES;
+      f32x16_t s0, s1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const bf16x8_t a0 = lds_b128(kt + koff[s]);
+        const bf16x8_t a1 = lds_b128(kt + koff[s] + 32 * 256);
+        s0 = mfma32(a0, qf[s], s0);
+        s1 = mfma32(a1, qf[s], s1);
+      }
+      if (CAUSAL && kv0 + BKV - 1 > qw0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kv0 + crow(r, h);
+          if (key > myq) s0[r] = -INFINITY;
+          if (key + 32 > myq) s1[r] = -INFINITY;
+        }
+      }
+      float mx = s0[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s0[r]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s1[r]);
+      mx = half_max(mx);
+      const float m_new = fmaxf(m, mx);
+      const float alpha = fexp2((m - m_new) * c);
+      m = m_new;
+      const f32x2_t nmc = {-m_new * c, -m_new * c};
+      f32x2_t ls2 = {0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        f32x2_t x0 = {s0[r], s0[r + 1]};
+        f32x2_t x1 = {s1[r], s1[r + 1]};
+        x0 = __builtin_elementwise_fma(x0, cc, nmc);
+        x1 = __builtin_elementwise_fma(x1, cc, nmc);
+        x0[0] = fexp2(x0[0]);
+        x0[1] = fexp2(x0[1]);
+        x1[0] = fexp2(x1[0]);
+        x1[1] = fexp2(x1[1]);
+        ls2 += x0 + x1;
+        s0[r] = x0[0];
+        s0[r + 1] = x0[1];
+        s1[r] = x1[0];
+        s1[r + 1] = x1[1];
+      }
+      l = l * alpha + (ls2[0] + ls2[1]);
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[db][r] *= alpha;
+      }
+      bf16x8_t pf[4];
+      pf[0] = pack8(s0, 0);
+      pf[1] = pack8(s0, 8);
+      pf[2] = pack8(s1, 0);
+      pf[3] = pack8(s1, 8);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const bf16x4_t lo = lds_tr_b64(vt + voff[db][0] + ks * 4096);
+          const bf16x4_t hi = lds_tr_b64(vt + voff[db][1] + ks * 4096);
+          acc[db] = mfma32(cat8(lo, hi), pf[ks], acc[db]);
+        }
+      }
+    }
+    // tile j+1 (own pieces) landed; the barrier publishes every wave's pieces
+    // and certifies that buffer buf is no longer read
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  if constexpr (UNROLL) {
+    for (int j = 0; j < nkv; j += 2) {
+      step(j, 0);
+      if (j + 1 < nkv) step(j + 1, 1);
+    }
+  } else {
+    for (int j = 0; j < nkv; ++j) step(j, j & 1);
+  }
+
+  const float lt = half_sum(l);
+  const float inv = 1.f / lt;
+  uint16_t* orow = o + (static_cast<long>(b) * S + myq) * Hq * D + static_cast<long>(hq) * D;
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * db + 8 * g + 4 * h;
+      uint2 pk;
+      pk.x = mxk::pack2bf(acc[db][4 * g] * inv, acc[db][4 * g + 1] * inv);
+      pk.y = mxk::pack2bf(acc[db][4 * g + 2] * inv, acc[db][4 * g + 3] * inv);
+      *reinterpret_cast<uint2*>(orow + d) = pk;
+    }
+  }
+  if (h == 0) lse[(static_cast<long>(b) * Hq + hq) * S + myq] = m * scale + logf(lt);
+}
+
+// ---------------------------------------------------------------------------
+// variant: 0 = register-staged K/V, 1 = LDS-DMA with the loop unrolled by 2
+// (static LDS buffer), 2 = LDS-DMA (default).  1 and 2 fall back to 0 when a
+// K/V panel exceeds the 32-bit buffer range.  B=8 Llama shape: 0.42 / 0.43 /
+// 0.38 ms (profiles/r1_attention/).
+MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, void* o, float* lse,
+                                 int B, int S, int Hq, int Hkv, int head_dim, long q_tok,
+                                 long k_tok, long v_tok, float scale, int causal, int variant,
+                                 hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv ||
-      q_tok % 8 || k_tok % 8 || v_tok % 8 ||
+      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 2 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) % 16)
     return static_cast<int>(hipErrorInvalidValue);
   const int nwg = B * Hq * (S / BQ);
-  if (causal)
-    hipLaunchKernelGGL(mxk_attn_fwd_kernel<true>, dim3(nwg), dim3(NT), 0, stream,
-                       static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k),
-                       static_cast<const uint16_t*>(v), static_cast<uint16_t*>(o), lse, S, Hq, Hkv,
-                       q_tok, k_tok, v_tok, scale);
-  else
-    hipLaunchKernelGGL(mxk_attn_fwd_kernel<false>, dim3(nwg), dim3(NT), 0, stream,
-                       static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k),
-                       static_cast<const uint16_t*>(v), static_cast<uint16_t*>(o), lse, S, Hq, Hkv,
-                       q_tok, k_tok, v_tok, scale);
+  const long span = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
+  if (variant != 0 && span >= (1L << 32)) variant = 0;
+  const auto* qp = static_cast<const uint16_t*>(q);
+  const auto* kp = static_cast<const uint16_t*>(k);
+  const auto* vp = static_cast<const uint16_t*>(v);
+  auto* op = static_cast<uint16_t*>(o);
+  if (variant == 1) {
+    if (causal)
+      hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<true, true>), dim3(nwg), dim3(NT), 0, stream, qp,
+                         kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    else
+      hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<false, true>), dim3(nwg), dim3(NT), 0, stream, qp,
+                         kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  } else if (variant == 2) {
+    if (causal)
+      hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<true, false>), dim3(nwg), dim3(NT), 0, stream, qp,
+                         kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    else
+      hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<false, false>), dim3(nwg), dim3(NT), 0, stream,
+                         qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  } else {
+    if (causal)
+      hipLaunchKernelGGL(mxk_attn_fwd_kernel<true>, dim3(nwg), dim3(NT), 0, stream, qp, kp, vp, op,
+                         lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    else
+      hipLaunchKernelGGL(mxk_attn_fwd_kernel<false>, dim3(nwg), dim3(NT), 0, stream, qp, kp, vp,
+                         op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  }
   MXK_RETURN_LAUNCH_STATUS();
+}
+
+MXK_API int mxk_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B,
+                         int S, int Hq, int Hkv, int head_dim, long q_tok, long k_tok, long v_tok,
+                         float scale, int causal, hipStream_t stream) {
+  return mxk_attn_fwd_variant(q, k, v, o, lse, B, S, Hq, Hkv, head_dim, q_tok, k_tok, v_tok,
+                              scale, causal, 2, stream);
 }
 
 // ===========================================================================

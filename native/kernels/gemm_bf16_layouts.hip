@@ -39,34 +39,9 @@ __device__ __forceinline__ void xmfma(f32x4_t& acc, bf16x8_t a, bf16x8_t b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-// LDS-DMA piece (16 B per lane, `buffer_load_dwordx4 ... offen lds`) issued
-// through inline asm: the compiler then sees no pending LDS write, so it does
-// not put an `s_waitcnt vmcnt(0)` in front of every ds_read_b64_tr_b16 (it
-// cannot prove the transposed reads do not alias the DMA and serialises
-// them, 2-4x slower).  Ordering is ours: counted vmcnt + s_barrier below.
-// M0 is compiler-owned: saved and restored around the load.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4 make_rsrc(const void* base, unsigned bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  u32x4 r;
-  r[0] = static_cast<unsigned>(a);
-  r[1] = static_cast<unsigned>(a >> 32);   // stride 0
-  r[2] = bytes;                            // num_records
-  r[3] = 0x00020000u;
-  return r;
-}
-__device__ __forceinline__ void dma16(const u32x4& rsrc, const char* lds, uint32_t voff,
-                                      uint32_t soff) {
-  const uint32_t m = __builtin_amdgcn_readfirstlane(
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds)));
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(m), "v"(voff), "s"(rsrc), "s"(soff)
-      : "memory");
-}
+using mxk::u32x4;
+using mxk::make_rsrc;
+using mxk::dma16;
 
 __device__ __forceinline__ bf16x4_t tr_b64(const char* p) {
   typedef short s4 __attribute__((ext_vector_type(4)));

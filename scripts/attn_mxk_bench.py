@@ -32,7 +32,7 @@ def bench(fn, iters=30):
 
 def main():
     dev = torch.device("cuda")
-    B, Hq, Hk, S, D = 1, 32, 8, int(os.environ.get("SEQ", 2048)), 128
+    B, Hq, Hk, S, D = int(os.environ.get("BATCH", 1)), 32, 8, int(os.environ.get("SEQ", 2048)), 128
     g = torch.Generator(device=dev).manual_seed(0)
     q = torch.randn(B, S, Hq, D, device=dev, generator=g).bfloat16()
     k = torch.randn(B, S, Hk, D, device=dev, generator=g).bfloat16()
@@ -40,6 +40,8 @@ def main():
     flops_fwd = 4 * B * Hq * S * S * D / 2
     res = {}
     res["mxk_fwd"] = bench(lambda: A.attn_fwd(q, k, v, causal=True))
+    res["mxk_fwd_v0"] = bench(lambda: A.attn_fwd(q, k, v, causal=True, variant=0))
+    res["mxk_fwd_v2"] = bench(lambda: A.attn_fwd(q, k, v, causal=True, variant=2))
     qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
     with torch.no_grad():
         res["sdpa_fwd"] = bench(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=True,
@@ -56,7 +58,7 @@ def main():
     res["sdpa_fwd_bwd"] = bench(sdpa_fb)
     res["mxk_fwd_bwd"] = res["mxk_fwd"] + res["mxk_bwd"]
     # useful FLOPs: fwd 2 products, bwd 5 products (causal halves all)
-    mult = {"mxk_fwd": 1.0, "sdpa_fwd": 1.0, "mxk_bwd": 2.5, "sdpa_fwd_bwd": 3.5, "mxk_fwd_bwd": 3.5}
+    mult = {"mxk_fwd": 1.0, "mxk_fwd_v0": 1.0, "mxk_fwd_v2": 1.0, "sdpa_fwd": 1.0, "mxk_bwd": 2.5, "sdpa_fwd_bwd": 3.5, "mxk_fwd_bwd": 3.5}
     for name, ms in res.items():
         print("RESULT " + json.dumps({"kernel": name, "ms": round(ms, 4), "S": S,
                                       "tflops": round(mult[name] * flops_fwd / ms / 1e9, 1)}),

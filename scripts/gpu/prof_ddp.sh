@@ -8,5 +8,5 @@ export TMPDIR=/tmp
 export PYTHONPATH=$R${PYTHONPATH:+:$PYTHONPATH}
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_ddp -o run -- \
-  python3 $R/bench.py --mode ddp --steps 4 --warmup 2 > $R/gpurun_out/prof_ddp.log 2>&1
+  python3 $R/bench.py --mode ddp --steps ${STEPS:-4} --warmup 2 > $R/gpurun_out/prof_ddp.log 2>&1
 rc=$?; echo "prof rc=$rc"; tail -2 $R/gpurun_out/prof_ddp.log; exit $rc

@@ -28,10 +28,11 @@ def _qkv(B, S, Hq, Hkv, dev, seed=0, fused=False):
     (1, 384, 4, 4, False, False),
     (1, 256, 4, 1, False, True),
 ])
-def test_attn_fwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_attn_fwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused, variant):
     q, k, v = _qkv(B, S, Hq, Hkv, cuda_device, fused=fused)
     assert A.supported(q, k, v)
-    o, lse = A.attn_fwd(q, k, v, causal=causal)
+    o, lse = A.attn_fwd(q, k, v, causal=causal, variant=variant)
     ref = A.attention_ref(q, k, v, causal=causal)
     err = (o.float() - ref.float()).abs().max().item()
     assert err < 2e-2, err
