@@ -105,8 +105,10 @@ def gpu_node(root: str, node: int, idx: int, bdf: str, numa: int, cpu_node_id: i
     _w(root, f"{pci}/numa_node", f"{numa}\n")
     _w(root, f"{pci}/vendor", f"0x{vendor:04x}\n")
     _w(root, f"{pci}/device", f"0x{device:04x}\n")
-    os.makedirs(os.path.join(root, pci, "drm", f"card{idx + 1}"), exist_ok=True)
-    os.makedirs(os.path.join(root, pci, "drm", f"renderD{128 + idx}"), exist_ok=True)
+    # a uevent file in each drm child keeps the directory alive in git
+    # (git drops empty directories, and discovery keys off their names)
+    _w(root, f"{pci}/drm/card{idx + 1}/uevent", f"MAJOR=226\nMINOR={idx + 1}\n")
+    _w(root, f"{pci}/drm/renderD{128 + idx}/uevent", f"MAJOR=226\nMINOR={128 + idx}\n")
     if render:
         _w(root, f"dev/dri/renderD{128 + idx}", "")
     _w(root, f"dev/dri/card{idx + 1}", "")
