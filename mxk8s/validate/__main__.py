@@ -98,7 +98,7 @@ def test_gemm(sizes: str, gpus: int) -> bool:
 def test_gemm_profile(sizes: str, out_dir: str) -> bool:
     from . import profile
     try:
-        summary = profile.profile_gemm(sizes.split(",")[0], out_dir)
+        summary = profile.profile_gemm(sizes.split(",")[0], out_dir, filt="gemm")
     except (RuntimeError, OSError, subprocess.TimeoutExpired) as e:
         emit({"test": "gemm_profile", "pass": False, "error": str(e)[-500:]})
         return False

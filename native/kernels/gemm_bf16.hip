@@ -678,7 +678,47 @@ __device__ __forceinline__ unsigned long long stamp() {
   return t;
 }
 
-template <int ABL = 0, int ORD = 0, int CP = 0>
+// Block -> 256x256 output tile.
+//  MAP 0: XCD remap + GROUP_M column sweep (each XCD owns GROUP_M tile rows
+//         and walks the columns; chip-wide every A panel is live at once).
+//  MAP 1: XCD-aware super-blocks.  The 8 XCDs x 32 CUs = 256 resident
+//         workgroups cover one 16x16-tile super-block per "round"; XCD x
+//         takes the 8 (M) x 4 (N) sub-block (x >> 2, x & 3) of it, so an XCD's
+//         L2 serves 12 panels to 32 tiles (the 81 % reuse of MAP 0) while the
+//         chip as a whole touches only 16 A + 16 B panels per round (Infinity
+//         Cache-sized at 16384^2) instead of every A panel.  Rounds snake over
+//         the super-block grid so consecutive rounds share their A panels.
+//         Needs tiles_m % 16 == tiles_n % 16 == 0; MAP 0 otherwise.
+template <int MAP>
+__device__ __forceinline__ void w4b_tile(int bid, int nwg, int tiles_m, int tiles_n, int* m0,
+                                         int* n0) {
+  if (MAP == 1 && (tiles_m & 15) == 0 && (tiles_n & 15) == 0) {
+    const int xcd = bid & 7, l = bid >> 3;
+    const int round = l >> 5, pos = l & 31;
+    const int sbn = tiles_n >> 4;
+    const int sm = round / sbn;
+    int sn = round - sm * sbn;
+    if (sm & 1) sn = sbn - 1 - sn;
+    *m0 = (sm * 16 + (xcd >> 2) * 8 + (pos & 7)) * BM;
+    *n0 = (sn * 16 + (xcd & 3) * 4 + (pos >> 3)) * BN;
+    return;
+  }
+  const int wgid = mxk::xcd_remap(bid, nwg);
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  *m0 = (first_m + in_group % gsize) * BM;
+  *n0 = (in_group / gsize) * BN;
+}
+
+// EPI 1: widened store tail (guide T21 with v_permlane16_swap): the bf16
+// quads of 16x16 tiles j and j+1 are exchanged between lane rows so every
+// lane holds 8 consecutive columns -> 32 global_store_dwordx4 per lane
+// instead of 64 dwordx2 (the tail is store-issue bound).  Needs ldc % 8 == 0
+// and a 16-B aligned C.
+template <int ABL = 0, int ORD = 0, int CP = 0, int MAP = 0, int EPI = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -691,14 +731,8 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   const int wn = wave & 1;
 
   const int tiles_m = M / BM, tiles_n = N / BN;
-  const int wgid = mxk::xcd_remap(blockIdx.x, gridDim.x);
-  const int per_group = GROUP_M * tiles_n;
-  const int group = wgid / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
-  const int in_group = wgid - group * per_group;
-  const int m0 = (first_m + in_group % gsize) * BM;
-  const int n0 = (in_group / gsize) * BN;
+  int m0, n0;
+  w4b_tile<MAP>(blockIdx.x, gridDim.x, tiles_m, tiles_n, &m0, &n0);
 
   const DmaStream64<CP> dma_a = make_dma64<CP>(A, lda, m0, lane, wave_s);
   const DmaStream64<CP> dma_b = make_dma64<CP>(Bt, ldb, n0, lane, wave_s);
@@ -841,19 +875,380 @@ mxk_gemm_bf16_tn_w4b(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   }
 
   const int crow = lane & 15;
-  const int ccol = (lane >> 4) * 4;
+  if constexpr (EPI == 1) {
+    // v_permlane16_swap(x, y): odd lane rows of x <-> even lane rows of y.
+    // Row q then holds tile j + (q & 1), columns (q >> 1) * 8 .. + 7.
+    const int q = lane >> 4;
+    const int ccol = (q & 1) * 16 + (q >> 1) * 8;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + crow;
-    uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 128 + ccol;
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + crow;
+      uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 128 + ccol;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f32x4_t v = acc[i][j];
-      uint2 pk;
-      pk.x = mxk::pack2bf(v[0], v[1]);
-      pk.y = mxk::pack2bf(v[2], v[3]);
-      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+      for (int j = 0; j < 8; j += 2) {
+        const uint32_t x0 = mxk::pack2bf(acc[i][j][0], acc[i][j][1]);
+        const uint32_t x1 = mxk::pack2bf(acc[i][j][2], acc[i][j][3]);
+        const uint32_t y0 = mxk::pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
+        const uint32_t y1 = mxk::pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        uint4 v;
+        v.x = s0[0];
+        v.y = s1[0];
+        v.z = s0[1];
+        v.w = s1[1];
+        *reinterpret_cast<uint4*>(cp + j * 16) = v;
+      }
     }
+  } else {
+    const int ccol = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + crow;
+      uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 128 + ccol;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const f32x4_t v = acc[i][j];
+        uint2 pk;
+        pk.x = mxk::pack2bf(v[0], v[1]);
+        pk.y = mxk::pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Schedule 22+ ("w4h"): the w4b tile, LDS image and DMA addressing on a
+// three-barrier K-tile — the structure of hipBLASLt's gfx950 MT256x256x64
+// kernel, read off its disassembly: the buffer X being consumed is refilled
+// IN PLACE with stage s+2 as soon as each operand's last fragment read of X
+// has retired, so the 16 DMA pieces spread over ~64 MFMAs and get ~130-200
+// MFMAs (instead of 64-128) to land.  Per K-tile, m = MFMA index 0..127:
+//   m  1..15  : A fragments of k-half 1 from X (8 reads)
+//   m  19     : lgkmcnt(0) + barrier #1   (X.A consumed by every wave)
+//   m 21..49  : B fragments of k-half 1 from X, one per 4 MFMAs
+//   m 23..51  : DMA of stage s+2, A pieces, into X.A
+//   m  55     : lgkmcnt(0) + barrier #2   (X.B consumed)
+//   m 57..85  : DMA of stage s+2, B pieces, into X.B
+//   m  91     : vmcnt(16) + barrier #3    (stage s+1 in Y landed everywhere)
+//   m 93..123 : k-half-0 fragments of stage s+1 from Y (B first, then A:
+//               the order the next K-tile's MFMAs consume them)
+// ---------------------------------------------------------------------------
+// Knobs (A/B variants): MO 1 = MFMA order j-outer (srcA fixed for 8 MFMAs,
+// as hipBLASLt's stream; next-k0 reads then A first).  LATE 1 = B pieces
+// every 6 MFMAs from m 57, barrier #3 after m 96 with vmcnt(15): the last
+// piece goes out after it (hipBLASLt waits vmcnt(13) with 3 pieces after).
+// PRIO 0 = no s_setprio around the MFMA stream.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N == 15 || N == 16, "vm_wait: add the count");
+  if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+}
+
+template <int MAP, int EPI, int MO = 0, int LATE = 0, int PRIO = 1>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4h(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  int m0, n0;
+  w4b_tile<MAP>(blockIdx.x, gridDim.x, tiles_m, tiles_n, &m0, &n0);
+  const DmaStream64<32> dma_a = make_dma64<32>(A, lda, m0, lane, wave_s);
+  const DmaStream64<32> dma_b = make_dma64<32>(Bt, ldb, n0, lane, wave_s);
+
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / BK;
+  auto kbytes = [&](int st) { return (st < ns ? st : ns - 1) * BK * 2; };
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_a.issue(smem + s * W4B_STAGE_BYTES, p, kbytes(s), wave_s);
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+      dma_b.issue(smem + s * W4B_STAGE_BYTES + W4B_OP_BYTES, p, kbytes(s), wave_s);
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // stage 0 (own pieces) landed
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
+  // drain everything (incl. kernel-argument scalar loads) so the compiler's
+  // per-register LDS waits inside the loop are exact counts
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+
+  constexpr int B3 = LATE ? 96 : 91;          // barrier #3 after MFMA B3
+  constexpr int BSP = LATE ? 6 : 4;           // B piece spacing from m 57
+  constexpr int NB3 = (B3 - 57) / BSP + 1 < 8 ? (B3 - 57) / BSP + 1 : 8;   // B pieces before it
+  for (int s = 0; s < ns; ++s) {
+    char* X = smem + (s & 1) * W4B_STAGE_BYTES;
+    char* Y = smem + ((s + 1) & 1) * W4B_STAGE_BYTES;
+    const int kb2 = kbytes(s + 2);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+          const int i = MO ? w : u, j = MO ? u : w;
+          const int m = h * 64 + u * 8 + w;
+          if (h == 0) mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
+          else mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
+          if (m < 16 && (m & 1)) f1a[m >> 1] = lds_read_b128(X + a_base + (m >> 1) * SUB + off_k1);
+          if (m == 19) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
+          }
+          if (m >= 20 && m < 52 && (m & 3) == 1)
+            f1b[(m - 21) >> 2] = lds_read_b128(X + b_base + ((m - 21) >> 2) * SUB + off_k1);
+          if (m >= 20 && m < 52 && (m & 3) == 3) dma_a.issue(X, (m - 23) >> 2, kb2, wave_s);
+          if (m == 55) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
+          }
+          if (m >= 57 && (m - 57) % BSP == 0 && (m - 57) / BSP < 8)
+            dma_b.issue(X + W4B_OP_BYTES, (m - 57) / BSP, kb2, wave_s);
+          if (m == B3) {
+            vm_wait<8 + NB3>();   // stage s+1 (last K-tile's pieces) landed
+            __builtin_amdgcn_s_barrier();
+          }
+          if (m > B3 && m < B3 + 32 && ((m - B3) & 1)) {
+            const int r = (m - B3 - 1) >> 1;   // 0..15
+            if (MO == 0) {
+              if (r < 8) f0b[r] = lds_read_b128(Y + b_base + r * SUB + off_k0);
+              else f0a[r - 8] = lds_read_b128(Y + a_base + (r - 8) * SUB + off_k0);
+            } else {
+              if (r < 8) f0a[r] = lds_read_b128(Y + a_base + r * SUB + off_k0);
+              else f0b[r - 8] = lds_read_b128(Y + b_base + (r - 8) * SUB + off_k0);
+            }
+          }
+        }
+      }
+    }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+  const int crow = lane & 15;
+  if constexpr (EPI == 1) {
+    const int q = lane >> 4;
+    const int ccol = (q & 1) * 16 + (q >> 1) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + crow;
+      uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 128 + ccol;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const uint32_t x0 = mxk::pack2bf(acc[i][j][0], acc[i][j][1]);
+        const uint32_t x1 = mxk::pack2bf(acc[i][j][2], acc[i][j][3]);
+        const uint32_t y0 = mxk::pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
+        const uint32_t y1 = mxk::pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        uint4 v;
+        v.x = s0[0];
+        v.y = s1[0];
+        v.z = s0[1];
+        v.w = s1[1];
+        *reinterpret_cast<uint4*>(cp + j * 16) = v;
+      }
+    }
+  } else {
+    const int ccol = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + crow;
+      uint16_t* cp = C + static_cast<size_t>(m) * ldc + n0 + wn * 128 + ccol;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const f32x4_t v = acc[i][j];
+        uint2 pk;
+        pk.x = mxk::pack2bf(v[0], v[1]);
+        pk.y = mxk::pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Schedule 21 ("w4p"): the default w4b schedule (ORD 4, VOFF DMA) made
+// persistent — one workgroup per CU walks tiles t = blockIdx.x + r * grid.
+// With one 128 KiB workgroup per CU a non-persistent grid leaves the CU idle
+// while a tile's store tail drains and the next workgroup refills two
+// stages; here the next tile's two prologue stages are issued into the
+// (barrier-certified) free LDS right BEFORE the current tile's widened store
+// tail (EPI 1), so the refill lands under the stores.  vmcnt bookkeeping at
+// the top of a tile: 32 DMA pieces then 32 stores are outstanding per wave;
+// vmcnt(48) retires exactly stage 0 (counts retire in issue order).
+// The grid is <= one workgroup per CU and every wave runs the same trip
+// count, so each wave reaches every barrier and the loop exits for all.
+template <int MAP>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4p(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int ntiles = tiles_m * tiles_n;
+
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
+  const int ns = K / BK;
+  auto kbytes = [&](int st) { return (st < ns ? st : ns - 1) * BK * 2; };
+
+  int t = blockIdx.x;
+  int m0, n0;
+  w4b_tile<MAP>(t, ntiles, tiles_m, tiles_n, &m0, &n0);
+  DmaStream64<32> dma_a = make_dma64<32>(A, lda, m0, lane, wave_s);
+  DmaStream64<32> dma_b = make_dma64<32>(Bt, ldb, n0, lane, wave_s);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      dma_a.issue(smem + s * W4B_STAGE_BYTES, p, kbytes(s), wave_s);
+      dma_b.issue(smem + s * W4B_STAGE_BYTES + W4B_OP_BYTES, p, kbytes(s), wave_s);
+    }
+  }
+  bool first = true;
+  while (true) {
+    if (first) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    f32x4_t acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+
+    for (int s = 0; s < ns; ++s) {
+      char* cur = smem + (s & 1) * W4B_STAGE_BYTES;
+      char* nxt = smem + ((s + 1) & 1) * W4B_STAGE_BYTES;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
+          const int m = i * 8 + j;
+          if (m % 3 == 1 && m / 3 < 16) {
+            const int r = m / 3;
+            if (r < 8) f1b[r] = lds_read_b128(cur + b_base + r * SUB + off_k1);
+            else f1a[r - 8] = lds_read_b128(cur + a_base + (r - 8) * SUB + off_k1);
+          }
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
+          if ((j & 3) == 1) {
+            const int r = i * 2 + (j >> 2);
+            if (r < 8) f0b[r] = lds_read_b128(nxt + b_base + r * SUB + off_k0);
+            else f0a[r - 8] = lds_read_b128(nxt + a_base + (r - 8) * SUB + off_k0);
+          }
+          if ((j & 3) == 3) {
+            const int p = i * 2 + (j >> 2);
+            if (p < 8) dma_a.issue(cur, p, kbytes(s + 2), wave_s);
+            else dma_b.issue(cur + W4B_OP_BYTES, p - 8, kbytes(s + 2), wave_s);
+          }
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+    // every wave's DMA landed and LDS reads retired: the LDS is free
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+
+    const int cm0 = m0, cn0 = n0;
+    const int tn = t + static_cast<int>(gridDim.x);
+    if (tn < ntiles) {
+      w4b_tile<MAP>(tn, ntiles, tiles_m, tiles_n, &m0, &n0);
+      dma_a = make_dma64<32>(A, lda, m0, lane, wave_s);
+      dma_b = make_dma64<32>(Bt, ldb, n0, lane, wave_s);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+          dma_a.issue(smem + s * W4B_STAGE_BYTES, p, kbytes(s), wave_s);
+          dma_b.issue(smem + s * W4B_STAGE_BYTES + W4B_OP_BYTES, p, kbytes(s), wave_s);
+        }
+      }
+    }
+
+    // widened store tail (EPI 1 of w4b)
+    const int crow = lane & 15;
+    const int q = lane >> 4;
+    const int ccol = (q & 1) * 16 + (q >> 1) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = cm0 + wm * 128 + i * 16 + crow;
+      uint16_t* cp = C + static_cast<size_t>(m) * ldc + cn0 + wn * 128 + ccol;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const uint32_t x0 = mxk::pack2bf(acc[i][j][0], acc[i][j][1]);
+        const uint32_t x1 = mxk::pack2bf(acc[i][j][2], acc[i][j][3]);
+        const uint32_t y0 = mxk::pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
+        const uint32_t y1 = mxk::pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        uint4 v;
+        v.x = s0[0];
+        v.y = s1[0];
+        v.z = s0[1];
+        v.w = s1[1];
+        *reinterpret_cast<uint4*>(cp + j * 16) = v;
+      }
+    }
+    if (tn >= ntiles) break;
+    t = tn;
+    first = false;
   }
 }
 
@@ -1367,11 +1762,43 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // Host launchers (C ABI, stream-ordered, capture-safe: no sync, no malloc).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kDefaultVariant = 13;
-constexpr int kNumVariants = 18;
+// w4h + XCD super-block map + widened stores; 22 (w4h, plain 8-B stores)
+// when C is not 16-B aligned or ldc % 8 != 0
+constexpr int kDefaultVariant = 24;
+constexpr int kDefaultVariantNarrowC = 22;
+constexpr int kNumVariants = 29;
 // timing ablations and stamp builds: wrong outputs or perturbed schedules
 __host__ __device__ constexpr bool is_ablation(int v) {
   return (v >= 9 && v <= 12) || v == 14 || v == 17;
+}
+
+// compute units of the current device (persistent grids: one workgroup per CU)
+int num_cus() {
+  static thread_local int dev_cached = -1, cus = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && dev != dev_cached) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      cus = n;
+    dev_cached = dev;
+  }
+  return cus;
+}
+
+// the default w4b schedule (ORD 4, VOFF DMA addressing) with tile map MAP and
+// epilogue EPI
+template <int MAP, int EPI>
+void launch_w4b(int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b, uint16_t* c,
+                int M, int N, int K, int lda, int ldb, int ldc) {
+  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, 4, 32, MAP, EPI>), dim3(nwg), dim3(W4_THREADS), 0,
+                     stream, a, b, c, M, N, K, lda, ldb, ldc);
+}
+
+template <int MAP, int EPI, int MO = 0, int LATE = 0, int PRIO = 1>
+void launch_w4h(int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b, uint16_t* c,
+                int M, int N, int K, int lda, int ldb, int ldc) {
+  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4h<MAP, EPI, MO, LATE, PRIO>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b,
+                     c, M, N, K, lda, ldb, ldc);
 }
 
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
@@ -1398,6 +1825,22 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 15: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4b<0, 5, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 16: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4q<0, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 17: hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4q<1, 32>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 18: launch_w4b<1, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 19: launch_w4b<0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 20: launch_w4b<1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 21: {
+      const int grid = nwg < num_cus() ? nwg : num_cus();
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4p<1>), dim3(grid), dim3(W4_THREADS), 0, stream, a, b,
+                         c, M, N, K, lda, ldb, ldc);
+      break;
+    }
+    case 22: launch_w4h<0, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 23: launch_w4h<0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 24: launch_w4h<1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 25: launch_w4h<1, 1, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 26: launch_w4h<1, 1, 0, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 27: launch_w4h<1, 1, 0, 0, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 28: launch_w4h<1, 1, 1, 1, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
   }
 }
 }  // namespace
@@ -1436,7 +1879,9 @@ MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int 
                     (reinterpret_cast<uintptr_t>(C) % 8 == 0);
   if (fast) {
     const int nwg = (M / BM) * (N / BN);
-    launch_256(kDefaultVariant, nwg, stream, A, Bt, C, M, N, K, lda, ldb, ldc);
+    const bool wide_c = (ldc % 8 == 0) && (reinterpret_cast<uintptr_t>(C) % 16 == 0);
+    launch_256(wide_c ? kDefaultVariant : kDefaultVariantNarrowC, nwg, stream, A, Bt, C, M, N, K,
+               lda, ldb, ldc);
   } else {
     dim3 grid((N + 63) / 64, (M + 63) / 64);
     hipLaunchKernelGGL(mxk_gemm_bf16_tn_generic, grid, dim3(256), 0, stream,

@@ -47,6 +47,40 @@ def test_gemm_fast_path_vs_fp32(cuda_device, M, N, K):
     assert err <= ref.abs().max().item() * 2 ** -7 + 1e-3, err
 
 
+def test_gemm_narrow_c_stride(cuda_device):
+    """ldc % 8 != 0 takes the 8-byte-store schedule (no widened dwordx4 tail)."""
+    M, N, K = 512, 512, 256
+    a = _rand((M, K), cuda_device, 21).bfloat16()
+    bt = _rand((N, K), cuda_device, 22).bfloat16()
+    buf = torch.zeros((M, N + 4), device=cuda_device, dtype=torch.bfloat16)
+    out = buf[:, :N]
+    gemm_bf16_tn(a, bt, out)
+    ref = a.float() @ bt.float().t()
+    assert (out.float() - ref).abs().max().item() <= ref.abs().max().item() * 2 ** -7 + 1e-3
+    assert torch.count_nonzero(buf[:, N:]) == 0   # nothing written past N
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 256), (1024, 768, 512)])
+def test_gemm_every_schedule_vs_fp32(cuda_device, M, N, K):
+    """Every non-ablation schedule of the 256x256 kernel; 4096^2 puts the
+    XCD super-block map (16x16 tiles) in play, 1024x768 its MAP-0 fallback."""
+    from mxk8s.ops import _lib
+    L = _lib.lib()
+    a = _rand((M, K), cuda_device, 23).bfloat16()
+    bt = _rand((N, K), cuda_device, 24).bfloat16()
+    ref = a.float() @ bt.float().t()
+    tol = ref.abs().max().item() * 2 ** -7 + 1e-3
+    for v in range(L.mxk_gemm_bf16_tn_num_variants()):
+        if L.mxk_gemm_bf16_tn_is_ablation(v):
+            continue
+        c = torch.full((M, N), float("nan"), device=cuda_device, dtype=torch.bfloat16)
+        st = L.mxk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
+                                        v, _lib.stream_ptr(cuda_device))
+        _lib.check(st, f"variant {v}")
+        err = (c.float() - ref).abs().max().item()
+        assert err <= tol, (v, err)
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (17, 33, 65), (100, 300, 200), (255, 257, 63)])
 def test_gemm_generic_path_vs_fp32(cuda_device, M, N, K):
     a = _rand((M, K), cuda_device, 7).bfloat16()
