@@ -1095,6 +1095,233 @@ mxk_gemm_bf16_tn_w4h(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// Schedule 29+ ("w4i"): w4h with the scalar work taken out of the K loop.
+// hipcc hoists the per-K-tile address arithmetic of w4h (stage-dependent
+// LDS bases for M0, the clamped k offset, a rebuilt buffer descriptor per
+// DMA stream) to the top of the loop, ~20 SALU ahead of the first MFMA
+// while the matrix pipe drains.  Here
+//  * the loop is unrolled by two, so X/Y (and every M0 value) are
+//    compile-time per parity;
+//  * the k step is the DMA's SGPR soffset on a fixed panel descriptor
+//    (one s_add per K-tile) instead of a new descriptor base per stage;
+//  * the last two K-tiles run without DMA (no clamped re-reads of the last
+//    stage), the last one without the next-k0 reads or barrier #3.
+// MODE 1: DMA of stage s+2, vmcnt(8 + NB3) at barrier #3; MODE 2: no DMA,
+// vmcnt(0) at barrier #3 (stage s+1 is the last one issued); MODE 3: no
+// DMA, no barrier #3, no next-k0 reads (last K-tile).
+struct DmaK {
+  __amdgpu_buffer_rsrc_t rsrc;   // 256-row panel, whole K
+  uint32_t voff[8];              // piece p: row-in-piece * ld * 2 + swizzled chunk + (4p + wave) * 8 rows
+  __device__ __forceinline__ void issue(char* lds_op, int p, int k_bytes, int wave_s) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_op + (p * 4 + wave_s) * 1024),
+                                             16, voff[p], k_bytes, 0, 0);
+  }
+};
+
+__device__ __forceinline__ DmaK make_dmak(const uint16_t* src, int ld, int row0, int lane,
+                                          int wave) {
+  DmaK d;
+  const uint16_t* base = src + static_cast<size_t>(row0) * ld;
+  d.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, 256 * ld * 2,
+                                             0x00020000);
+  const int r = lane >> 3;
+  const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & 7);
+  const uint32_t lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+    d.voff[p] = lane_off + static_cast<uint32_t>((p * 4 + wave) * 8 * ld * 2);
+  return d;
+}
+
+// PAR 0/1: the K-tile reads stage buffer PAR (compile-time LDS bases);
+// PAR 2: runtime parity `par` (the once-per-tile tail: one instantiation per
+// MODE keeps the register assignment of the unrolled loop intact — a
+// runtime-parity branch between two static tails spilled ~1300 VGPRs).
+template <int PAR, int MODE, int LATE, int R1 = 0>
+__device__ __forceinline__ void w4i_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
+                                          bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
+                                          bf16x8_t (&f1b)[8], char* smem, int a_base, int b_base,
+                                          int off_k0, int off_k1, const DmaK& dma_a,
+                                          const DmaK& dma_b, int kb2, int wave_s, int par = 0) {
+  constexpr int SUB = 2048;
+  constexpr int B3 = LATE ? 96 : 91;
+  constexpr int BSP = LATE ? 6 : 4;
+  constexpr int NB3 = (B3 - 57) / BSP + 1 < 8 ? (B3 - 57) / BSP + 1 : 8;
+  const int px = PAR == 2 ? par : PAR;
+  char* X = smem + px * W4B_STAGE_BYTES;
+  char* Y = smem + (px ^ 1) * W4B_STAGE_BYTES;
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = h * 64 + i * 8 + j;
+        if (h == 0) mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
+        else mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
+        // R1 1: A k-half-1 reads at even m 0..14 and barrier #1 after m 21
+        // (7 MFMAs between the last read and its lgkmcnt(0), as hipBLASLt)
+        if (m < 16 && (m & 1) == (R1 ? 0 : 1))
+          f1a[m >> 1] = lds_read_b128(X + a_base + (m >> 1) * SUB + off_k1);
+        if (MODE == 1 && m == (R1 ? 21 : 19)) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_s_barrier();
+        }
+        if (m >= 20 && m < 52 && (m & 3) == 1)
+          f1b[(m - 21) >> 2] = lds_read_b128(X + b_base + ((m - 21) >> 2) * SUB + off_k1);
+        if (MODE == 1 && m >= 20 && m < 52 && (m & 3) == 3)
+          dma_a.issue(X, (m - 23) >> 2, kb2, wave_s);
+        if (MODE == 1 && m == 55) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_s_barrier();
+        }
+        if (MODE == 1 && m >= 57 && (m - 57) % BSP == 0 && (m - 57) / BSP < 8)
+          dma_b.issue(X + W4B_OP_BYTES, (m - 57) / BSP, kb2, wave_s);
+        if (MODE != 3 && m == B3) {
+          if constexpr (MODE == 1) vm_wait<8 + NB3>();
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        if (MODE != 3 && m > B3 && m < B3 + 32 && ((m - B3) & 1)) {
+          const int r = (m - B3 - 1) >> 1;
+          if (r < 8) f0b[r] = lds_read_b128(Y + b_base + r * SUB + off_k0);
+          else f0a[r - 8] = lds_read_b128(Y + a_base + (r - 8) * SUB + off_k0);
+        }
+      }
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// bf16 store of a wave's 128x128 accumulator block, widened to dwordx4 by
+// v_permlane16_swap (w4b EPI 1).
+__device__ __forceinline__ void store_block_wide(const f32x4_t (&acc)[8][8], uint16_t* C, int ldc,
+                                                 int row0, int col0, int lane) {
+  const int crow = lane & 15;
+  const int q = lane >> 4;
+  const int ccol = (q & 1) * 16 + (q >> 1) * 8;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint16_t* cp = C + static_cast<size_t>(row0 + i * 16 + crow) * ldc + col0 + ccol;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const uint32_t x0 = mxk::pack2bf(acc[i][j][0], acc[i][j][1]);
+      const uint32_t x1 = mxk::pack2bf(acc[i][j][2], acc[i][j][3]);
+      const uint32_t y0 = mxk::pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
+      const uint32_t y1 = mxk::pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+      uint4 v;
+      v.x = s0[0];
+      v.y = s1[0];
+      v.z = s0[1];
+      v.w = s1[1];
+      *reinterpret_cast<uint4*>(cp + j * 16) = v;
+    }
+  }
+}
+
+__device__ __forceinline__ void store_block_narrow(const f32x4_t (&acc)[8][8], uint16_t* C, int ldc,
+                                                   int row0, int col0, int lane) {
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint16_t* cp = C + static_cast<size_t>(row0 + i * 16 + crow) * ldc + col0 + ccol;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint2 pk;
+      pk.x = mxk::pack2bf(acc[i][j][0], acc[i][j][1]);
+      pk.y = mxk::pack2bf(acc[i][j][2], acc[i][j][3]);
+      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+    }
+  }
+}
+
+template <int MAP, int EPI, int LATE = 0, int R1 = 0>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
+  int m0, n0;
+  w4b_tile<MAP>(blockIdx.x, gridDim.x, M / BM, N / BN, &m0, &n0);
+  const DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
+  const DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
+
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / BK;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_OP_BYTES, p, 0, wave_s);
+  if (ns > 1) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_a.issue(smem + W4B_STAGE_BYTES, p, BK * 2, wave_s);
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+      dma_b.issue(smem + W4B_STAGE_BYTES + W4B_OP_BYTES, p, BK * 2, wave_s);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+
+  // K-tiles 0 .. ns-3 carry the DMA of stage s+2 (k offset kb = (s+2)*128 B)
+  int s = 0;
+  int kb = 2 * BK * 2;
+  for (; s + 2 <= ns - 2; s += 2) {
+    w4i_ktile<0, 1, LATE, R1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                          dma_b, kb, wave_s);
+    w4i_ktile<1, 1, LATE, R1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                          dma_b, kb + BK * 2, wave_s);
+    kb += 2 * BK * 2;
+  }
+  if (s < ns - 2) {   // s even
+    w4i_ktile<0, 1, LATE, R1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                          dma_b, kb, wave_s);
+    ++s;
+  }
+  // the last two K-tiles (or the only one): no DMA
+  if (ns >= 2) {
+    w4i_ktile<2, 2, LATE, R1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                          dma_b, 0, wave_s, s & 1);
+    ++s;
+  }
+  w4i_ktile<2, 3, LATE, R1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                        dma_b, 0, wave_s, s & 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  if constexpr (EPI == 1) store_block_wide(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+  else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+}
+
+// ---------------------------------------------------------------------------
 // Schedule 21 ("w4p"): the default w4b schedule (ORD 4, VOFF DMA) made
 // persistent — one workgroup per CU walks tiles t = blockIdx.x + r * grid.
 // With one 128 KiB workgroup per CU a non-persistent grid leaves the CU idle
@@ -1764,9 +1991,9 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 namespace {
 // w4h + XCD super-block map + widened stores; 22 (w4h, plain 8-B stores)
 // when C is not 16-B aligned or ldc % 8 != 0
-constexpr int kDefaultVariant = 24;
-constexpr int kDefaultVariantNarrowC = 22;
-constexpr int kNumVariants = 29;
+constexpr int kDefaultVariant = 30;
+constexpr int kDefaultVariantNarrowC = 31;
+constexpr int kNumVariants = 34;
 // timing ablations and stamp builds: wrong outputs or perturbed schedules
 __host__ __device__ constexpr bool is_ablation(int v) {
   return (v >= 9 && v <= 12) || v == 14 || v == 17;
@@ -1799,6 +2026,13 @@ void launch_w4h(int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* 
                 int M, int N, int K, int lda, int ldb, int ldc) {
   hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4h<MAP, EPI, MO, LATE, PRIO>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b,
                      c, M, N, K, lda, ldb, ldc);
+}
+
+template <int MAP, int EPI, int LATE, int R1 = 0>
+void launch_w4i(int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b, uint16_t* c,
+                int M, int N, int K, int lda, int ldb, int ldc) {
+  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4i<MAP, EPI, LATE, R1>), dim3(nwg), dim3(W4_THREADS), 0, stream,
+                     a, b, c, M, N, K, lda, ldb, ldc);
 }
 
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
@@ -1841,6 +2075,11 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 26: launch_w4h<1, 1, 0, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 27: launch_w4h<1, 1, 0, 0, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 28: launch_w4h<1, 1, 1, 1, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 29: launch_w4i<1, 1, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 30: launch_w4i<1, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 31: launch_w4i<1, 0, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 32: launch_w4i<1, 1, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 33: launch_w4i<1, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
   }
 }
 }  // namespace
