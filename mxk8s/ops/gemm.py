@@ -58,14 +58,16 @@ def gemm_flops(M: int, N: int, K: int) -> float:
 
 
 def gemm_bf16_ex(a: torch.Tensor, b: torch.Tensor, a_kmajor: bool, b_kmajor: bool,
-                 out: torch.Tensor) -> bool:
+                 out: torch.Tensor, variant: int = 1) -> bool:
     """``out[M][N] = A . B`` on the layout-generic MFMA kernel
     (``native/kernels/gemm_bf16_layouts.hip``).
 
     ``a`` is [M, K] if ``a_kmajor`` else [K, M]; ``b`` is [N, K] if
     ``b_kmajor`` else [K, N]; all row-major with unit inner stride, bf16.
     Returns False (nothing launched) when the shape does not tile exactly
-    (M, N multiples of 256, K of 64) so the caller can use the library GEMM."""
+    (M, N multiples of 256, K of 64) so the caller can use the library GEMM.
+    ``variant`` 1 (default) = the three-barrier x2 schedule (both-K-major
+    problems run the validator's TN kernel); 0 = the one-barrier x kernel."""
     if a.dim() != 2 or b.dim() != 2 or a.stride(1) != 1 or b.stride(1) != 1 or \
             out.stride(1) != 1 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         return False
@@ -73,9 +75,10 @@ def gemm_bf16_ex(a: torch.Tensor, b: torch.Tensor, a_kmajor: bool, b_kmajor: boo
     N, K2 = (b.shape if b_kmajor else (b.shape[1], b.shape[0]))
     if K != K2 or tuple(out.shape) != (M, N) or not is_fast_shape(M, N, K):
         return False
-    st = _lib.lib().mxk_gemm_bf16_ex(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K,
-                                     a.stride(0), b.stride(0), out.stride(0), int(a_kmajor),
-                                     int(b_kmajor), _lib.stream_ptr(a.device))
+    st = _lib.lib().mxk_gemm_bf16_ex_variant(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K,
+                                             a.stride(0), b.stride(0), out.stride(0),
+                                             int(a_kmajor), int(b_kmajor), int(variant),
+                                             _lib.stream_ptr(a.device))
     if st == 1:   # hipErrorInvalidValue: layout/stride limits -> library GEMM
         return False
     _lib.check(st, "mxk_gemm_bf16_ex")

@@ -23,6 +23,11 @@ from .gemm import gemm_bf16_ex
 # layout-generic MFMA kernel beats hipBLASLt there (profiles/r1_gemm_layouts:
 # +10-29 % on the Llama-3-8B wo/w13/w2 shapes); MXK_WGRAD=0 selects hipBLASLt.
 _USE_MXK_WGRAD = os.environ.get("MXK_WGRAD", "1") != "0"
+# dx = dy W has a K-major dy and an N-major W: the x2 schedule of the layout
+# kernel runs it at 1390-1450 TF/s on the Llama-3-8B shapes (16k tokens)
+# against hipBLASLt's 1350-1390 (profiles/r1_gemm_w4h/gemm_layouts_x2.log);
+# MXK_DGRAD=0 selects hipBLASLt.
+_USE_MXK_DGRAD = os.environ.get("MXK_DGRAD", "1") != "0"
 
 
 def _tail_heavy(M: int, N: int, cus: int = 256) -> bool:
@@ -39,6 +44,15 @@ def _wgrad_into(sink: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None
     torch.matmul(dy2.t(), x2, out=sink)
 
 
+def _dgrad(dy: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    if _USE_MXK_DGRAD and dy.is_cuda and dy.is_contiguous() and weight.is_contiguous():
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        out = torch.empty((dy2.shape[0], weight.shape[1]), device=dy.device, dtype=dy.dtype)
+        if not _tail_heavy(*out.shape) and gemm_bf16_ex(dy2, weight, True, False, out):
+            return out.view(*dy.shape[:-1], weight.shape[1])
+    return torch.matmul(dy, weight)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
@@ -48,7 +62,7 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        dx = torch.matmul(dy, weight) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(dy, weight) if ctx.needs_input_grad[0] else None
         if not ctx.needs_input_grad[1]:
             return dx, None
         x2 = x.reshape(-1, x.shape[-1])

@@ -7,27 +7,28 @@
 // K-contiguous, which is what the MFMA A/B lane maps want, so neither tile
 // needs a transpose on the way into LDS.
 //
-// Design (MI355X-first, see /opt/skills/guides/cdna_hip_programming.md §5):
-//  * 256x256 macro tile, BK = 64, 512 threads = 8 waves laid out 2 (M) x 4 (N);
-//    each wave owns a 128 x 64 output block = 8 x 4 tiles of 16x16.
-//  * v_mfma_f32_16x16x32_bf16: on random data this shape holds a higher clock
-//    than 32x32x16 at equal cycles/FLOP (MI355X_MICROARCH 'DVFS give-back' 7).
-//  * Operands are swapped in the MFMA (D' = Bt·A^T) so every lane ends up
-//    holding 4 consecutive N-columns of one C row -> one 8-byte store per
-//    16x16 tile instead of four 2-byte stores.
-//  * Global -> LDS by LDS-DMA (global_load_lds_dwordx4): the LDS image is
-//    lane-linear, so the bank-conflict swizzle is applied to the per-lane
-//    SOURCE address and undone on the ds_read address (rule 21).
-//    Swizzle: 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7); every
-//    16-lane ds_read_b128 group then touches 16 distinct 16-B bank slots
-//    (checked by tests/test_gemm_swizzle.py against the §LDS lane groups).
-//  * Phased software pipeline: each 64-deep K tile is split into four phases
-//    (k-step x M-half, 16 MFMAs each); every phase issues one quarter of the
-//    NEXT K tile's LDS-DMA (one glds per operand per thread) right after its
-//    fragment reads, so the DMA streams under the MFMAs.  Two 64 KiB stages
-//    (128 KiB LDS, 1 workgroup/CU); one wait + raw s_barrier per K tile.
-//  * XCD-aware bijective block remap + GROUP_M tile ordering so the blocks
-//    that share an XCD's L2 share A/B panels (T1).
+// Design (MI355X-first, see /opt/skills/guides/cdna_hip_programming.md §5).
+// The default schedule is w4i (variant 34, below); the older schedules stay
+// as A/B variants (mxk_gemm_bf16_tn_variant, python -m mxk8s.validate.gemm):
+//  * 256x256 macro tile, BK = 64, 256 threads = 4 waves (one per SIMD), each
+//    owning a 128x128 block = 8x8 v_mfma_f32_16x16x32_bf16 tiles with the
+//    fp32 accumulators pinned to AGPRs.  16x16x32 holds a higher clock than
+//    32x32x16 on random data (MI355X_MICROARCH 'DVFS give-back' 7).
+//  * Operands swapped in the MFMA (D' = Bt·A^T): a lane holds 4 consecutive
+//    N-columns of one C row; v_permlane16_swap pairs two 16x16 tiles so the
+//    store tail is 32 dwordx4 (non-temporal) per lane.
+//  * Global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds) into two 64 KiB
+//    stages; lane-linear image, XOR swizzle applied to the source address
+//    (rule 21): chunk c of row r at c ^ ((r >> 1) & 7), conflict-free
+//    ds_read_b128 (tests/test_gemm_swizzle.py).
+//  * Three barriers per K-tile (hipBLASLt's gfx950 structure): the stage just
+//    consumed is refilled in place with stage s+2 once each operand's last
+//    fragment read retired, so DMA pieces spread over ~64 MFMAs and have
+//    ~130-200 MFMAs to land; counted vmcnt, raw s_barrier.
+//  * K loop unrolled by two (compile-time LDS bases), k step as the DMA's
+//    soffset: no address arithmetic ahead of the MFMA stream.
+//  * XCD-aware super-block tile map: 256 resident tiles = one 16x16 block,
+//    8x4 per XCD (L2 reuse) and 32 panels chip-wide (Infinity Cache reuse).
 #include "mx_common.h"
 
 namespace {
@@ -678,40 +679,7 @@ __device__ __forceinline__ unsigned long long stamp() {
   return t;
 }
 
-// Block -> 256x256 output tile.
-//  MAP 0: XCD remap + GROUP_M column sweep (each XCD owns GROUP_M tile rows
-//         and walks the columns; chip-wide every A panel is live at once).
-//  MAP 1: XCD-aware super-blocks.  The 8 XCDs x 32 CUs = 256 resident
-//         workgroups cover one 16x16-tile super-block per "round"; XCD x
-//         takes the 8 (M) x 4 (N) sub-block (x >> 2, x & 3) of it, so an XCD's
-//         L2 serves 12 panels to 32 tiles (the 81 % reuse of MAP 0) while the
-//         chip as a whole touches only 16 A + 16 B panels per round (Infinity
-//         Cache-sized at 16384^2) instead of every A panel.  Rounds snake over
-//         the super-block grid so consecutive rounds share their A panels.
-//         Needs tiles_m % 16 == tiles_n % 16 == 0; MAP 0 otherwise.
-template <int MAP>
-__device__ __forceinline__ void w4b_tile(int bid, int nwg, int tiles_m, int tiles_n, int* m0,
-                                         int* n0) {
-  if (MAP == 1 && (tiles_m & 15) == 0 && (tiles_n & 15) == 0) {
-    const int xcd = bid & 7, l = bid >> 3;
-    const int round = l >> 5, pos = l & 31;
-    const int sbn = tiles_n >> 4;
-    const int sm = round / sbn;
-    int sn = round - sm * sbn;
-    if (sm & 1) sn = sbn - 1 - sn;
-    *m0 = (sm * 16 + (xcd >> 2) * 8 + (pos & 7)) * BM;
-    *n0 = (sn * 16 + (xcd & 3) * 4 + (pos >> 3)) * BN;
-    return;
-  }
-  const int wgid = mxk::xcd_remap(bid, nwg);
-  const int per_group = GROUP_M * tiles_n;
-  const int group = wgid / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
-  const int in_group = wgid - group * per_group;
-  *m0 = (first_m + in_group % gsize) * BM;
-  *n0 = (in_group / gsize) * BN;
-}
+using mxk::w4b_tile;
 
 // EPI 1: widened store tail (guide T21 with v_permlane16_swap): the bf16
 // quads of 16x16 tiles j and j+1 are exchanged between lane rows so every
@@ -1194,50 +1162,8 @@ __device__ __forceinline__ void w4i_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
   __builtin_amdgcn_s_setprio(0);
 }
 
-// bf16 store of a wave's 128x128 accumulator block, widened to dwordx4 by
-// v_permlane16_swap (w4b EPI 1).
-__device__ __forceinline__ void store_block_wide(const f32x4_t (&acc)[8][8], uint16_t* C, int ldc,
-                                                 int row0, int col0, int lane) {
-  const int crow = lane & 15;
-  const int q = lane >> 4;
-  const int ccol = (q & 1) * 16 + (q >> 1) * 8;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint16_t* cp = C + static_cast<size_t>(row0 + i * 16 + crow) * ldc + col0 + ccol;
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const uint32_t x0 = mxk::pack2bf(acc[i][j][0], acc[i][j][1]);
-      const uint32_t x1 = mxk::pack2bf(acc[i][j][2], acc[i][j][3]);
-      const uint32_t y0 = mxk::pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
-      const uint32_t y1 = mxk::pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
-      const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-      const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-      uint4 v;
-      v.x = s0[0];
-      v.y = s1[0];
-      v.z = s0[1];
-      v.w = s1[1];
-      *reinterpret_cast<uint4*>(cp + j * 16) = v;
-    }
-  }
-}
-
-__device__ __forceinline__ void store_block_narrow(const f32x4_t (&acc)[8][8], uint16_t* C, int ldc,
-                                                   int row0, int col0, int lane) {
-  const int crow = lane & 15;
-  const int ccol = (lane >> 4) * 4;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint16_t* cp = C + static_cast<size_t>(row0 + i * 16 + crow) * ldc + col0 + ccol;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      uint2 pk;
-      pk.x = mxk::pack2bf(acc[i][j][0], acc[i][j][1]);
-      pk.y = mxk::pack2bf(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
-    }
-  }
-}
+using mxk::store_block_wide;
+using mxk::store_block_narrow;
 
 template <int MAP, int EPI, int LATE = 0, int R1 = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
@@ -1317,7 +1243,8 @@ mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict_
                         dma_b, 0, wave_s, s & 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  if constexpr (EPI == 1) store_block_wide(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+  if constexpr (EPI == 1) store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+  else if constexpr (EPI == 2) store_block_wide<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
@@ -1989,11 +1916,12 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // Host launchers (C ABI, stream-ordered, capture-safe: no sync, no malloc).
 // ---------------------------------------------------------------------------
 namespace {
-// w4h + XCD super-block map + widened stores; 22 (w4h, plain 8-B stores)
-// when C is not 16-B aligned or ldc % 8 != 0
-constexpr int kDefaultVariant = 30;
+// w4i (three-barrier K-tile, scalar-free unrolled loop) + XCD super-block
+// map + widened non-temporal stores; 31 (the same with 8-B stores) when C is
+// not 16-B aligned or ldc % 8 != 0.  A/B logs: profiles/r1_gemm_w4h/.
+constexpr int kDefaultVariant = 34;
 constexpr int kDefaultVariantNarrowC = 31;
-constexpr int kNumVariants = 34;
+constexpr int kNumVariants = 35;
 // timing ablations and stamp builds: wrong outputs or perturbed schedules
 __host__ __device__ constexpr bool is_ablation(int v) {
   return (v >= 9 && v <= 12) || v == 14 || v == 17;
@@ -2080,6 +2008,7 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 31: launch_w4i<1, 0, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 32: launch_w4i<1, 1, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 33: launch_w4i<1, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 34: launch_w4i<1, 2, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
   }
 }
 }  // namespace

@@ -84,6 +84,11 @@ struct XOp<false> {
     // hipBLASLt-style addressing: per-piece VGPR offset, k folded into the base
     dma16(make_rsrc(base + kstage * (XBK * 2), bytes), lds + g * 1024, voff[p], 0);
   }
+  // x2 kernel: fixed panel descriptor, the k offset of the stage as soffset
+  __device__ __forceinline__ uint32_t kstep() const { return XBK * 2; }
+  __device__ __forceinline__ void issue_s(char* lds, int p, uint32_t soff, int wave) const {
+    dma16(rsrc, lds + (p * 4 + wave) * 1024, voff[p], soff);
+  }
   // fragment of 16-row subtile i (i = 0..15 over the 256 rows), k-step ks
   __device__ __forceinline__ bf16x8_t frag(const char* lds, int i, int ks) const {
     return *reinterpret_cast<const bf16x8_t*>(lds + i * 2048 + (ks ? off1 : off0));
@@ -121,6 +126,10 @@ struct XOp<true> {
   __device__ __forceinline__ void issue(char* lds, int p, int kstage, int wave) const {
     const uint32_t k_off = kstage * kstride;
     dma16(make_rsrc(base + k_off, bytes - k_off), lds + p * TGROUP + wave * 1024, voff[p], 0);
+  }
+  __device__ __forceinline__ uint32_t kstep() const { return kstride; }
+  __device__ __forceinline__ void issue_s(char* lds, int p, uint32_t soff, int wave) const {
+    dma16(rsrc, lds + p * TGROUP + wave * 1024, voff[p], soff);
   }
   __device__ __forceinline__ bf16x8_t frag(const char* lds, int i, int ks) const {
     const char* p = lds + base_off + ks * KSTEP_T + ((32 * i) ^ qx);
@@ -253,12 +262,175 @@ mxk_gemm_bf16_x_kernel(const uint16_t* __restrict__ A, const uint16_t* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// x2: the layout-generic GEMM on gemm_bf16.hip's w4i schedule (three
+// barriers per K-tile with in-place refill of the consumed stage, K loop
+// unrolled by two with compile-time LDS bases, the stage's k offset as the
+// DMA soffset on a fixed descriptor, DMA-free last two K-tiles, XCD
+// super-block tile map, widened store tail).  m = MFMA index 0..127 of a
+// K-tile; "read" = one operand fragment (one ds_read_b128 for a K-major
+// operand, two ds_read_b64_tr_b16 for an N/M-major one):
+//   m 1..15 odd   A k-half-1 fragments from X           m 19  barrier #1
+//   m 21..49 /4   B k-half-1 fragments from X
+//   m 23..51 /4   DMA of stage s+2, A pieces -> X.A     m 55  barrier #2
+//   m 57..99 /6   DMA of stage s+2, B pieces -> X.B
+//   m 96          vmcnt(15) + barrier #3 (stage s+1 in Y landed everywhere)
+//   m 97..127 odd next k-half-0 fragments from Y (B, then A)
+// MODE 1: with DMA; 2: no DMA, vmcnt(0) at barrier #3; 3: last K-tile.
+// ---------------------------------------------------------------------------
+template <bool AN, bool BN, int PAR, int MODE>
+__device__ __forceinline__ void x2_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
+                                         bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
+                                         bf16x8_t (&f1b)[8], char* smem, const XOp<AN>& oa,
+                                         const XOp<BN>& ob, int wm, int wn, uint32_t soa,
+                                         uint32_t sob, int wave, int par = 0) {
+  constexpr int A_BYTES = XOp<AN>::BYTES;
+  constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
+  const int px = PAR == 2 ? par : PAR;
+  char* X = smem + px * STAGE;
+  char* Y = smem + (px ^ 1) * STAGE;
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = h * 64 + i * 8 + j;
+        if (h == 0) xmfma(acc[i][j], f0b[j], f0a[i]);
+        else xmfma(acc[i][j], f1b[j], f1a[i]);
+        if (m < 16 && (m & 1)) f1a[m >> 1] = oa.frag(X, wm * 8 + (m >> 1), 1);
+        if (MODE == 1 && m == 19) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_s_barrier();
+        }
+        if (m >= 20 && m < 52 && (m & 3) == 1)
+          f1b[(m - 21) >> 2] = ob.frag(X + A_BYTES, wn * 8 + ((m - 21) >> 2), 1);
+        if (MODE == 1 && m >= 20 && m < 52 && (m & 3) == 3) oa.issue_s(X, (m - 23) >> 2, soa, wave);
+        if (MODE == 1 && m == 55) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_s_barrier();
+        }
+        if (MODE == 1 && m >= 57 && (m - 57) % 6 == 0 && (m - 57) / 6 < 8)
+          ob.issue_s(X + A_BYTES, (m - 57) / 6, sob, wave);
+        if (MODE != 3 && m == 96) {
+          if constexpr (MODE == 1) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        if (MODE != 3 && m > 96 && (m & 1)) {
+          const int r = (m - 97) >> 1;
+          if (r < 8) f0b[r] = ob.frag(Y + A_BYTES, wn * 8 + r, 0);
+          else f0a[r - 8] = oa.frag(Y, wm * 8 + r - 8, 0);
+        }
+      }
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <bool AN, bool BN, int EPI>
+__global__ void __launch_bounds__(XT, 1)
+mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                        uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  constexpr int A_BYTES = XOp<AN>::BYTES;
+  constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1;
+  const int wn = wave & 1;
+  int m0, n0;
+  mxk::w4b_tile<1>(blockIdx.x, gridDim.x, M / XBM, N / XBM, &m0, &n0);
+
+  XOp<AN> oa;
+  XOp<BN> ob;
+  oa.init(A, lda, m0, K, lane, wave);
+  ob.init(B, ldb, n0, K, lane, wave);
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / XBK;
+  const uint32_t ka = oa.kstep(), kb = ob.kstep();
+#pragma unroll
+  for (int p = 0; p < 8; ++p) oa.issue_s(smem, p, 0, wave);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) ob.issue_s(smem + A_BYTES, p, 0, wave);
+  if (ns > 1) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) oa.issue_s(smem + STAGE, p, ka, wave);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) ob.issue_s(smem + STAGE + A_BYTES, p, kb, wave);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f0b[j] = ob.frag(smem + A_BYTES, wn * 8 + j, 0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f0a[i] = oa.frag(smem, wm * 8 + i, 0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+
+  int s = 0;
+  uint32_t sa = 2 * ka, sb = 2 * kb;
+  for (; s + 2 <= ns - 2; s += 2) {
+    x2_ktile<AN, BN, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, wave);
+    x2_ktile<AN, BN, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa + ka, sb + kb, wave);
+    sa += 2 * ka;
+    sb += 2 * kb;
+  }
+  if (s < ns - 2) {
+    x2_ktile<AN, BN, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, wave);
+    ++s;
+  }
+  if (ns >= 2) {
+    x2_ktile<AN, BN, 2, 2>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
+    ++s;
+  }
+  x2_ktile<AN, BN, 2, 3>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  if constexpr (EPI == 1)
+    mxk::store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+  else
+    mxk::store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+}
+
+template <bool AN, bool BN>
+static void launch_x(int v, bool wide, int nwg, hipStream_t stream, const uint16_t* a,
+                     const uint16_t* b, uint16_t* c, int M, int N, int K, int lda, int ldb,
+                     int ldc) {
+  if (v == 0)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<AN, BN>), dim3(nwg), dim3(XT), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc);
+  else if (wide)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 1>), dim3(nwg), dim3(XT), 0, stream, a, b,
+                       c, M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 0>), dim3(nwg), dim3(XT), 0, stream, a, b,
+                       c, M, N, K, lda, ldb, ldc);
+}
+
+MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,
+                             int lda, int ldb, int ldc, hipStream_t stream);
+
 // a_kmajor: A stored [M][K] (1) or [K][M] (0); b_kmajor: B stored [N][K] (1)
 // or [K][N] (0).  Row strides lda/ldb/ldc in elements.  Tiles exactly:
 // M % 256, N % 256, K % 64; returns hipErrorInvalidValue otherwise (callers
-// keep the library GEMM for other shapes).
-MXK_API int mxk_gemm_bf16_ex(const void* A, const void* B, void* C, int M, int N, int K, int lda,
-                             int ldb, int ldc, int a_kmajor, int b_kmajor, hipStream_t stream) {
+// keep the library GEMM for other shapes).  variant 0 = the one-barrier x
+// kernel, 1 = x2 (default); both-K-major problems go to the validator's
+// TN kernel (gemm_bf16.hip) under variant 1.
+MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int M, int N, int K,
+                                     int lda, int ldb, int ldc, int a_kmajor, int b_kmajor,
+                                     int variant, hipStream_t stream) {
   const auto bytes = [](long rows, long ld) { return rows * ld * 2; };
   const bool ok = M > 0 && N > 0 && K > 0 && M % XBM == 0 && N % XBM == 0 && K % XBK == 0 &&
                   lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 &&
@@ -267,23 +439,27 @@ MXK_API int mxk_gemm_bf16_ex(const void* A, const void* B, void* C, int M, int N
                   (b_kmajor || bytes(K, ldb) < (1L << 32)) &&
                   reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(C) % 8 == 0;
+                  reinterpret_cast<uintptr_t>(C) % 8 == 0 && (variant == 0 || variant == 1);
   if (!ok) return static_cast<int>(hipErrorInvalidValue);
+  if (variant == 1 && a_kmajor && b_kmajor)
+    return mxk_gemm_bf16_tn(A, B, C, M, N, K, lda, ldb, ldc, stream);
   const int nwg = (M / XBM) * (N / XBM);
+  const bool wide = (ldc % 8 == 0) && (reinterpret_cast<uintptr_t>(C) % 16 == 0);
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);
   if (a_kmajor && b_kmajor)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<false, false>), dim3(nwg), dim3(XT), 0, stream, a,
-                       b, c, M, N, K, lda, ldb, ldc);
+    launch_x<false, false>(variant, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
   else if (a_kmajor)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<false, true>), dim3(nwg), dim3(XT), 0, stream, a,
-                       b, c, M, N, K, lda, ldb, ldc);
+    launch_x<false, true>(variant, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
   else if (b_kmajor)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<true, false>), dim3(nwg), dim3(XT), 0, stream, a,
-                       b, c, M, N, K, lda, ldb, ldc);
+    launch_x<true, false>(variant, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
   else
-    hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<true, true>), dim3(nwg), dim3(XT), 0, stream, a,
-                       b, c, M, N, K, lda, ldb, ldc);
+    launch_x<true, true>(variant, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
   MXK_RETURN_LAUNCH_STATUS();
+}
+
+MXK_API int mxk_gemm_bf16_ex(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                             int ldb, int ldc, int a_kmajor, int b_kmajor, hipStream_t stream) {
+  return mxk_gemm_bf16_ex_variant(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor, 1, stream);
 }

@@ -85,6 +85,94 @@ __device__ __forceinline__ void dma16(const u32x4& rsrc, const char* lds, uint32
       : "memory");
 }
 
+// Block -> 256x256 output tile of the MFMA GEMMs (gemm_bf16*.hip).
+//  MAP 0: XCD remap + GROUP_M column sweep (each XCD owns GROUP_M tile rows
+//         and walks the columns; chip-wide every A panel is live at once).
+//  MAP 1: XCD-aware super-blocks.  The 8 XCDs x 32 CUs = 256 resident
+//         workgroups cover one 16x16-tile super-block per "round"; XCD x
+//         takes the 8 (M) x 4 (N) sub-block (x >> 2, x & 3) of it, so an XCD's
+//         L2 serves 12 panels to 32 tiles (the 81 % reuse of MAP 0) while the
+//         chip as a whole touches only 16 A + 16 B panels per round (Infinity
+//         Cache-sized at 16384^2) instead of every A panel.  Rounds snake over
+//         the super-block grid so consecutive rounds share their A panels.
+//         Needs tiles_m % 16 == tiles_n % 16 == 0; MAP 0 otherwise.
+template <int MAP>
+__device__ __forceinline__ void w4b_tile(int bid, int nwg, int tiles_m, int tiles_n, int* m0,
+                                         int* n0) {
+  if (MAP == 1 && (tiles_m & 15) == 0 && (tiles_n & 15) == 0) {
+    const int xcd = bid & 7, l = bid >> 3;
+    const int round = l >> 5, pos = l & 31;
+    const int sbn = tiles_n >> 4;
+    const int sm = round / sbn;
+    int sn = round - sm * sbn;
+    if (sm & 1) sn = sbn - 1 - sn;
+    *m0 = (sm * 16 + (xcd >> 2) * 8 + (pos & 7)) * 256;
+    *n0 = (sn * 16 + (xcd & 3) * 4 + (pos >> 3)) * 256;
+    return;
+  }
+  const int wgid = xcd_remap(bid, nwg);
+  constexpr int GROUP_M = 8;
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  *m0 = (first_m + in_group % gsize) * 256;
+  *n0 = (in_group / gsize) * 256;
+}
+
+// bf16 store of a wave's 128x128 accumulator block, widened to dwordx4 by
+// v_permlane16_swap (w4b EPI 1).  NT: non-temporal stores (C is written once
+// and not re-read by this kernel; keeps it from displacing A/B panels).
+template <bool NT = false>
+__device__ __forceinline__ void store_block_wide(const f32x4_t (&acc)[8][8], uint16_t* C, int ldc,
+                                                 int row0, int col0, int lane) {
+  const int crow = lane & 15;
+  const int q = lane >> 4;
+  const int ccol = (q & 1) * 16 + (q >> 1) * 8;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint16_t* cp = C + static_cast<size_t>(row0 + i * 16 + crow) * ldc + col0 + ccol;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const uint32_t x0 = pack2bf(acc[i][j][0], acc[i][j][1]);
+      const uint32_t x1 = pack2bf(acc[i][j][2], acc[i][j][3]);
+      const uint32_t y0 = pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
+      const uint32_t y1 = pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+      if constexpr (NT) {
+        const u32x4_t v = {s0[0], s1[0], s0[1], s1[1]};
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(cp + j * 16));
+      } else {
+        uint4 v;
+        v.x = s0[0];
+        v.y = s1[0];
+        v.z = s0[1];
+        v.w = s1[1];
+        *reinterpret_cast<uint4*>(cp + j * 16) = v;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void store_block_narrow(const f32x4_t (&acc)[8][8], uint16_t* C, int ldc,
+                                                   int row0, int col0, int lane) {
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint16_t* cp = C + static_cast<size_t>(row0 + i * 16 + crow) * ldc + col0 + ccol;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint2 pk;
+      pk.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+      pk.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+      *reinterpret_cast<uint2*>(cp + j * 16) = pk;
+    }
+  }
+}
+
 }  // namespace mxk
 
 // Host-side error plumbing: every launcher returns hipError_t as int so the

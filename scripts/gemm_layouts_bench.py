@@ -11,6 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mxk8s.ops.gemm import gemm_bf16_ex  # noqa: E402
 
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1").split(",")]
 SHAPES = [(4096, 6144, "wqkv"), (4096, 4096, "wo"), (4096, 28672, "w13"), (14336, 4096, "w2")]
 
 
@@ -44,20 +45,23 @@ def main():
         }
         for kind, (a, b, ak, bk, shp, ref_fn) in cases.items():
             out = torch.empty(shp, device=dev, dtype=torch.bfloat16)
-            ok = gemm_bf16_ex(a, b, ak, bk, out)
             ref = ref_fn()
-            rel = ((out.float() - ref.float()).norm() / ref.float().norm()).item() if ok else None
             K = din if kind == "fwd" else (dout if kind == "dgrad" else T)
             flops = 2.0 * shp[0] * shp[1] * K
-            t_mxk = timeit(lambda: gemm_bf16_ex(a, b, ak, bk, out)) if ok else None
-            t_lib = timeit(ref_fn)
-            print("RESULT " + json.dumps({
-                "gemm": f"{name}.{kind}", "M": shp[0], "N": shp[1], "K": K, "launched": ok,
-                "rel_err_vs_hipblaslt": rel,
-                "mxk_tflops": round(flops / t_mxk / 1e9, 1) if ok else None,
-                "hipblaslt_tflops": round(flops / t_lib / 1e9, 1)}), flush=True)
-            if ok and not rel < 1e-2:
-                raise SystemExit(f"{name}.{kind}: wrong result rel {rel}")
+            res = {"gemm": f"{name}.{kind}", "M": shp[0], "N": shp[1], "K": K}
+            for v in VARIANTS:
+                out.zero_()
+                ok = gemm_bf16_ex(a, b, ak, bk, out, variant=v)
+                if not ok:
+                    res[f"mxk_v{v}_tflops"] = None
+                    continue
+                rel = ((out.float() - ref.float()).norm() / ref.float().norm()).item()
+                if not rel < 1e-2:
+                    raise SystemExit(f"{name}.{kind} variant {v}: wrong result rel {rel}")
+                t = timeit(lambda: gemm_bf16_ex(a, b, ak, bk, out, variant=v))
+                res[f"mxk_v{v}_tflops"] = round(flops / t / 1e9, 1)
+            res["hipblaslt_tflops"] = round(flops / timeit(ref_fn) / 1e9, 1)
+            print("RESULT " + json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":
