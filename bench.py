@@ -56,9 +56,15 @@ def run_validator(args) -> dict:
     from mxk8s.parallel.dist import init_distributed, max_over_ranks, barrier
 
     world, rank, local = _dist_env()
+    # MXK_BENCH_BACKEND=gloo rehearses the multi-rank path on a box with fewer
+    # GPUs than ranks (ranks share GPUs round-robin; RCCL refuses that).  The
+    # measured configuration is always the default: RCCL, one rank per GPU.
+    backend = os.environ.get("MXK_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    init_distributed(backend="nccl", device=dev)
+    init_distributed(backend=backend, device=dev)
 
     M = N = K = args.size
     g = torch.Generator(device=dev)

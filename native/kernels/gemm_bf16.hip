@@ -1249,6 +1249,121 @@ mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// Schedule 35 ("w4ip"): w4i made persistent (grid <= one workgroup per CU,
+// tiles t = blockIdx.x + r * grid).  Between tiles the LDS is free once every
+// wave passed the last K-tile (barrier), so the next tile's two prologue
+// stages are issued BEFORE the finished tile's store tail and land under it.
+// vmcnt at the top of a later tile: 32 DMA pieces then 32 stores per wave
+// are outstanding, vmcnt(48) retires exactly stage 0 (16 pieces + 32 stores
+// -> vmcnt(32) when K has a single stage).  Every wave runs the same trip
+// count, so all reach every barrier and leave the loop together.
+template <int MAP, int EPI>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4ip(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  static_assert(EPI == 1 || EPI == 2, "w4ip counts 32 store instructions per wave");
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int ns = K / BK;
+
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
+
+  int t = blockIdx.x;
+  int m0, n0;
+  w4b_tile<MAP>(t, ntiles, tiles_m, tiles_n, &m0, &n0);
+  DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
+  DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
+  auto prologue = [&]() {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_OP_BYTES, p, 0, wave_s);
+    if (ns > 1) {
+#pragma unroll
+      for (int p = 0; p < 8; ++p) dma_a.issue(smem + W4B_STAGE_BYTES, p, BK * 2, wave_s);
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+        dma_b.issue(smem + W4B_STAGE_BYTES + W4B_OP_BYTES, p, BK * 2, wave_s);
+    }
+  };
+  prologue();
+  bool first = true;
+  while (true) {
+    if (first) {
+      if (ns > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (ns > 1) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+
+    f32x4_t acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+
+    int s = 0;
+    int kb = 2 * BK * 2;
+    for (; s + 2 <= ns - 2; s += 2) {
+      w4i_ktile<0, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                         dma_b, kb, wave_s);
+      w4i_ktile<1, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                         dma_b, kb + BK * 2, wave_s);
+      kb += 2 * BK * 2;
+    }
+    if (s < ns - 2) {
+      w4i_ktile<0, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                         dma_b, kb, wave_s);
+      ++s;
+    }
+    if (ns >= 2) {
+      w4i_ktile<2, 2, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                         dma_b, 0, wave_s, s & 1);
+      ++s;
+    }
+    w4i_ktile<2, 3, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                       dma_b, 0, wave_s, s & 1);
+    // every wave's LDS reads retired (and no DMA is in flight): LDS is free
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+
+    const int cm0 = m0, cn0 = n0;
+    const int tn = t + static_cast<int>(gridDim.x);
+    if (tn < ntiles) {
+      w4b_tile<MAP>(tn, ntiles, tiles_m, tiles_n, &m0, &n0);
+      dma_a = make_dmak(A, lda, m0, lane, wave_s);
+      dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
+      prologue();
+    }
+    store_block_wide<EPI == 2>(acc, C, ldc, cm0 + wm * 128, cn0 + wn * 128, lane);
+    if (tn >= ntiles) break;
+    t = tn;
+    first = false;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
 // Schedule 21 ("w4p"): the default w4b schedule (ORD 4, VOFF DMA) made
 // persistent — one workgroup per CU walks tiles t = blockIdx.x + r * grid.
 // With one 128 KiB workgroup per CU a non-persistent grid leaves the CU idle
@@ -1921,7 +2036,7 @@ namespace {
 // not 16-B aligned or ldc % 8 != 0.  A/B logs: profiles/r1_gemm_w4h/.
 constexpr int kDefaultVariant = 34;
 constexpr int kDefaultVariantNarrowC = 31;
-constexpr int kNumVariants = 35;
+constexpr int kNumVariants = 36;
 // timing ablations and stamp builds: wrong outputs or perturbed schedules
 __host__ __device__ constexpr bool is_ablation(int v) {
   return (v >= 9 && v <= 12) || v == 14 || v == 17;
@@ -2009,6 +2124,12 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 32: launch_w4i<1, 1, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 33: launch_w4i<1, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 34: launch_w4i<1, 2, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 35: {
+      const int grid = nwg < num_cus() ? nwg : num_cus();
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4ip<1, 2>), dim3(grid), dim3(W4_THREADS), 0, stream, a,
+                         b, c, M, N, K, lda, ldb, ldc);
+      break;
+    }
   }
 }
 }  // namespace
