@@ -62,12 +62,14 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
                                                 K, K, N, v, stream())
                 if st:
                     _lib.check(st, f"gemm variant {v}")
-            kernels[f"mxk_v{v}"] = mk
+            name = L.mxk_gemm_bf16_tn_variant_name(v)
+            kernels[f"mxk_v{v}_{name.decode() if name else '?'}"] = mk
         kernels["mxk_default"] = lambda: gemm_bf16_tn(A, Bt, C)
         kernels["hipblaslt"] = lambda: torch.matmul(A, Bt.t(), out=C)
         # correctness of every hand-written schedule
         checks = {}
-        ablations = set(f"mxk_v{v}" for v in variants if is_ablation(v))
+        ablations = set(k for k in kernels if k.startswith("mxk_v") and
+                        is_ablation(int(k[5:].split("_")[0])))
         for name, fn in kernels.items():
             if name == "hipblaslt" or name in ablations:
                 continue

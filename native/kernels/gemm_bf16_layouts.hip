@@ -243,7 +243,8 @@ mxk_gemm_bf16_x_kernel(const uint16_t* __restrict__ A, const uint16_t* __restric
     }
     __builtin_amdgcn_s_setprio(0);
   }
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  mxk::mfma_drain(acc);
 
   const int crow = lane & 15;
   const int ccol = (lane >> 4) * 4;
@@ -397,6 +398,7 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
   }
   x2_ktile<AN, BN, 2, 3>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  mxk::mfma_drain(acc);
 
   if constexpr (EPI == 1)
     mxk::store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);

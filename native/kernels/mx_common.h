@@ -44,6 +44,25 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + bid / kXcds;
 }
 
+// Inline-asm MFMAs (used to pin accumulators to AGPRs) are invisible to
+// hipcc's hazard recognizer: it knows the asm's "+a" outputs but not that the
+// MFMA writes them ~16 cycles after issue.  Nothing then stops the register
+// allocator from copying an accumulator to a VGPR (v_accvgpr_read) right
+// behind the asm MFMA that last writes it — seen on two GEMM schedules after
+// unrelated edits: acc[0][0..1] resp. acc[7][7] read one instruction after
+// their final MFMA, wrong outputs.  Call after the last MFMA, before the
+// accumulators are read: the s_nops cover the write latency and the empty
+// asms redefine every accumulator behind them, so each later read (and any
+// register copy of it) depends on a value that only exists after the nops.
+template <int NI, int NJ>
+__device__ __forceinline__ void mfma_drain(f32x4_t (&acc)[NI][NJ]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(acc[i][j]));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);

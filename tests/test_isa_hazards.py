@@ -1,0 +1,76 @@
+"""ISA audit of the inline-asm MFMA GEMM kernels (CPU: hipcc cross-compiles).
+
+The GEMMs pin their accumulators to AGPRs with inline-asm MFMAs, which hipcc's
+hazard recognizer cannot see.  A v_accvgpr_read/mov of an accumulator issued
+within a few instructions of the asm MFMA that writes it reads a stale value
+(two schedules produced wrong tiles this way: register-allocator copies at the
+K-loop exit, ahead of the drain).  ``mxk::mfma_drain`` must sit between the last
+MFMA and every accumulator read; this test scans the generated code for any
+read of an AGPR within 12 instructions (an ``s_nop 7`` counts 8) of an MFMA
+that wrote it.
+"""
+from __future__ import annotations
+
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+
+def _asm(src: str, out: str) -> str:
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    "-I" + os.path.join(REPO, "native", "kernels"), "--cuda-device-only", "-S",
+                    os.path.join(REPO, "native", "kernels", src), "-o", out],
+                   check=True, capture_output=True)
+    with open(out) as f:
+        return f.read()
+
+
+def close_accumulator_reads(asm: str) -> dict[str, int]:
+    bad = {}
+    for name in re.findall(r"^(_Z[^\s:]+):", asm, re.M):
+        i = asm.find(name + ":")
+        j = asm.find(".Lfunc_end", i)
+        body = [ln.split(";")[0].strip() for ln in asm[i:j].split("\n")]
+        body = [ln for ln in body if ln and not ln.startswith(".")]
+        pend: dict[int, int] = {}
+        n = 0
+        for ln in body:
+            if ln.startswith("v_mfma"):
+                pend = {r: c + 1 for r, c in pend.items()}
+                m = re.match(r"v_mfma\S*\s+a\[(\d+):(\d+)\]", ln)
+                if m:
+                    for r in range(int(m.group(1)), int(m.group(2)) + 1):
+                        pend[r] = 0
+                continue
+            step = 8 if ln.startswith("s_nop 7") else 1
+            pend = {r: c + step for r, c in pend.items() if c + step < 40}
+            if ln.startswith(("v_accvgpr_read", "v_accvgpr_mov")):
+                ops = ln.split(" ", 1)[1] if " " in ln else ""
+                for m in re.finditer(r"\ba(\d+)\b", ops):
+                    if int(m.group(1)) in pend and pend[int(m.group(1))] < 12:
+                        n += 1
+        if n:
+            bad[name] = n
+    return bad
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src", ["gemm_bf16.hip", "gemm_bf16_layouts.hip"])
+def test_no_accumulator_read_right_after_asm_mfma(src, tmp_path):
+    asm = _asm(src, str(tmp_path / (src + ".s")))
+    assert "v_mfma" in asm
+    assert close_accumulator_reads(asm) == {}
+
+
+def test_detector_flags_a_close_read():
+    asm = ("_Zfoo:\n\tv_mfma_f32_16x16x32_bf16 a[0:3], v[0:3], v[4:7], a[0:3]\n"
+           "\ts_add_u32 s0, s0, 1\n\tv_accvgpr_read_b32 v8, a2\n.Lfunc_end0:\n")
+    assert close_accumulator_reads(asm) == {"_Zfoo": 1}
+    safe = asm.replace("\ts_add_u32 s0, s0, 1\n", "\ts_nop 7\n\ts_nop 7\n")
+    assert close_accumulator_reads(safe) == {}
