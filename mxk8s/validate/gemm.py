@@ -48,9 +48,9 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
     stream = lambda: _lib.stream_ptr(dev)  # noqa: E731
     results = []
     for n in sizes:
-        M = N = K = n
+        M, N, K = n if isinstance(n, tuple) else (n, n, n)
         g = torch.Generator(device=dev)
-        g.manual_seed(n)
+        g.manual_seed(M * 7 + N * 3 + K)
         A = (torch.rand((M, K), device=dev, generator=g) * 2 - 1).bfloat16()
         Bt = (torch.rand((N, K), device=dev, generator=g) * 2 - 1).bfloat16()
         C = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
@@ -111,6 +111,7 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
 def main(argv=None) -> int:
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--sizes", default="4096,8192,16384")
+    p.add_argument("--shapes", default="", help="extra MxNxK shapes, comma separated")
     p.add_argument("--variants", default="", help="'all' or comma list of schedule ids")
     p.add_argument("--iters", type=int, default=60)
     p.add_argument("--rounds", type=int, default=6)
@@ -126,7 +127,9 @@ def main(argv=None) -> int:
         variants = [int(x) for x in a.variants.split(",")]
     else:
         variants = []
-    run([int(x) for x in a.sizes.split(",")], variants, a.iters, a.warmup_s, a.rounds,
+    sizes = [int(x) for x in a.sizes.split(",")] if a.sizes else []
+    sizes += [tuple(int(v) for v in x.split("x")) for x in a.shapes.split(",") if x]
+    run(sizes, variants, a.iters, a.warmup_s, a.rounds,
         is_ablation=lambda v: bool(_lib.lib().mxk_gemm_bf16_tn_is_ablation(v)))
     return 0
 

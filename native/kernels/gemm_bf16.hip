@@ -33,13 +33,14 @@
 //
 // Schedules (mxk_gemm_bf16_tn_variant, A/B-timed by python -m
 // mxk8s.validate.gemm --variants all):
-//   0 w4i   default: super-block map, non-temporal widened stores, late barrier #3
+//   0 w4i   super-block map, non-temporal widened stores, late barrier #3
 //   1 w4i   8-byte stores (C not 16-B aligned or ldc % 8 != 0)
 //   2 w4i   widened plain stores, barrier #3 after m 91
 //   3 w4i   widened plain stores, barrier #3 after m 96
 //   4 w4i   variant 3 with A k1 reads at even m and barrier #1 after m 21
 //   5 w4ip  persistent w4i (one workgroup per CU)
-//   6 w4j   every read/DMA/wait at hipBLASLt's MFMA positions
+//   6 w4j   default: w4i with every read/DMA/wait at hipBLASLt's MFMA
+//           positions (+0.5-2 % over 0 on squares and the Llama-3-8B shapes)
 // The earlier schedules (one-barrier w4b, 8-wave, 4-deep ring, w4h, ...)
 // were retired when an ISA audit (tests/test_isa_hazards.py) found their
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
@@ -547,7 +548,7 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int kNumVariants = 7;
-constexpr int kDefaultVariant = 0;
+constexpr int kDefaultVariant = 6;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
     "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb"};
