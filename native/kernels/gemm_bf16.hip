@@ -41,6 +41,7 @@
 //   5 w4ip  persistent w4i (one workgroup per CU)
 //   6 w4j   default: w4i with every read/DMA/wait at hipBLASLt's MFMA
 //           positions (+0.5-2 % over 0 on squares and the Llama-3-8B shapes)
+//   7 w4j   two barriers per K-tile (SchedTwoBarrier)
 // The earlier schedules (one-barrier w4b, 8-wave, 4-deep ring, w4h, ...)
 // were retired when an ISA audit (tests/test_isa_hazards.py) found their
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
@@ -197,25 +198,52 @@ __device__ __forceinline__ void w4i_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
 // lgkmcnt(0) after 50 + barrier after 51; B pieces 61, 64, 85, 87, 89, 96,
 // 100, 124; vmcnt(13) after 91 + barrier after 92 (three pieces still to
 // go); next-k0 reads 93..123 (front-loaded).
-__host__ __device__ constexpr int hb_b1(int m) {
-  return m == 24 ? 0 : m == 27 ? 1 : m == 30 ? 2 : m == 33 ? 3 : m == 36 ? 4 : m == 38 ? 5
-       : m == 40 ? 6 : m == 42 ? 7 : -1;
-}
-__host__ __device__ constexpr int hb_adma(int m) {
-  return m == 22 ? 0 : m == 25 ? 1 : m == 28 ? 2 : m == 31 ? 3 : m == 34 ? 4 : m == 52 ? 5
-       : m == 55 ? 6 : m == 58 ? 7 : -1;
-}
-__host__ __device__ constexpr int hb_bdma(int m) {
-  return m == 61 ? 0 : m == 64 ? 1 : m == 85 ? 2 : m == 87 ? 3 : m == 89 ? 4 : m == 96 ? 5
-       : m == 100 ? 6 : m == 124 ? 7 : -1;
-}
-__host__ __device__ constexpr int hb_k0(int m) {
-  return m == 93 ? 0 : m == 94 ? 1 : m == 95 ? 2 : m == 97 ? 3 : m == 98 ? 4 : m == 102 ? 5
-       : m == 103 ? 6 : m == 104 ? 7 : m == 105 ? 8 : m == 106 ? 9 : m == 109 ? 10
-       : m == 112 ? 11 : m == 114 ? 12 : m == 117 ? 13 : m == 120 ? 14 : m == 123 ? 15 : -1;
-}
+struct SchedHB {
+  static constexpr int W1 = 20, B1 = 21, W2 = 50, B2 = 51, W3 = 91, VM3 = 13, B3 = 92;
+  __host__ __device__ static constexpr int a1(int m) { return m < 16 && (m & 1) == 0 ? m >> 1 : -1; }
+  __host__ __device__ static constexpr int b1(int m) {
+    return m == 24 ? 0 : m == 27 ? 1 : m == 30 ? 2 : m == 33 ? 3 : m == 36 ? 4 : m == 38 ? 5
+         : m == 40 ? 6 : m == 42 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int adma(int m) {
+    return m == 22 ? 0 : m == 25 ? 1 : m == 28 ? 2 : m == 31 ? 3 : m == 34 ? 4 : m == 52 ? 5
+         : m == 55 ? 6 : m == 58 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int bdma(int m) {
+    return m == 61 ? 0 : m == 64 ? 1 : m == 85 ? 2 : m == 87 ? 3 : m == 89 ? 4 : m == 96 ? 5
+         : m == 100 ? 6 : m == 124 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int k0(int m) {
+    return m == 93 ? 0 : m == 94 ? 1 : m == 95 ? 2 : m == 97 ? 3 : m == 98 ? 4 : m == 102 ? 5
+         : m == 103 ? 6 : m == 104 ? 7 : m == 105 ? 8 : m == 106 ? 9 : m == 109 ? 10
+         : m == 112 ? 11 : m == 114 ? 12 : m == 117 ? 13 : m == 120 ? 14 : m == 123 ? 15 : -1;
+  }
+};
 
-template <int PAR, int MODE>
+// SCHED 2: two barriers per K-tile — all k-half-1 fragments (A at even m
+// 0..14, B at even m 16..30) retire before ONE barrier after m 35, then the
+// 16 pieces of stage s+2 go out interleaved (A at 36 + 6p, B at 39 + 6p);
+// vmcnt(16) + barrier #3 after m 96; next-k0 reads at odd m 97..127.
+struct SchedTwoBarrier {
+  static constexpr int W1 = 34, B1 = 35, W2 = -1, B2 = -1, W3 = 95, VM3 = 16, B3 = 96;
+  __host__ __device__ static constexpr int a1(int m) { return m < 16 && (m & 1) == 0 ? m >> 1 : -1; }
+  __host__ __device__ static constexpr int b1(int m) {
+    return m >= 16 && m < 32 && (m & 1) == 0 ? (m - 16) >> 1 : -1;
+  }
+  __host__ __device__ static constexpr int adma(int m) {
+    return m >= 36 && (m - 36) % 6 == 0 && (m - 36) / 6 < 8 ? (m - 36) / 6 : -1;
+  }
+  __host__ __device__ static constexpr int bdma(int m) {
+    return m >= 39 && (m - 39) % 6 == 0 && (m - 39) / 6 < 8 ? (m - 39) / 6 : -1;
+  }
+  __host__ __device__ static constexpr int k0(int m) {
+    return m >= 97 && (m & 1) ? (m - 97) >> 1 : -1;
+  }
+};
+
+// Table-driven K-tile: S gives, per MFMA index m, the fragment reads, DMA
+// pieces, waits and barriers that follow MFMA m (see w4i_ktile for MODE).
+template <class S, int PAR, int MODE>
 __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                           bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                           bf16x8_t (&f1b)[8], char* smem, int a_base, int b_base,
@@ -234,23 +262,22 @@ __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
         const int m = h * 64 + i * 8 + j;
         if (h == 0) mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
         else mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
-        if (m < 16 && (m & 1) == 0)
-          f1a[m >> 1] = lds_read_b128(X + a_base + (m >> 1) * SUB + off_k1);
-        if (MODE == 1 && m == 20) __builtin_amdgcn_s_waitcnt(0xC07F);
-        if (MODE == 1 && m == 21) __builtin_amdgcn_s_barrier();
-        if (MODE == 1 && hb_adma(m) >= 0) dma_a.issue(X, hb_adma(m), kb2, wave_s);
-        if (hb_b1(m) >= 0) f1b[hb_b1(m)] = lds_read_b128(X + b_base + hb_b1(m) * SUB + off_k1);
-        if (MODE == 1 && m == 50) __builtin_amdgcn_s_waitcnt(0xC07F);
-        if (MODE == 1 && m == 51) __builtin_amdgcn_s_barrier();
-        if (MODE == 1 && hb_bdma(m) >= 0)
-          dma_b.issue(X + W4B_OP_BYTES, hb_bdma(m), kb2, wave_s);
-        if (MODE != 3 && m == 91) {
-          if constexpr (MODE == 1) vm_wait<13>();
+        if (S::a1(m) >= 0) f1a[S::a1(m)] = lds_read_b128(X + a_base + S::a1(m) * SUB + off_k1);
+        if (MODE == 1 && m == S::W1) __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (MODE == 1 && m == S::B1) __builtin_amdgcn_s_barrier();
+        if (MODE == 1 && S::adma(m) >= 0) dma_a.issue(X, S::adma(m), kb2, wave_s);
+        if (S::b1(m) >= 0) f1b[S::b1(m)] = lds_read_b128(X + b_base + S::b1(m) * SUB + off_k1);
+        if (MODE == 1 && m == S::W2) __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (MODE == 1 && m == S::B2) __builtin_amdgcn_s_barrier();
+        if (MODE == 1 && S::bdma(m) >= 0)
+          dma_b.issue(X + W4B_OP_BYTES, S::bdma(m), kb2, wave_s);
+        if (MODE != 3 && m == S::W3) {
+          if constexpr (MODE == 1) vm_wait<S::VM3>();
           else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        if (MODE != 3 && m == 92) __builtin_amdgcn_s_barrier();
-        if (MODE != 3 && hb_k0(m) >= 0) {
-          const int r = hb_k0(m);
+        if (MODE != 3 && m == S::B3) __builtin_amdgcn_s_barrier();
+        if (MODE != 3 && S::k0(m) >= 0) {
+          const int r = S::k0(m);
           if (r < 8) f0b[r] = lds_read_b128(Y + b_base + r * SUB + off_k0);
           else f0a[r - 8] = lds_read_b128(Y + a_base + (r - 8) * SUB + off_k0);
         }
@@ -262,7 +289,8 @@ __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
 using mxk::store_block_wide;
 using mxk::store_block_narrow;
 
-// K-tile of schedule SCHED (0: w4i knobs LATE/R1, 1: hipBLASLt positions)
+// K-tile of schedule SCHED (0: w4i knobs LATE/R1, 1: hipBLASLt positions,
+// 2: two barriers)
 template <int SCHED, int PAR, int MODE, int LATE, int R1>
 __device__ __forceinline__ void ktile_sched(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                             bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
@@ -270,8 +298,11 @@ __device__ __forceinline__ void ktile_sched(f32x4_t (&acc)[8][8], bf16x8_t (&f0a
                                             int off_k0, int off_k1, const DmaK& dma_a,
                                             const DmaK& dma_b, int kb2, int wave_s, int par = 0) {
   if constexpr (SCHED == 1)
-    w4j_ktile<PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                         dma_b, kb2, wave_s, par);
+    w4j_ktile<SchedHB, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                  dma_a, dma_b, kb2, wave_s, par);
+  else if constexpr (SCHED == 2)
+    w4j_ktile<SchedTwoBarrier, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,
+                                          off_k1, dma_a, dma_b, kb2, wave_s, par);
   else
     w4i_ktile<PAR, MODE, LATE, R1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
                                    dma_a, dma_b, kb2, wave_s, par);
@@ -547,11 +578,11 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // Host launchers (C ABI, stream-ordered, capture-safe: no sync, no malloc).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kNumVariants = 7;
+constexpr int kNumVariants = 8;
 constexpr int kDefaultVariant = 6;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
-    "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb"};
+    "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -591,6 +622,7 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
       break;
     }
     case 6: launch_w4i<1, 2, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 7: launch_w4i<1, 2, 1, 0, 2>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
   }
 }
 
