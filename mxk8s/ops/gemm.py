@@ -66,8 +66,10 @@ def gemm_bf16_ex(a: torch.Tensor, b: torch.Tensor, a_kmajor: bool, b_kmajor: boo
     ``b_kmajor`` else [K, N]; all row-major with unit inner stride, bf16.
     Returns False (nothing launched) when the shape does not tile exactly
     (M, N multiples of 256, K of 64) so the caller can use the library GEMM.
-    ``variant`` 1 (default) = the three-barrier x2 schedule (both-K-major
-    problems run the validator's TN kernel); 0 = the one-barrier x kernel."""
+    ``variant`` 1 (default) picks per layout: both K-major -> the validator's
+    TN kernel, both N/M-major (weight gradients) -> the x2 schedule at
+    hipBLASLt's instruction positions, mixed (dgrad) -> x2; 2 / 3 / 0 force
+    x2-hipBLASLt-positions / x2 / the one-barrier x kernel (A/B)."""
     if a.dim() != 2 or b.dim() != 2 or a.stride(1) != 1 or b.stride(1) != 1 or \
             out.stride(1) != 1 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         return False

@@ -330,7 +330,69 @@ __device__ __forceinline__ void x2_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <bool AN, bool BN, int EPI>
+// SCHED 1: the same K-tile at hipBLASLt's instruction positions
+// (mxk::SchedHB; a "read" is one operand fragment as above).
+template <class S, bool AN, bool BN, int PAR, int MODE>
+__device__ __forceinline__ void x2_ktile_tab(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
+                                             bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
+                                             bf16x8_t (&f1b)[8], char* smem, const XOp<AN>& oa,
+                                             const XOp<BN>& ob, int wm, int wn, uint32_t soa,
+                                             uint32_t sob, int wave, int par = 0) {
+  constexpr int A_BYTES = XOp<AN>::BYTES;
+  constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
+  const int px = PAR == 2 ? par : PAR;
+  char* X = smem + px * STAGE;
+  char* Y = smem + (px ^ 1) * STAGE;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = h * 64 + i * 8 + j;
+        if (h == 0) xmfma(acc[i][j], f0b[j], f0a[i]);
+        else xmfma(acc[i][j], f1b[j], f1a[i]);
+        if (S::a1(m) >= 0) f1a[S::a1(m)] = oa.frag(X, wm * 8 + S::a1(m), 1);
+        if (MODE == 1 && m == S::W1) __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (MODE == 1 && m == S::B1) __builtin_amdgcn_s_barrier();
+        if (MODE == 1 && S::adma(m) >= 0) oa.issue_s(X, S::adma(m), soa, wave);
+        if (S::b1(m) >= 0) f1b[S::b1(m)] = ob.frag(X + A_BYTES, wn * 8 + S::b1(m), 1);
+        if (MODE == 1 && m == S::W2) __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (MODE == 1 && m == S::B2) __builtin_amdgcn_s_barrier();
+        if (MODE == 1 && S::bdma(m) >= 0) ob.issue_s(X + A_BYTES, S::bdma(m), sob, wave);
+        if (MODE != 3 && m == S::W3) {
+          if constexpr (MODE == 1) {
+            static_assert(S::VM3 == 13, "x2 tables: add the vmcnt");
+            asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        }
+        if (MODE != 3 && m == S::B3) __builtin_amdgcn_s_barrier();
+        if (MODE != 3 && S::k0(m) >= 0) {
+          const int r = S::k0(m);
+          if (r < 8) f0b[r] = ob.frag(Y + A_BYTES, wn * 8 + r, 0);
+          else f0a[r - 8] = oa.frag(Y, wm * 8 + r - 8, 0);
+        }
+      }
+    }
+  }
+}
+
+template <int SCHED, bool AN, bool BN, int PAR, int MODE>
+__device__ __forceinline__ void x2_ktile_s(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
+                                           bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
+                                           bf16x8_t (&f1b)[8], char* smem, const XOp<AN>& oa,
+                                           const XOp<BN>& ob, int wm, int wn, uint32_t soa,
+                                           uint32_t sob, int wave, int par = 0) {
+  if constexpr (SCHED == 1)
+    x2_ktile_tab<mxk::SchedHB, AN, BN, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn,
+                                                  soa, sob, wave, par);
+  else
+    x2_ktile<AN, BN, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, soa, sob, wave, par);
+}
+
+template <bool AN, bool BN, int EPI, int SCHED = 0>
 __global__ void __launch_bounds__(XT, 1)
 mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                         uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -383,20 +445,20 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
   int s = 0;
   uint32_t sa = 2 * ka, sb = 2 * kb;
   for (; s + 2 <= ns - 2; s += 2) {
-    x2_ktile<AN, BN, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, wave);
-    x2_ktile<AN, BN, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa + ka, sb + kb, wave);
+    x2_ktile_s<SCHED, AN, BN, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, wave);
+    x2_ktile_s<SCHED, AN, BN, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa + ka, sb + kb, wave);
     sa += 2 * ka;
     sb += 2 * kb;
   }
   if (s < ns - 2) {
-    x2_ktile<AN, BN, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, wave);
+    x2_ktile_s<SCHED, AN, BN, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, wave);
     ++s;
   }
   if (ns >= 2) {
-    x2_ktile<AN, BN, 2, 2>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
+    x2_ktile_s<SCHED, AN, BN, 2, 2>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
     ++s;
   }
-  x2_ktile<AN, BN, 2, 3>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
+  x2_ktile_s<SCHED, AN, BN, 2, 3>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   mxk::mfma_drain(acc);
 
@@ -407,12 +469,19 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
 }
 
 template <bool AN, bool BN>
-static void launch_x(int v, bool wide, int nwg, hipStream_t stream, const uint16_t* a,
+static void launch_x(int sched, bool wide, int nwg, hipStream_t stream, const uint16_t* a,
                      const uint16_t* b, uint16_t* c, int M, int N, int K, int lda, int ldb,
                      int ldc) {
-  if (v == 0)
+  // sched: -1 = the one-barrier x kernel, 0 = x2, 1 = x2 at hipBLASLt positions
+  if (sched < 0)
     hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<AN, BN>), dim3(nwg), dim3(XT), 0, stream, a, b, c,
                        M, N, K, lda, ldb, ldc);
+  else if (sched == 1 && wide)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 1, 1>), dim3(nwg), dim3(XT), 0, stream, a,
+                       b, c, M, N, K, lda, ldb, ldc);
+  else if (sched == 1)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 1>), dim3(nwg), dim3(XT), 0, stream, a,
+                       b, c, M, N, K, lda, ldb, ldc);
   else if (wide)
     hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 1>), dim3(nwg), dim3(XT), 0, stream, a, b,
                        c, M, N, K, lda, ldb, ldc);
@@ -427,9 +496,12 @@ MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int 
 // a_kmajor: A stored [M][K] (1) or [K][M] (0); b_kmajor: B stored [N][K] (1)
 // or [K][N] (0).  Row strides lda/ldb/ldc in elements.  Tiles exactly:
 // M % 256, N % 256, K % 64; returns hipErrorInvalidValue otherwise (callers
-// keep the library GEMM for other shapes).  variant 0 = the one-barrier x
-// kernel, 1 = x2 (default); both-K-major problems go to the validator's
-// TN kernel (gemm_bf16.hip) under variant 1.
+// keep the library GEMM for other shapes).  variant:
+//   1 (default) both K-major -> the validator's TN kernel (gemm_bf16.hip);
+//     both N/M-major (weight gradients) -> x2 at hipBLASLt's positions
+//     (+2-10 % on the Llama-3-8B wgrad shapes); mixed (dgrad) -> x2
+//   2 x2 at hipBLASLt's positions, 3 x2, 0 the one-barrier x kernel
+//   (2, 3 and 0 run every layout on the layout kernel, for A/B)
 MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int M, int N, int K,
                                      int lda, int ldb, int ldc, int a_kmajor, int b_kmajor,
                                      int variant, hipStream_t stream) {
@@ -441,23 +513,25 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                   (b_kmajor || bytes(K, ldb) < (1L << 32)) &&
                   reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(C) % 8 == 0 && (variant == 0 || variant == 1);
+                  reinterpret_cast<uintptr_t>(C) % 8 == 0 && variant >= 0 && variant <= 3;
   if (!ok) return static_cast<int>(hipErrorInvalidValue);
   if (variant == 1 && a_kmajor && b_kmajor)
     return mxk_gemm_bf16_tn(A, B, C, M, N, K, lda, ldb, ldc, stream);
+  const int sched = variant == 0 ? -1 : variant == 2 ? 1 : variant == 3 ? 0
+                  : (!a_kmajor && !b_kmajor) ? 1 : 0;
   const int nwg = (M / XBM) * (N / XBM);
   const bool wide = (ldc % 8 == 0) && (reinterpret_cast<uintptr_t>(C) % 16 == 0);
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);
   if (a_kmajor && b_kmajor)
-    launch_x<false, false>(variant, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
+    launch_x<false, false>(sched, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
   else if (a_kmajor)
-    launch_x<false, true>(variant, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
+    launch_x<false, true>(sched, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
   else if (b_kmajor)
-    launch_x<true, false>(variant, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
+    launch_x<true, false>(sched, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
   else
-    launch_x<true, true>(variant, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
+    launch_x<true, true>(sched, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
   MXK_RETURN_LAUNCH_STATUS();
 }
 

@@ -192,6 +192,53 @@ __device__ __forceinline__ void store_block_narrow(const f32x4_t (&acc)[8][8], u
   }
 }
 
+// Per-K-tile instruction positions of the three-barrier GEMM schedules (see
+// gemm_bf16.hip): for MFMA index m (0..127) the fragment read / DMA piece
+// index that follows it (-1: none), and the MFMA after which each wait and
+// barrier sits.
+struct SchedHB {
+  static constexpr int W1 = 20, B1 = 21, W2 = 50, B2 = 51, W3 = 91, VM3 = 13, B3 = 92;
+  __host__ __device__ static constexpr int a1(int m) { return m < 16 && (m & 1) == 0 ? m >> 1 : -1; }
+  __host__ __device__ static constexpr int b1(int m) {
+    return m == 24 ? 0 : m == 27 ? 1 : m == 30 ? 2 : m == 33 ? 3 : m == 36 ? 4 : m == 38 ? 5
+         : m == 40 ? 6 : m == 42 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int adma(int m) {
+    return m == 22 ? 0 : m == 25 ? 1 : m == 28 ? 2 : m == 31 ? 3 : m == 34 ? 4 : m == 52 ? 5
+         : m == 55 ? 6 : m == 58 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int bdma(int m) {
+    return m == 61 ? 0 : m == 64 ? 1 : m == 85 ? 2 : m == 87 ? 3 : m == 89 ? 4 : m == 96 ? 5
+         : m == 100 ? 6 : m == 124 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int k0(int m) {
+    return m == 93 ? 0 : m == 94 ? 1 : m == 95 ? 2 : m == 97 ? 3 : m == 98 ? 4 : m == 102 ? 5
+         : m == 103 ? 6 : m == 104 ? 7 : m == 105 ? 8 : m == 106 ? 9 : m == 109 ? 10
+         : m == 112 ? 11 : m == 114 ? 12 : m == 117 ? 13 : m == 120 ? 14 : m == 123 ? 15 : -1;
+  }
+};
+
+// SCHED 2: two barriers per K-tile — all k-half-1 fragments (A at even m
+// 0..14, B at even m 16..30) retire before ONE barrier after m 35, then the
+// 16 pieces of stage s+2 go out interleaved (A at 36 + 6p, B at 39 + 6p);
+// vmcnt(16) + barrier #3 after m 96; next-k0 reads at odd m 97..127.
+struct SchedTwoBarrier {
+  static constexpr int W1 = 34, B1 = 35, W2 = -1, B2 = -1, W3 = 95, VM3 = 16, B3 = 96;
+  __host__ __device__ static constexpr int a1(int m) { return m < 16 && (m & 1) == 0 ? m >> 1 : -1; }
+  __host__ __device__ static constexpr int b1(int m) {
+    return m >= 16 && m < 32 && (m & 1) == 0 ? (m - 16) >> 1 : -1;
+  }
+  __host__ __device__ static constexpr int adma(int m) {
+    return m >= 36 && (m - 36) % 6 == 0 && (m - 36) / 6 < 8 ? (m - 36) / 6 : -1;
+  }
+  __host__ __device__ static constexpr int bdma(int m) {
+    return m >= 39 && (m - 39) % 6 == 0 && (m - 39) / 6 < 8 ? (m - 39) / 6 : -1;
+  }
+  __host__ __device__ static constexpr int k0(int m) {
+    return m >= 97 && (m & 1) ? (m - 97) >> 1 : -1;
+  }
+};
+
 }  // namespace mxk
 
 // Host-side error plumbing: every launcher returns hipError_t as int so the

@@ -11,7 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mxk8s.ops.gemm import gemm_bf16_ex  # noqa: E402
 
-VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1").split(",")]
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1").split(",")]
 SHAPES = [(4096, 6144, "wqkv"), (4096, 4096, "wo"), (4096, 28672, "w13"), (14336, 4096, "w2")]
 
 

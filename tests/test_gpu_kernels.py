@@ -191,12 +191,15 @@ def test_add_rmsnorm_fwd_bwd(cuda_device, rows, H):
     assert (w.grad.float() - wr.grad).abs().max() <= 2e-2 * wr.grad.abs().max() + 1e-2
 
 
-@pytest.mark.parametrize("layout", ["tn", "nn", "nt_wgrad"])
-def test_gemm_layouts_vs_fp32(cuda_device, layout):
-    """Layout-generic MFMA GEMM (K-major / N-major operands, tr_b16 reads)."""
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("layout", ["tn", "nn", "nt_wgrad", "tt"])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 320), (4096, 4096, 192)])
+def test_gemm_layouts_vs_fp32(cuda_device, layout, variant, M, N, K):
+    """Layout-generic MFMA GEMM (K-major / N-major operands, tr_b16 reads);
+    every schedule (auto, x, x2, x2 at hipBLASLt positions); 4096^2 puts the XCD
+    super-block tile map in play."""
     from mxk8s.ops.gemm import gemm_bf16_ex
     g = torch.Generator(device=cuda_device).manual_seed(11)
-    M, N, K = 512, 768, 320
     r = lambda *s: (torch.rand(*s, device=cuda_device, generator=g) * 2 - 1).bfloat16()  # noqa: E731
     if layout == "tn":
         a, b, ak, bk = r(M, K), r(N, K), True, True
@@ -204,15 +207,18 @@ def test_gemm_layouts_vs_fp32(cuda_device, layout):
     elif layout == "nn":
         a, b, ak, bk = r(M, K), r(K, N), True, False
         ref = a.float() @ b.float()
+    elif layout == "tt":
+        a, b, ak, bk = r(K, M), r(N, K), False, True
+        ref = a.float().t() @ b.float().t()
     else:
         a, b, ak, bk = r(K, M), r(K, N), False, False
         ref = a.float().t() @ b.float()
-    out = torch.empty(M, N, device=cuda_device, dtype=torch.bfloat16)
-    assert gemm_bf16_ex(a, b, ak, bk, out)
+    out = torch.full((M, N), float("nan"), device=cuda_device, dtype=torch.bfloat16)
+    assert gemm_bf16_ex(a, b, ak, bk, out, variant=variant)
     err = (out.float() - ref).abs().max().item()
     assert err <= 2 ** -7 * ref.abs().max().item() + 1e-3, err
     # shapes that do not tile fall back (nothing launched)
-    assert not gemm_bf16_ex(a[:, :-64] if ak else a[:-64], b, ak, bk, out)
+    assert not gemm_bf16_ex(a[:, :-64] if ak else a[:-64], b, ak, bk, out, variant=variant)
 
 
 @pytest.mark.parametrize("T,V", [(4, 128256), (300, 1000), (7, 8)])
