@@ -56,6 +56,9 @@ _SIGNATURES = {
     "mxk_attn_fwd_variant": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _l, _l, _l, _f, _i, _i,
                                   _vp]),
     "mxk_attn_bwd_workspace": (_l, [_i, _i, _i]),
+    "mxk_attn_bwd_workspace_variant": (_l, [_i, _i, _i, _i]),
+    "mxk_attn_bwd_variant": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i,
+                                  _i, _l, _l, _l, _l, _l, _f, _i, _i, _vp]),
     "mxk_attn_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i,
                           _l, _l, _l, _l, _l, _f, _i, _vp]),
     "mxk_xent_fwd": (_i, [_vp, _vp, _vp, _vp, _l, _i, _l, _vp]),

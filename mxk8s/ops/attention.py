@@ -71,11 +71,13 @@ def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None, variant: 
 
 
 def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = None,
-             dk=None, dv=None):
+             dk=None, dv=None, variant: int = 1):
     """HIP backward: returns (dq [B,S,Hq,D], dk [B,S,Hkv,D], dv [B,S,Hkv,D]).
 
     ``dk``/``dv`` may be preallocated views (e.g. slices of a fused dQKV
-    buffer) with a token stride; by default they are fresh contiguous tensors."""
+    buffer) with a token stride; by default they are fresh contiguous tensors.
+    ``variant`` 1 (default): dK/dV accumulated over the query-head group in
+    one workgroup, bf16 out; 0: per-query-head fp32 partials + GQA reduce."""
     B, S, Hq, D = q.shape
     Hkv = k.shape[2]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -86,11 +88,14 @@ def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = N
     if dv is None:
         dv = torch.empty((B, S, Hkv, D), dtype=v.dtype, device=v.device)
     L = _lib.lib()
-    ws = torch.empty(L.mxk_attn_bwd_workspace(B, S, Hq) // 4, dtype=torch.float32, device=q.device)
-    st = L.mxk_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
-                        lse.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), ws.data_ptr(),
-                        B, S, Hq, Hkv, D, q.stride(1), k.stride(1), v.stride(1), dk.stride(1),
-                        dv.stride(1), float(scale), int(causal), _lib.stream_ptr(q.device))
+    ws = torch.empty(L.mxk_attn_bwd_workspace_variant(B, S, Hq, int(variant)) // 4,
+                     dtype=torch.float32, device=q.device)
+    st = L.mxk_attn_bwd_variant(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                dout.data_ptr(), lse.data_ptr(), dq.data_ptr(), dk.data_ptr(),
+                                dv.data_ptr(), ws.data_ptr(), B, S, Hq, Hkv, D, q.stride(1),
+                                k.stride(1), v.stride(1), dk.stride(1), dv.stride(1),
+                                float(scale), int(causal), int(variant),
+                                _lib.stream_ptr(q.device))
     _lib.check(st, "mxk_attn_bwd")
     return dq, dk, dv
 

@@ -938,13 +938,21 @@ __device__ __forceinline__ bf16x8_t pack2x4(const f32x4_t& lo, const f32x4_t& hi
 constexpr int NT16 = 512;
 }  // namespace
 
-template <bool CAUSAL>
+// GQA: one workgroup per (batch, KV head, key block) walks every query head
+// of the group, so dK^T / dV^T of its keys accumulate in registers over the
+// whole group and are written once, in bf16, straight into dk / dv (token
+// strides dk_tok / dv_tok).  Without it, one workgroup per query head writes
+// fp32 partials that mxk_attn_bwd_gqa_reduce_kernel sums (4x the grid,
+// ~1.1 GB more HBM traffic per Llama-3-8B layer at B = 8).
+template <bool CAUSAL, bool GQA = false>
 __global__ void __launch_bounds__(NT16, 1)
 mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                            const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
                            const float* __restrict__ lse, const float* __restrict__ delta,
                            float* __restrict__ dk_p, float* __restrict__ dv_p, int S, int Hq,
-                           int Hkv, long q_tok, long k_tok, long v_tok, float scale) {
+                           int Hkv, long q_tok, long k_tok, long v_tok, float scale,
+                           uint16_t* __restrict__ dk = nullptr, uint16_t* __restrict__ dv = nullptr,
+                           long dk_tok = 0, long dv_tok = 0) {
   __shared__ __attribute__((aligned(16))) char smem[2][2 * BQB * 256];   // [buf][Q | dO]
   __shared__ __attribute__((aligned(16))) float srow[2][2][BQB];       // [buf][-lse/scale | -delta]
   const int tid = threadIdx.x;
@@ -960,18 +968,15 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
     map_block(blockIdx.x, gridDim.x / nkb, nkb, CAUSAL, &bh, &qbi);
     kb = CAUSAL ? nkb - 1 - qbi : qbi;
   }
-  const int b = bh / Hq, hq = bh % Hq;
-  const int hkv = hq / (Hq / Hkv);
+  const int grp = Hq / Hkv;
+  const int b = GQA ? bh / Hkv : bh / Hq;
+  const int hq0 = GQA ? (bh % Hkv) * grp : bh % Hq;
+  const int hkv = GQA ? bh % Hkv : hq0 / grp;
   const int k0 = kb * BQ;
   const int kw0 = k0 + wave * 16;
   const int mykey = kw0 + c16;
-
-  const uint16_t* qb_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
-  const uint16_t* dob_ptr = dout + static_cast<long>(b) * S * Hq * D + static_cast<long>(hq) * D;
   const uint16_t* kb_ptr = k + static_cast<long>(b) * S * k_tok + static_cast<long>(hkv) * D;
   const uint16_t* vb_ptr = v + static_cast<long>(b) * S * v_tok + static_cast<long>(hkv) * D;
-  const float* lse_b = lse + (static_cast<long>(b) * Hq + hq) * S;
-  const float* dl_b = delta + (static_cast<long>(b) * Hq + hq) * S;
 
   // B operands of S / dP: lane holds K[mykey][32 s + 8 G .. +7]
   bf16x8_t kf[4], vf[4];
@@ -983,8 +988,24 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
   const float c = scale * 1.4426950408889634f;
   const float inv_c = 1.f / c;
 
+  f32x4_t dka[8], dva[8];
+#pragma unroll
+  for (int db = 0; db < 8; ++db) {
+    dka[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    dva[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  // transposed-read lane constants: row 4G + (i >> 2), column block 4 (i & 3)
+  const int tr_row = 4 * G + (c16 >> 2);
+  const int tr_chb = (c16 & 3) >> 1;
+  const int tr_byte = 8 * (c16 & 1);
   const int q_begin = CAUSAL ? k0 : 0;
   const int nsl = (S - q_begin) / BQB;
+  for (int gq = 0; gq < (GQA ? grp : 1); ++gq) {
+  const int hq = hq0 + gq;
+  const uint16_t* qb_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
+  const uint16_t* dob_ptr = dout + static_cast<long>(b) * S * Hq * D + static_cast<long>(hq) * D;
+  const float* lse_b = lse + (static_cast<long>(b) * Hq + hq) * S;
+  const float* dl_b = delta + (static_cast<long>(b) * Hq + hq) * S;
   // loader: 512 threads x 2 chunks per tile (64 rows x 16 chunks)
   const int ld_row = tid >> 4, ld_ch = tid & 15;
   bf16x8_t qst[2], dst[2];
@@ -1014,16 +1035,6 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
   store_slice(0);
   __syncthreads();
 
-  f32x4_t dka[8], dva[8];
-#pragma unroll
-  for (int db = 0; db < 8; ++db) {
-    dka[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    dva[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  }
-  // transposed-read lane constants: row 4G + (i >> 2), column block 4 (i & 3)
-  const int tr_row = 4 * G + (c16 >> 2);
-  const int tr_chb = (c16 & 3) >> 1;
-  const int tr_byte = 8 * (c16 & 1);
 
   for (int t = 0; t < nsl; ++t) {
     const int buf = t & 1;
@@ -1081,15 +1092,33 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
     if (t + 1 < nsl) store_slice(buf ^ 1);
     __syncthreads();
   }
+  }   // query heads of the group
   // lane = key, registers r: d = 16 db + 4 G + r
-  const long prow = ((static_cast<long>(b) * S + mykey) * Hq + hq) * D;
+  if constexpr (GQA) {
+    uint16_t* dkr = dk + (static_cast<long>(b) * S + mykey) * dk_tok + static_cast<long>(hkv) * D;
+    uint16_t* dvr = dv + (static_cast<long>(b) * S + mykey) * dv_tok + static_cast<long>(hkv) * D;
 #pragma unroll
-  for (int db = 0; db < 8; ++db) {
-    const int d = 16 * db + 4 * G;
-    *reinterpret_cast<float4*>(dk_p + prow + d) =
-        make_float4(dka[db][0] * scale, dka[db][1] * scale, dka[db][2] * scale, dka[db][3] * scale);
-    *reinterpret_cast<float4*>(dv_p + prow + d) =
-        make_float4(dva[db][0], dva[db][1], dva[db][2], dva[db][3]);
+    for (int db = 0; db < 8; ++db) {
+      const int d = 16 * db + 4 * G;
+      uint2 pk;
+      pk.x = mxk::pack2bf(dka[db][0] * scale, dka[db][1] * scale);
+      pk.y = mxk::pack2bf(dka[db][2] * scale, dka[db][3] * scale);
+      *reinterpret_cast<uint2*>(dkr + d) = pk;
+      pk.x = mxk::pack2bf(dva[db][0], dva[db][1]);
+      pk.y = mxk::pack2bf(dva[db][2], dva[db][3]);
+      *reinterpret_cast<uint2*>(dvr + d) = pk;
+    }
+  } else {
+    const long prow = ((static_cast<long>(b) * S + mykey) * Hq + hq0) * D;
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      const int d = 16 * db + 4 * G;
+      *reinterpret_cast<float4*>(dk_p + prow + d) =
+          make_float4(dka[db][0] * scale, dka[db][1] * scale, dka[db][2] * scale,
+                      dka[db][3] * scale);
+      *reinterpret_cast<float4*>(dv_p + prow + d) =
+          make_float4(dva[db][0], dva[db][1], dva[db][2], dva[db][3]);
+    }
   }
 }
 
@@ -1122,21 +1151,25 @@ mxk_attn_bwd_gqa_reduce_kernel(const float* __restrict__ dk_p, const float* __re
   *reinterpret_cast<uint2*>(dv + bs * dv_tok + hkv * D + d) = pk;
 }
 
-// Workspace: delta [B*Hq*S] fp32 + dk/dv partials 2 x [B*S*Hq*128] fp32.
-MXK_API long mxk_attn_bwd_workspace(int B, int S, int Hq) {
+// Workspace: delta [B*Hq*S] fp32 (+ dk/dv partials 2 x [B*S*Hq*128] fp32 for
+// variant 0, the per-query-head dK/dV kernel).
+MXK_API long mxk_attn_bwd_workspace_variant(int B, int S, int Hq, int variant) {
   const long rows = static_cast<long>(B) * Hq * S;
-  return rows * 4 + 2 * rows * D * 4;
+  return rows * 4 + (variant == 0 ? 2 * rows * D * 4 : 0);
+}
+MXK_API long mxk_attn_bwd_workspace(int B, int S, int Hq) {
+  return mxk_attn_bwd_workspace_variant(B, S, Hq, 0);
 }
 
-// dout, o, dq: [B, S, Hq, 128] contiguous; dk/dv written at token strides
-// dk_tok/dv_tok (they may be views into one fused dQKV buffer).
-MXK_API int mxk_attn_bwd(const void* q, const void* k, const void* v, const void* o,
-                         const void* dout, const float* lse, void* dq, void* dk, void* dv,
-                         void* workspace, int B, int S, int Hq, int Hkv, int head_dim, long q_tok,
-                         long k_tok, long v_tok, long dk_tok, long dv_tok, float scale, int causal,
-                         hipStream_t stream) {
+// variant 1 (default): dK/dV per (batch, KV head, key block) over the whole
+// query-head group, bf16 out; 0: per query head + fp32 partials + GQA reduce.
+MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, const void* o,
+                                 const void* dout, const float* lse, void* dq, void* dk, void* dv,
+                                 void* workspace, int B, int S, int Hq, int Hkv, int head_dim,
+                                 long q_tok, long k_tok, long v_tok, long dk_tok, long dv_tok,
+                                 float scale, int causal, int variant, hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv || q_tok % 8 ||
-      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 ||
+      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 1 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
        reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
@@ -1145,31 +1178,58 @@ MXK_API int mxk_attn_bwd(const void* q, const void* k, const void* v, const void
     return static_cast<int>(hipErrorInvalidValue);
   const long rows = static_cast<long>(B) * Hq * S;
   float* delta = static_cast<float*>(workspace);
-  float* dk_p = delta + rows;
-  float* dv_p = dk_p + rows * D;
+  float* dk_p = variant == 0 ? delta + rows : nullptr;
+  float* dv_p = variant == 0 ? dk_p + rows * D : nullptr;
   const auto* Q = static_cast<const uint16_t*>(q);
   const auto* K = static_cast<const uint16_t*>(k);
   const auto* V = static_cast<const uint16_t*>(v);
   const auto* dO = static_cast<const uint16_t*>(dout);
+  auto* dK = static_cast<uint16_t*>(dk);
+  auto* dV = static_cast<uint16_t*>(dv);
   hipLaunchKernelGGL(mxk_attn_bwd_delta_kernel, dim3((rows * 16 + 255) / 256), dim3(256), 0,
                      stream, static_cast<const uint16_t*>(o), dO, delta, S, Hq, rows);
   const int nwg = B * Hq * (S / BQ);
-  if (causal) {
-    hipLaunchKernelGGL(mxk_attn_bwd_dkdv16_kernel<true>, dim3(nwg), dim3(NT16), 0, stream, Q, K, V,
-                       dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  const int nwg_kv = B * Hkv * (S / BQ);
+  if (variant == 1) {
+    if (causal)
+      hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<true, true>), dim3(nwg_kv), dim3(NT16), 0,
+                         stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok,
+                         v_tok, scale, dK, dV, dk_tok, dv_tok);
+    else
+      hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<false, true>), dim3(nwg_kv), dim3(NT16), 0,
+                         stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok,
+                         v_tok, scale, dK, dV, dk_tok, dv_tok);
+  } else if (causal) {
+    hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<true, false>), dim3(nwg), dim3(NT16), 0, stream,
+                       Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok, v_tok, scale,
+                       nullptr, nullptr, 0L, 0L);
+  } else {
+    hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<false, false>), dim3(nwg), dim3(NT16), 0,
+                       stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok,
+                       v_tok, scale, nullptr, nullptr, 0L, 0L);
+  }
+  if (causal)
     hipLaunchKernelGGL(mxk_attn_bwd_dq_kernel<true>, dim3(nwg), dim3(NT), 0, stream, Q, K, V, dO,
                        lse, delta, static_cast<uint16_t*>(dq), S, Hq, Hkv, q_tok, k_tok, v_tok,
                        scale);
-  } else {
-    hipLaunchKernelGGL(mxk_attn_bwd_dkdv16_kernel<false>, dim3(nwg), dim3(NT16), 0, stream, Q, K, V,
-                       dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
-    hipLaunchKernelGGL(mxk_attn_bwd_dq_kernel<false>, dim3(nwg), dim3(NT), 0, stream, Q, K, V,
-                       dO, lse, delta, static_cast<uint16_t*>(dq), S, Hq, Hkv, q_tok, k_tok,
-                       v_tok, scale);
+  else
+    hipLaunchKernelGGL(mxk_attn_bwd_dq_kernel<false>, dim3(nwg), dim3(NT), 0, stream, Q, K, V, dO,
+                       lse, delta, static_cast<uint16_t*>(dq), S, Hq, Hkv, q_tok, k_tok, v_tok,
+                       scale);
+  if (variant == 0) {
+    const long n_out = static_cast<long>(B) * S * Hkv * D;
+    hipLaunchKernelGGL(mxk_attn_bwd_gqa_reduce_kernel, dim3((n_out / 4 + 255) / 256), dim3(256), 0,
+                       stream, dk_p, dv_p, dK, dV, n_out, Hq, Hkv, dk_tok, dv_tok);
   }
-  const long n_out = static_cast<long>(B) * S * Hkv * D;
-  hipLaunchKernelGGL(mxk_attn_bwd_gqa_reduce_kernel, dim3((n_out / 4 + 255) / 256), dim3(256), 0,
-                     stream, dk_p, dv_p, static_cast<uint16_t*>(dk), static_cast<uint16_t*>(dv),
-                     n_out, Hq, Hkv, dk_tok, dv_tok);
   MXK_RETURN_LAUNCH_STATUS();
+}
+
+MXK_API int mxk_attn_bwd(const void* q, const void* k, const void* v, const void* o,
+                         const void* dout, const float* lse, void* dq, void* dk, void* dv,
+                         void* workspace, int B, int S, int Hq, int Hkv, int head_dim, long q_tok,
+                         long k_tok, long v_tok, long dk_tok, long dv_tok, float scale, int causal,
+                         hipStream_t stream) {
+  return mxk_attn_bwd_variant(q, k, v, o, dout, lse, dq, dk, dv, workspace, B, S, Hq, Hkv,
+                              head_dim, q_tok, k_tok, v_tok, dk_tok, dv_tok, scale, causal, 0,
+                              stream);
 }

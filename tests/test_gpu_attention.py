@@ -66,3 +66,31 @@ def test_attn_bwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
         err = (got.float() - want).abs().max().item()
         tol = 3e-2 * max(1.0, want.abs().max().item())
         assert err < tol, (name, err, tol)
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
+    (1, 256, 8, 2, True),
+    (2, 384, 4, 1, True),
+    (1, 256, 4, 4, False),
+])
+def test_attn_bwd_variants_into_strided_dkdv(cuda_device, B, S, Hq, Hkv, causal, variant):
+    """Both dK/dV schedules (per-q-head partials + reduce, GQA-fused), writing
+    dk/dv into slices of one fused [dq | dk | dv] buffer (token stride)."""
+    q, k, v = _qkv(B, S, Hq, Hkv, cuda_device, seed=3, fused=True)
+    o, lse = A.attn_fwd(q, k, v, causal=causal)
+    g = torch.Generator(device=cuda_device).manual_seed(9)
+    dout = torch.randn(B, S, Hq, 128, device=cuda_device, generator=g).bfloat16()
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    A.attention_ref(qr, kr, vr, causal=causal).backward(dout.float())
+    fused = torch.full((B, S, (Hq + 2 * Hkv) * 128), float("nan"), device=cuda_device,
+                       dtype=torch.bfloat16)
+    dk = fused[..., Hq * 128:(Hq + Hkv) * 128].view(B, S, Hkv, 128)
+    dv = fused[..., (Hq + Hkv) * 128:].view(B, S, Hkv, 128)
+    dq, dk2, dv2 = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, dk=dk, dv=dv, variant=variant)
+    assert dk2.data_ptr() == dk.data_ptr() and dv2.data_ptr() == dv.data_ptr()
+    assert torch.isnan(fused[..., :Hq * 128]).all()   # the dq slice is not touched
+    for name, got, want in (("dq", dq, qr.grad), ("dk", dk, kr.grad), ("dv", dv, vr.grad)):
+        err = (got.float() - want).abs().max().item()
+        tol = 3e-2 * max(1.0, want.abs().max().item())
+        assert err < tol, (name, variant, err, tol)
