@@ -27,7 +27,7 @@ import torch.nn.functional as F
 from ..ops.attention import flash_attention, supported as flash_supported
 from ..ops.linear import Linear
 from ..ops.xent import cross_entropy
-from ..ops.fused import add_rmsnorm, rmsnorm, rope, rope_tables, swiglu
+from ..ops.fused import add_rmsnorm, qkv_rope, rmsnorm, rope_tables, swiglu
 
 
 @dataclasses.dataclass
@@ -92,10 +92,9 @@ class Attention(nn.Module):
         c = self.cfg
         hd = c.head_dim
         qkv = self.wqkv(x)
-        q, k, v = qkv.split([c.n_heads * hd, c.n_kv_heads * hd, c.n_kv_heads * hd], dim=-1)
-        q = rope(q.reshape(B, S, c.n_heads, hd), cos, sin)
-        k = rope(k.reshape(B, S, c.n_kv_heads, hd), cos, sin)
-        v = v.reshape(B, S, c.n_kv_heads, hd)   # view into qkv: token stride (Hq+2Hkv)*hd
+        # q, k rotated straight out of their qkv slices; v a view into qkv
+        # (token stride (Hq+2Hkv)*hd); one d(qkv) buffer in the backward
+        q, k, v = qkv_rope(qkv, cos, sin, c.n_heads, c.n_kv_heads, hd)
         if flash_supported(q, k, v):
             # hand-written gfx950 flash attention: [B,S,H,D] in and out, no transposes
             o = flash_attention(q, k, v, causal=True)

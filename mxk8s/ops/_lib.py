@@ -48,6 +48,7 @@ _SIGNATURES = {
     "mxk_swiglu_fwd": (_i, [_vp, _vp, _l, _i, _vp]),
     "mxk_swiglu_bwd": (_i, [_vp, _vp, _vp, _l, _i, _vp]),
     "mxk_rope": (_i, [_vp, _vp, _vp, _vp, _l, _i, _i, _i, _f, _vp]),
+    "mxk_rope_strided": (_i, [_vp, _vp, _vp, _vp, _l, _i, _i, _i, _f, _l, _l, _vp]),
     "mxk_sumsq_partials": (_i, [_l]),
     "mxk_grad_clip_scale": (_i, [_vp, _l, _vp, _f, _f, _vp, _vp]),
     "mxk_grad_sumsq": (_i, [_vp, _l, _vp, _vp, _vp]),

@@ -13,6 +13,7 @@ log-sum-exp that the backward kernel uses to recompute P.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -70,8 +71,11 @@ def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None, variant: 
     return o, lse
 
 
+_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "1"))
+
+
 def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = None,
-             dk=None, dv=None, variant: int = 1):
+             dk=None, dv=None, variant: int | None = None):
     """HIP backward: returns (dq [B,S,Hq,D], dk [B,S,Hkv,D], dv [B,S,Hkv,D]).
 
     ``dk``/``dv`` may be preallocated views (e.g. slices of a fused dQKV
@@ -80,6 +84,7 @@ def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = N
     one workgroup, bf16 out; 0: per-query-head fp32 partials + GQA reduce."""
     B, S, Hq, D = q.shape
     Hkv = k.shape[2]
+    variant = _BWD_VARIANT if variant is None else variant
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     dout = dout.contiguous()
     dq = torch.empty((B, S, Hq, D), dtype=q.dtype, device=q.device)

@@ -188,12 +188,19 @@ def swiglu(gu: torch.Tensor) -> torch.Tensor:
 # ----------------------------------------------------------------------------
 
 
-def _rope_launch(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, sign: float) -> torch.Tensor:
+def _rope_launch(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, sign: float,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """RoPE of x [B, S, H, D] into ``out`` (fresh contiguous by default).  x and
+    out may be token-strided views ([B, S, H, D] with unit head/dim strides),
+    e.g. slices of the fused QKV projection or of its gradient buffer."""
     B, S, H, D = x.shape
-    xc = x.contiguous()
-    y = torch.empty_like(xc)
-    st = _lib.lib().mxk_rope(xc.data_ptr(), y.data_ptr(), cos.data_ptr(), sin.data_ptr(),
-                             B * S, H, D, S, float(sign), _lib.stream_ptr(x.device))
+    if not (x.stride(3) == 1 and x.stride(2) == D and x.stride(0) == S * x.stride(1)):
+        x = x.contiguous()
+    y = torch.empty((B, S, H, D), dtype=x.dtype, device=x.device) if out is None else out
+    assert y.stride(3) == 1 and y.stride(2) == D and y.stride(0) == S * y.stride(1)
+    st = _lib.lib().mxk_rope_strided(x.data_ptr(), y.data_ptr(), cos.data_ptr(), sin.data_ptr(),
+                                     B * S, H, D, S, float(sign), x.stride(1), y.stride(1),
+                                     _lib.stream_ptr(x.device))
     _lib.check(st, "mxk_rope")
     return y
 
@@ -210,6 +217,56 @@ class _RoPE(torch.autograd.Function):
         return _rope_launch(dy, cos, sin, -1.0), None, None
 
 
+class _QKVRoPE(torch.autograd.Function):
+    """Split of the fused QKV projection output + RoPE of q and k in one node:
+    q and k are rotated straight out of their qkv slices (no contiguous
+    copies), and the backward writes d(qkv) slice by slice into one buffer
+    (RoPE-backward output strided into it) instead of autograd's split
+    backward concatenating dq, dk and dv."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, hq: int, hkv: int, hd: int):
+        B, S, _ = qkv.shape
+        q = qkv[..., :hq * hd].view(B, S, hq, hd)
+        k = qkv[..., hq * hd:(hq + hkv) * hd].view(B, S, hkv, hd)
+        v = qkv[..., (hq + hkv) * hd:].view(B, S, hkv, hd)
+        ctx.save_for_backward(cos, sin)
+        ctx.dims = (hq, hkv, hd)
+        return _rope_launch(q, cos, sin, 1.0), _rope_launch(k, cos, sin, 1.0), v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        cos, sin = ctx.saved_tensors
+        hq, hkv, hd = ctx.dims
+        ref = dq if dq is not None else (dk if dk is not None else dv)
+        B, S = ref.shape[:2]
+        dqkv = torch.empty((B, S, (hq + 2 * hkv) * hd), dtype=ref.dtype, device=ref.device)
+        for g, lo, h in ((dq, 0, hq), (dk, hq, hkv)):
+            sl = dqkv[..., lo * hd:(lo + h) * hd].view(B, S, h, hd)
+            if g is None:
+                sl.zero_()
+            else:
+                _rope_launch(g, cos, sin, -1.0, out=sl)
+        vs = dqkv[..., (hq + hkv) * hd:].view(B, S, hkv, hd)
+        if dv is None:
+            vs.zero_()
+        else:
+            vs.copy_(dv)
+        return dqkv, None, None, None, None, None
+
+
+def qkv_rope(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, hq: int, hkv: int,
+             hd: int):
+    """(q, k, v) of a fused projection output qkv [B, S, (hq + 2 hkv) hd], with
+    rotary embedding applied to q and k; v is a view of qkv."""
+    B, S, _ = qkv.shape
+    if qkv.device.type == "cpu" or qkv.dtype != torch.bfloat16:
+        q, k, v = qkv.split([hq * hd, hkv * hd, hkv * hd], dim=-1)
+        return (rope_ref(q.reshape(B, S, hq, hd), cos, sin),
+                rope_ref(k.reshape(B, S, hkv, hd), cos, sin), v.reshape(B, S, hkv, hd))
+    return _QKVRoPE.apply(qkv, cos[:S].contiguous(), sin[:S].contiguous(), hq, hkv, hd)
+
+
 def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     """Apply rotary embedding to x [B, S, H, D] with tables [>=S, D/2]."""
     if x.device.type == "cpu" or x.dtype != torch.bfloat16:
@@ -220,5 +277,5 @@ def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     return _RoPE.apply(x, cos_s, sin_s)
 
 
-__all__ = ["rmsnorm", "add_rmsnorm", "swiglu", "rope", "rope_tables", "rmsnorm_ref", "swiglu_ref",
-           "rope_ref"]
+__all__ = ["rmsnorm", "add_rmsnorm", "swiglu", "rope", "qkv_rope", "rope_tables", "rmsnorm_ref",
+           "swiglu_ref", "rope_ref"]

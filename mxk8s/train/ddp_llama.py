@@ -160,6 +160,7 @@ def run_ddp_bench(args) -> dict:
         "bucket_mb": bucket_mb,
         "tuned_gemms": tuned,
         "grad_norm_last": float(opt.last_grad_norm.item()),
+        "losses": [round(float(x), 6) for x in torch.stack(losses).float().tolist()] if losses else [],
     }
 
 

@@ -307,7 +307,7 @@ mxk_swiglu_bwd_kernel(const uint16_t* __restrict__ gu, const uint16_t* __restric
 __global__ void __launch_bounds__(256)
 mxk_rope_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                 const float* __restrict__ cos_t, const float* __restrict__ sin_t, long tokens,
-                int heads, int D, int S, float sign) {
+                int heads, int D, int S, float sign, long x_tok, long y_tok) {
   const int half = D / 2;
   const int vph = half / 8;   // 8-pair vectors per head
   const long nvec = tokens * heads * vph;
@@ -316,8 +316,9 @@ mxk_rope_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
     const long th = i / vph;             // token*heads + head
     const int p0 = static_cast<int>(i - th * vph) * 8;
     const long tok = th / heads;
+    const int hd = static_cast<int>(th - tok * heads);
     const int pos = static_cast<int>(tok % S);
-    const uint16_t* xr = x + th * D;
+    const uint16_t* xr = x + tok * x_tok + static_cast<long>(hd) * D;
     float a[8], b[8], ca[8], sa[8];
     load8(xr + p0, a);
     load8(xr + half + p0, b);
@@ -335,7 +336,7 @@ mxk_rope_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
       oa[e] = a[e] * ca[e] - b[e] * s;
       ob[e] = b[e] * ca[e] + a[e] * s;
     }
-    uint16_t* yr = y + th * D;
+    uint16_t* yr = y + tok * y_tok + static_cast<long>(hd) * D;
     store8(yr + p0, oa);
     store8(yr + half + p0, ob);
   }
@@ -447,13 +448,25 @@ MXK_API int mxk_swiglu_bwd(const void* gu, const void* dh, void* dgu, long rows,
   MXK_RETURN_LAUNCH_STATUS();
 }
 
-MXK_API int mxk_rope(const void* x, void* y, const float* cos_t, const float* sin_t, long tokens,
-                     int heads, int D, int S, float sign, hipStream_t s) {
+// x / y: [tokens][heads][D] rows at token strides x_tok / y_tok (elements),
+// e.g. q or k read straight out of the fused QKV projection output, or the
+// gradient written straight into its slice of the fused dQKV buffer.
+MXK_API int mxk_rope_strided(const void* x, void* y, const float* cos_t, const float* sin_t,
+                             long tokens, int heads, int D, int S, float sign, long x_tok,
+                             long y_tok, hipStream_t s) {
   if (tokens <= 0) return 0;
-  if (D % 16 || !aligned16(x) || !aligned16(y) || !aligned16(cos_t) || !aligned16(sin_t))
+  if (D % 16 || x_tok % 8 || y_tok % 8 || x_tok < static_cast<long>(heads) * D ||
+      y_tok < static_cast<long>(heads) * D || !aligned16(x) || !aligned16(y) ||
+      !aligned16(cos_t) || !aligned16(sin_t))
     return static_cast<int>(hipErrorInvalidValue);
   hipLaunchKernelGGL(mxk_rope_kernel, dim3(grid_cap(tokens * heads * (D / 16))), dim3(256), 0, s,
                      static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), cos_t, sin_t,
-                     tokens, heads, D, S, sign);
+                     tokens, heads, D, S, sign, x_tok, y_tok);
   MXK_RETURN_LAUNCH_STATUS();
+}
+
+MXK_API int mxk_rope(const void* x, void* y, const float* cos_t, const float* sin_t, long tokens,
+                     int heads, int D, int S, float sign, hipStream_t s) {
+  const long t = static_cast<long>(heads) * D;
+  return mxk_rope_strided(x, y, cos_t, sin_t, tokens, heads, D, S, sign, t, t, s);
 }

@@ -238,3 +238,24 @@ def test_fused_cross_entropy_vs_fp32(cuda_device, T, V):
     loss.backward()
     err = (x.grad.float() - ref_in.grad).abs().max().item()
     assert err <= 2 ** -8 * ref_in.grad.abs().max().item() + 1e-6, err
+
+
+def test_qkv_rope_matches_split_rope(cuda_device):
+    """Fused QKV split + RoPE (strided rope in/out, one d(qkv) buffer) equals
+    split -> contiguous rope -> autograd concat, forward and backward."""
+    from mxk8s.ops.fused import qkv_rope
+    B, S, hq, hkv, hd = 2, 256, 8, 2, 128
+    cos, sin = rope_tables(S, hd, device=cuda_device)
+    qkv = _rand((B, S, (hq + 2 * hkv) * hd), cuda_device, 31, 2.0).bfloat16().requires_grad_()
+    q, k, v = qkv_rope(qkv, cos, sin, hq, hkv, hd)
+    ref_in = qkv.detach().clone().requires_grad_()
+    rq, rk, rv = ref_in.split([hq * hd, hkv * hd, hkv * hd], dim=-1)
+    rq = rope(rq.reshape(B, S, hq, hd).contiguous(), cos, sin)
+    rk = rope(rk.reshape(B, S, hkv, hd).contiguous(), cos, sin)
+    rv = rv.reshape(B, S, hkv, hd)
+    for got, want in ((q, rq), (k, rk), (v, rv)):
+        assert torch.equal(got, want)
+    gq, gk, gv = (_rand(t.shape, cuda_device, 40 + i).bfloat16() for i, t in enumerate((q, k, v)))
+    torch.autograd.backward((q, k, v), (gq, gk, gv))
+    torch.autograd.backward((rq, rk, rv), (gq, gk, gv))
+    assert torch.equal(qkv.grad, ref_in.grad)
