@@ -49,8 +49,9 @@ __device__ __forceinline__ bf16x8_t lds_b128(const char* p) {
 
 __device__ __forceinline__ bf16x4_t lds_tr_b64(const char* p) {
   typedef short s4 __attribute__((ext_vector_type(4)));
-  s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s4*)(reinterpret_cast<uintptr_t>(p)));
+  // plain address-space cast (not via an integer): `base + constant` stays
+  // visible and the constant folds into the instruction's offset field
+  s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)p);
   return v;
 }
 

@@ -45,8 +45,9 @@ using mxk::dma16;
 
 __device__ __forceinline__ bf16x4_t tr_b64(const char* p) {
   typedef short s4 __attribute__((ext_vector_type(4)));
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s4*)(reinterpret_cast<uintptr_t>(p)));
+  // a plain address-space cast (not via an integer) keeps `base + constant`
+  // visible, so the constant lands in the instruction's offset field
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)p);
 }
 
 template <bool NMAJOR>
@@ -104,7 +105,7 @@ struct XOp<true> {
   uint32_t voff[8];
   const char* base;
   unsigned bytes;
-  int base_off, qx;
+  int roff[4];                   // read offset of subtile r (mod 4), XOR folded in
   __device__ __forceinline__ void init(const uint16_t* src, int ld, int col0, int K, int lane,
                                        int wave) {
     rsrc = make_rsrc(src + col0, static_cast<unsigned>(K) * ld * 2u);
@@ -120,8 +121,11 @@ struct XOp<true> {
     for (int p = 0; p < 8; ++p) voff[p] = lane_off + (p * 4 + wave) * piece_stride;
     // transposed-read lane constants: group G, row q, column pair b, half-chunk
     const int G = lane >> 4, i16 = lane & 15, q = i16 >> 2;
-    base_off = G * TGROUP + q * 512 + ((i16 & 3) >> 1) * 16 + 8 * (i16 & 1);
-    qx = 32 * q;
+    // subtile i sits at column byte (32 i) ^ 32q = 32 (i & ~3) + ((32 (i & 3)) ^ 32q):
+    // one VGPR per (i & 3), everything else an immediate offset of the read
+    const int base_off = G * TGROUP + q * 512 + ((i16 & 3) >> 1) * 16 + 8 * (i16 & 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) roff[r] = base_off + ((32 * r) ^ (32 * q));
   }
   __device__ __forceinline__ void issue(char* lds, int p, int kstage, int wave) const {
     const uint32_t k_off = kstage * kstride;
@@ -132,7 +136,7 @@ struct XOp<true> {
     dma16(rsrc, lds + p * TGROUP + wave * 1024, voff[p], soff);
   }
   __device__ __forceinline__ bf16x8_t frag(const char* lds, int i, int ks) const {
-    const char* p = lds + base_off + ks * KSTEP_T + ((32 * i) ^ qx);
+    const char* p = lds + roff[i & 3] + 32 * (i & ~3) + ks * KSTEP_T;
     const bf16x4_t lo = tr_b64(p);
     const bf16x4_t hi = tr_b64(p + 2048);
     bf16x8_t a;
