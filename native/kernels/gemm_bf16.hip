@@ -42,6 +42,9 @@
 //   6 w4j   default: w4i with every read/DMA/wait at hipBLASLt's MFMA
 //           positions (+0.5-2 % over 0 on squares and the Llama-3-8B shapes)
 //   7 w4j   two barriers per K-tile (SchedTwoBarrier)
+//   8 w4j   variant 6 with plain (temporal) widened stores
+//   9 x2    the layout kernel of gemm_bf16_layouts.hip (same schedule as 6,
+//           inline-asm LDS-DMA with the LDS address bound to M0)
 // The earlier schedules (one-barrier w4b, 8-wave, 4-deep ring, w4h, ...)
 // were retired when an ISA audit (tests/test_isa_hazards.py) found their
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
@@ -537,12 +540,17 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 // ---------------------------------------------------------------------------
 // Host launchers (C ABI, stream-ordered, capture-safe: no sync, no malloc).
 // ---------------------------------------------------------------------------
+MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int M, int N, int K,
+                                     int lda, int ldb, int ldc, int a_kmajor, int b_kmajor,
+                                     int variant, hipStream_t stream);
+
 namespace {
-constexpr int kNumVariants = 8;
+constexpr int kNumVariants = 10;
 constexpr int kDefaultVariant = 6;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
-    "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar"};
+    "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar",
+    "w4j_hb_st", "x2_hb"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -583,6 +591,11 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     }
     case 6: launch_w4i<1, 2, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 7: launch_w4i<1, 2, 1, 0, 2>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 8: launch_w4i<1, 1, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 9:
+      // the layout kernel (gemm_bf16_layouts.hip) on K-major operands
+      mxk_gemm_bf16_ex_variant(A, Bt, C, M, N, K, lda, ldb, ldc, 1, 1, 2, stream);
+      break;
   }
 }
 

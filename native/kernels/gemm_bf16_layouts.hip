@@ -87,8 +87,16 @@ struct XOp<false> {
   }
   // x2 kernel: fixed panel descriptor, the k offset of the stage as soffset
   __device__ __forceinline__ uint32_t kstep() const { return XBK * 2; }
+  // x2 kernel: LDS destinations as smem32 + (lds - smem), scalar arithmetic
+  const char* sm = nullptr;
+  uint32_t sm32 = 0;
+  __device__ __forceinline__ void set_lds(const char* smem, uint32_t smem32) {
+    sm = smem;
+    sm32 = smem32;
+  }
   __device__ __forceinline__ void issue_s(char* lds, int p, uint32_t soff, int wave) const {
-    dma16(rsrc, lds + (p * 4 + wave) * 1024, voff[p], soff);
+    mxk::dma16m(rsrc, sm32 + static_cast<uint32_t>(lds - sm) + (p * 4 + wave) * 1024, voff[p],
+                soff);
   }
   // fragment of 16-row subtile i (i = 0..15 over the 256 rows), k-step ks
   __device__ __forceinline__ bf16x8_t frag(const char* lds, int i, int ks) const {
@@ -132,8 +140,15 @@ struct XOp<true> {
     dma16(make_rsrc(base + k_off, bytes - k_off), lds + p * TGROUP + wave * 1024, voff[p], 0);
   }
   __device__ __forceinline__ uint32_t kstep() const { return kstride; }
+  const char* sm = nullptr;
+  uint32_t sm32 = 0;
+  __device__ __forceinline__ void set_lds(const char* smem, uint32_t smem32) {
+    sm = smem;
+    sm32 = smem32;
+  }
   __device__ __forceinline__ void issue_s(char* lds, int p, uint32_t soff, int wave) const {
-    dma16(rsrc, lds + p * TGROUP + wave * 1024, voff[p], soff);
+    mxk::dma16m(rsrc, sm32 + static_cast<uint32_t>(lds - sm) + p * TGROUP + wave * 1024, voff[p],
+                soff);
   }
   __device__ __forceinline__ bf16x8_t frag(const char* lds, int i, int ks) const {
     const char* p = lds + roff[i & 3] + 32 * (i & ~3) + ks * KSTEP_T;
@@ -415,6 +430,8 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
   XOp<BN> ob;
   oa.init(A, lda, m0, K, lane, wave);
   ob.init(B, ldb, n0, K, lane, wave);
+  oa.set_lds(smem, mxk::lds_addr32(smem));
+  ob.set_lds(smem, mxk::lds_addr32(smem));
 
   f32x4_t acc[8][8];
 #pragma unroll

@@ -104,6 +104,28 @@ __device__ __forceinline__ void dma16(const u32x4& rsrc, const char* lds, uint32
       : "memory");
 }
 
+// dma16 with the LDS destination given as a 32-bit LDS address that the
+// caller keeps scalar, bound straight to M0 ("{m0}"): the compiler writes M0
+// with the address arithmetic itself (one s_add into m0), with no
+// v_readfirstlane and no save/restore of M0 around every piece.  The LDS
+// write stays invisible to the compiler (inline asm), so it inserts no
+// conservative vmcnt(0) before transposed LDS reads, which the builtin
+// __builtin_amdgcn_raw_ptr_buffer_load_lds does.
+__device__ __forceinline__ void dma16m(const u32x4& rsrc, uint32_t lds_addr, uint32_t voff,
+                                       uint32_t soff) {
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+               :
+               : "v"(voff), "s"(rsrc), "s"(soff), "{m0}"(lds_addr)
+               : "memory");
+}
+
+// 32-bit LDS address of a __shared__ array (a constant after folding)
+template <class T>
+__device__ __forceinline__ uint32_t lds_addr32(T* shared_array) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) char*)shared_array));
+}
+
 // Block -> 256x256 output tile of the MFMA GEMMs (gemm_bf16*.hip).
 //  MAP 0: XCD remap + GROUP_M column sweep (each XCD owns GROUP_M tile rows
 //         and walks the columns; chip-wide every A panel is live at once).
