@@ -38,8 +38,11 @@ def _tail_heavy(M: int, N: int, cus: int = 256) -> bool:
 
 
 def _wgrad_into(sink: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
+    # no tail-heavy exception here: even the 384-tile wqkv wgrad (6144 x 4096,
+    # 1.5 rounds on 256 CUs) runs 1215 TF/s on the layout kernel against
+    # hipBLASLt's 1150 (profiles/r1_gemm_m0/llama_*.log)
     if _USE_MXK_WGRAD and sink.is_cuda and dy2.is_contiguous() and x2.is_contiguous() and \
-            not _tail_heavy(*sink.shape) and gemm_bf16_ex(dy2, x2, False, False, sink):
+            gemm_bf16_ex(dy2, x2, False, False, sink):
         return
     torch.matmul(dy2.t(), x2, out=sink)
 

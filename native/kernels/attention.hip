@@ -348,11 +348,14 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
   }
   const uint32_t k_step = static_cast<uint32_t>(BKV * k_tok * 2);
   const uint32_t v_step = static_cast<uint32_t>(BKV * v_tok * 2);
+  // LDS destinations as scalar 32-bit addresses bound to M0 (mxk::dma16m)
+  const uint32_t sm32 = mxk::lds_addr32(&smem[0][0]);
   auto issue = [&](int j, int buf) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      mxk::dma16(rk, smem[buf] + (4 * wave + p) * 1024, kvo[p], j * k_step);
-      mxk::dma16(rv, smem[buf] + TILE_BYTES + (4 * wave + p) * 1024, vvo[p], j * v_step);
+      const uint32_t d = sm32 + buf * (2 * TILE_BYTES) + (4 * wave + p) * 1024;
+      mxk::dma16m(rk, d, kvo[p], j * k_step);
+      mxk::dma16m(rv, d + TILE_BYTES, vvo[p], j * v_step);
     }
   };
   issue(0, 0);
