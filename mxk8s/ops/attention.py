@@ -71,7 +71,7 @@ def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None, variant: 
     return o, lse
 
 
-_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "1"))
+_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "2"))
 
 
 def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = None,
@@ -80,8 +80,11 @@ def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = N
 
     ``dk``/``dv`` may be preallocated views (e.g. slices of a fused dQKV
     buffer) with a token stride; by default they are fresh contiguous tensors.
-    ``variant`` 1 (default): dK/dV accumulated over the query-head group in
-    one workgroup, bf16 out; 0: per-query-head fp32 partials + GQA reduce."""
+    ``variant`` 2 (default): dK/dV accumulated over the query-head group in
+    one workgroup, bf16 out, K/V and Q/dO tiles by LDS-DMA (1.21 vs 1.31-1.36
+    ms per Llama-3-8B layer at B 8, bit-identical: profiles/r1_attention/);
+    1: the same with register-staged tiles; 0: per-query-head fp32 partials
+    + GQA reduce."""
     B, S, Hq, D = q.shape
     Hkv = k.shape[2]
     variant = _BWD_VARIANT if variant is None else variant

@@ -47,6 +47,13 @@ __device__ __forceinline__ bf16x8_t lds_b128(const char* p) {
   return *reinterpret_cast<const bf16x8_t*>(p);
 }
 
+// s_waitcnt vmcnt(0) through the builtin rather than inline asm: the
+// compiler's wait-insertion pass then knows every earlier load has landed and
+// adds no waits of its own further on (with inline asm it re-waits, e.g. on a
+// register a finished load wrote - and such a wait also waits for the DMA of
+// the next tile, which the compiler cannot see).
+__device__ __forceinline__ void vm_wait0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 __device__ __forceinline__ bf16x4_t lds_tr_b64(const char* p) {
   typedef short s4 __attribute__((ext_vector_type(4)));
   // plain address-space cast (not via an integer): `base + constant` stays
@@ -391,7 +398,7 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
   // would also wait for the next tile's (untracked) DMA.
 #pragma unroll
   for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile 0
+  vm_wait0();   // tile 0
   __syncthreads();
 
   // the loop body; UNROLL makes the LDS buffer a compile-time constant (read
@@ -473,7 +480,7 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
     }
     // tile j+1 (own pieces) landed; the barrier publishes every wave's pieces
     // and certifies that buffer buf is no longer read
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait0();
     __syncthreads();
   };
   if constexpr (UNROLL) {
@@ -607,7 +614,11 @@ mxk_attn_bwd_delta_kernel(const uint16_t* __restrict__ o, const uint16_t* __rest
   }
 }
 
-template <bool CAUSAL>
+// DMA: K/V tiles by LDS-DMA straight into the swizzled image (the forward
+// kernel's piece mapping, destinations bound to M0) instead of register
+// staging - frees the 32 staging VGPRs that made this kernel spill at two
+// waves per SIMD, and the ds_writes.  Requires S * token_stride * 2 < 2^32.
+template <bool CAUSAL, bool DMA = false>
 __global__ void __launch_bounds__(NT, 2)
 mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                        const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
@@ -666,8 +677,46 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
       *reinterpret_cast<bf16x8_t*>(smem[buf] + TILE_BYTES + off) = vst[i];
     }
   };
-  load_tile(0);
-  store_tile(0);
+  // DMA pieces: wave w moves 1-KiB pieces g = 4w + p (rows 4g .. 4g+3) of K
+  // and V, lane i at row 4g + (i >> 4), chunk (i & 15) ^ ((i >> 4) << 2 | p)
+  mxk::u32x4 rk{}, rv{};
+  uint32_t kvo[4] = {}, vvo[4] = {};
+  const uint32_t sm32 = mxk::lds_addr32(&smem[0][0]);
+  const uint32_t k_step = static_cast<uint32_t>(BKV * k_tok * 2);
+  const uint32_t v_step = static_cast<uint32_t>(BKV * v_tok * 2);
+  if constexpr (DMA) {
+    rk = mxk::make_rsrc(kb_ptr, static_cast<unsigned>(S * k_tok * 2));
+    rv = mxk::make_rsrc(vb_ptr, static_cast<unsigned>(S * v_tok * 2));
+    const int prow = lane >> 4, pslot = lane & 15;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int r = 4 * (4 * wave + p) + prow;
+      const int ch = pslot ^ ((prow << 2) | p);
+      kvo[p] = static_cast<uint32_t>(r * k_tok * 2 + ch * 16);
+      vvo[p] = static_cast<uint32_t>(r * v_tok * 2 + ch * 16);
+    }
+  }
+  auto issue = [&](int j, int buf) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const uint32_t d = sm32 + buf * (2 * TILE_BYTES) + (4 * wave + p) * 1024;
+      mxk::dma16m(rk, d, kvo[p], j * k_step);
+      mxk::dma16m(rv, d + TILE_BYTES, vvo[p], j * v_step);
+    }
+  };
+  if constexpr (DMA) {
+    issue(0, 0);
+    // consume the per-query loads here, so the compiler's vmcnt waits for
+    // them sit before the loop and not inside it (where they would also wait
+    // for the next tile's untracked DMA)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]), "v"(dof[s]));
+    asm volatile("" ::"v"(lse2), "v"(dlt));
+    vm_wait0();
+  } else {
+    load_tile(0);
+    store_tile(0);
+  }
   __syncthreads();
 
   f32x16_t acc[4];
@@ -680,7 +729,11 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
 
   for (int j = 0; j < nkv; ++j) {
     const int buf = j & 1;
-    if (j + 1 < nkv) load_tile(j + 1);
+    // DMA: buffer buf^1 was last read in iteration j-1 (barrier-certified)
+    if (j + 1 < nkv) {
+      if constexpr (DMA) issue(j + 1, buf ^ 1);
+      else load_tile(j + 1);
+    }
     const int kv0 = j * BKV;
     if (!CAUSAL || kv0 <= qw0 + 31) {
       const char* kt = smem[buf];
@@ -723,7 +776,11 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
         }
       }
     }
-    if (j + 1 < nkv) store_tile(buf ^ 1);
+    if constexpr (DMA) {
+      vm_wait0();   // own pieces of tile j+1
+    } else {
+      if (j + 1 < nkv) store_tile(buf ^ 1);
+    }
     __syncthreads();
   }
   uint16_t* row = dq + (static_cast<long>(b) * S + myq) * Hq * D + static_cast<long>(hq) * D;
@@ -948,7 +1005,9 @@ constexpr int NT16 = 512;
 // strides dk_tok / dv_tok).  Without it, one workgroup per query head writes
 // fp32 partials that mxk_attn_bwd_gqa_reduce_kernel sums (4x the grid,
 // ~1.1 GB more HBM traffic per Llama-3-8B layer at B = 8).
-template <bool CAUSAL, bool GQA = false>
+// DMA: Q / dO slices by LDS-DMA (wave w moves the 1-KiB pieces 2w, 2w + 1 of
+// each), as in the dQ kernel; the lse / delta rows stay register-staged.
+template <bool CAUSAL, bool GQA = false, bool DMA = false>
 __global__ void __launch_bounds__(NT16, 1)
 mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                            const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
@@ -988,6 +1047,13 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
   for (int s = 0; s < 4; ++s) {
     kf[s] = *reinterpret_cast<const bf16x8_t*>(kb_ptr + static_cast<long>(mykey) * k_tok + 32 * s + 8 * G);
     vf[s] = *reinterpret_cast<const bf16x8_t*>(vb_ptr + static_cast<long>(mykey) * v_tok + 32 * s + 8 * G);
+  }
+  if constexpr (DMA) {
+    // wait for the K / V fragments here, before the loops: a compiler wait
+    // at their first use inside the slice loop would also wait for the
+    // untracked DMA of the next slice
+#pragma unroll
+    for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(kf[s]), "v"(vf[s]));
   }
   const float c = scale * 1.4426950408889634f;
   const float inv_c = 1.f / c;
@@ -1035,14 +1101,65 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
     }
     if (tid < 2 * BQB) srow[buf][tid / BQB][tid & (BQB - 1)] = rst;
   };
-  load_slice(0);
-  store_slice(0);
+  // raw load at the top, arithmetic at the store: math right after the load
+  // would put a vmcnt(0) there, which also waits for the slice DMA just issued
+  auto load_row = [&](int t) {
+    if (tid < 2 * BQB) {
+      const long qi = q_begin + static_cast<long>(t) * BQB + (tid & (BQB - 1));
+      rst = (tid < BQB ? lse_b : dl_b)[qi];
+    }
+  };
+  auto store_row = [&](int buf) {
+    if (tid < 2 * BQB)
+      srow[buf][tid / BQB][tid & (BQB - 1)] = tid < BQB ? -rst * 1.4426950408889634f * inv_c : -rst;
+  };
+  mxk::u32x4 rq{}, rd{};
+  uint32_t qvo[2] = {}, dvo[2] = {};
+  const uint32_t sm32 = mxk::lds_addr32(&smem[0][0]);
+  if constexpr (DMA) {
+    rq = mxk::make_rsrc(qb_ptr, static_cast<unsigned>(S * q_tok * 2));
+    rd = mxk::make_rsrc(dob_ptr, static_cast<unsigned>(static_cast<long>(S) * Hq * D * 2));
+    // lane i lands at row 4g + (i >> 4), slot i & 15 = chunk ^ 2 (row & 7)
+    const int prow = lane >> 4, pslot = lane & 15;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int r = 4 * (2 * wave + p) + prow;
+      const int ch = pslot ^ (2 * (r & 7));
+      qvo[p] = static_cast<uint32_t>(r * q_tok * 2 + ch * 16);
+      dvo[p] = static_cast<uint32_t>(r * Hq * D * 2 + ch * 16);
+    }
+  }
+  auto issue = [&](int t, int buf) {
+    const long row0 = q_begin + static_cast<long>(t) * BQB;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const uint32_t d = sm32 + buf * (2 * BQB * 256) + (2 * wave + p) * 1024;
+      mxk::dma16m(rq, d, qvo[p], static_cast<uint32_t>(row0 * q_tok * 2));
+      mxk::dma16m(rd, d + BQB * 256, dvo[p], static_cast<uint32_t>(row0 * Hq * D * 2));
+    }
+  };
+  if constexpr (DMA) {
+    issue(0, 0);
+    load_row(0);
+    vm_wait0();
+    store_row(0);
+  } else {
+    load_slice(0);
+    store_slice(0);
+  }
   __syncthreads();
 
 
   for (int t = 0; t < nsl; ++t) {
     const int buf = t & 1;
-    if (t + 1 < nsl) load_slice(t + 1);
+    if (t + 1 < nsl) {
+      if constexpr (DMA) {
+        issue(t + 1, buf ^ 1);   // buf ^ 1 last read in slice t - 1 (barrier-certified)
+        load_row(t + 1);
+      } else {
+        load_slice(t + 1);
+      }
+    }
     const int qs0 = q_begin + t * BQB;
     if (!CAUSAL || qs0 + BQB - 1 >= kw0) {
       const char* qt = smem[buf];
@@ -1093,7 +1210,12 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
         }
       }
     }
-    if (t + 1 < nsl) store_slice(buf ^ 1);
+    if constexpr (DMA) {
+      vm_wait0();   // own pieces of slice t+1
+      if (t + 1 < nsl) store_row(buf ^ 1);
+    } else {
+      if (t + 1 < nsl) store_slice(buf ^ 1);
+    }
     __syncthreads();
   }
   }   // query heads of the group
@@ -1165,15 +1287,17 @@ MXK_API long mxk_attn_bwd_workspace(int B, int S, int Hq) {
   return mxk_attn_bwd_workspace_variant(B, S, Hq, 0);
 }
 
-// variant 1 (default): dK/dV per (batch, KV head, key block) over the whole
-// query-head group, bf16 out; 0: per query head + fp32 partials + GQA reduce.
+// variant 1: dK/dV per (batch, KV head, key block) over the whole query-head
+// group, bf16 out; 2: variant 1 with LDS-DMA tile loads in the dQ and dK/dV
+// kernels (register-staged when a panel exceeds the 32-bit buffer range);
+// 0: per query head + fp32 partials + GQA reduce.
 MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, const void* o,
                                  const void* dout, const float* lse, void* dq, void* dk, void* dv,
                                  void* workspace, int B, int S, int Hq, int Hkv, int head_dim,
                                  long q_tok, long k_tok, long v_tok, long dk_tok, long dv_tok,
                                  float scale, int causal, int variant, hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv || q_tok % 8 ||
-      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 1 ||
+      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 2 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
        reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
@@ -1194,7 +1318,16 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
                      stream, static_cast<const uint16_t*>(o), dO, delta, S, Hq, rows);
   const int nwg = B * Hq * (S / BQ);
   const int nwg_kv = B * Hkv * (S / BQ);
-  if (variant == 1) {
+  const long qspan = static_cast<long>(S) * (q_tok > static_cast<long>(Hq) * D ? q_tok : Hq * D) * 2;
+  if (variant == 2 && causal && qspan < (1L << 32)) {
+    hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<true, true, true>), dim3(nwg_kv), dim3(NT16), 0,
+                       stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok,
+                       v_tok, scale, dK, dV, dk_tok, dv_tok);
+  } else if (variant == 2 && qspan < (1L << 32)) {
+    hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<false, true, true>), dim3(nwg_kv), dim3(NT16),
+                       0, stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok,
+                       v_tok, scale, dK, dV, dk_tok, dv_tok);
+  } else if (variant >= 1) {
     if (causal)
       hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<true, true>), dim3(nwg_kv), dim3(NT16), 0,
                          stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok,
@@ -1212,14 +1345,21 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
                        stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok,
                        v_tok, scale, nullptr, nullptr, 0L, 0L);
   }
-  if (causal)
-    hipLaunchKernelGGL(mxk_attn_bwd_dq_kernel<true>, dim3(nwg), dim3(NT), 0, stream, Q, K, V, dO,
-                       lse, delta, static_cast<uint16_t*>(dq), S, Hq, Hkv, q_tok, k_tok, v_tok,
-                       scale);
+  const long span = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
+  const bool dq_dma = variant == 2 && span < (1L << 32);
+  auto* dQ = static_cast<uint16_t*>(dq);
+  if (causal && dq_dma)
+    hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<true, true>), dim3(nwg), dim3(NT), 0, stream, Q, K,
+                       V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  else if (causal)
+    hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<true, false>), dim3(nwg), dim3(NT), 0, stream, Q, K,
+                       V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  else if (dq_dma)
+    hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<false, true>), dim3(nwg), dim3(NT), 0, stream, Q, K,
+                       V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
   else
-    hipLaunchKernelGGL(mxk_attn_bwd_dq_kernel<false>, dim3(nwg), dim3(NT), 0, stream, Q, K, V, dO,
-                       lse, delta, static_cast<uint16_t*>(dq), S, Hq, Hkv, q_tok, k_tok, v_tok,
-                       scale);
+    hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<false, false>), dim3(nwg), dim3(NT), 0, stream, Q,
+                       K, V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
   if (variant == 0) {
     const long n_out = static_cast<long>(B) * S * Hkv * D;
     hipLaunchKernelGGL(mxk_attn_bwd_gqa_reduce_kernel, dim3((n_out / 4 + 255) / 256), dim3(256), 0,

@@ -21,13 +21,18 @@ def main():
     o, lse = A.attn_fwd(q, k, v, causal=True)
     dout = torch.randn(B, S, Hq, D, device=dev, generator=g).bfloat16()
     fl = 2.5 * 4 * B * Hq * S * S * D / 2    # causal fwd FLOPs x 2.5
-    ts = {0: [], 1: []}
+    variants = [int(x) for x in os.environ.get("VARIANTS", "0,1").split(",")]
+    ts = {vv: [] for vv in variants}
+    outs = {vv: A.attn_bwd(q, k, v, o, lse, dout, variant=vv) for vv in variants}
+    for vv in variants[1:]:
+        same = all(torch.equal(x, y) for x, y in zip(outs[variants[0]], outs[vv]))
+        print(f"RESULT variant={vv} bit-identical to variant={variants[0]}: {same}", flush=True)
     for _ in range(3):
-        for vv in (0, 1):
+        for vv in variants:
             A.attn_bwd(q, k, v, o, lse, dout, variant=vv)
     torch.cuda.synchronize()
     for _ in range(10):
-        for vv in (0, 1):
+        for vv in variants:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(5):

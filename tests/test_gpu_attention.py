@@ -68,7 +68,7 @@ def test_attn_bwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
         assert err < tol, (name, err, tol)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
     (1, 256, 8, 2, True),
     (2, 384, 4, 1, True),
