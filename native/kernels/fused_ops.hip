@@ -184,11 +184,17 @@ mxk_rmsnorm_bwd_wave_kernel(const uint16_t* __restrict__ dy, const uint16_t* __r
   for (int r = gw; r < rows; r += nw) {
     const size_t off = static_cast<size_t>(r) * H + 8 * lane;
     const float rs = rstd[r];
-    bf16x8_t gy[NC], gx[NC];
+    bf16x8_t gy[NC], gx[NC], gr[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       gy[c] = *reinterpret_cast<const bf16x8_t*>(dy + off + 512 * c);
       gx[c] = *reinterpret_cast<const bf16x8_t*>(x + off + 512 * c);
+    }
+    // the residual gradient is loaded with dy / x, not after the row's
+    // reduction, where its latency would sit on the critical path
+    if (dres) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) gr[c] = *reinterpret_cast<const bf16x8_t*>(dres + off + 512 * c);
     }
     float dot = 0.f;
 #pragma unroll
@@ -209,10 +215,8 @@ mxk_rmsnorm_bwd_wave_kernel(const uint16_t* __restrict__ dy, const uint16_t* __r
         dwacc[c][e] += a * b * rs;
       }
       if (dres) {
-        float rr[8];
-        load8(dres + off + 512 * c, rr);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] += rr[e];
+        for (int e = 0; e < 8; ++e) o[e] += mxk::bf2f(static_cast<uint16_t>(gr[c][e]));
       }
       store8(dx + off + 512 * c, o);
     }
@@ -383,7 +387,8 @@ MXK_API int mxk_add_rmsnorm_fwd(const void* x, const void* delta, const void* w,
 
 // Workspace size (bytes) the backward needs for its dw slab.
 namespace {
-// one block per CU keeps the dw slab small (256 x H fp32) while every CU works
+// one block per CU keeps the dw slab small (256 x H fp32) while every CU
+// works (512 blocks: +15 % time without the residual gradient, -3 % with it)
 constexpr int kBwdBlocks = 256;
 }
 
