@@ -88,3 +88,55 @@ def test_allreduce_binary_single_gpu():
     pts = [r for r in _results(out) if r["test"] == "allreduce"]
     assert len(pts) >= 3, out[-2000:]
     assert all(r["pass"] and r["ngpus"] == 1 and r["algbw_GBps"] > 0 for r in pts), pts
+
+
+def test_device_plugin_on_live_box_registers_and_allocates():
+    """The real plugin (live sysfs, live amd-smi events) against the fake
+    kubelet: amd.com/gpu registers, every visible GPU is healthy, and
+    Allocate hands out the CDI name plus /dev/kfd and the render node."""
+    import tempfile
+
+    from mxk8s.deviceplugin import api
+    from mxk8s.deviceplugin.fake_kubelet import FakeKubelet
+    from mxk8s.deviceplugin.plugin import AmdGpuDevicePlugin, PluginConfig
+
+    d = tempfile.mkdtemp(prefix="mxdp", dir="/tmp")
+    kube = FakeKubelet(d).start()
+    plugin = AmdGpuDevicePlugin(PluginConfig(plugin_dir=d, health_interval=0.2,
+                                             watch_interval=0.2)).start()
+    try:
+        reg = kube.wait_registration()
+        assert reg.resource_name == "amd.com/gpu"
+        stub = kube.plugin_stub(reg.endpoint)
+        first = next(iter(stub.ListAndWatch(api.Empty(), timeout=10)))
+        n = len(node.enumerate_gpus(""))
+        assert len(first.devices) == n >= 1
+        assert all(dv.health == api.HEALTHY for dv in first.devices)
+        req = api.AllocateRequest()
+        req.container_requests.add(devices_ids=["0"])
+        c = stub.Allocate(req, timeout=10).container_responses[0]
+        assert [x.name for x in c.cdi_devices] == ["amd.com/gpu=0"]
+        paths = [x.host_path for x in c.devices]
+        assert "/dev/kfd" in paths and any(p.startswith("/dev/dri/renderD") for p in paths)
+    finally:
+        plugin.stop()
+        kube.stop()
+
+
+def test_exporter_on_live_box_serves_amd_smi_metrics():
+    import urllib.request
+
+    from mxk8s.exporter import Exporter, ExporterConfig, SmiBackend
+
+    ex = Exporter(ExporterConfig(port=0, interval=0.2), backend=SmiBackend("")).start()
+    try:
+        body = urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/metrics", timeout=10).read().decode()
+    finally:
+        ex.stop()
+    assert 'amd_gpu_stack_component_up{component="amd_smi"} 1' in body
+    total = [float(line.rsplit(" ", 1)[1]) for line in body.splitlines()
+             if line.startswith("amd_gpu_memory_total_bytes{")]
+    assert total and all(250 * 2 ** 30 <= t <= 300 * 2 ** 30 for t in total), total
+    assert any(line.startswith("amd_gpu_power_watts{") for line in body.splitlines())
+    assert any(line.startswith("amd_gpu_device_healthy{") and line.endswith(" 1")
+               for line in body.splitlines())
