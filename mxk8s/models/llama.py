@@ -25,9 +25,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.attention import flash_attention, supported as flash_supported
-from ..ops.linear import Linear
+from ..ops.linear import Linear, SwiGLULinear
 from ..ops.xent import cross_entropy
-from ..ops.fused import add_rmsnorm, qkv_rope, rmsnorm, rope_tables, swiglu
+from ..ops.fused import add_rmsnorm, qkv_rope, rmsnorm, rope_tables
 
 
 @dataclasses.dataclass
@@ -108,10 +108,12 @@ class MLP(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.w13 = Linear(cfg.dim, 2 * cfg.ffn_dim)   # [gate | up]
-        self.w2 = Linear(cfg.ffn_dim, cfg.dim)
+        # w2(swiglu(.)) as one node: the SwiGLU backward runs in the epilogue
+        # of w2's input-gradient GEMM
+        self.w2 = SwiGLULinear(cfg.ffn_dim, cfg.dim)
 
     def forward(self, x):
-        return self.w2(swiglu(self.w13(x)))
+        return self.w2(self.w13(x))
 
 
 class Block(nn.Module):

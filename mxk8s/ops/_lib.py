@@ -34,6 +34,7 @@ _SIGNATURES = {
     "mxk_gemm_bf16_tn_is_fast": (_i, [_i, _i, _i]),
     "mxk_gemm_bf16_ex": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_ex_variant": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "mxk_gemm_bf16_dgrad_swiglu": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_tn_variant": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_tn_num_variants": (_i, []),
     "mxk_gemm_bf16_tn_is_ablation": (_i, [_i]),

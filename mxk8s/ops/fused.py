@@ -176,6 +176,28 @@ class _SwiGLU(torch.autograd.Function):
         return dgu.view(ctx.shape)
 
 
+def swiglu_fwd(gu: torch.Tensor) -> torch.Tensor:
+    """silu(g) * u of gu = [g | u] (bf16, GPU), no autograd node."""
+    F = gu.shape[-1] // 2
+    g2 = gu.contiguous().view(-1, 2 * F)
+    h = torch.empty((g2.shape[0], F), dtype=gu.dtype, device=gu.device)
+    _lib.check(_lib.lib().mxk_swiglu_fwd(g2.data_ptr(), h.data_ptr(), g2.shape[0], F,
+                                         _lib.stream_ptr(gu.device)), "mxk_swiglu_fwd")
+    return h.view(*gu.shape[:-1], F)
+
+
+def swiglu_bwd(gu: torch.Tensor, dh: torch.Tensor) -> torch.Tensor:
+    """d[g | u] from gu = [g | u] and dh = d(silu(g) * u) (bf16, GPU)."""
+    F = gu.shape[-1] // 2
+    g2 = gu.contiguous().view(-1, 2 * F)
+    dh2 = dh.contiguous().view(-1, F)
+    dgu = torch.empty_like(g2)
+    _lib.check(_lib.lib().mxk_swiglu_bwd(g2.data_ptr(), dh2.data_ptr(), dgu.data_ptr(),
+                                         g2.shape[0], F, _lib.stream_ptr(gu.device)),
+               "mxk_swiglu_bwd")
+    return dgu.view(gu.shape)
+
+
 def swiglu(gu: torch.Tensor) -> torch.Tensor:
     if gu.device.type == "cpu" or gu.dtype != torch.bfloat16:
         g, u = gu.chunk(2, dim=-1)

@@ -411,10 +411,14 @@ __device__ __forceinline__ void x2_ktile_s(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)
     x2_ktile<AN, BN, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, soa, sob, wave, par);
 }
 
+// EPI 0: 8-B stores, 1: widened 16-B stores, 2: SwiGLU backward
+// (mxk::swiglu_bwd_block: C = d[g | u], aux = [g | u], both row stride ldc,
+// u at column offset N).
 template <bool AN, bool BN, int EPI, int SCHED = 0>
 __global__ void __launch_bounds__(XT, 1)
 mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
-                        uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+                        uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc,
+                        const uint16_t* __restrict__ aux = nullptr) {
   constexpr int A_BYTES = XOp<AN>::BYTES;
   constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
@@ -483,7 +487,9 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   mxk::mfma_drain(acc);
 
-  if constexpr (EPI == 1)
+  if constexpr (EPI == 2)
+    mxk::swiglu_bwd_block(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane);
+  else if constexpr (EPI == 1)
     mxk::store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else
     mxk::store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
@@ -553,6 +559,29 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
     launch_x<true, false>(sched, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
   else
     launch_x<true, true>(sched, wide, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// Down-projection input gradient with the SwiGLU backward fused into the
+// epilogue: d(act) = dy W2 (dy [M][K] K-major, W2 [K][F] F-major) never
+// reaches memory; dgu [M][2F] = d[g | u] is written from gu [M][2F].
+// Tiles exactly (M % 256, F % 256, K % 64); hipErrorInvalidValue otherwise.
+MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const void* gu, void* dgu,
+                                       int M, int F, int K, int ld_dy, int ld_w2,
+                                       hipStream_t stream) {
+  const bool ok = M > 0 && F > 0 && K > 0 && M % XBM == 0 && F % XBM == 0 && K % XBK == 0 &&
+                  ld_dy % 8 == 0 && ld_w2 % 8 == 0 && ld_dy >= K && ld_w2 >= F &&
+                  static_cast<long>(K) * ld_w2 * 2 < (1L << 32) &&
+                  reinterpret_cast<uintptr_t>(dy) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(w2) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(gu) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(dgu) % 8 == 0;
+  if (!ok) return static_cast<int>(hipErrorInvalidValue);
+  const int nwg = (M / XBM) * (F / XBM);
+  hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<false, true, 2, 0>), dim3(nwg), dim3(XT), 0, stream,
+                     static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
+                     static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
+                     static_cast<const uint16_t*>(gu));
   MXK_RETURN_LAUNCH_STATUS();
 }
 

@@ -214,6 +214,67 @@ __device__ __forceinline__ void store_block_narrow(const f32x4_t (&acc)[8][8], u
   }
 }
 
+// Fused SwiGLU-backward epilogue of the down-projection's input-gradient GEMM:
+// the block's accumulators are d(act) = dY W2 for act = silu(g) * u, and the
+// lane's 4 consecutive columns of row r are combined with g, u read from
+// gu = [g | u] (row stride ld, u at column offset F) into
+//   dg = d u s (1 + g (1 - s)),  du = d g s,   s = sigmoid(g)
+// written to dgu (same layout as gu).  d(act) itself never reaches memory.
+// The g / u loads run two 16-row blocks ahead of the math (software
+// pipeline), so their latency overlaps the previous block's math and stores.
+__device__ __forceinline__ void swiglu_bwd_rows(const f32x4_t (&acc)[8][8], int i,
+                                                const uint2 (&gw)[8], const uint2 (&uw)[8],
+                                                uint16_t* dgu, long off, int F) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t gp[2] = {gw[j].x, gw[j].y};
+    const uint32_t up[2] = {uw[j].x, uw[j].y};
+    float dg[4], du[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t gbits = (e & 1) ? (gp[e >> 1] & 0xFFFF0000u) : (gp[e >> 1] << 16);
+      const uint32_t ubits = (e & 1) ? (up[e >> 1] & 0xFFFF0000u) : (up[e >> 1] << 16);
+      const float g = __uint_as_float(gbits);
+      const float u = __uint_as_float(ubits);
+      const float d = acc[i][j][e];
+      const float sg = 1.f / (1.f + __expf(-g));
+      du[e] = d * g * sg;
+      dg[e] = d * u * sg * (1.f + g * (1.f - sg));
+    }
+    uint2 pg, pu;
+    pg.x = pack2bf(dg[0], dg[1]);
+    pg.y = pack2bf(dg[2], dg[3]);
+    pu.x = pack2bf(du[0], du[1]);
+    pu.y = pack2bf(du[2], du[3]);
+    *reinterpret_cast<uint2*>(dgu + off + j * 16) = pg;
+    *reinterpret_cast<uint2*>(dgu + off + F + j * 16) = pu;
+  }
+}
+
+__device__ __forceinline__ void swiglu_bwd_block(const f32x4_t (&acc)[8][8], const uint16_t* gu,
+                                                 uint16_t* dgu, long ld, int F, int row0,
+                                                 int col0, int lane) {
+  const int crow = lane & 15;
+  const int ccol = (lane >> 4) * 4;
+  const long off0 = static_cast<long>(row0 + crow) * ld + col0 + ccol;
+  const long step = 16 * ld;
+  uint2 gw[2][8], uw[2][8];
+  auto load = [&](int i, int b) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      gw[b][j] = *reinterpret_cast<const uint2*>(gu + off0 + i * step + j * 16);
+      uw[b][j] = *reinterpret_cast<const uint2*>(gu + off0 + i * step + F + j * 16);
+    }
+  };
+  load(0, 0);
+  load(1, 1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    swiglu_bwd_rows(acc, i, gw[i & 1], uw[i & 1], dgu, off0 + i * step, F);
+    if (i + 2 < 8) load(i + 2, i & 1);
+  }
+}
+
 // Per-K-tile instruction positions of the three-barrier GEMM schedules (see
 // gemm_bf16.hip): for MFMA index m (0..127) the fragment read / DMA piece
 // index that follows it (-1: none), and the MFMA after which each wait and

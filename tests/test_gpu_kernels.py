@@ -153,6 +153,40 @@ def test_swiglu_fwd_bwd(cuda_device, rows, F):
     assert (gu.grad.float() - gr.grad).abs().max() <= 2e-2 * gr.grad.abs().max() + 1e-2
 
 
+@pytest.mark.parametrize("T,F,K", [(512, 768, 512), (2048, 1024, 4096)])
+def test_swiglu_down_projection_fused_backward(cuda_device, T, F, K):
+    """w2(swiglu(gu)) as one node: the SwiGLU backward runs in the epilogue of
+    the input-gradient GEMM (mxk_gemm_bf16_dgrad_swiglu) - checked against an
+    fp32 autograd reference of the plain composition, and the native kernel is
+    checked to be the one that ran (no silent unfused fallback)."""
+    from mxk8s.ops import _lib
+    from mxk8s.ops.linear import SwiGLULinear, _dgrad_swiglu
+    lin = SwiGLULinear(F, K).to(cuda_device).bfloat16()
+    with torch.no_grad():
+        lin.weight.copy_(_rand((K, F), cuda_device, 31, 0.05))
+    gu = _rand((T, 2 * F), cuda_device, 32, 3.0).bfloat16().requires_grad_()
+    y = lin(gu)
+    dy = _rand((T, K), cuda_device, 33).bfloat16()
+    y.backward(dy)
+    gr = gu.detach().float().requires_grad_()
+    wr = lin.weight.detach().float().requires_grad_()
+    g, u = gr.chunk(2, -1)
+    yr = (torch.nn.functional.silu(g) * u) @ wr.t()
+    yr.backward(dy.float())
+    assert (y.float() - yr).norm() / yr.norm() < 1e-2
+    for got, ref, name in ((gu.grad, gr.grad, "dgu"), (lin.weight.grad, wr.grad, "dW")):
+        rel = ((got.float() - ref).norm() / ref.norm()).item()
+        assert rel < 1e-2, (name, rel)
+    # the fused kernel itself accepts this shape
+    dgu = torch.empty_like(gu)
+    w = lin.weight.detach()
+    st = _lib.lib().mxk_gemm_bf16_dgrad_swiglu(dy.data_ptr(), w.data_ptr(), gu.data_ptr(),
+                                              dgu.data_ptr(), T, F, K, K, F,
+                                              _lib.stream_ptr(cuda_device))
+    assert st == 0
+    assert torch.equal(dgu, _dgrad_swiglu(dy, w, gu.detach()))
+
+
 @pytest.mark.parametrize("B,S,H,D", [(1, 2048, 32, 128), (2, 17, 8, 128), (1, 5, 3, 64)])
 def test_rope_fwd_bwd(cuda_device, B, S, H, D):
     cos, sin = rope_tables(S, D, device=cuda_device)
