@@ -30,6 +30,23 @@ _USE_MXK_WGRAD = os.environ.get("MXK_WGRAD", "1") != "0"
 _USE_MXK_DGRAD = os.environ.get("MXK_DGRAD", "1") != "0"
 
 
+# y = x W^T (both operands K-major) on the hand-written TN kernel instead of
+# hipBLASLt; off by default: hipBLASLt's tuned picks are 1-2 % faster on the
+# Llama-3-8B forward shapes in isolation (profiles/r1_gemm_w4h/gemm_fwd_shapes.log)
+# and the whole step runs 25.5k vs 26.0k tok/s with MXK_FWD=1
+# (profiles/r1_swiglu/fwd_*.log).
+_USE_MXK_FWD = os.environ.get("MXK_FWD", "0") != "0"
+
+
+def _fwd(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    if _USE_MXK_FWD and x.is_cuda and x.is_contiguous() and weight.is_contiguous():
+        x2 = x.reshape(-1, x.shape[-1])
+        out = torch.empty((x2.shape[0], weight.shape[0]), device=x.device, dtype=x.dtype)
+        if not _tail_heavy(*out.shape) and gemm_bf16_ex(x2, weight, True, True, out):
+            return out.view(*x.shape[:-1], weight.shape[0])
+    return torch.matmul(x, weight.t())
+
+
 def _tail_heavy(M: int, N: int, cus: int = 256) -> bool:
     """Few 256x256 tiles with a half-empty last round (e.g. 384 tiles on 256
     CUs): hipBLASLt's stream-K kernels balance that tail, ours do not."""
@@ -79,7 +96,7 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
         ctx.save_for_backward(x, weight)
-        return torch.matmul(x, weight.t())
+        return _fwd(x, weight)
 
     @staticmethod
     def backward(ctx, dy):
@@ -121,7 +138,7 @@ class _SwiGLULinearFn(torch.autograd.Function):
         from .fused import swiglu_fwd
         h = swiglu_fwd(gu)
         ctx.save_for_backward(gu, h, weight)
-        return torch.matmul(h, weight.t())
+        return _fwd(h, weight)
 
     @staticmethod
     def backward(ctx, dy):
