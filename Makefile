@@ -79,7 +79,7 @@ $(OUT_BIN)/mx-vector-add: $(BUILD)/tools/vector_add_main.o $(BUILD)/kernels/vect
 	@mkdir -p $(OUT_BIN)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^
 
-$(OUT_BIN)/mx-gemm-bench: $(BUILD)/tools/gemm_bench_main.o $(BUILD)/kernels/gemm_bf16.o
+$(OUT_BIN)/mx-gemm-bench: $(BUILD)/tools/gemm_bench_main.o $(BUILD)/kernels/gemm_bf16.o $(BUILD)/kernels/gemm_bf16_layouts.o
 	@mkdir -p $(OUT_BIN)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrocblas -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
 
