@@ -120,6 +120,26 @@ __device__ __forceinline__ void map_block(int w, int nbh, int nqb, bool causal, 
     *qb = v / nbh;
   }
 }
+
+// XCD-local work order.  Workgroups are dispatched round-robin over the 8
+// XCDs (each with its own L2), so with map_block the blocks resident on one
+// XCD at a time belong to many different heads and share little.  Here
+// mxk::xcd_remap gives each XCD a contiguous range of logical ids, and
+// consecutive logical ids are the `grp` query heads of one KV head x all
+// their blocks (heaviest first when causal): about one such group is
+// resident per XCD, so its K/V (1 MiB) stays in that L2.  Forward 0.408 ->
+// 0.368 ms, dQ 570 -> 526 us per Llama-3-8B layer (profiles/r1_attention/).
+// Not used by dK/dV: its per-group Q/dO (4 MiB) is the whole L2, and the same
+// order there ran 8 % slower.
+__device__ __forceinline__ void map_block_xcd(int w, int nwg, int nqb, int grp, bool causal,
+                                              int* bh, int* qb) {
+  const int L = mxk::xcd_remap(w, nwg);
+  const int per = grp * nqb;
+  const int g = L / per, r = L - g * per;
+  const int j = r / grp;
+  *bh = g * grp + (r - j * grp);
+  *qb = causal ? nqb - 1 - j : j;
+}
 }  // namespace
 
 template <bool CAUSAL>
@@ -319,7 +339,7 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
 
   const int nqb = S / BQ;
   int bh, qb;
-  map_block(blockIdx.x, gridDim.x / nqb, nqb, CAUSAL, &bh, &qb);
+  map_block_xcd(blockIdx.x, gridDim.x, nqb, Hq / Hkv, CAUSAL, &bh, &qb);
   const int b = bh / Hq, hq = bh % Hq;
   const int hkv = hq / (Hq / Hkv);
   const int q0 = qb * BQ;
@@ -634,7 +654,7 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
 
   const int nqb = S / BQ;
   int bh, qb;
-  map_block(blockIdx.x, gridDim.x / nqb, nqb, CAUSAL, &bh, &qb);
+  map_block_xcd(blockIdx.x, gridDim.x, nqb, Hq / Hkv, CAUSAL, &bh, &qb);
   const int b = bh / Hq, hq = bh % Hq;
   const int hkv = hq / (Hq / Hkv);
   const int q0 = qb * BQ;
