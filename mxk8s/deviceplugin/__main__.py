@@ -24,13 +24,20 @@ def main(argv=None) -> int:
     p.add_argument("--device-specs", type=_bool, default=True)
     p.add_argument("--fault-file", default=None)
     p.add_argument("--no-smi-events", action="store_true")
+    p.add_argument("--replicas", type=int, default=1,
+                   help="time-slicing: advertise each GPU this many times")
+    p.add_argument("--fail-requests-greater-than-one", type=_bool, default=False)
+    p.add_argument("--rename-shared", type=_bool, default=False,
+                   help="with --replicas>1 advertise <resource-name>.shared")
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
     cfg = PluginConfig(resource_name=a.resource_name, plugin_dir=a.plugin_dir,
                        socket_name=a.socket_name, sysfs_root=a.sysfs_root,
                        health_interval=a.health_interval, event_quarantine_s=a.event_quarantine,
                        use_cdi=a.cdi, use_device_specs=a.device_specs,
-                       use_smi_events=not a.no_smi_events)
+                       use_smi_events=not a.no_smi_events, replicas=a.replicas,
+                       fail_requests_greater_than_one=a.fail_requests_greater_than_one,
+                       rename_shared=a.rename_shared)
     if a.fault_file:
         cfg.fault_file = a.fault_file
     run_forever(cfg)

@@ -18,6 +18,13 @@ checked at README.md:288-296 and README.md:341-345).  Behaviour:
   with /etc/cdi/amd.com-gpu.json; no runtime shim) plus, as a fallback when CDI
   is off, explicit DeviceSpecs for /dev/kfd and /dev/dri/renderD<m> (+card<n>);
 * ``GetPreferredAllocation``: the native xGMI-hive / NUMA aware policy;
+* time-slicing (``replicas`` > 1): the GPU Operator's device-plugin sharing
+  config [ext, SURVEY.md §2.1 R26d] re-designed for KFD: each GPU is advertised
+  as ``<i>::<r>`` replicas that share one render node; Allocate de-duplicates
+  replicas to physical GPUs, GetPreferredAllocation spreads replicas over the
+  least-loaded GPUs, health is per physical GPU, and
+  ``fail_requests_greater_than_one`` rejects multi-replica requests (a second
+  replica of the same GPU buys no extra compute);
 * kubelet restarts: the kubelet wipes the plugin directory when it restarts,
   so a watcher re-creates our socket and re-registers when it vanishes or
   kubelet.sock is re-created.
@@ -59,6 +66,15 @@ class PluginConfig:
     event_quarantine_s: float = 60.0
     use_smi_events: bool = True
     register: bool = True
+    replicas: int = 1                        # time-slicing: >1 advertises <i>::<r> IDs
+    fail_requests_greater_than_one: bool = False
+    rename_shared: bool = False              # replicas>1: advertise <resource>.shared
+
+    def __post_init__(self):
+        if self.replicas < 1:
+            raise ValueError(f"replicas must be >= 1, got {self.replicas}")
+        if self.replicas > 1 and self.rename_shared and not self.resource_name.endswith(".shared"):
+            self.resource_name += ".shared"
 
     @property
     def socket_path(self) -> str:
@@ -72,8 +88,9 @@ class PluginConfig:
 class DeviceState:
     """Thread-safe device list + health with change notification."""
 
-    def __init__(self, gpus: list[node.GpuInfo]):
+    def __init__(self, gpus: list[node.GpuInfo], replicas: int = 1):
         self._cv = threading.Condition()
+        self.replicas = replicas
         self.gpus = {str(g.index): g for g in gpus}
         self.health = {i: api.HEALTHY for i in self.gpus}
         self.reasons = {i: "healthy" for i in self.gpus}
@@ -96,11 +113,26 @@ class DeviceState:
             out = []
             for i in sorted(self.gpus, key=int):
                 g = self.gpus[i]
-                d = api.Device(ID=i, health=self.health[i])
-                if g.numa_node >= 0:
-                    d.topology.nodes.add(ID=g.numa_node)
-                out.append(d)
+                for did in self.replica_ids(i):
+                    d = api.Device(ID=did, health=self.health[i])
+                    if g.numa_node >= 0:
+                        d.topology.nodes.add(ID=g.numa_node)
+                    out.append(d)
             return out
+
+    def replica_ids(self, phys: str) -> list[str]:
+        if self.replicas == 1:
+            return [phys]
+        return [f"{phys}::{r}" for r in range(self.replicas)]
+
+    def physical(self, dev_id: str) -> Optional[str]:
+        """Advertised ID -> physical GPU index, or None when not one of ours."""
+        if self.replicas == 1:
+            return dev_id if dev_id in self.gpus else None
+        phys, sep, rep = dev_id.partition("::")
+        if not sep or phys not in self.gpus or not rep.isdigit() or int(rep) >= self.replicas:
+            return None
+        return phys
 
     def wait_change(self, seen: int, timeout: float) -> int:
         with self._cv:
@@ -121,7 +153,7 @@ class AmdGpuDevicePlugin:
                  gpus: Optional[list[node.GpuInfo]] = None):
         self.cfg = config or PluginConfig()
         self.gpus = gpus if gpus is not None else node.enumerate_gpus(self.cfg.sysfs_root)
-        self.state = DeviceState(self.gpus)
+        self.state = DeviceState(self.gpus, self.cfg.replicas)
         self._server: Optional[grpc.Server] = None
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
@@ -148,6 +180,16 @@ class AmdGpuDevicePlugin:
 
     def GetPreferredAllocation(self, request, context):
         resp = api.PreferredAllocationResponse()
+        if self.cfg.replicas > 1:
+            for creq in request.container_requests:
+                try:
+                    ids = self.preferred_replicas(list(creq.available_deviceIDs),
+                                                  list(creq.must_include_deviceIDs),
+                                                  creq.allocation_size)
+                except ValueError as e:
+                    context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+                resp.container_responses.add(deviceIDs=ids)
+            return resp
         for creq in request.container_requests:
             avail = [int(x) for x in creq.available_deviceIDs]
             must = [int(x) for x in creq.must_include_deviceIDs]
@@ -162,13 +204,22 @@ class AmdGpuDevicePlugin:
     def Allocate(self, request, context):
         resp = api.AllocateResponse()
         for creq in request.container_requests:
-            ids = list(creq.devices_ids)
-            for i in ids:
-                if i not in self.state.gpus:
-                    context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unknown device id {i!r}")
+            requested = list(creq.devices_ids)
+            if (self.cfg.replicas > 1 and self.cfg.fail_requests_greater_than_one
+                    and len(requested) > 1):
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT,
+                              f"time-sliced {self.cfg.resource_name}: request for "
+                              f"{len(requested)} replicas refused (limit 1 per container)")
+            ids: list[str] = []
+            for did in requested:
+                i = self.state.physical(did)
+                if i is None:
+                    context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unknown device id {did!r}")
                 if self.state.health.get(i) != api.HEALTHY:
                     context.abort(grpc.StatusCode.FAILED_PRECONDITION,
                                   f"device {i} is unhealthy: {self.state.reasons.get(i)}")
+                if i not in ids:
+                    ids.append(i)
             resp.container_responses.append(self.container_response(ids))
         return resp
 
@@ -176,6 +227,36 @@ class AmdGpuDevicePlugin:
         return api.PreStartContainerResponse()
 
     # -------------------------------------------------------------- helpers
+    def preferred_replicas(self, avail: list[str], must: list[str], size: int) -> list[str]:
+        """Replica choice under time-slicing: keep ``must``, then take one replica
+        at a time from the physical GPU with the most free replicas that this
+        request does not use yet (spread before stacking; ties -> lowest index),
+        so co-scheduled pods land on the least-shared GPUs."""
+        free: dict[str, list[str]] = {}
+        for did in avail:
+            phys = self.state.physical(did)
+            if phys is None:
+                raise ValueError(f"unknown device id {did!r}")
+            free.setdefault(phys, []).append(did)
+        if len(must) > size or size > len(avail):
+            raise ValueError(f"cannot pick {size} of {len(avail)} (must include {len(must)})")
+        chosen, used = [], {}
+        for did in must:
+            phys = self.state.physical(did)
+            if phys is None or did not in free.get(phys, []):
+                raise ValueError(f"must-include id {did!r} is not available")
+            free[phys].remove(did)
+            chosen.append(did)
+            used[phys] = used.get(phys, 0) + 1
+        while len(chosen) < size:
+            phys = min((p for p in free if free[p]),
+                       key=lambda p: (used.get(p, 0), -len(free[p]), int(p)))
+            did = sorted(free[phys], key=lambda x: int(x.partition("::")[2]))[0]
+            free[phys].remove(did)
+            chosen.append(did)
+            used[phys] = used.get(phys, 0) + 1
+        return chosen
+
     def container_response(self, ids: list[str]):
         c = api.ContainerAllocateResponse()
         gpus = [self.state.gpus[i] for i in sorted(ids, key=int)]

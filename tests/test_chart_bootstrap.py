@@ -102,6 +102,15 @@ def test_chart_values_overrides():
         render.render(render.load_values(sets=["validator.gpus=9"]))
 
 
+def test_chart_time_slicing_args():
+    v = render.load_values(sets=["devicePlugin.sharing.timeSlicing.replicas=4",
+                                 "devicePlugin.sharing.timeSlicing.failRequestsGreaterThanOne=true"])
+    dp = next(d for d in _docs(v) if d["metadata"]["name"] == "amd-gpu-stack-device-plugin")
+    args = dp["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert "--replicas=4" in args and "--fail-requests-greater-than-one=true" in args
+    assert "--rename-shared=false" in args
+
+
 def test_deploy_files_are_up_to_date():
     """deploy/ must equal what the generators produce (single source of truth)."""
     with open(os.path.join(REPO, "deploy", "amd-gpu-stack.yaml")) as f:

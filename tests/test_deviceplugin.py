@@ -215,3 +215,73 @@ def test_golden_wire_bytes():
                                                 must_include_deviceIDs=["2"], allocation_size=3)
     assert p.SerializeToString() == b"\x0a\x011\x12\x012\x18\x03"
     assert api.method_path("DevicePlugin", "ListAndWatch") == "/v1beta1.DevicePlugin/ListAndWatch"
+
+
+def test_time_slicing_replicas(plugin_dir):
+    """GPU Operator time-slicing parity: <i>::<r> replicas, de-duplicated Allocate,
+    spread-first preferred allocation, per-GPU health on every replica."""
+    kube, plugin = _start(plugin_dir, replicas=3)
+    try:
+        reg = kube.wait_registration()
+        assert reg.resource_name == "amd.com/gpu"
+        stub = kube.plugin_stub(reg.endpoint)
+        first = next(iter(stub.ListAndWatch(api.Empty(), timeout=5)))
+        ids = [d.ID for d in first.devices]
+        assert len(ids) == 24 and ids[:4] == ["0::0", "0::1", "0::2", "1::0"]
+        assert [d.topology.nodes[0].ID for d in first.devices][12] == 1
+        req = api.AllocateRequest()
+        req.container_requests.add(devices_ids=["2::1", "2::0", "0::2"])
+        c = stub.Allocate(req, timeout=5).container_responses[0]
+        assert [d.name for d in c.cdi_devices] == ["amd.com/gpu=0", "amd.com/gpu=2"]
+        assert c.envs["AMD_GPU_DEVICE_IDS"] == "0,2"
+        for bad_id in ("2", "2::3", "9::0", "x::y"):
+            bad = api.AllocateRequest()
+            bad.container_requests.add(devices_ids=[bad_id])
+            with pytest.raises(grpc.RpcError) as e:
+                stub.Allocate(bad, timeout=5)
+            assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT, bad_id
+        # preferred: GPU 0 already has one replica taken (0::0 missing) -> spread over
+        # GPUs with the most free replicas first, one replica per GPU before stacking
+        pref = api.PreferredAllocationRequest()
+        avail = [f"{g}::{r}" for g in range(3) for r in range(3) if (g, r) != (0, 0)]
+        pref.container_requests.add(available_deviceIDs=avail, allocation_size=3)
+        pref.container_requests.add(available_deviceIDs=avail, must_include_deviceIDs=["0::2"],
+                                    allocation_size=2)
+        r = stub.GetPreferredAllocation(pref, timeout=5)
+        assert list(r.container_responses[0].deviceIDs) == ["1::0", "2::0", "0::1"]
+        assert list(r.container_responses[1].deviceIDs) == ["0::2", "1::0"]
+    finally:
+        plugin.stop()
+        kube.stop()
+
+
+def test_time_slicing_health_rename_and_limit(plugin_dir, tmp_path):
+    ff = tmp_path / "faults"
+    ff.write_text("")
+    kube, plugin = _start(plugin_dir, fault_file=str(ff), replicas=2, rename_shared=True,
+                          fail_requests_greater_than_one=True)
+    try:
+        reg = kube.wait_registration()
+        assert reg.resource_name == "amd.com/gpu.shared"
+        stub = kube.plugin_stub(reg.endpoint)
+        stream = stub.ListAndWatch(api.Empty(), timeout=20)
+        assert len(next(stream).devices) == 16
+        ff.write_text("5\n")
+        health = {d.ID: d.health for d in next(stream).devices}
+        assert health["5::0"] == health["5::1"] == api.UNHEALTHY
+        assert sum(h == api.HEALTHY for h in health.values()) == 14
+        stream.cancel()
+        two = api.AllocateRequest()
+        two.container_requests.add(devices_ids=["1::0", "1::1"])
+        with pytest.raises(grpc.RpcError) as e:
+            stub.Allocate(two, timeout=5)
+        assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+        one = api.AllocateRequest()
+        one.container_requests.add(devices_ids=["1::1"])
+        assert [d.name for d in stub.Allocate(one, timeout=5).container_responses[0].cdi_devices] \
+            == ["amd.com/gpu=1"]
+    finally:
+        plugin.stop()
+        kube.stop()
+    with pytest.raises(ValueError):
+        PluginConfig(replicas=0)
