@@ -13,6 +13,13 @@ Kubernetes label-value grammar):
   amd.com/gpu.xgmi=true           amd.com/gpu.xgmi-links=7
   amd.com/gpu.xgmi-hive=<hex>     amd.com/gpu.numa-nodes=2
   amd.com/gpu.driver-version=...  amd.com/gpu.rocm-version=7.2.0
+  amd.com/gpu.compute-partitioning-mode=spx|dpx|qpx|cpx|mixed
+  amd.com/gpu.memory-partitioning-mode=nps1|nps2|nps4|mixed
+
+The partition modes (the MI355X counterpart of the MIG-mode facts GFD
+publishes) come from amdgpu's
+``current_{compute,memory}_partition`` sysfs files; they are omitted when the
+driver does not expose them.
 
 Also writes an NFD ``features.d`` file so a stock Node Feature Discovery
 (local source) publishes the same facts under feature.node.kubernetes.io/.
@@ -54,7 +61,28 @@ def rocm_version(root: str = "") -> str:
     return ""
 
 
-def compute_labels(gpus: Iterable[GpuInfo], driver_version: str = "", rocm: str = "") -> dict:
+def partition_modes(gpus: Iterable[GpuInfo], root: str = "") -> dict:
+    """{"compute": mode, "memory": mode} from amdgpu's per-device sysfs files,
+    lower-cased; "mixed" when GPUs disagree; a key is absent when no GPU has it."""
+    out = {}
+    for kind in ("compute", "memory"):
+        seen = set()
+        for g in gpus:
+            path = os.path.join(root or "/", "sys/bus/pci/devices", g.bdf,
+                                f"current_{kind}_partition")
+            try:
+                with open(path) as f:
+                    seen.add(f.read().strip().lower())
+            except OSError:
+                continue
+        seen.discard("")
+        if seen:
+            out[kind] = seen.pop() if len(seen) == 1 else "mixed"
+    return out
+
+
+def compute_labels(gpus: Iterable[GpuInfo], driver_version: str = "", rocm: str = "",
+                   partitions: Optional[dict] = None) -> dict:
     gpus = list(gpus)
     if not gpus:
         return {PREFIX + "present": "false", PREFIX + "count": "0"}
@@ -85,6 +113,8 @@ def compute_labels(gpus: Iterable[GpuInfo], driver_version: str = "", rocm: str 
         labels["driver-version"] = driver_version
     if rocm:
         labels["rocm-version"] = rocm
+    for kind, mode in (partitions or {}).items():
+        labels[f"{kind}-partitioning-mode"] = mode
     out = {}
     for k, v in labels.items():
         s = sanitize(v)
@@ -112,8 +142,9 @@ def label_patch(current: dict, desired: dict) -> dict:
 
 
 def run_once(client, node_name: str, gpus, driver: str = "", rocm: str = "",
-             nfd_dir: Optional[str] = None) -> dict:
-    desired = compute_labels(gpus, driver, rocm)
+             nfd_dir: Optional[str] = None, sysfs_root: str = "") -> dict:
+    gpus = list(gpus)
+    desired = compute_labels(gpus, driver, rocm, partition_modes(gpus, sysfs_root))
     node = client.get_node(node_name)
     current = node.get("metadata", {}).get("labels", {}) or {}
     patch = label_patch(current, desired)

@@ -33,7 +33,8 @@ def main(argv=None) -> int:
     while True:
         try:
             gpus = node.enumerate_gpus(a.sysfs_root)
-            patch = run_once(client, a.node_name, gpus, driver, rocm_version(), a.nfd_features_dir)
+            patch = run_once(client, a.node_name, gpus, driver, rocm_version(), a.nfd_features_dir,
+                             a.sysfs_root)
             log.info("node %s: %d GPU(s); patched %d label(s)", a.node_name, len(gpus), len(patch))
         except Exception as e:   # keep the DaemonSet alive; retry next interval
             log.error("labelling failed: %s", e)

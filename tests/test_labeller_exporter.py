@@ -39,6 +39,22 @@ def test_compute_labels_mi355x():
         assert len(v) <= 63 and labeller._LABEL_VALUE.match(v)
 
 
+def test_partition_mode_labels(tmp_path):
+    gpus = node.enumerate_gpus(os.path.join(FX, "mi355x_8gpu"))
+    assert labeller.partition_modes(gpus, str(tmp_path)) == {}   # driver without the files
+    for k, g in enumerate(gpus):
+        d = tmp_path / "sys/bus/pci/devices" / g.bdf
+        d.mkdir(parents=True)
+        (d / "current_compute_partition").write_text("CPX\n" if k else "SPX\n")
+        (d / "current_memory_partition").write_text("NPS1\n")
+    modes = labeller.partition_modes(gpus, str(tmp_path))
+    assert modes == {"compute": "mixed", "memory": "nps1"}
+    labels = labeller.compute_labels(gpus, partitions=modes)
+    assert labels["amd.com/gpu.compute-partitioning-mode"] == "mixed"
+    assert labels["amd.com/gpu.memory-partitioning-mode"] == "nps1"
+    assert "amd.com/gpu.compute-partitioning-mode" not in labeller.compute_labels(gpus)
+
+
 def test_label_sanitize_and_patch():
     assert labeller.sanitize("Linux version 6.8 (gcc 12)!") == "Linux-version-6.8-gcc-12"
     assert len(labeller.sanitize("x" * 200)) == 63
