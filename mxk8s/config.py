@@ -76,6 +76,12 @@ VALUES: dict = {
     "devicePlugin": {"enabled": F("boolean"), "cdiDevices": F("boolean"), "deviceSpecs": F("boolean"),
                      "healthInterval": F("integer", "seconds", minimum=1, maximum=3600),
                      "eventQuarantineSeconds": F("integer", "", minimum=0, maximum=86400),
+                     "sharing": {"timeSlicing": {
+                         "replicas": F("integer", "advertise each GPU this many times",
+                                       minimum=1, maximum=64),
+                         "renameByDefault": F("boolean", "advertise <resourceName>.shared"),
+                         "failRequestsGreaterThanOne": F("boolean",
+                                                         "refuse requests for >1 replica")}},
                      "privileged": F("boolean"), "priorityClassName": F("string"),
                      "resources": RESOURCES},
     "labeller": {"enabled": F("boolean"), "nfdFeatureFile": F("boolean"),
