@@ -32,8 +32,8 @@ NODE_SRCS := $(wildcard native/libmxnode/*.cc)
 NODE_OBJS := $(patsubst native/libmxnode/%.cc,$(BUILD)/node/%.o,$(NODE_SRCS))
 NODE_HDRS := $(wildcard native/libmxnode/*.h)
 
-.PHONY: all kernels node tools clean test-native test-native-tsan
-all: kernels node tools
+.PHONY: all kernels node tools clean test-native test-native-tsan fake-amdsmi
+all: kernels node tools fake-amdsmi
 
 kernels: $(OUT_LIB)/libmxkernels.so
 
@@ -86,6 +86,13 @@ $(OUT_BIN)/mx-gemm-bench: $(BUILD)/tools/gemm_bench_main.o $(BUILD)/kernels/gemm
 $(OUT_BIN)/mx-allreduce-perf: $(BUILD)/tools/allreduce_perf.o
 	@mkdir -p $(OUT_BIN)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lrocprofiler-sdk-roctx -lpthread -Wl,-rpath,$(ROCM)/lib
+
+# ---- scriptable fake libamd_smi.so (CPU test tier: MXK8S_AMDSMI_LIB) ----
+fake-amdsmi: $(BUILD)/test/libfake_amdsmi.so
+
+$(BUILD)/test/libfake_amdsmi.so: native/libmxnode/tests/fake_amdsmi.cc
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -shared -o $@ $< -lpthread
 
 # ---- host tests (sanitized) ----
 test-native: $(BUILD)/asan/test_mxnode

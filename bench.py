@@ -2,30 +2,46 @@
 """Headline benchmark: validator HIP GEMM TFLOPS + RCCL all-reduce bus-bw.
 
 BASELINE.json names the metric "validator HIP GEMM TFLOPS + RCCL allreduce
-bus-bw at 1/2/4/8 amd.com/gpu" (configs 3 and 4).  One process per GPU
-(``torch.distributed`` over RCCL when WORLD_SIZE > 1):
+bus-bw at 1/2/4/8 amd.com/gpu" (configs 3 and 4).  One process per GPU, and
+``torch.distributed`` over RCCL at every N (a 1-rank communicator at N = 1,
+so the all-reduce is a real ``ncclAllReduce`` there too).
+
+Protocol (BASELINE.md "Measurement protocol"):
 
 * a *step* is one 8192^3 bf16 GEMM on this rank's GPU through the hand-written
   CDNA4 MFMA kernel (``native/kernels/gemm_bf16.hip``), random uniform
   [-1, 1) operands (random data, never zeros: the chip clocks higher on zeros);
-* W untimed warm-up steps, then exactly K timed steps bracketed by a barrier
-  and ``torch.cuda.synchronize()``; the slowest rank's time is used;
-* ``value`` = whole-job GEMM TFLOP/s = N x 2*M*N*K*K_steps / max-rank time;
-* after the GEMM phase, an RCCL all-reduce (sum) of a 256 MiB bf16 buffer is
-  timed across all ranks and reported as algbw / busbw = algbw * 2(n-1)/n;
-* the same-shape hipBLASLt GEMM (``torch.matmul``) is timed for context.
+* correctness gate: the WHOLE output of the first launch and of the last timed
+  launch is compared with an fp32 ``torch.matmul`` on the device, tolerance
+  2^-7 * max|ref| (bf16 output rounding is 2^-8 relative);
+* warm-up: ``--warmup`` launches, then more until ``--warmup-s`` (default 2 s)
+  of back-to-back launches have run, whatever ``--warmup`` says (the GPU
+  ramps its clock over ~1 s; a 5-launch warm-up times a cold chip);
+* exactly K timed steps bracketed by a barrier and ``torch.cuda.synchronize()``
+  on both sides; the slowest rank's wall time gives ``value`` = whole-job
+  TFLOP/s = N x 2MNK x K / max-rank time.  Each step also sits between two
+  hipEvents, reported as the per-launch median;
+* hipBLASLt (``torch.mm``) on the same operands is timed A/B-interleaved with
+  the hand-written kernel under the same event protocol (context, not the
+  metric);
+* RCCL all-reduce (sum, bf16): a correctness check, then a 1 MiB - 1 GiB size
+  sweep with algbw = bytes/t and busbw = algbw * 2(n-1)/n (0 at n = 1 by
+  definition); the slowest rank's time per size.
 
 ``--mode ddp`` runs the Llama-3-8B DDP training step (config 5) instead.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
              bench.py --gpus N
+On a host without a GPU (the CPU test tier) the same code runs over gloo with
+the PyTorch reference GEMM, so the multi-rank plumbing is testable anywhere.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -48,23 +64,154 @@ def _log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def run_validator(args) -> dict:
+class _Timer:
+    """Per-launch timing: hipEvents on a GPU, perf_counter on the CPU tier."""
+
+    def __init__(self, dev):
+        import torch
+        self.cuda = dev.type == "cuda"
+        self.torch = torch
+
+    def marks(self, n):
+        if self.cuda:
+            return [self.torch.cuda.Event(enable_timing=True) for _ in range(n)]
+        return [None] * n
+
+    def record(self, marks, i):
+        if self.cuda:
+            marks[i].record()
+        else:
+            marks[i] = time.perf_counter()
+
+    def elapsed_ms(self, marks):
+        if self.cuda:
+            self.torch.cuda.synchronize()
+            return [marks[i].elapsed_time(marks[i + 1]) for i in range(len(marks) - 1)]
+        return [(marks[i + 1] - marks[i]) * 1e3 for i in range(len(marks) - 1)]
+
+
+def _sync(dev):
+    import torch
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _init_group(backend, dev, world, rank):
+    """Default process group at every N.  At N = 1 a 1-rank group on an
+    in-process store: RCCL builds a real 1-rank communicator."""
+    import torch.distributed as dist
+    from mxk8s.parallel.dist import init_distributed
+
+    if world > 1:
+        init_distributed(backend=backend, device=dev if backend == "nccl" else None)
+    elif not dist.is_initialized():
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(backend=backend, store=dist.HashStore(), rank=0, world_size=1, **kw)
+    return dist.group.WORLD
+
+
+def _barrier(dev):
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl":
+        dist.barrier(device_ids=[dev.index])
+    else:
+        dist.barrier()
+
+
+def _max_over_ranks(x, dev):
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64,
+                     device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _full_check(A, Bt, C):
+    """max |C - A.Bt^T| over the whole output against an fp32 GEMM on the same
+    device; returns (max_abs_err, tolerance)."""
+    import torch
+    ref = torch.matmul(A.float(), Bt.float().t())
+    err = (C.float() - ref).abs().max().item()
+    tol = 2.0 ** -7 * ref.abs().max().item()
+    del ref
+    return err, tol
+
+
+def run_allreduce(args, dev, world, rank) -> dict:
+    """Real collective (RCCL at every N on GPUs): correctness, then a size sweep."""
     import torch
     import torch.distributed as dist
 
+    # correctness: every rank contributes rank+1; sum is exact in bf16 for n <= 8
+    probe = torch.full(((1 << 20) // 2,), float(rank + 1), device=dev, dtype=torch.bfloat16)
+    dist.all_reduce(probe)
+    _sync(dev)
+    want = world * (world + 1) / 2
+    bad = int((probe != want).sum().item())
+    if bad:
+        raise SystemExit(f"all-reduce check failed on rank {rank}: {bad} elements != {want}")
+
+    sizes_mib = [int(s) for s in args.allreduce_sizes.split(",") if s]
+    sweep = []
+    for mib in sizes_mib:
+        nbytes = mib << 20
+        buf = torch.ones(nbytes // 2, device=dev, dtype=torch.bfloat16)
+        iters = max(3, min(20, (2048 // max(mib, 1))))
+        for _ in range(2):
+            dist.all_reduce(buf)
+        _sync(dev)
+        _barrier(dev)
+        _sync(dev)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(buf)
+        _sync(dev)
+        dt = (time.perf_counter() - t0) / iters
+        dt = _max_over_ranks(dt, dev)
+        algbw = nbytes / dt / 1e9
+        busbw = algbw * 2 * (world - 1) / world
+        sweep.append({"bytes": nbytes, "ms": round(dt * 1e3, 4), "iters": iters,
+                      "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2)})
+        del buf
+    head = next((s for s in sweep if s["bytes"] == args.allreduce_mib << 20), sweep[-1] if sweep else None)
+    return {
+        "backend": dist.get_backend(),
+        "rccl_ranks": dist.get_world_size(),
+        "dtype": "bf16", "op": "sum", "check": "exact (sum of rank+1)",
+        "bytes": head["bytes"] if head else None,
+        "ms": head["ms"] if head else None,
+        "algbw_GBps": head["algbw_GBps"] if head else None,
+        "busbw_GBps": head["busbw_GBps"] if head else None,
+        "sweep": sweep,
+        "note": ("1-rank communicator: RCCL completes an in-place all-reduce without moving "
+                 "data, so algbw here is not a bandwidth; busbw is 0 by definition")
+        if world == 1 else None,
+    }
+
+
+def run_validator(args) -> dict:
+    import torch
+
     from mxk8s.ops import gemm_bf16_tn
-    from mxk8s.parallel.dist import init_distributed, max_over_ranks, barrier
 
     world, rank, local = _dist_env()
+    cpu = os.environ.get("MXK_BENCH_DEVICE") == "cpu" or not torch.cuda.is_available()
     # MXK_BENCH_BACKEND=gloo rehearses the multi-rank path on a box with fewer
     # GPUs than ranks (ranks share GPUs round-robin; RCCL refuses that).  The
     # measured configuration is always the default: RCCL, one rank per GPU.
-    backend = os.environ.get("MXK_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % torch.cuda.device_count()
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    init_distributed(backend=backend, device=dev)
+    backend = "gloo" if cpu else os.environ.get("MXK_BENCH_BACKEND", "nccl")
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        if backend != "nccl":
+            local = local % torch.cuda.device_count()
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    _init_group(backend, dev, world, rank)
+    timer = _Timer(dev)
 
     M = N = K = args.size
     g = torch.Generator(device=dev)
@@ -72,112 +219,85 @@ def run_validator(args) -> dict:
     A = (torch.rand((M, K), device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
     Bt = (torch.rand((N, K), device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
     C = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+    C_ref = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
 
-    # correctness gate on a sub-block before timing (fp32 reference)
-    gemm_bf16_tn(A, Bt, C)
-    torch.cuda.synchronize()
-    ref = A[:256].float() @ Bt[:512].float().t()
-    err = (C[:256, :512].float() - ref).abs().max().item()
-    tol = 2e-2 * ref.abs().max().item() + 1e-2
-    if not err <= tol:
-        raise SystemExit(f"GEMM self-check failed: max|err| {err} > {tol}")
+    def mxk():
+        gemm_bf16_tn(A, Bt, C)
 
-    _log(rank, f"[bench] GEMM {M}x{N}x{K} bf16 self-check ok (max err {err:.3g}); "
-               f"warmup {args.warmup}, steps {args.steps}, "
-               f"{'hipGraph replay' if args.graph else 'eager launches'}")
-    # The K timed steps are K real GEMM launches.  With --graph they replay
-    # from a hipGraph holding `chunk` back-to-back launches of the kernel (the
-    # launcher is capture-safe: no sync, no allocation); steps not divisible by
-    # the chunk run the remainder eagerly.  A 0.69 ms kernel already hides the
-    # launch path, so eager is the default (graph replay measured equal).
-    chunk = max(1, min(args.graph_chunk, args.steps))
-    graph = None
-    if args.graph:
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            gemm_bf16_tn(A, Bt, C)   # first launch outside capture (lazy init)
-        torch.cuda.current_stream(dev).wait_stream(side)
-        torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for _ in range(chunk):
-                gemm_bf16_tn(A, Bt, C)
-        torch.cuda.synchronize()
+    def blas():
+        torch.mm(A, Bt.t(), out=C_ref)
 
-    def run_steps(n):
-        if graph is None:
-            for _ in range(n):
-                gemm_bf16_tn(A, Bt, C)
-            return
-        for _ in range(n // chunk):
-            graph.replay()
-        for _ in range(n % chunk):
-            gemm_bf16_tn(A, Bt, C)
+    # correctness gate before timing: the whole output vs fp32
+    C.zero_()
+    mxk()
+    _sync(dev)
+    err0, tol = _full_check(A, Bt, C)
+    if not err0 <= tol:
+        raise SystemExit(f"GEMM self-check failed: max|err| {err0} > {tol} (2^-7 max|ref|)")
+    _log(rank, f"[bench] GEMM {M}x{N}x{K} bf16 full-output check ok "
+               f"(max err {err0:.3g} <= {tol:.3g}); warmup >= {args.warmup} launches "
+               f"and >= {args.warmup_s} s, steps {args.steps}")
 
-    run_steps(args.warmup)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
+    # time-floored warm-up; both kernels launched so neither is timed cold
+    blas()
+    t_w = time.perf_counter()
+    n_warm = 0
+    while True:
+        for _ in range(10):
+            mxk()
+        n_warm += 10
+        _sync(dev)
+        if n_warm >= args.warmup and time.perf_counter() - t_w >= args.warmup_s:
+            break
+    warmup_s = time.perf_counter() - t_w
+
+    # the timed region: exactly K launches, barrier + sync on both sides
+    marks = timer.marks(args.steps + 1)
+    _sync(dev)
+    _barrier(dev)
+    _sync(dev)
     t0 = time.perf_counter()
-    run_steps(args.steps)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    dt_max = max_over_ranks(dt, dev)
+    for i in range(args.steps):
+        timer.record(marks, i)
+        mxk()
+    timer.record(marks, args.steps)
+    _sync(dev)
+    dt = time.perf_counter() - t0   # the K launches, up to their completion
+    _barrier(dev)
+    _sync(dev)
+    step_ms = timer.elapsed_ms(marks)
+    dt_max = _max_over_ranks(dt, dev)
     flops = 2.0 * M * N * K
     per_gpu_tflops = flops * args.steps / dt / 1e12
     agg_tflops = world * flops * args.steps / dt_max / 1e12
+    ev_med = statistics.median(step_ms)
 
-    # hipBLASLt reference on the same data (context only; not the metric)
-    ref_tflops = None
+    # the output of the last timed launch, whole, vs fp32
+    err1, _ = _full_check(A, Bt, C)
+    if not err1 <= tol:
+        raise SystemExit(f"GEMM check after the timed loop failed: max|err| {err1} > {tol}")
+
+    # A/B-interleaved hipBLASLt under the same event protocol
+    ab = None
     if not args.no_reference:
-        for _ in range(max(3, args.warmup // 4)):
-            torch.matmul(A, Bt.t())
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        nref = max(5, args.steps // 2)
-        for _ in range(nref):
-            torch.matmul(A, Bt.t())
-        torch.cuda.synchronize()
-        ref_tflops = flops * nref / (time.perf_counter() - t1) / 1e12
+        n_ab = max(args.steps, 20)
+        t_mxk, t_blas = [], []
+        for r in range(args.ab_rounds):
+            for fn, out in ((mxk, t_mxk), (blas, t_blas)) if r % 2 == 0 else ((blas, t_blas), (mxk, t_mxk)):
+                mk = timer.marks(n_ab + 1)
+                for i in range(n_ab):
+                    timer.record(mk, i)
+                    fn()
+                timer.record(mk, n_ab)
+                out.extend(timer.elapsed_ms(mk))
+        m_mxk, m_blas = statistics.median(t_mxk), statistics.median(t_blas)
+        ab = {"launches_each": len(t_mxk), "rounds": args.ab_rounds,
+              "mxk_median_ms": round(m_mxk, 4), "hipblaslt_median_ms": round(m_blas, 4),
+              "mxk_tflops": round(flops / m_mxk / 1e9, 2),
+              "hipblaslt_tflops": round(flops / m_blas / 1e9, 2),
+              "mxk_over_hipblaslt": round(m_blas / m_mxk, 4)}
 
-    # RCCL all-reduce over xGMI
-    ar = None
-    if not args.no_allreduce:
-        nbytes = args.allreduce_mib << 20
-        buf = torch.ones(nbytes // 2, device=dev, dtype=torch.bfloat16)
-        iters = max(5, min(args.steps, 20))
-        if world > 1:
-            for _ in range(3):
-                dist.all_reduce(buf)
-            torch.cuda.synchronize()
-            barrier()
-            t2 = time.perf_counter()
-            for _ in range(iters):
-                dist.all_reduce(buf)
-            torch.cuda.synchronize()
-            barrier()
-            ta = max_over_ranks((time.perf_counter() - t2) / iters, dev)
-            algbw = nbytes / ta / 1e9
-            busbw = algbw * 2 * (world - 1) / world
-        else:
-            # n = 1: no peer; busbw is 0 by definition — report the local
-            # reduction-free copy rate as algbw (what RCCL does at n=1).
-            tmp = torch.empty_like(buf)
-            for _ in range(3):
-                tmp.copy_(buf)
-            torch.cuda.synchronize()
-            t2 = time.perf_counter()
-            for _ in range(iters):
-                tmp.copy_(buf)
-            torch.cuda.synchronize()
-            ta = (time.perf_counter() - t2) / iters
-            algbw = nbytes / ta / 1e9
-            busbw = 0.0
-        ar = {"bytes": nbytes, "dtype": "bf16", "op": "sum", "ms": ta * 1e3,
-              "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2)}
+    ar = None if args.no_allreduce else run_allreduce(args, dev, world, rank)
 
     return {
         "metric": METRIC,
@@ -195,10 +315,17 @@ def run_validator(args) -> dict:
         "config": {"model": f"validator bf16 MFMA GEMM M=N=K={M} + RCCL allreduce",
                    "global_batch": world, "seq_len": None,
                    "parallelism": f"dp{world} (one GEMM per amd.com/gpu)"},
+        "device": "cpu (reference GEMM, plumbing test)" if cpu else "cuda",
         "per_gpu_tflops": round(per_gpu_tflops, 2),
-        "hipblaslt_tflops_same_shape": None if ref_tflops is None else round(ref_tflops, 2),
-        "gemm_self_check_max_abs_err": err,
-        "launch": f"hipGraph x{chunk}" if graph is not None else "eager",
+        "warmup_launches": n_warm,
+        "warmup_s": round(warmup_s, 3),
+        "event_median_ms": round(ev_med, 4),
+        "event_median_tflops": round(flops / ev_med / 1e9, 2),
+        "gemm_check": {"max_abs_err_first": err0, "max_abs_err_after_timed": err1,
+                       "tolerance": tol, "elements": M * N, "reference": "fp32 torch.matmul"},
+        "hipblaslt_ab": ab,
+        "hipblaslt_tflops_same_shape": None if ab is None else ab["hipblaslt_tflops"],
+        "launch": "eager",
         "allreduce": ar,
     }
 
@@ -208,16 +335,16 @@ def main(argv=None) -> int:
     p.add_argument("--gpus", type=int, default=None, help="number of GPUs (= WORLD_SIZE)")
     p.add_argument("--steps", type=int, default=None)
     p.add_argument("--warmup", type=int, default=None)
+    p.add_argument("--warmup-s", type=float, default=2.0,
+                   help="validator mode: minimum seconds of warm-up launches")
     p.add_argument("--mode", choices=["validator", "ddp"], default="validator")
     p.add_argument("--size", type=int, default=8192, help="GEMM M=N=K (validator mode)")
-    p.add_argument("--allreduce-mib", type=int, default=256)
+    p.add_argument("--allreduce-mib", type=int, default=256, help="headline all-reduce size")
+    p.add_argument("--allreduce-sizes", default="1,4,16,64,256,1024",
+                   help="all-reduce sweep sizes in MiB (comma list)")
+    p.add_argument("--ab-rounds", type=int, default=6, help="A/B-interleaved hipBLASLt rounds")
     p.add_argument("--no-reference", action="store_true")
     p.add_argument("--no-allreduce", action="store_true")
-    p.add_argument("--graph", dest="graph", action="store_true", default=False,
-                   help="validator mode: replay the timed GEMMs from a hipGraph "
-                        "(measured equal to eager at 8192^3: profiles/r1_gemm_w4h/bench_graph_ab.log)")
-    p.add_argument("--no-graph", dest="graph", action="store_false")
-    p.add_argument("--graph-chunk", type=int, default=20, help="GEMM launches per captured graph")
     p.add_argument("--seq-len", type=int, default=2048, help="ddp mode")
     p.add_argument("--micro-batch", type=int, default=8, help="ddp mode: sequences per GPU per step (8 x 2048 tokens: 197 GiB peak of 288 at 1 GPU)")
     p.add_argument("--layers", type=int, default=None, help="ddp mode: override (NOT headline)")
@@ -228,21 +355,27 @@ def main(argv=None) -> int:
 
     world, rank, _ = _dist_env()
     if args.gpus is not None and args.gpus != world:
-        if world == 1 and args.gpus > 1:
-            # launched without torchrun: spawn ourselves under torch.distributed.run
+        if world == 1 and args.gpus > 1 and "TORCHELASTIC_RUN_ID" not in os.environ:
+            # launched without torchrun: run ourselves under torch.distributed.run
+            # as a child (never exec: nothing here has touched the GPU yet, but
+            # a child keeps that true by construction)
+            import socket
             import subprocess
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                    f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
-                   f"--master-port={29500 + os.getpid() % 1000}", os.path.abspath(__file__)] + \
-                (argv if argv is not None else sys.argv[1:])
+                   f"--master-port={port}", os.path.abspath(__file__)] + \
+                (list(argv) if argv is not None else sys.argv[1:])
             return subprocess.call(cmd)
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
 
     if args.mode == "validator":
         if args.steps is None:
-            args.steps = 200
+            args.steps = 50
         if args.warmup is None:
-            args.warmup = 100
+            args.warmup = 10
         out = run_validator(args)
     else:
         if args.steps is None:

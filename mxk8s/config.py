@@ -70,12 +70,18 @@ VALUES: dict = {
                       items={"type": "object", "additionalProperties": {"type": "string"}}),
     "resourceName": F("string", "extended resource advertised by the device plugin",
                       pattern=r"^[a-z0-9.-]+/[a-z0-9.-]+$"),
+    "logFormat": F("string", "node daemon log format", enum=["json", "text"]),
+    "stateDir": F("string", "host dir for the ECC baseline and health.json", pattern=r"^/"),
     "cdi": {"hostDir": F("string", "CDI spec directory on the host", pattern=r"^/"),
             "specFile": F("string", "spec file name", pattern=r"^[A-Za-z0-9._-]+\.(json|yaml)$"),
             "generate": F("boolean", "regenerate the spec from the plugin's init container")},
     "devicePlugin": {"enabled": F("boolean"), "cdiDevices": F("boolean"), "deviceSpecs": F("boolean"),
                      "healthInterval": F("integer", "seconds", minimum=1, maximum=3600),
                      "eventQuarantineSeconds": F("integer", "", minimum=0, maximum=86400),
+                     "eccQuarantineSeconds": F("integer", "0 = out until reboot", minimum=0,
+                                               maximum=86400 * 30),
+                     "reconcileSeconds": F("integer", "GPU-set / CDI-spec resync, 0 = off",
+                                           minimum=0, maximum=86400),
                      "sharing": {"timeSlicing": {
                          "replicas": F("integer", "advertise each GPU this many times",
                                        minimum=1, maximum=64),

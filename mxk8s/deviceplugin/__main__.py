@@ -2,9 +2,9 @@
 from __future__ import annotations
 
 import argparse
-import logging
 import sys
 
+from ..utils.logs import setup_logging
 from .plugin import PluginConfig, run_forever
 
 
@@ -29,15 +29,27 @@ def main(argv=None) -> int:
     p.add_argument("--fail-requests-greater-than-one", type=_bool, default=False)
     p.add_argument("--rename-shared", type=_bool, default=False,
                    help="with --replicas>1 advertise <resource-name>.shared")
+    p.add_argument("--ecc-quarantine", type=float, default=0.0,
+                   help="seconds a GPU stays out after an uncorrectable-ECC increase "
+                        "(0 = until reboot)")
+    p.add_argument("--state-dir", default=None,
+                   help="ECC baseline + health.json for the exporter (hostPath)")
+    p.add_argument("--cdi-spec", default=None,
+                   help="CDI spec file to keep in sync with the live render nodes")
+    p.add_argument("--reconcile-interval", type=float, default=30.0,
+                   help="seconds between GPU-set / CDI-spec reconciliations (0 = off)")
+    p.add_argument("--log-format", choices=["json", "text"], default="json")
     a = p.parse_args(argv)
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    setup_logging(a.log_format)
     cfg = PluginConfig(resource_name=a.resource_name, plugin_dir=a.plugin_dir,
                        socket_name=a.socket_name, sysfs_root=a.sysfs_root,
                        health_interval=a.health_interval, event_quarantine_s=a.event_quarantine,
                        use_cdi=a.cdi, use_device_specs=a.device_specs,
                        use_smi_events=not a.no_smi_events, replicas=a.replicas,
                        fail_requests_greater_than_one=a.fail_requests_greater_than_one,
-                       rename_shared=a.rename_shared)
+                       rename_shared=a.rename_shared, ecc_quarantine_s=a.ecc_quarantine,
+                       state_dir=a.state_dir, cdi_spec_path=a.cdi_spec,
+                       reconcile_interval=a.reconcile_interval)
     if a.fault_file:
         cfg.fault_file = a.fault_file
     run_forever(cfg)

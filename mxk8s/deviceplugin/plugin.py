@@ -10,10 +10,18 @@ checked at README.md:288-296 and README.md:341-345).  Behaviour:
 * ``ListAndWatch``: sends the device list, then re-sends on every health
   change (HOT loop = a blocking wait on a condition variable, no polling of
   the stream);
-* health: a checker thread re-runs ``mx_health_check`` (KFD node present,
-  render node present, fault-injection file) every ``health_interval`` s and,
-  when amd-smi is available, an event thread marks a GPU unhealthy on reset /
-  VM-fault events for ``event_quarantine_s``;
+* health: the native N02 state machine (``native/libmxnode/monitor.cc``,
+  ``node.HealthMonitor``) — KFD node / render node present, fault-injection
+  file, amd-smi VM-fault / pre-reset events (quarantine ``event_quarantine_s``
+  after the last one), uncorrectable ECC above the per-boot baseline (sticky
+  until reboot, or ``ecc_quarantine_s``), thermal-throttle events counted and
+  logged; every verdict change re-sends ListAndWatch and gates Allocate, and
+  the verdicts are written to ``<state_dir>/health.json`` for the exporter;
+* operand reconciliation (the GPU Operator's ClusterPolicy controller,
+  README.md:269-271, in miniature): every ``reconcile_interval`` s the plugin
+  re-enumerates the GPUs (re-advertising when the set or a render minor
+  changed) and rewrites the CDI spec atomically when it no longer matches the
+  live render nodes (a driver reload / GPU reset can renumber them);
 * ``Allocate``: CDI device names ``amd.com/gpu=<id>`` (containerd resolves them
   with /etc/cdi/amd.com-gpu.json; no runtime shim) plus, as a fallback when CDI
   is off, explicit DeviceSpecs for /dev/kfd and /dev/dri/renderD<m> (+card<n>);
@@ -33,6 +41,7 @@ from __future__ import annotations
 
 import concurrent.futures
 import dataclasses
+import json
 import logging
 import os
 import threading
@@ -69,6 +78,10 @@ class PluginConfig:
     replicas: int = 1                        # time-slicing: >1 advertises <i>::<r> IDs
     fail_requests_greater_than_one: bool = False
     rename_shared: bool = False              # replicas>1: advertise <resource>.shared
+    ecc_quarantine_s: float = 0.0            # <= 0: uncorrectable ECC is sticky until reboot
+    state_dir: Optional[str] = None          # ECC baseline + health.json (hostPath /var/lib/mxk8s)
+    cdi_spec_path: Optional[str] = None      # reconcile this CDI spec file (None: don't)
+    reconcile_interval: float = 30.0
 
     def __post_init__(self):
         if self.replicas < 1:
@@ -145,6 +158,16 @@ class DeviceState:
             self.closed = True
             self._cv.notify_all()
 
+    def replace_gpus(self, gpus: list[node.GpuInfo]) -> None:
+        """New GPU set (reconciliation): known IDs keep their health, new ones
+        start healthy, vanished ones are withdrawn; ListAndWatch re-sends."""
+        with self._cv:
+            self.gpus = {str(g.index): g for g in gpus}
+            self.health = {i: self.health.get(i, api.HEALTHY) for i in self.gpus}
+            self.reasons = {i: self.reasons.get(i, "healthy") for i in self.gpus}
+            self.generation += 1
+            self._cv.notify_all()
+
 
 class AmdGpuDevicePlugin:
     """gRPC servicer + lifecycle (serve, register, health, kubelet-restart watch)."""
@@ -157,7 +180,9 @@ class AmdGpuDevicePlugin:
         self._server: Optional[grpc.Server] = None
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
-        self._smi_quarantine: dict[str, float] = {}
+        self._mon_lock = threading.Lock()
+        self.monitor = self._new_monitor()
+        self.reconciles = {"gpus_changed": 0, "cdi_rewritten": 0}
         self.registrations = 0
         self._socket_ino: Optional[int] = None
         self._kubelet_ino: Optional[int] = None
@@ -228,10 +253,12 @@ class AmdGpuDevicePlugin:
 
     # -------------------------------------------------------------- helpers
     def preferred_replicas(self, avail: list[str], must: list[str], size: int) -> list[str]:
-        """Replica choice under time-slicing: keep ``must``, then take one replica
-        at a time from the physical GPU with the most free replicas that this
-        request does not use yet (spread before stacking; ties -> lowest index),
-        so co-scheduled pods land on the least-shared GPUs."""
+        """Replica choice under time-slicing.  Keep ``must``; then decide which
+        physical GPUs the request spans — one replica per GPU before any GPU
+        gets a second (spread before stacking), drawn from the least-shared GPUs
+        (most free replicas), and among those the xGMI-hive / NUMA-compact set
+        the native policy picks for exclusive requests (``mx_preferred_allocation``);
+        finally take replicas round-robin over that set."""
         free: dict[str, list[str]] = {}
         for did in avail:
             phys = self.state.physical(did)
@@ -240,6 +267,8 @@ class AmdGpuDevicePlugin:
             free.setdefault(phys, []).append(did)
         if len(must) > size or size > len(avail):
             raise ValueError(f"cannot pick {size} of {len(avail)} (must include {len(must)})")
+        for p in free:
+            free[p].sort(key=lambda x: int(x.partition("::")[2]))
         chosen, used = [], {}
         for did in must:
             phys = self.state.physical(did)
@@ -248,12 +277,28 @@ class AmdGpuDevicePlugin:
             free[phys].remove(did)
             chosen.append(did)
             used[phys] = used.get(phys, 0) + 1
+        rest = size - len(chosen)
+        if rest == 0:
+            return chosen
+        spare = [p for p in free if free[p] and p not in used]
+        n_new = min(rest, len(spare))           # new GPUs this request spreads onto
+        span = list(used)
+        if n_new:
+            # least-shared tier: every spare GPU with at least as many free
+            # replicas as the n_new-th best one, then the topology policy
+            counts = sorted((len(free[p]) for p in spare), reverse=True)
+            tier = [p for p in spare if len(free[p]) >= counts[n_new - 1]]
+            try:
+                pick = node.preferred_allocation([int(p) for p in tier] + [int(p) for p in used],
+                                                 [int(p) for p in used], len(used) + n_new,
+                                                 self.cfg.sysfs_root)
+                span += [str(i) for i in pick if str(i) not in used]
+            except (ValueError, RuntimeError):
+                span += sorted(tier, key=lambda p: (-len(free[p]), int(p)))[:n_new]
         while len(chosen) < size:
-            phys = min((p for p in free if free[p]),
-                       key=lambda p: (used.get(p, 0), -len(free[p]), int(p)))
-            did = sorted(free[phys], key=lambda x: int(x.partition("::")[2]))[0]
-            free[phys].remove(did)
-            chosen.append(did)
+            cand = [p for p in span if free[p]] or [p for p in free if free[p]]
+            phys = min(cand, key=lambda p: (used.get(p, 0), -len(free[p]), int(p)))
+            chosen.append(free[phys].pop(0))
             used[phys] = used.get(phys, 0) + 1
         return chosen
 
@@ -277,17 +322,78 @@ class AmdGpuDevicePlugin:
                                   permissions="rw")
         return c
 
-    def check_health_once(self) -> None:
-        now = time.monotonic()
-        for i, g in self.state.gpus.items():
-            code = node.health_check(g.index, self.cfg.sysfs_root or self.cfg.dev_root,
-                                     self.cfg.fault_file)
-            if code == node.HEALTHY and self._smi_quarantine.get(i, 0) > now:
-                code = node.UNHEALTHY_SMI_EVENT
-            changed = self.state.set_health(i, code == node.HEALTHY, node.health_reason(code))
-            if changed:
-                log.warning("device %s -> %s (%s)", i, self.state.health[i],
-                            node.health_reason(code))
+    def _new_monitor(self) -> node.HealthMonitor:
+        return node.HealthMonitor(root=self.cfg.sysfs_root or self.cfg.dev_root,
+                                  fault_file=self.cfg.fault_file, state_dir=self.cfg.state_dir,
+                                  event_quarantine_s=self.cfg.event_quarantine_s,
+                                  ecc_quarantine_s=self.cfg.ecc_quarantine_s,
+                                  use_smi=self.cfg.use_smi_events)
+
+    @property
+    def health_state_path(self) -> Optional[str]:
+        return os.path.join(self.cfg.state_dir, "health.json") if self.cfg.state_dir else None
+
+    def check_health_once(self, wait_ms: int = 0) -> None:
+        """One N02 pass (waits up to ``wait_ms`` for amd-smi events), then map
+        the verdicts onto the advertised devices (matched by PCI BDF)."""
+        with self._mon_lock:
+            mon = self.monitor
+        mon.step(wait_ms)
+        by_bdf = {g.bdf: str(g.index) for g in self.state.gpus.values()}
+        for ev in mon.new_events():
+            dev = by_bdf.get(mon_bdf(mon, ev.index)) if ev.index >= 0 else None
+            level = logging.INFO if ev.kind in (node.EVT_GPU_POST_RESET,
+                                                node.EVT_THERMAL_THROTTLE) else logging.WARNING
+            log.log(level, "device %s: %s", dev, ev.message,
+                    extra={"device": dev, "event": ev.name, "value": ev.value})
+        for st in mon.status():
+            dev = by_bdf.get(st.bdf)
+            if dev is None:
+                continue
+            if self.state.set_health(dev, st.healthy, st.reason):
+                log.warning("device %s -> %s (%s)", dev, "Healthy" if st.healthy else "Unhealthy",
+                            st.reason, extra={"device": dev, "event": "health_change",
+                                              "reason": st.reason, "bdf": st.bdf})
+        if self.health_state_path:
+            os.makedirs(self.cfg.state_dir, exist_ok=True)
+            mon.write_state(self.health_state_path)
+
+    def reconcile_once(self) -> dict:
+        """Re-check the operands this plugin owns: the GPU set it advertises
+        and the CDI spec containerd resolves its device names with."""
+        out = {"gpus_changed": False, "cdi_rewritten": False}
+        gpus = node.enumerate_gpus(self.cfg.sysfs_root)
+        ident = [(g.index, g.bdf, g.render_minor, g.card, g.uuid) for g in gpus]
+        if ident != [(g.index, g.bdf, g.render_minor, g.card, g.uuid) for g in self.gpus]:
+            log.warning("GPU set changed (%d -> %d GPUs or renumbered); re-advertising",
+                        len(self.gpus), len(gpus), extra={"event": "gpus_changed"})
+            self.gpus = gpus
+            with self._mon_lock:
+                old, self.monitor = self.monitor, self._new_monitor()
+            old.close()
+            self.state.replace_gpus(gpus)
+            out["gpus_changed"] = True
+            self.reconciles["gpus_changed"] += 1
+        if self.cfg.cdi_spec_path:
+            text = node.cdi_spec_text(self.cfg.sysfs_root, self.cfg.cdi_kind)
+            try:
+                with open(self.cfg.cdi_spec_path) as f:
+                    have = json.load(f)
+            except (OSError, ValueError):
+                have = None
+            if have != json.loads(text):
+                d = os.path.dirname(self.cfg.cdi_spec_path) or "."
+                os.makedirs(d, exist_ok=True)
+                tmp = self.cfg.cdi_spec_path + ".tmp"
+                with open(tmp, "w") as f:
+                    f.write(text)
+                os.replace(tmp, self.cfg.cdi_spec_path)
+                log.warning("CDI spec %s %s; rewritten from the live render nodes",
+                            self.cfg.cdi_spec_path, "missing/unreadable" if have is None else "stale",
+                            extra={"event": "cdi_rewritten"})
+                out["cdi_rewritten"] = True
+                self.reconciles["cdi_rewritten"] += 1
+        return out
 
     # ------------------------------------------------------------ lifecycle
     def serve(self) -> None:
@@ -325,8 +431,6 @@ class AmdGpuDevicePlugin:
             self.register()
         self._spawn(self._health_loop, "health")
         self._spawn(self._watch_loop, "kubelet-watch")
-        if self.cfg.use_smi_events:
-            self._spawn(self._smi_event_loop, "smi-events")
         return self
 
     def stop(self) -> None:
@@ -341,6 +445,8 @@ class AmdGpuDevicePlugin:
             os.unlink(self.cfg.socket_path)
         except FileNotFoundError:
             pass
+        with self._mon_lock:
+            self.monitor.close()
 
     def _spawn(self, fn: Callable[[], None], name: str) -> None:
         t = threading.Thread(target=fn, name=f"mxk8s-dp-{name}", daemon=True)
@@ -348,33 +454,21 @@ class AmdGpuDevicePlugin:
         self._threads.append(t)
 
     def _health_loop(self) -> None:
+        last_reconcile = time.monotonic()
         while not self._stop.is_set():
+            # with amd-smi the pass blocks on the event queue (an event wakes it
+            # at once); without it, a plain interval
+            smi = self.monitor.smi_active
             try:
-                self.check_health_once()
+                self.check_health_once(int(min(1.0, self.cfg.health_interval) * 1000) if smi else 0)
+                if (self.cfg.reconcile_interval > 0 and
+                        time.monotonic() - last_reconcile >= self.cfg.reconcile_interval):
+                    last_reconcile = time.monotonic()
+                    self.reconcile_once()
             except Exception:   # keep serving; a failed probe is logged, not fatal
                 log.exception("health check failed")
-            self._stop.wait(self.cfg.health_interval)
-
-    def _smi_event_loop(self) -> None:
-        ok, err = node.smi_open()
-        if not ok:
-            log.info("amd-smi events unavailable: %s", err)
-            return
-        # amd-smi enumeration order vs our KFD order: match by BDF
-        by_bdf = {g.bdf: str(g.index) for g in self.gpus}
-        smi_to_id = {}
-        for k in range(max(0, node.smi_count())):
-            s = node.smi_sample(k)
-            if s.bdf in by_bdf:
-                smi_to_id[k] = by_bdf[s.bdf]
-        while not self._stop.is_set():
-            for gi, ev in node.smi_wait_events(1000):
-                dev = smi_to_id.get(gi)
-                if dev is None:
-                    continue
-                if ev in (1, 3):   # VM fault, pre-reset
-                    self._smi_quarantine[dev] = time.monotonic() + self.cfg.event_quarantine_s
-                    self.state.set_health(dev, False, node.health_reason(node.UNHEALTHY_SMI_EVENT))
+            if not smi:
+                self._stop.wait(self.cfg.health_interval)
 
     def _watch_loop(self) -> None:
         while not self._stop.wait(self.cfg.watch_interval):
@@ -394,6 +488,13 @@ class AmdGpuDevicePlugin:
             except Exception:
                 log.exception("re-registration failed; retrying")
                 self._socket_ino = None
+
+
+def mon_bdf(mon: node.HealthMonitor, index: int) -> Optional[str]:
+    for st in mon.status():
+        if st.index == index:
+            return st.bdf
+    return None
 
 
 def _inode(path: str) -> Optional[int]:

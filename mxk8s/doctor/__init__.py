@@ -134,17 +134,40 @@ def check_gpu(h: Host) -> list[Check]:
         out.append(Check("device plugin pods", "ok" if running else "fail",
                          f"{len(running)}/{len(pods)} running",
                          "`helm install amd-gpu-stack ./charts/amd-gpu-stack -n amd-gpu --create-namespace`"))
+        resource, replicas = plugin_sharing(pods)
         rc, txt = h.kubectl("get", "nodes", "-o", "json")
         if rc == 0:
             items = json.loads(txt).get("items", [])
-            alloc = sum(int(n.get("status", {}).get("allocatable", {}).get("amd.com/gpu", 0))
+            alloc = sum(int(n.get("status", {}).get("allocatable", {}).get(resource, 0))
                         for n in items)
-            want_n = len(gpus)
+            want_n = len(gpus) * replicas
             good = alloc == want_n and want_n > 0
-            out.append(Check("allocatable amd.com/gpu", "ok" if good else "fail",
-                             f"{alloc} allocatable, {want_n} healthy on host",
-                             "unhealthy devices? `kubectl describe node | grep amd.com/gpu`"))
+            shared = f" ({len(gpus)} GPUs x {replicas} time-sliced replicas)" if replicas > 1 else ""
+            out.append(Check(f"allocatable {resource}", "ok" if good else "fail",
+                             f"{alloc} allocatable, {want_n} expected{shared}",
+                             f"unhealthy devices? `kubectl describe node | grep {resource}`"))
     return out
+
+
+def plugin_sharing(pods: list) -> tuple[str, int]:
+    """(advertised resource name, replicas per GPU) from the running device
+    plugin's arguments: time-slicing advertises replicas x GPUs, under
+    ``<resource>.shared`` when renaming is on."""
+    resource, replicas, rename = "amd.com/gpu", 1, False
+    for p in pods:
+        for c in p.get("spec", {}).get("containers", []):
+            for a in c.get("args", []) or []:
+                k, _, v = a.partition("=")
+                if k == "--resource-name" and v:
+                    resource = v
+                elif k == "--replicas" and v.isdigit():
+                    replicas = max(1, int(v))
+                elif k == "--rename-shared":
+                    rename = v.lower() in ("1", "true", "yes", "on")
+        break
+    if replicas > 1 and rename and not resource.endswith(".shared"):
+        resource += ".shared"
+    return resource, replicas
 
 
 def check_node(h: Host) -> list[Check]:

@@ -11,17 +11,29 @@ driver:
   amd_gpu_temperature_celsius{sensor}    amd_gpu_power_watts / _power_limit_watts
   amd_gpu_clock_mhz{type=sclk|mclk}      amd_gpu_ecc_errors_total{type}
   amd_gpu_processes                      amd_gpu_xgmi_links
-  amd_gpu_link_up{peer,type=xgmi|pcie}   amd_gpu_link_max_bandwidth_bytes{peer,type}
-  amd_gpu_device_healthy                 amd_gpu_info{arch,product,uuid,bdf,...}
+  amd_gpu_topology_link{peer,type}       amd_gpu_link_max_bandwidth_bytes{peer,type}
+  amd_gpu_xgmi_link_up{link,peer_bdf}    (live amd-smi xGMI link state)
+  amd_gpu_xgmi_read_bytes_total / _write_bytes_total{link,peer_bdf}
+  amd_gpu_xgmi_link_bitrate_gbps{link,peer_bdf}
+  amd_gpu_process_memory_bytes{pid,process,pod_uid,...}  (per-process VRAM)
+  amd_gpu_pod_info{namespace,pod,container}  amd_gpu_pods (time-sliced owners)
+  amd_gpu_device_healthy{source,reason}  (the device plugin's own verdict)
+  amd_gpu_vm_faults_total / _resets_total / _thermal_throttle_events_total
+  amd_gpu_info{arch,product,uuid,bdf,...}
   amd_gpu_stack_component_up{component}  amd_gpu_exporter_sample_seconds
 
 Per-GPU labels: gpu, bdf, uuid and — through the kubelet PodResources API —
-namespace, pod, container of the workload the GPU is allocated to.
+namespace, pod, container of the workload the GPU is allocated to (when a
+time-sliced GPU has several owners, one amd_gpu_pod_info series per owner).
+Health is read from the device plugin's ``health.json`` (same verdicts as
+ListAndWatch, including amd-smi quarantines and ECC) when it is fresh, and
+falls back to the stateless sysfs check otherwise.
 """
 from __future__ import annotations
 
 import dataclasses
 import http.server
+import json
 import logging
 import os
 import threading
@@ -69,6 +81,7 @@ class SmiBackend:
         self.sysfs_root = sysfs_root
         self.ok, self.err = node.smi_open()
         self.driver = node.smi_driver_version() if self.ok else ""
+        self._smi_index: dict[str, int] = {}
 
     def gpus(self) -> list[node.GpuInfo]:
         return node.enumerate_gpus(self.sysfs_root)
@@ -81,7 +94,16 @@ class SmiBackend:
             s = node.smi_sample(i)
             if s.valid:
                 out[s.bdf] = s
+                self._smi_index[s.bdf] = i
         return out
+
+    def xgmi(self, bdf: str) -> Optional[list]:
+        i = self._smi_index.get(bdf)
+        return None if i is None else node.smi_xgmi_links(i)
+
+    def processes(self, bdf: str) -> list:
+        i = self._smi_index.get(bdf)
+        return [] if i is None else node.smi_processes(i)
 
     def health(self, index: int) -> int:
         return node.health_check(index, self.sysfs_root, os.environ.get("MXK8S_FAULT_FILE"))
@@ -90,35 +112,118 @@ class SmiBackend:
         return node.links(self.sysfs_root)
 
 
+def pod_uid_of(pid: int, proc_root: str = "/proc") -> Optional[str]:
+    """Kubernetes pod UID of a host PID from its cgroup path
+    (``.../kubepods-besteffort-pod<uid>.slice/...`` or ``.../pod<uid>/...``)."""
+    try:
+        with open(os.path.join(proc_root, str(pid), "cgroup")) as f:
+            text = f.read()
+    except OSError:
+        return None
+    for part in text.replace("\n", "/").split("/"):
+        seg = part.rsplit("-", 1)[-1] if part.endswith(".slice") else part
+        seg = seg[:-6] if seg.endswith(".slice") else seg
+        if seg.startswith("pod") and len(seg) >= 35:
+            return seg[3:].replace("_", "-")
+    return None
+
+
+def load_health_state(path: Optional[str], max_age_s: float = 120.0) -> Optional[dict]:
+    """The device plugin's verdicts (``<state_dir>/health.json``), by BDF, or
+    None when missing or stale (plugin down: fall back to sysfs)."""
+    if not path:
+        return None
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if time.time() * 1000 - float(doc.get("unix_ms", 0)) > max_age_s * 1000:
+        return None
+    return {g["bdf"]: g for g in doc.get("gpus", [])}
+
+
+def _owner_list(v) -> list:
+    if not v:
+        return []
+    return [tuple(v)] if isinstance(v, tuple) else [tuple(o) for o in v]
+
+
 def render_metrics(gpus, samples: dict, health: Callable[[int], int], owners: dict,
                    driver: str, components: dict, sample_seconds: float,
-                   links: Optional[list] = None) -> str:
+                   links: Optional[list] = None, plugin_health: Optional[dict] = None,
+                   xgmi: Optional[Callable[[str], Optional[list]]] = None,
+                   processes: Optional[Callable[[str], list]] = None,
+                   pod_uid: Callable[[int], Optional[str]] = pod_uid_of) -> str:
     w = MetricWriter()
     by_gpu: dict = {}
     for l in links or []:
         by_gpu.setdefault(l.from_index, []).append(l)
     for g in gpus:
         base = {"gpu": str(g.index), "bdf": g.bdf, "uuid": g.uuid}
-        own = owners.get(str(g.index))
-        if own:
-            base.update(namespace=own[0], pod=own[1], container=own[2])
+        own = _owner_list(owners.get(str(g.index)))
+        if len(own) == 1:     # unambiguous: label every series (dcgm-exporter style)
+            base.update(namespace=own[0][0], pod=own[0][1], container=own[0][2])
+        for ns, pod, ctr in own:
+            w.add("amd_gpu_pod_info", "gauge", "One series per container the GPU is allocated to.",
+                  1, {"gpu": str(g.index), "bdf": g.bdf, "uuid": g.uuid, "namespace": ns,
+                      "pod": pod, "container": ctr})
+        w.add("amd_gpu_pods", "gauge", "Containers the GPU is allocated to (time-slicing: > 1).",
+              len(own), {"gpu": str(g.index), "bdf": g.bdf, "uuid": g.uuid})
         w.add("amd_gpu_info", "gauge", "Static GPU facts (value is always 1).", 1,
               {**base, "arch": g.arch, "product": g.product, "device_id": f"0x{g.device_id:04x}",
                "driver_version": driver, "numa_node": str(g.numa_node)})
-        h = health(g.index)
-        w.add("amd_gpu_device_healthy", "gauge", "1 if the device plugin would report Healthy.",
-              1 if h == 0 else 0, base)
+        ph = (plugin_health or {}).get(g.bdf)
+        if ph is not None:
+            w.add("amd_gpu_device_healthy", "gauge",
+                  "1 if the device plugin reports the GPU Healthy in ListAndWatch.",
+                  1 if ph.get("healthy") else 0,
+                  {**base, "source": "device-plugin", "reason": ph.get("reason", "")})
+            for key, name, help_ in (("vm_faults", "amd_gpu_vm_faults_total", "amd-smi VM-fault events."),
+                                     ("resets", "amd_gpu_resets_total", "amd-smi GPU pre-reset events."),
+                                     ("thermal_throttles", "amd_gpu_thermal_throttle_events_total",
+                                      "amd-smi thermal-throttle events.")):
+                w.add(name, "counter", help_ + " (device plugin, this boot)", int(ph.get(key, 0)), base)
+            w.add("amd_gpu_quarantine_seconds", "gauge",
+                  "Time left in the device plugin's event/ECC quarantine (s).",
+                  float(ph.get("quarantine_left_ms", 0)) / 1000.0, base)
+        else:
+            h = health(g.index)
+            w.add("amd_gpu_device_healthy", "gauge",
+                  "1 if the device plugin reports the GPU Healthy in ListAndWatch.",
+                  1 if h == 0 else 0, {**base, "source": "sysfs", "reason": node.health_reason(h)})
         w.add("amd_gpu_xgmi_links", "gauge", "xGMI links of the GPU (KFD topology).", g.xgmi_links, base)
         for l in by_gpu.get(g.index, []):
             kind = "xgmi" if l.is_xgmi else "pcie" if l.type == node.LINK_PCIE else str(l.type)
             peer = str(l.to_index) if l.to_index >= 0 else "cpu"
             lab = {**base, "peer": peer, "type": kind}
-            # a link listed in the KFD topology is trained and usable
-            w.add("amd_gpu_link_up", "gauge", "1 for every GPU link in the KFD topology.", 1, lab)
+            w.add("amd_gpu_topology_link", "gauge", "1 for every GPU link in the KFD topology.", 1, lab)
             if l.max_bandwidth_mbps:
                 w.add("amd_gpu_link_max_bandwidth_bytes", "gauge",
                       "Link bandwidth advertised by KFD (bytes/s).",
                       int(l.max_bandwidth_mbps) * 125000, lab)
+        live = xgmi(g.bdf) if xgmi else None
+        for x in live or []:
+            lab = {**base, "link": str(x.link), "peer_bdf": x.peer_bdf}
+            if x.status != "unknown":
+                w.add("amd_gpu_xgmi_link_up", "gauge",
+                      "Live xGMI link state from amd-smi (1 up, 0 down or disabled).",
+                      1 if x.status == "up" else 0, {**lab, "status": x.status})
+            if x.read_bytes is not None:
+                w.add("amd_gpu_xgmi_read_bytes_total", "counter",
+                      "Bytes received on the xGMI link (amd-smi link metrics).", x.read_bytes, lab)
+                w.add("amd_gpu_xgmi_write_bytes_total", "counter",
+                      "Bytes sent on the xGMI link (amd-smi link metrics).", x.write_bytes, lab)
+            if x.bit_rate_gbps:
+                w.add("amd_gpu_xgmi_link_bitrate_gbps", "gauge", "Current xGMI link speed (Gb/s).",
+                      x.bit_rate_gbps, lab)
+        for pr in (processes(g.bdf) if processes else []):
+            lab = {**base, "pid": str(pr.pid), "process": pr.name}
+            uid = pod_uid(pr.pid)
+            if uid:
+                lab["pod_uid"] = uid
+            w.add("amd_gpu_process_memory_bytes", "gauge", "VRAM held by a process (bytes).",
+                  pr.vram_bytes, lab)
         s = samples.get(g.bdf)
         if s is None:
             continue
@@ -156,12 +261,16 @@ class ExporterConfig:
     pod_resources_socket: Optional[str] = None
     plugin_socket: str = "/var/lib/kubelet/device-plugins/amd-gpu.sock"
     cdi_spec: str = "/etc/cdi/amd.com-gpu.json"
+    resource_name: str = "amd.com/gpu"
+    health_state_file: Optional[str] = None   # the device plugin's <state_dir>/health.json
+    sysfs_root: str = ""
+    pod_resources: bool = True
 
 
 class Exporter:
     def __init__(self, cfg: ExporterConfig, backend=None):
         self.cfg = cfg
-        self.backend = backend or SmiBackend()
+        self.backend = backend or SmiBackend(cfg.sysfs_root)
         self._text = "# no sample yet\n"
         self._lock = threading.Lock()
         self._stop = threading.Event()
@@ -180,17 +289,21 @@ class Exporter:
         gpus = self.backend.gpus()
         samples = self.backend.samples()
         owners = {}
-        if self.cfg.pod_resources_socket and os.path.exists(self.cfg.pod_resources_socket):
+        if (self.cfg.pod_resources and self.cfg.pod_resources_socket
+                and os.path.exists(self.cfg.pod_resources_socket)):
             try:
                 from .podresources import gpu_owners
-                owners = gpu_owners(self.cfg.pod_resources_socket)
+                owners = gpu_owners(self.cfg.pod_resources_socket, self.cfg.resource_name)
             except Exception as e:   # kubelet busy/old: metrics without pod labels
                 log.debug("pod-resources unavailable: %s", e)
         links_fn = getattr(self.backend, "links", None)
         links = links_fn() if links_fn else []
         text = render_metrics(gpus, samples, self.backend.health, owners,
                               getattr(self.backend, "driver", ""), self.components(),
-                              time.perf_counter() - t0, links)
+                              time.perf_counter() - t0, links,
+                              plugin_health=load_health_state(self.cfg.health_state_file),
+                              xgmi=getattr(self.backend, "xgmi", None),
+                              processes=getattr(self.backend, "processes", None))
         with self._lock:
             self._text = text
         self.samples_taken += 1

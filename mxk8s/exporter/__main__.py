@@ -6,6 +6,7 @@ import logging
 import sys
 import time
 
+from ..utils.logs import setup_logging
 from . import Exporter, ExporterConfig
 
 
@@ -14,11 +15,19 @@ def main(argv=None) -> int:
     p.add_argument("--port", type=int, default=9400)
     p.add_argument("--interval", type=float, default=5.0)
     p.add_argument("--pod-resources-socket", default=None)
+    p.add_argument("--resource-name", default="amd.com/gpu",
+                   help="device-plugin resource (its .shared rename is matched too)")
+    p.add_argument("--health-state-file", default=None,
+                   help="the device plugin's health.json (same verdicts as ListAndWatch)")
+    p.add_argument("--sysfs-root", default="")
     p.add_argument("--once", action="store_true", help="print one sample and exit")
+    p.add_argument("--log-format", choices=["json", "text"], default="json")
     a = p.parse_args(argv)
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(message)s")
+    setup_logging(a.log_format)
     ex = Exporter(ExporterConfig(port=a.port, interval=a.interval,
-                                 pod_resources_socket=a.pod_resources_socket))
+                                 pod_resources_socket=a.pod_resources_socket,
+                                 resource_name=a.resource_name,
+                                 health_state_file=a.health_state_file, sysfs_root=a.sysfs_root))
     if a.once:
         sys.stdout.write(ex.sample_once())
         return 0

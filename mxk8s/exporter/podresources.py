@@ -52,10 +52,20 @@ ListPodResourcesResponse = _C["ListPodResourcesResponse"]
 LIST_METHOD = "/v1.PodResourcesLister/List"
 
 
+def physical_id(device_id: str) -> str:
+    """Device-plugin ID -> physical GPU index: time-sliced replicas are
+    advertised as ``<i>::<r>`` (mxk8s.deviceplugin.plugin.DeviceState)."""
+    return device_id.partition("::")[0]
+
+
 def gpu_owners(socket_path: str, resource: str = "amd.com/gpu", timeout: float = 2.0) -> dict:
-    """device id -> (namespace, pod, container) from the kubelet socket."""
+    """physical GPU index -> [(namespace, pod, container), ...] from the kubelet
+    socket.  Counts both ``resource`` and its time-sliced ``<resource>.shared``
+    rename, maps ``<i>::<r>`` replica IDs to GPU ``i`` and keeps every owner
+    of a shared GPU (in first-seen order, no duplicates)."""
     import grpc
-    out = {}
+    names = {resource, resource + ".shared"}
+    out: dict = {}
     with grpc.insecure_channel("unix:" + socket_path) as ch:
         call = ch.unary_unary(LIST_METHOD, request_serializer=ListPodResourcesRequest.SerializeToString,
                               response_deserializer=ListPodResourcesResponse.FromString)
@@ -63,9 +73,13 @@ def gpu_owners(socket_path: str, resource: str = "amd.com/gpu", timeout: float =
     for pr in resp.pod_resources:
         for c in pr.containers:
             for d in c.devices:
-                if d.resource_name == resource:
-                    for i in d.device_ids:
-                        out[i] = (pr.namespace, pr.name, c.name)
+                if d.resource_name not in names:
+                    continue
+                for i in d.device_ids:
+                    owner = (pr.namespace, pr.name, c.name)
+                    lst = out.setdefault(physical_id(i), [])
+                    if owner not in lst:
+                        lst.append(owner)
     return out
 
 

@@ -10,6 +10,7 @@ import time
 from . import rocm_version, run_once
 from ..native import node
 from ..utils.kube import KubeClient
+from ..utils.logs import setup_logging
 
 
 def main(argv=None) -> int:
@@ -20,8 +21,9 @@ def main(argv=None) -> int:
     p.add_argument("--nfd-features-dir", default=None)
     p.add_argument("--server", default=None, help="API server URL (default: in-cluster)")
     p.add_argument("--token", default=None)
+    p.add_argument("--log-format", choices=["json", "text"], default="json")
     a = p.parse_args(argv)
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(message)s")
+    setup_logging(a.log_format)
     log = logging.getLogger("mxk8s.labeller")
     if not a.node_name:
         p.error("--node-name (or NODE_NAME) is required")

@@ -65,6 +65,40 @@ class _Sample(ctypes.Structure):
     ]
 
 
+class _HealthOpts(ctypes.Structure):
+    _fields_ = [("root", ctypes.c_char_p), ("fault_file", ctypes.c_char_p),
+                ("state_dir", ctypes.c_char_p), ("boot_id_file", ctypes.c_char_p),
+                ("event_quarantine_ms", ctypes.c_int), ("ecc_quarantine_ms", ctypes.c_int),
+                ("use_smi", ctypes.c_int)]
+
+
+class _HealthStatus(ctypes.Structure):
+    _fields_ = [("index", ctypes.c_int), ("code", ctypes.c_int), ("smi_index", ctypes.c_int),
+                ("ecc_valid", ctypes.c_int), ("ecc_uncorrectable", ctypes.c_uint64),
+                ("ecc_baseline", ctypes.c_uint64), ("vm_faults", ctypes.c_uint64),
+                ("thermal_throttles", ctypes.c_uint64), ("resets", ctypes.c_uint64),
+                ("quarantine_left_ms", ctypes.c_int64), ("bdf", ctypes.c_char * 20)]
+
+
+class _HealthEvent(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_uint64), ("index", ctypes.c_int), ("kind", ctypes.c_int),
+                ("value", ctypes.c_int64), ("unix_ms", ctypes.c_int64),
+                ("message", ctypes.c_char * 96)]
+
+
+class _XgmiLink(ctypes.Structure):
+    _fields_ = [("link", ctypes.c_int), ("status", ctypes.c_int), ("link_type", ctypes.c_int),
+                ("has_traffic", ctypes.c_int), ("peer_bdf", ctypes.c_char * 20),
+                ("bit_rate_gbps", ctypes.c_uint32), ("max_bandwidth_gbps", ctypes.c_uint32),
+                ("read_kb", ctypes.c_uint64), ("write_kb", ctypes.c_uint64)]
+
+
+class _Proc(ctypes.Structure):
+    _fields_ = [("pid", ctypes.c_uint32), ("cu_occupancy", ctypes.c_uint32),
+                ("name", ctypes.c_char * 64), ("container", ctypes.c_char * 64),
+                ("vram_bytes", ctypes.c_uint64), ("gtt_bytes", ctypes.c_uint64)]
+
+
 @dataclasses.dataclass(frozen=True)
 class GpuInfo:
     index: int
@@ -177,6 +211,26 @@ def lib() -> ctypes.CDLL:
             L.mx_smi_wait_events.argtypes = [i, ip, ip, i]
             L.mx_smi_wait_events.restype = i
             L.mx_smi_driver_version.restype = cp
+            L.mx_smi_xgmi_links.argtypes = [i, ctypes.POINTER(_XgmiLink), i]
+            L.mx_smi_xgmi_links.restype = i
+            L.mx_smi_processes.argtypes = [i, ctypes.POINTER(_Proc), i]
+            L.mx_smi_processes.restype = i
+            L.mx_smi_close.restype = None
+            vp = ctypes.c_void_p
+            L.mx_hm_create.argtypes = [ctypes.POINTER(_HealthOpts), cp, sz]
+            L.mx_hm_create.restype = vp
+            L.mx_hm_destroy.argtypes = [vp]
+            L.mx_hm_destroy.restype = None
+            L.mx_hm_smi_active.argtypes = [vp]
+            L.mx_hm_smi_active.restype = i
+            L.mx_hm_step.argtypes = [vp, i]
+            L.mx_hm_step.restype = i
+            L.mx_hm_status.argtypes = [vp, ctypes.POINTER(_HealthStatus), i]
+            L.mx_hm_status.restype = i
+            L.mx_hm_events.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(_HealthEvent), i]
+            L.mx_hm_events.restype = i
+            L.mx_hm_write_state.argtypes = [vp, cp]
+            L.mx_hm_write_state.restype = i
             _lib = L
     return _lib
 
@@ -228,6 +282,17 @@ def cdi_spec(root: Optional[str] = None, kind: str = "amd.com/gpu") -> dict:
     buf = ctypes.create_string_buffer(need + 1)
     lib().mx_cdi_spec(_root(root), kind.encode(), buf, need + 1, err, len(err))
     return json.loads(buf.value.decode())
+
+
+def cdi_spec_text(root: Optional[str] = None, kind: str = "amd.com/gpu") -> str:
+    """The CDI spec exactly as ``mx-cdi-gen`` writes it."""
+    err = ctypes.create_string_buffer(512)
+    need = lib().mx_cdi_spec(_root(root), kind.encode(), None, 0, err, len(err))
+    if need < 0:
+        raise RuntimeError(err.value.decode())
+    buf = ctypes.create_string_buffer(need + 1)
+    lib().mx_cdi_spec(_root(root), kind.encode(), buf, need + 1, err, len(err))
+    return buf.value.decode()
 
 
 def _iarr(vals):
@@ -308,3 +373,167 @@ def smi_wait_events(timeout_ms: int, max_events: int = 32) -> list[tuple[int, in
     if n < 0:
         return []
     return [(g[k], e[k]) for k in range(n)]
+
+
+def smi_close() -> None:
+    lib().mx_smi_close()
+
+
+@dataclasses.dataclass(frozen=True)
+class XgmiLink:
+    link: int
+    status: str                   # "up" / "down" / "disabled" / "unknown"
+    link_type: int
+    peer_bdf: str
+    bit_rate_gbps: int
+    max_bandwidth_gbps: int
+    read_bytes: Optional[int]     # cumulative; None when amd-smi has no traffic counters
+    write_bytes: Optional[int]
+
+
+_LINK_STATUS = {0: "down", 1: "up", 2: "disabled"}
+
+
+def smi_xgmi_links(i: int) -> Optional[list[XgmiLink]]:
+    """xGMI link state + cumulative traffic of amd-smi GPU ``i``; None when
+    amd-smi supports neither query here."""
+    arr = (_XgmiLink * 64)()
+    n = lib().mx_smi_xgmi_links(i, arr, 64)
+    if n < 0:
+        return None
+    out = []
+    for k in range(n):
+        a = arr[k]
+        out.append(XgmiLink(link=a.link, status=_LINK_STATUS.get(a.status, "unknown"),
+                            link_type=a.link_type, peer_bdf=a.peer_bdf.decode(),
+                            bit_rate_gbps=a.bit_rate_gbps, max_bandwidth_gbps=a.max_bandwidth_gbps,
+                            read_bytes=a.read_kb * 1024 if a.has_traffic else None,
+                            write_bytes=a.write_kb * 1024 if a.has_traffic else None))
+    return out
+
+
+@dataclasses.dataclass(frozen=True)
+class GpuProcess:
+    pid: int
+    name: str
+    container: str
+    vram_bytes: int
+    gtt_bytes: int
+    cu_occupancy: int
+
+
+def smi_processes(i: int, max_procs: int = 256) -> list[GpuProcess]:
+    arr = (_Proc * max_procs)()
+    n = lib().mx_smi_processes(i, arr, max_procs)
+    return [GpuProcess(pid=arr[k].pid, name=arr[k].name.decode(errors="replace"),
+                       container=arr[k].container.decode(errors="replace"),
+                       vram_bytes=arr[k].vram_bytes, gtt_bytes=arr[k].gtt_bytes,
+                       cu_occupancy=arr[k].cu_occupancy) for k in range(max(0, n))]
+
+
+# ---- N02 health monitor ----
+
+EVT_VMFAULT = 1
+EVT_THERMAL_THROTTLE = 2
+EVT_GPU_PRE_RESET = 3
+EVT_GPU_POST_RESET = 4
+EVT_ECC_UNCORRECTABLE = 100
+EVT_HEALTH_CHANGE = 101
+EVENT_NAMES = {EVT_VMFAULT: "vm_fault", EVT_THERMAL_THROTTLE: "thermal_throttle",
+               EVT_GPU_PRE_RESET: "gpu_pre_reset", EVT_GPU_POST_RESET: "gpu_post_reset",
+               EVT_ECC_UNCORRECTABLE: "ecc_uncorrectable", EVT_HEALTH_CHANGE: "health_change"}
+
+
+@dataclasses.dataclass(frozen=True)
+class HealthStatus:
+    index: int
+    code: int
+    reason: str
+    smi_index: int
+    ecc_valid: bool
+    ecc_uncorrectable: int
+    ecc_baseline: int
+    vm_faults: int
+    thermal_throttles: int
+    resets: int
+    quarantine_left_ms: int
+    bdf: str
+
+    @property
+    def healthy(self) -> bool:
+        return self.code == HEALTHY
+
+
+@dataclasses.dataclass(frozen=True)
+class HealthEvent:
+    seq: int
+    index: int
+    kind: int
+    value: int
+    unix_ms: int
+    message: str
+
+    @property
+    def name(self) -> str:
+        return EVENT_NAMES.get(self.kind, f"event_{self.kind}")
+
+
+class HealthMonitor:
+    """The C++ N02 state machine (``native/libmxnode/monitor.cc``)."""
+
+    def __init__(self, root: Optional[str] = None, fault_file: Optional[str] = None,
+                 state_dir: Optional[str] = None, event_quarantine_s: float = 60.0,
+                 ecc_quarantine_s: float = 0.0, use_smi: bool = True,
+                 boot_id_file: Optional[str] = None):
+        self._keep = [(root or "").encode(), (fault_file or "").encode(),
+                      (state_dir or "").encode(), (boot_id_file or "").encode()]
+        opts = _HealthOpts(self._keep[0], self._keep[1], self._keep[2] or None,
+                           self._keep[3] or None, int(event_quarantine_s * 1000),
+                           int(ecc_quarantine_s * 1000), int(use_smi))
+        err = ctypes.create_string_buffer(512)
+        self._h = lib().mx_hm_create(ctypes.byref(opts), err, len(err))
+        if not self._h:
+            raise RuntimeError(err.value.decode() or "mx_hm_create failed")
+        self._seq = 0
+
+    @property
+    def smi_active(self) -> bool:
+        return bool(lib().mx_hm_smi_active(self._h))
+
+    def step(self, wait_ms: int = 0) -> int:
+        return lib().mx_hm_step(self._h, int(wait_ms))
+
+    def status(self) -> list[HealthStatus]:
+        arr = (_HealthStatus * MAX_GPUS)()
+        n = lib().mx_hm_status(self._h, arr, MAX_GPUS)
+        return [HealthStatus(index=a.index, code=a.code, reason=health_reason(a.code),
+                             smi_index=a.smi_index, ecc_valid=bool(a.ecc_valid),
+                             ecc_uncorrectable=a.ecc_uncorrectable, ecc_baseline=a.ecc_baseline,
+                             vm_faults=a.vm_faults, thermal_throttles=a.thermal_throttles,
+                             resets=a.resets, quarantine_left_ms=a.quarantine_left_ms,
+                             bdf=a.bdf.decode()) for a in arr[:max(0, n)]]
+
+    def new_events(self) -> list[HealthEvent]:
+        """Events since the previous call (oldest first)."""
+        arr = (_HealthEvent * 256)()
+        n = lib().mx_hm_events(self._h, self._seq, arr, 256)
+        out = [HealthEvent(seq=a.seq, index=a.index, kind=a.kind, value=a.value,
+                           unix_ms=a.unix_ms, message=a.message.decode(errors="replace"))
+               for a in arr[:max(0, n)]]
+        if out:
+            self._seq = out[-1].seq
+        return out
+
+    def write_state(self, path: str) -> bool:
+        return lib().mx_hm_write_state(self._h, path.encode()) == 0
+
+    def close(self) -> None:
+        if self._h:
+            lib().mx_hm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

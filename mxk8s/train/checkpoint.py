@@ -16,7 +16,12 @@ state dicts, no pickles:
 Loading checks the layout fingerprint (parameter shapes, offsets, bucket
 padding) and, for sharded state, the world size, and refuses mismatches.
 Files are written to a temporary name and renamed, so a crash mid-save never
-leaves a truncated checkpoint in place.
+leaves a truncated file in place; ``meta.json`` — the commit record — is
+written by rank 0 only after a barrier that every rank reaches once its shard
+is on disk, and every shard carries its own ``step_count`` / ``layout`` /
+``save_step``, which ``load`` checks against ``meta.json``: a rank that died
+mid-save leaves the previous meta.json next to a newer shard, and that mix is
+refused instead of silently resumed.
 """
 from __future__ import annotations
 
@@ -46,6 +51,18 @@ def _atomic_save(tensors: dict, path: str, meta: Optional[dict] = None) -> None:
     os.replace(tmp, path)
 
 
+def _check_shard(path: str, meta: dict, want: dict) -> None:
+    """A shard's own safetensors metadata must match the commit record."""
+    from safetensors import safe_open
+    with safe_open(path, framework="pt") as f:
+        have = f.metadata() or {}
+    bad = {k: (have.get(k), v) for k, v in want.items() if have.get(k) != v}
+    if bad:
+        raise ValueError(f"{path}: shard does not match meta.json (step {meta['step']}): "
+                         + ", ".join(f"{k}={h!r} expected {w!r}" for k, (h, w) in bad.items())
+                         + " — a save was interrupted; resume from an older checkpoint")
+
+
 def save(ckpt_dir: str, ddp, opt, step: int) -> None:
     """Collective: every rank calls it (rank 0 writes params + meta)."""
     world, rank, _ = mxdist.world_info()
@@ -55,10 +72,13 @@ def save(ckpt_dir: str, ddp, opt, step: int) -> None:
     if sharded or rank == 0:
         _atomic_save({"master": opt.master, "exp_avg": opt.exp_avg, "exp_avg_sq": opt.exp_avg_sq},
                       os.path.join(ckpt_dir, f"optim-rank{rank if sharded else 0}.safetensors"),
-                      {"step_count": opt.step_count, "layout": fp})
+                      {"step_count": opt.step_count, "layout": fp, "save_step": step})
     if rank == 0:
         _atomic_save({"params": ddp.space.param_buf}, os.path.join(ckpt_dir, "params.safetensors"),
-                     {"layout": fp})
+                     {"layout": fp, "save_step": step})
+    # every shard is on disk before the commit record names this step
+    mxdist.barrier()
+    if rank == 0:
         meta = {"step": step, "optimizer_step": opt.step_count, "world_size": world,
                 "sharded": sharded, "layout": fp, "numel": ddp.space.numel,
                 "format": "mxk8s-flat-v1"}
@@ -84,10 +104,15 @@ def load(ckpt_dir: str, ddp, opt) -> int:
         raise ValueError(f"{ckpt_dir}: saved with world_size={meta['world_size']} "
                          f"sharded={meta['sharded']}, running world_size={world} sharded={sharded}")
     dev = ddp.space.param_buf.device
-    params = load_file(os.path.join(ckpt_dir, "params.safetensors"))["params"]
+    ppath = os.path.join(ckpt_dir, "params.safetensors")
+    opath = os.path.join(ckpt_dir, f"optim-rank{rank if sharded else 0}.safetensors")
+    _check_shard(ppath, meta, {"layout": meta["layout"], "save_step": str(meta["step"])})
+    _check_shard(opath, meta, {"layout": meta["layout"], "save_step": str(meta["step"]),
+                               "step_count": str(meta["optimizer_step"])})
+    params = load_file(ppath)["params"]
     with torch.no_grad():
         ddp.space.param_buf.copy_(params.to(dev))
-        st = load_file(os.path.join(ckpt_dir, f"optim-rank{rank if sharded else 0}.safetensors"))
+        st = load_file(opath)
         opt.master.copy_(st["master"].to(dev))
         opt.exp_avg.copy_(st["exp_avg"].to(dev))
         opt.exp_avg_sq.copy_(st["exp_avg_sq"].to(dev))

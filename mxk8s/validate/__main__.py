@@ -145,6 +145,18 @@ def test_ddp(gpus: int, seq_len: int, steps: int) -> bool:
     return rc == 0 and bool(lines)
 
 
+def check_allocation(gpus: int, env=None) -> tuple[bool, list[str]]:
+    """Compare the physical GPUs the device plugin handed this pod
+    (AMD_GPU_DEVICE_IDS, de-duplicated from time-sliced replicas) with the
+    requested count.  Outside a plugin-allocated pod the variable is unset and
+    the check passes."""
+    env = os.environ if env is None else env
+    ids = [x for x in env.get("AMD_GPU_DEVICE_IDS", "").split(",") if x]
+    if not ids:
+        return True, []
+    return len(ids) == gpus, ids
+
+
 def main(argv=None) -> int:
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--tests", default="rocminfo,vectoradd,gemm,rccl")
@@ -170,6 +182,13 @@ def main(argv=None) -> int:
         tests.append("ddp")
     t0 = time.time()
     status = {}
+    ok_alloc, got = check_allocation(a.gpus)
+    if not ok_alloc:
+        emit({"test": "allocation", "pass": False, "expected_gpus": a.gpus, "allocated": got,
+              "message": f"the device plugin allocated {len(got)} physical GPU(s) {got} but "
+                         f"--gpus is {a.gpus}: time-sliced replicas of one GPU were stacked "
+                         f"into this pod; request exclusive amd.com/gpu or lower --gpus"})
+        return 1
     for t in tests:
         if t == "rocminfo":
             status[t] = test_rocminfo(a.gpus)

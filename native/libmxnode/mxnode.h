@@ -100,6 +100,75 @@ int mx_preferred_allocation_topo(int n, const int* numa, const uint64_t* hive,
 int mx_health_check(const char* root, int index, const char* fault_file);
 const char* mx_health_reason(int code);
 
+// ---- N02 health monitor: sysfs checks + amd-smi events + RAS ECC ----------
+// One monitor per device plugin.  mx_hm_step() runs one pass: it drains the
+// amd-smi event queue (waiting up to wait_ms for the first event), samples the
+// uncorrectable ECC count of every GPU, re-runs the sysfs checks and updates
+// each GPU's verdict:
+//   * sysfs (KFD node / render node gone, fault injected) — while it lasts;
+//   * VM fault or GPU pre-reset event  -> MX_UNHEALTHY_SMI_EVENT for
+//     event_quarantine_ms after the LAST such event;
+//   * uncorrectable ECC above the per-boot baseline -> MX_UNHEALTHY_ECC:
+//     sticky until reboot when ecc_quarantine_ms <= 0, otherwise for
+//     ecc_quarantine_ms after the increase (the new count becomes the
+//     baseline).  The baseline is the first count seen this boot, kept in
+//     <state_dir>/ecc-baseline keyed by the kernel boot id, so a plugin
+//     restart neither forgets nor forgives an error;
+//   * thermal-throttle and post-reset events are counted and logged only.
+// All entry points are thread-safe.
+#define MX_EVT_VMFAULT 1
+#define MX_EVT_THERMAL_THROTTLE 2
+#define MX_EVT_GPU_PRE_RESET 3
+#define MX_EVT_GPU_POST_RESET 4
+#define MX_EVT_ECC_UNCORRECTABLE 100    // value = increase over the baseline
+#define MX_EVT_HEALTH_CHANGE 101        // value = new code (MX_HEALTHY / MX_UNHEALTHY_*)
+
+typedef struct mx_health_opts {
+  const char* root;                 // sysfs/dev root ("" = host)
+  const char* fault_file;           // fault-injection file or NULL
+  const char* state_dir;            // ECC baseline directory or NULL (in-memory only)
+  const char* boot_id_file;         // NULL = /proc/sys/kernel/random/boot_id
+  int event_quarantine_ms;
+  int ecc_quarantine_ms;            // <= 0: sticky until reboot
+  int use_smi;                      // 0: sysfs checks only
+} mx_health_opts;
+
+typedef struct mx_health_status {
+  int index;
+  int code;                         // MX_HEALTHY or MX_UNHEALTHY_*
+  int smi_index;                    // amd-smi index matched by BDF, -1 if none
+  int ecc_valid;
+  uint64_t ecc_uncorrectable;
+  uint64_t ecc_baseline;
+  uint64_t vm_faults;
+  uint64_t thermal_throttles;
+  uint64_t resets;
+  int64_t quarantine_left_ms;       // 0 if not quarantined
+  char bdf[20];
+} mx_health_status;
+
+typedef struct mx_health_event {
+  uint64_t seq;                     // 1, 2, ... per monitor
+  int index;                        // GPU index (KFD order), -1 unknown
+  int kind;                         // MX_EVT_*
+  int64_t value;
+  int64_t unix_ms;
+  char message[96];
+} mx_health_event;
+
+typedef struct mx_health_monitor mx_health_monitor;
+mx_health_monitor* mx_hm_create(const mx_health_opts* opts, char* err, size_t errlen);
+void mx_hm_destroy(mx_health_monitor* m);
+// 1 if the amd-smi event/ECC source is live.
+int mx_hm_smi_active(mx_health_monitor* m);
+// One pass; returns the number of GPUs whose code changed.
+int mx_hm_step(mx_health_monitor* m, int wait_ms);
+int mx_hm_status(mx_health_monitor* m, mx_health_status* out, int max);
+// Events with seq > after_seq (oldest first, the last 1024 are kept).
+int mx_hm_events(mx_health_monitor* m, uint64_t after_seq, mx_health_event* out, int max);
+// Atomically write the verdicts as JSON (tmp + rename) for the exporter.
+int mx_hm_write_state(mx_health_monitor* m, const char* path);
+
 // ---- amd-smi backed sampling (dlopen("libamd_smi.so"); no link dependency) ----
 typedef struct mx_gpu_sample {
   int index;
@@ -128,10 +197,39 @@ void mx_smi_close(void);
 int mx_smi_count(void);
 // Sample GPU i (amd-smi enumeration order, matched to BDF by the caller).
 int mx_smi_sample(int i, mx_gpu_sample* out);
+// RAS error counts of GPU i; 1 on success.
+int mx_smi_ecc(int i, uint64_t* correctable, uint64_t* uncorrectable);
 // Block up to timeout_ms for amd-smi GPU events (reset / thermal / VM fault).
 // Writes up to `max` (gpu_bdf_index, event_code) pairs; returns count or -1.
 int mx_smi_wait_events(int timeout_ms, int* gpu_out, int* event_out, int max);
 const char* mx_smi_driver_version(void);
+
+// xGMI link state + traffic of GPU i (amd-smi order).  Returns links written,
+// -1 if amd-smi supports neither amdsmi_get_gpu_xgmi_link_status nor
+// amdsmi_get_link_metrics here.
+typedef struct mx_xgmi_link_sample {
+  int link;                         // link index
+  int status;                       // 0 down, 1 up, 2 disabled, -1 unknown
+  int link_type;                    // amdsmi_link_type_t (2 = xGMI), -1 unknown
+  int has_traffic;                  // read_kb / write_kb valid
+  char peer_bdf[20];
+  uint32_t bit_rate_gbps;
+  uint32_t max_bandwidth_gbps;
+  uint64_t read_kb;                 // cumulative KB received on the link
+  uint64_t write_kb;                // cumulative KB sent
+} mx_xgmi_link_sample;
+int mx_smi_xgmi_links(int i, mx_xgmi_link_sample* out, int max);
+
+// Per-process GPU memory of GPU i (amdsmi_get_gpu_process_list).
+typedef struct mx_proc_sample {
+  uint32_t pid;
+  uint32_t cu_occupancy;
+  char name[64];
+  char container[64];
+  uint64_t vram_bytes;
+  uint64_t gtt_bytes;
+} mx_proc_sample;
+int mx_smi_processes(int i, mx_proc_sample* out, int max);
 
 #ifdef __cplusplus
 }

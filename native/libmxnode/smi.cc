@@ -7,6 +7,7 @@
 #include <amd_smi/amdsmi.h>
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -43,6 +44,8 @@ struct SmiApi {
   MX_SMI_FN(amdsmi_set_gpu_event_notification_mask);
   MX_SMI_FN(amdsmi_get_gpu_event_notification);
   MX_SMI_FN(amdsmi_stop_gpu_event_notification);
+  MX_SMI_FN(amdsmi_get_gpu_xgmi_link_status);
+  MX_SMI_FN(amdsmi_get_link_metrics);
   std::vector<amdsmi_processor_handle> gpus;
   bool events_on = false;
   std::string driver_version;
@@ -99,6 +102,9 @@ extern "C" int mx_smi_open(char* err, size_t errlen) {
   bind(h, "amdsmi_set_gpu_event_notification_mask", &api->amdsmi_set_gpu_event_notification_mask);
   bind(h, "amdsmi_get_gpu_event_notification", &api->amdsmi_get_gpu_event_notification);
   bind(h, "amdsmi_stop_gpu_event_notification", &api->amdsmi_stop_gpu_event_notification);
+  // xGMI link state / traffic: optional too (guest / older amd-smi)
+  bind(h, "amdsmi_get_gpu_xgmi_link_status", &api->amdsmi_get_gpu_xgmi_link_status);
+  bind(h, "amdsmi_get_link_metrics", &api->amdsmi_get_link_metrics);
   if (!ok) {
     mx::set_err(err, errlen, "libamd_smi.so lacks required symbols");
     dlclose(h);
@@ -209,6 +215,18 @@ extern "C" int mx_smi_sample(int i, mx_gpu_sample* o) {
   return 1;
 }
 
+// Accumulated RAS counts of GPU i only (the health monitor's per-pass probe).
+extern "C" int mx_smi_ecc(int i, uint64_t* correctable, uint64_t* uncorrectable) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_api || i < 0 || i >= static_cast<int>(g_api->gpus.size())) return 0;
+  amdsmi_error_count_t e;
+  std::memset(&e, 0, sizeof(e));
+  if (g_api->amdsmi_get_gpu_total_ecc_count(g_api->gpus[i], &e) != AMDSMI_STATUS_SUCCESS) return 0;
+  *correctable = e.correctable_count;
+  *uncorrectable = e.uncorrectable_count;
+  return 1;
+}
+
 extern "C" int mx_smi_wait_events(int timeout_ms, int* gpu_out, int* event_out, int max) {
   SmiApi* a;
   {
@@ -241,4 +259,77 @@ extern "C" int mx_smi_wait_events(int timeout_ms, int* gpu_out, int* event_out, 
     ++count;
   }
   return count;
+}
+
+// xGMI links of GPU i: link state (amdsmi_get_gpu_xgmi_link_status) merged by
+// link index with the per-link traffic counters (amdsmi_get_link_metrics).
+// Returns the number of links written, 0 if the GPU has none, -1 if amd-smi
+// supports neither query on this host.
+extern "C" int mx_smi_xgmi_links(int i, mx_xgmi_link_sample* out, int max) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_api || i < 0 || i >= static_cast<int>(g_api->gpus.size()) || max <= 0) return -1;
+  SmiApi& a = *g_api;
+  amdsmi_processor_handle h = a.gpus[i];
+  int nstat = -1, nmet = -1;
+  amdsmi_xgmi_link_status_t ls;
+  std::memset(&ls, 0, sizeof(ls));
+  if (a.amdsmi_get_gpu_xgmi_link_status &&
+      a.amdsmi_get_gpu_xgmi_link_status(h, &ls) == AMDSMI_STATUS_SUCCESS)
+    nstat = static_cast<int>(std::min<uint32_t>(ls.total_links, AMDSMI_MAX_NUM_XGMI_LINKS));
+  static thread_local amdsmi_link_metrics_t lm;   // ~3 KiB: keep it off the stack
+  std::memset(&lm, 0, sizeof(lm));
+  if (a.amdsmi_get_link_metrics && a.amdsmi_get_link_metrics(h, &lm) == AMDSMI_STATUS_SUCCESS)
+    nmet = static_cast<int>(std::min<uint32_t>(lm.num_links, AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK));
+  if (nstat < 0 && nmet < 0) return -1;
+  const int n = std::min(max, std::max(nstat, nmet));
+  for (int k = 0; k < n; ++k) {
+    mx_xgmi_link_sample& o = out[k];
+    std::memset(&o, 0, sizeof(o));
+    o.link = k;
+    o.status = k < nstat ? static_cast<int>(ls.status[k]) : -1;
+    if (k < nmet) {
+      const auto& L = lm.links[k];
+      std::snprintf(o.peer_bdf, sizeof(o.peer_bdf), "%04llx:%02llx:%02llx.%llx",
+                    static_cast<unsigned long long>(L.bdf.domain_number & 0xffff),
+                    static_cast<unsigned long long>(L.bdf.bus_number),
+                    static_cast<unsigned long long>(L.bdf.device_number),
+                    static_cast<unsigned long long>(L.bdf.function_number));
+      o.link_type = static_cast<int>(L.link_type);
+      o.bit_rate_gbps = L.bit_rate;
+      o.max_bandwidth_gbps = L.max_bandwidth;
+      o.read_kb = L.read;
+      o.write_kb = L.write;
+      o.has_traffic = 1;
+    } else {
+      o.link_type = -1;
+    }
+  }
+  return n;
+}
+
+// Processes holding GPU i (amdsmi_get_gpu_process_list): pid, name, VRAM.
+// Returns the count written (<= max), -1 if amd-smi is not open.
+extern "C" int mx_smi_processes(int i, mx_proc_sample* out, int max) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_api || i < 0 || i >= static_cast<int>(g_api->gpus.size())) return -1;
+  SmiApi& a = *g_api;
+  uint32_t n = 0;
+  if (a.amdsmi_get_gpu_process_list(a.gpus[i], &n, nullptr) != AMDSMI_STATUS_SUCCESS) return 0;
+  if (n == 0 || max <= 0) return 0;
+  std::vector<amdsmi_proc_info_t> ps(n);
+  uint32_t got = n;
+  const amdsmi_status_t st = a.amdsmi_get_gpu_process_list(a.gpus[i], &got, ps.data());
+  if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return 0;
+  const int cnt = std::min<int>(max, static_cast<int>(std::min<uint32_t>(got, n)));
+  for (int k = 0; k < cnt; ++k) {
+    mx_proc_sample& o = out[k];
+    std::memset(&o, 0, sizeof(o));
+    o.pid = ps[k].pid;
+    std::snprintf(o.name, sizeof(o.name), "%s", ps[k].name);
+    std::snprintf(o.container, sizeof(o.container), "%s", ps[k].container_name);
+    o.vram_bytes = ps[k].memory_usage.vram_mem ? ps[k].memory_usage.vram_mem : ps[k].mem;
+    o.gtt_bytes = ps[k].memory_usage.gtt_mem;
+    o.cu_occupancy = ps[k].cu_occupancy;
+  }
+  return cnt;
 }

@@ -111,6 +111,46 @@ def test_chart_time_slicing_args():
     assert "--rename-shared=false" in args
 
 
+def test_validator_follows_time_slicing():
+    """The validator Job asks for the resource the plugin really advertises,
+    and a request the plugin would refuse fails at render time."""
+    v = render.load_values(sets=["devicePlugin.sharing.timeSlicing.replicas=2",
+                                 "devicePlugin.sharing.timeSlicing.renameByDefault=true",
+                                 "validator.gpus=2"])
+    job = next(d for d in _docs(v) if d["kind"] == "Job")
+    lim = job["spec"]["template"]["spec"]["containers"][0]["resources"]["limits"]
+    assert lim["amd.com/gpu.shared"] == 2 and "amd.com/gpu" not in lim
+    with pytest.raises(gotpl.FailError, match="failRequestsGreaterThanOne"):
+        render.render(render.load_values(sets=[
+            "devicePlugin.sharing.timeSlicing.replicas=2",
+            "devicePlugin.sharing.timeSlicing.failRequestsGreaterThanOne=true", "validator.gpus=4"]))
+    # replicas alone keep the plain resource name
+    v = render.load_values(sets=["devicePlugin.sharing.timeSlicing.replicas=2"])
+    job = next(d for d in _docs(v) if d["kind"] == "Job")
+    assert "amd.com/gpu" in job["spec"]["template"]["spec"]["containers"][0]["resources"]["limits"]
+
+
+def test_validator_detects_stacked_replicas():
+    from mxk8s.validate.__main__ import check_allocation
+    assert check_allocation(2, {"AMD_GPU_DEVICE_IDS": "0,1"}) == (True, ["0", "1"])
+    assert check_allocation(2, {"AMD_GPU_DEVICE_IDS": "3"}) == (False, ["3"])
+    assert check_allocation(4, {}) == (True, [])
+
+
+def test_chart_plugin_health_and_reconcile_args():
+    dp = next(d for d in _docs(render.load_values()) if d["metadata"]["name"] == "amd-gpu-stack-device-plugin")
+    c = dp["spec"]["template"]["spec"]["containers"][0]
+    args = c["args"]
+    assert "--ecc-quarantine=0" in args and "--state-dir=/var/lib/mxk8s" in args
+    assert "--cdi-spec=/host/etc/cdi/amd.com-gpu.json" in args and "--log-format=json" in args
+    mounts = {m["name"]: m["mountPath"] for m in c["volumeMounts"]}
+    assert mounts["cdi"] == "/host/etc/cdi" and mounts["state"] == "/var/lib/mxk8s"
+    ex = next(d for d in _docs(render.load_values()) if d["metadata"]["name"] == "amd-gpu-stack-metrics-exporter")
+    ec = ex["spec"]["template"]["spec"]["containers"][0]
+    assert "--health-state-file=/var/lib/mxk8s/health.json" in ec["args"]
+    assert any(m["name"] == "state" and m.get("readOnly") for m in ec["volumeMounts"])
+
+
 def test_deploy_files_are_up_to_date():
     """deploy/ must equal what the generators produce (single source of truth)."""
     with open(os.path.join(REPO, "deploy", "amd-gpu-stack.yaml")) as f:
@@ -274,6 +314,24 @@ def test_doctor_gpu_reports_first_failure(tmp_path):
     lines = []
     assert doctor.run(checks, out=lines.append) == 1
     assert "first failure: CDI spec" in lines[-1] and "fix:" in lines[-1]
+
+
+def test_doctor_allocatable_with_time_slicing(tmp_path):
+    root = _fake_root(tmp_path)
+    ctx = phases.Context(root=root, dry_run=True, out=lambda s: None)
+    phases.run(ctx, only=["runtime", "cdi"])
+    os.makedirs(os.path.join(root, "var/lib/kubelet/device-plugins"))
+    open(os.path.join(root, "var/lib/kubelet/device-plugins/amd-gpu.sock"), "w").close()
+    pods = [{"status": {"phase": "Running"},
+             "spec": {"containers": [{"args": ["--resource-name=amd.com/gpu", "--replicas=4",
+                                               "--rename-shared=true"]}]}}]
+    nodes = [{"metadata": {"name": "n"}, "status": {"allocatable": {"amd.com/gpu.shared": "32"}}}]
+    checks = doctor.check_gpu(doctor.Host(root, kubectl=_kubectl_fake(nodes, pods)))
+    c = next(c for c in checks if c.name.startswith("allocatable"))
+    assert c.name == "allocatable amd.com/gpu.shared" and c.status == "ok", c
+    nodes[0]["status"]["allocatable"] = {"amd.com/gpu": "8"}
+    checks = doctor.check_gpu(doctor.Host(root, kubectl=_kubectl_fake(nodes, pods)))
+    assert next(c for c in checks if c.name.startswith("allocatable")).status == "fail"
 
 
 def test_doctor_pod_taint_diagnosis():

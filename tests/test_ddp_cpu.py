@@ -278,3 +278,24 @@ def test_checkpoint_rejects_layout_mismatch(tmp_path):
     d2 = FlatDDP(m2)
     with pytest.raises(ValueError, match="layout"):
         checkpoint.load(str(tmp_path / "ck"), d2, FlatAdamW(d2.space))
+
+
+def test_checkpoint_rejects_interrupted_overwrite(tmp_path):
+    """A rank that died mid-save leaves a newer shard beside the previous
+    meta.json: load refuses the mix instead of resuming it."""
+    from mxk8s.train import checkpoint
+    torch.manual_seed(0)
+    model = Llama(LlamaConfig.tiny())
+    ddp = FlatDDP(model)
+    opt = FlatAdamW(ddp.space)
+    ck = str(tmp_path / "ck")
+    checkpoint.save(ck, ddp, opt, step=5)
+    assert checkpoint.load(ck, ddp, opt) == 5
+    # the optimizer shard of a later save landed, its meta.json never did
+    opt.step_count += 3
+    checkpoint._atomic_save({"master": opt.master, "exp_avg": opt.exp_avg, "exp_avg_sq": opt.exp_avg_sq},
+                            os.path.join(ck, "optim-rank0.safetensors"),
+                            {"step_count": opt.step_count, "layout": checkpoint.layout_fingerprint(ddp.space),
+                             "save_step": 8})
+    with pytest.raises(ValueError, match="shard does not match meta.json"):
+        checkpoint.load(ck, ddp, opt)

@@ -285,3 +285,27 @@ def test_time_slicing_health_rename_and_limit(plugin_dir, tmp_path):
         kube.stop()
     with pytest.raises(ValueError):
         PluginConfig(replicas=0)
+
+
+def test_time_slicing_preferred_allocation_is_numa_compact(plugin_dir):
+    """Replica requests spanning several GPUs use the native hive/NUMA policy:
+    with GPU 0 fully taken, 4 replicas land on NUMA node 1 (GPUs 4-7) instead
+    of the lowest indices 1-4, which would cross NUMA nodes."""
+    kube, plugin = _start(plugin_dir, replicas=2)
+    try:
+        stub = kube.plugin_stub(kube.wait_registration().endpoint)
+        pref = api.PreferredAllocationRequest()
+        avail = [f"{g}::{r}" for g in range(1, 8) for r in range(2)]
+        pref.container_requests.add(available_deviceIDs=avail, allocation_size=4)
+        r = stub.GetPreferredAllocation(pref, timeout=5)
+        got = list(r.container_responses[0].deviceIDs)
+        assert sorted(got) == ["4::0", "5::0", "6::0", "7::0"], got
+        # more replicas than GPUs in the compact set: spread first, then stack
+        pref = api.PreferredAllocationRequest()
+        pref.container_requests.add(available_deviceIDs=avail, allocation_size=9)
+        got = list(stub.GetPreferredAllocation(pref, timeout=5).container_responses[0].deviceIDs)
+        phys = [g.partition("::")[0] for g in got]
+        assert len(set(phys)) == 7 and len(got) == len(set(got)) == 9
+    finally:
+        plugin.stop()
+        kube.stop()

@@ -156,8 +156,8 @@ def test_exporter_http_and_pod_resources():
     c.devices.add(resource_name="cpu-other", device_ids=["5"])
     srv = pr.serve_fake(sock, resp)
     try:
-        assert pr.gpu_owners(sock) == {"0": ("train", "llama-0", "worker"),
-                                       "1": ("train", "llama-0", "worker")}
+        assert pr.gpu_owners(sock) == {"0": [("train", "llama-0", "worker")],
+                                       "1": [("train", "llama-0", "worker")]}
         g = gpus8()
         ex = Exporter(ExporterConfig(port=0, interval=0.05, pod_resources_socket=sock),
                       backend=FakeBackend(g)).start()
@@ -176,8 +176,54 @@ def test_link_metrics_from_kfd_topology():
     root = os.path.join(FX, "mi355x_8gpu")
     g = node.enumerate_gpus(root)
     text = render_metrics(g, {}, lambda i: 0, {}, "", {}, 0.0, node.links(root))
-    up = [l for l in text.splitlines() if l.startswith("amd_gpu_link_up{")]
+    up = [l for l in text.splitlines() if l.startswith("amd_gpu_topology_link{")]
     assert len([l for l in up if 'type="xgmi"' in l]) == 56          # 8 GPUs x 7 peers
     assert len([l for l in up if 'type="pcie"' in l]) == 8
-    assert 'amd_gpu_link_up{gpu="0",bdf="0000:05:00.0",uuid="GPU-f4071d07e8ac5500",peer="7",type="xgmi"} 1' in text
+    assert 'amd_gpu_topology_link{gpu="0",bdf="0000:05:00.0",uuid="GPU-f4071d07e8ac5500",peer="7",type="xgmi"} 1' in text
+    # no live amd-smi link state: no amd_gpu_xgmi_link_up series is invented
+    assert "amd_gpu_xgmi_link_up" not in text
     assert "# TYPE amd_gpu_link_max_bandwidth_bytes gauge" in text
+
+
+def test_time_sliced_owner_attribution():
+    """Replica IDs <i>::<r> under amd.com/gpu or its .shared rename map to GPU i;
+    a GPU shared by two pods gets one amd_gpu_pod_info series per owner."""
+    d = tempfile.mkdtemp(prefix="mxpr", dir="/tmp")
+    sock = os.path.join(d, "kubelet.sock")
+    resp = pr.ListPodResourcesResponse()
+    for pod, ids, res in (("a-0", ["1::0"], "amd.com/gpu.shared"), ("b-0", ["1::1", "2::0"], "amd.com/gpu.shared"),
+                          ("c-0", ["3"], "amd.com/gpu")):
+        c = resp.pod_resources.add(name=pod, namespace="ml").containers.add(name="main")
+        c.devices.add(resource_name=res, device_ids=ids)
+    srv = pr.serve_fake(sock, resp)
+    try:
+        own = pr.gpu_owners(sock)
+        assert own == {"1": [("ml", "a-0", "main"), ("ml", "b-0", "main")],
+                       "2": [("ml", "b-0", "main")], "3": [("ml", "c-0", "main")]}
+        g = gpus8()
+        text = render_metrics(g, FakeBackend(g).samples(), FakeBackend(g).health, own, "", {}, 0.0)
+        info = [l for l in text.splitlines() if l.startswith('amd_gpu_pod_info{gpu="1"')]
+        assert len(info) == 2 and 'pod="a-0"' in info[0] and 'pod="b-0"' in info[1]
+        assert [l for l in text.splitlines() if l.startswith('amd_gpu_pods{gpu="1"')][0].endswith(" 2")
+        # shared GPU: no single pod label on its series; exclusive GPU: labelled
+        util1 = [l for l in text.splitlines() if l.startswith('amd_gpu_utilization_percent{gpu="1"')][0]
+        assert "pod=" not in util1
+        util2 = [l for l in text.splitlines() if l.startswith('amd_gpu_utilization_percent{gpu="2"')][0]
+        assert 'pod="b-0"' in util2
+    finally:
+        srv.stop(0)
+
+
+def test_pod_uid_from_cgroup(tmp_path):
+    from mxk8s.exporter import pod_uid_of
+    (tmp_path / "42").mkdir()
+    (tmp_path / "42" / "cgroup").write_text(
+        "0::/kubepods.slice/kubepods-besteffort.slice/"
+        "kubepods-besteffort-pod3f2c8a1e_5b7d_4c1a_9e0f_2a6b8c4d1e7f.slice/"
+        "cri-containerd-0123abcd.scope\n")
+    assert pod_uid_of(42, str(tmp_path)) == "3f2c8a1e-5b7d-4c1a-9e0f-2a6b8c4d1e7f"
+    (tmp_path / "43").mkdir()
+    (tmp_path / "43" / "cgroup").write_text(
+        "12:memory:/kubepods/burstable/pod0b1c2d3e-aaaa-bbbb-cccc-0123456789ab/deadbeef\n")
+    assert pod_uid_of(43, str(tmp_path)) == "0b1c2d3e-aaaa-bbbb-cccc-0123456789ab"
+    assert pod_uid_of(44, str(tmp_path)) is None
