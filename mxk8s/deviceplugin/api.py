@@ -5,7 +5,8 @@ The schema reproduces ``k8s.io/kubelet/pkg/apis/deviceplugin/v1beta1/api.proto``
 wire bytes are what the kubelet sends and expects.  The descriptors are
 assembled with ``descriptor_pb2`` into a private pool and the message classes
 are generated from it; gRPC handlers/stubs are wired with explicit
-(de)serializers.  ``tests/test_deviceplugin_api.py`` pins golden wire bytes.
+(de)serializers.  ``tests/test_deviceplugin.py::test_golden_wire_bytes`` pins the
+golden wire bytes.
 
 This replaces the Go device plugin inside the reference's GPU Operator
 (/root/reference/README.md:264-272).

@@ -45,6 +45,15 @@
 //   8 w4j   variant 6 with plain (temporal) widened stores
 //   9 x2    the layout kernel of gemm_bf16_layouts.hip (same schedule as 6,
 //           inline-asm LDS-DMA with the LDS address bound to M0)
+//  10 DIAG  variant 6 without the C store tail (timing ablation only)
+//  11 w4ip  persistent, schedule 6, plain (temporal) widened stores
+//  12 w4ip  persistent, schedule 6, non-temporal widened stores
+//  13 w4j   schedule 6 with every B piece before the stage wait (vmcnt 16)
+//  14 w4j   schedule 6 with the next-k0 reads spread over odd m 93..123
+//  15 w4j   schedule 6, B fragment as the outer MFMA loop
+//  16 w4j   schedule 6 under s_setprio 1
+//  17 w4j   schedule 6, K loop rotated per XCD (different K-slices per XCD)
+//  18 w4j   schedule 6, K loop rotated per workgroup
 // The earlier schedules (one-barrier w4b, 8-wave, 4-deep ring, w4h, ...)
 // were retired when an ISA audit (tests/test_isa_hazards.py) found their
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
@@ -206,7 +215,7 @@ using mxk::SchedTwoBarrier;
 
 // Table-driven K-tile: S gives, per MFMA index m, the fragment reads, DMA
 // pieces, waits and barriers that follow MFMA m (see w4i_ktile for MODE).
-template <class S, int PAR, int MODE>
+template <class S, int PAR, int MODE, int ORDER = 0, int PRIO = 0>
 __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                           bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                           bf16x8_t (&f1b)[8], char* smem, int a_base, int b_base,
@@ -216,13 +225,16 @@ __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
   const int px = PAR == 2 ? par : PAR;
   char* X = smem + px * W4B_STAGE_BYTES;
   char* Y = smem + (px ^ 1) * W4B_STAGE_BYTES;
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int o = 0; o < 8; ++o) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = h * 64 + i * 8 + j;
+      for (int q = 0; q < 8; ++q) {
+        const int m = h * 64 + o * 8 + q;
+        // ORDER 0: A fragment outer (consecutive MFMAs share srcB); 1: B outer
+        const int i = ORDER ? q : o, j = ORDER ? o : q;
         if (h == 0) mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
         else mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
         if (S::a1(m) >= 0) f1a[S::a1(m)] = lds_read_b128(X + a_base + S::a1(m) * SUB + off_k1);
@@ -247,6 +259,7 @@ __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
       }
     }
   }
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 using mxk::store_block_wide;
@@ -263,6 +276,18 @@ __device__ __forceinline__ void ktile_sched(f32x4_t (&acc)[8][8], bf16x8_t (&f0a
   if constexpr (SCHED == 1)
     w4j_ktile<SchedHB, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
                                   dma_a, dma_b, kb2, wave_s, par);
+  else if constexpr (SCHED == 3)
+    w4j_ktile<mxk::SchedEarlyB, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,
+                                           off_k1, dma_a, dma_b, kb2, wave_s, par);
+  else if constexpr (SCHED == 4)
+    w4j_ktile<mxk::SchedSpreadK0, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,
+                                             off_k1, dma_a, dma_b, kb2, wave_s, par);
+  else if constexpr (SCHED == 5)   // SchedHB, B fragment outer
+    w4j_ktile<SchedHB, PAR, MODE, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                     dma_a, dma_b, kb2, wave_s, par);
+  else if constexpr (SCHED == 6)   // SchedHB with raised wave priority
+    w4j_ktile<SchedHB, PAR, MODE, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,
+                                        off_k1, dma_a, dma_b, kb2, wave_s, par);
   else if constexpr (SCHED == 2)
     w4j_ktile<SchedTwoBarrier, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,
                                           off_k1, dma_a, dma_b, kb2, wave_s, par);
@@ -271,7 +296,7 @@ __device__ __forceinline__ void ktile_sched(f32x4_t (&acc)[8][8], bf16x8_t (&f0a
                                    dma_a, dma_b, kb2, wave_s, par);
 }
 
-template <int MAP, int EPI, int LATE = 0, int R1 = 0, int SCHED = 0>
+template <int MAP, int EPI, int LATE = 0, int R1 = 0, int SCHED = 0, int ROT = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -301,16 +326,30 @@ mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict_
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int ns = K / BK;
+  // ROT 1: the K loop starts at K-tile (xcd * ns / 8) and wraps, so the eight
+  // XCDs stream different K-slices at any moment (spreads the HBM / MALL
+  // channels a lockstep K sweep piles onto); ROT 2: a per-workgroup start.
+  // The DMA stage offset is wrapped modulo the K extent in bytes.
+  const int kbytes = K * 2;
+  int rot = 0;
+  if constexpr (ROT == 1) rot = ((blockIdx.x & 7) * ns / 8) * BK * 2;
+  else if constexpr (ROT == 2) rot = ((blockIdx.x * 37) % ns) * BK * 2;
+  rot = __builtin_amdgcn_readfirstlane(rot);
+  auto wrap = [&](int kb) {
+    if constexpr (ROT == 0) return kb;
+    const int r = kb + rot;
+    return r >= kbytes ? r - kbytes : r;
+  };
 #pragma unroll
-  for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+  for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, wrap(0), wave_s);
 #pragma unroll
-  for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_OP_BYTES, p, 0, wave_s);
+  for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_OP_BYTES, p, wrap(0), wave_s);
   if (ns > 1) {
 #pragma unroll
-    for (int p = 0; p < 8; ++p) dma_a.issue(smem + W4B_STAGE_BYTES, p, BK * 2, wave_s);
+    for (int p = 0; p < 8; ++p) dma_a.issue(smem + W4B_STAGE_BYTES, p, wrap(BK * 2), wave_s);
 #pragma unroll
     for (int p = 0; p < 8; ++p)
-      dma_b.issue(smem + W4B_STAGE_BYTES + W4B_OP_BYTES, p, BK * 2, wave_s);
+      dma_b.issue(smem + W4B_STAGE_BYTES + W4B_OP_BYTES, p, wrap(BK * 2), wave_s);
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -329,14 +368,14 @@ mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   int kb = 2 * BK * 2;
   for (; s + 2 <= ns - 2; s += 2) {
     ktile_sched<SCHED, 0, 1, LATE, R1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                          dma_b, kb, wave_s);
+                          dma_b, wrap(kb), wave_s);
     ktile_sched<SCHED, 1, 1, LATE, R1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                          dma_b, kb + BK * 2, wave_s);
+                          dma_b, wrap(kb + BK * 2), wave_s);
     kb += 2 * BK * 2;
   }
   if (s < ns - 2) {   // s even
     ktile_sched<SCHED, 0, 1, LATE, R1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                          dma_b, kb, wave_s);
+                          dma_b, wrap(kb), wave_s);
     ++s;
   }
   // the last two K-tiles (or the only one): no DMA
@@ -352,7 +391,11 @@ mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 
   if constexpr (EPI == 1) store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else if constexpr (EPI == 2) store_block_wide<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
-  else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+  else if constexpr (EPI == 3) {
+    // DIAGNOSTIC ONLY (ablation variant 10): one lane per wave stores one value,
+    // so the timing shows what the C store tail costs; the output is NOT C
+    if (lane == 0) C[static_cast<size_t>(m0 + wm * 128) * ldc + n0 + wn * 128] = mxk::f2bf(acc[0][0][0]);
+  } else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -364,7 +407,7 @@ mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 // are outstanding, vmcnt(48) retires exactly stage 0 (16 pieces + 32 stores
 // -> vmcnt(32) when K has a single stage).  Every wave runs the same trip
 // count, so all reach every barrier and leave the loop together.
-template <int MAP, int EPI>
+template <int MAP, int EPI, int SCHED = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4ip(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                       uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -432,24 +475,24 @@ mxk_gemm_bf16_tn_w4ip(const uint16_t* __restrict__ A, const uint16_t* __restrict
     int s = 0;
     int kb = 2 * BK * 2;
     for (; s + 2 <= ns - 2; s += 2) {
-      w4i_ktile<0, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                         dma_b, kb, wave_s);
-      w4i_ktile<1, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                         dma_b, kb + BK * 2, wave_s);
+      ktile_sched<SCHED, 0, 1, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                     dma_a, dma_b, kb, wave_s);
+      ktile_sched<SCHED, 1, 1, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                     dma_a, dma_b, kb + BK * 2, wave_s);
       kb += 2 * BK * 2;
     }
     if (s < ns - 2) {
-      w4i_ktile<0, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                         dma_b, kb, wave_s);
+      ktile_sched<SCHED, 0, 1, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                     dma_a, dma_b, kb, wave_s);
       ++s;
     }
     if (ns >= 2) {
-      w4i_ktile<2, 2, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                         dma_b, 0, wave_s, s & 1);
+      ktile_sched<SCHED, 2, 2, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                     dma_a, dma_b, 0, wave_s, s & 1);
       ++s;
     }
-    w4i_ktile<2, 3, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                       dma_b, 0, wave_s, s & 1);
+    ktile_sched<SCHED, 2, 3, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                   dma_a, dma_b, 0, wave_s, s & 1);
     // every wave's LDS reads retired (and no DMA is in flight): LDS is free
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
@@ -545,12 +588,13 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                                      int variant, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 10;
+constexpr int kNumVariants = 19;
 constexpr int kDefaultVariant = 6;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
     "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar",
-    "w4j_hb_st", "x2_hb"};
+    "w4j_hb_st", "x2_hb", "diag_nostore", "w4ip_hb_st", "w4ip_hb_nt", "w4j_earlyb",
+    "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -565,10 +609,10 @@ int num_cus() {
   return cus;
 }
 
-template <int MAP, int EPI, int LATE, int R1 = 0, int SCHED = 0>
+template <int MAP, int EPI, int LATE, int R1 = 0, int SCHED = 0, int ROT = 0>
 void launch_w4i(int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b, uint16_t* c,
                 int M, int N, int K, int lda, int ldb, int ldc) {
-  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4i<MAP, EPI, LATE, R1, SCHED>), dim3(nwg), dim3(W4_THREADS),
+  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4i<MAP, EPI, LATE, R1, SCHED, ROT>), dim3(nwg), dim3(W4_THREADS),
                      0, stream, a, b, c, M, N, K, lda, ldb, ldc);
 }
 
@@ -596,6 +640,24 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
       // the layout kernel (gemm_bf16_layouts.hip) on K-major operands
       mxk_gemm_bf16_ex_variant(A, Bt, C, M, N, K, lda, ldb, ldc, 1, 1, 2, stream);
       break;
+    case 10: launch_w4i<1, 3, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 13: launch_w4i<1, 2, 1, 0, 3>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 14: launch_w4i<1, 2, 1, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 15: launch_w4i<1, 2, 1, 0, 5>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 16: launch_w4i<1, 2, 1, 0, 6>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 17: launch_w4i<1, 2, 1, 0, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 18: launch_w4i<1, 2, 1, 0, 1, 2>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 11:
+    case 12: {
+      const int grid = nwg < num_cus() ? nwg : num_cus();
+      if (v == 11)
+        hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4ip<1, 1, 1>), dim3(grid), dim3(W4_THREADS), 0, stream,
+                           a, b, c, M, N, K, lda, ldb, ldc);
+      else
+        hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4ip<1, 2, 1>), dim3(grid), dim3(W4_THREADS), 0, stream,
+                           a, b, c, M, N, K, lda, ldb, ldc);
+      break;
+    }
   }
 }
 
@@ -619,8 +681,8 @@ MXK_API int mxk_gemm_bf16_tn_num_variants(void) { return kNumVariants; }
 MXK_API const char* mxk_gemm_bf16_tn_variant_name(int variant) {
   return variant >= 0 && variant < kNumVariants ? kVariantNames[variant] : nullptr;
 }
-// No schedule is a timing ablation any more (kept for the validator's API).
-MXK_API int mxk_gemm_bf16_tn_is_ablation(int variant) { return 0; }
+// Variant 10 is a timing ablation (no C store): never correctness-checked or used.
+MXK_API int mxk_gemm_bf16_tn_is_ablation(int variant) { return variant == 10; }
 
 MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,
                              int lda, int ldb, int ldc, hipStream_t stream) {

@@ -301,6 +301,24 @@ struct SchedHB {
   }
 };
 
+// SCHED 3 ("HB-earlyB"): SchedHB with every B piece of stage s+2 issued
+// before the stage-(s+1) wait (59..80 every 3), so that wait covers only
+// pieces issued a full K-tile earlier: vmcnt(16).
+struct SchedEarlyB : SchedHB {
+  static constexpr int VM3 = 16;
+  __host__ __device__ static constexpr int bdma(int m) {
+    return m >= 59 && m <= 80 && (m - 59) % 3 == 0 ? (m - 59) / 3 : -1;
+  }
+};
+
+// SCHED 4 ("HB-spread"): SchedHB with the 16 next-k0 fragment reads spread
+// one per two MFMAs (odd m 93..123) instead of front-loaded.
+struct SchedSpreadK0 : SchedHB {
+  __host__ __device__ static constexpr int k0(int m) {
+    return m >= 93 && m <= 123 && (m & 1) ? (m - 93) >> 1 : -1;
+  }
+};
+
 // SCHED 2: two barriers per K-tile — all k-half-1 fragments (A at even m
 // 0..14, B at even m 16..30) retire before ONE barrier after m 35, then the
 // 16 pieces of stage s+2 go out interleaved (A at 36 + 6p, B at 39 + 6p);

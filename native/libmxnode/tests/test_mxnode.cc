@@ -2,6 +2,7 @@
 // Built with -fsanitize=address,undefined by `make test-native`.
 //   test_mxnode <fixtures/sysfs dir>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <string>
@@ -118,6 +119,51 @@ static void test_health(const std::string& fx) {
   CHECK(std::strcmp(mx_health_reason(MX_UNHEALTHY_NO_RENDER_NODE), "render node missing") == 0);
 }
 
+static void test_monitor(const std::string& fx) {
+  const std::string root = fx + "/mi355x_8gpu";
+  char tmpl[] = "/tmp/mxhmXXXXXX";
+  const std::string dir = mkdtemp(tmpl) ? tmpl : "/tmp";
+  const std::string fault = dir + "/faults";
+  { FILE* f = std::fopen(fault.c_str(), "w"); std::fclose(f); }
+  mx_health_opts o{};
+  o.root = root.c_str();
+  o.fault_file = fault.c_str();
+  o.state_dir = dir.c_str();
+  o.event_quarantine_ms = 1000;
+  o.ecc_quarantine_ms = 0;
+  o.use_smi = 0;
+  char err[256] = {0};
+  mx_health_monitor* m = mx_hm_create(&o, err, sizeof err);
+  CHECK(m != nullptr);
+  if (!m) return;
+  CHECK(mx_hm_smi_active(m) == 0);
+  CHECK(mx_hm_step(m, 0) == 0);
+  mx_health_status st[MX_MAX_GPUS];
+  CHECK(mx_hm_status(m, st, MX_MAX_GPUS) == 8);
+  for (int i = 0; i < 8; ++i) CHECK(st[i].code == MX_HEALTHY && st[i].smi_index == -1);
+  { FILE* f = std::fopen(fault.c_str(), "w"); std::fputs("6\n", f); std::fclose(f); }
+  CHECK(mx_hm_step(m, 0) == 1);
+  mx_hm_status(m, st, MX_MAX_GPUS);
+  CHECK(st[6].code == MX_UNHEALTHY_FAULT_INJECTED && st[5].code == MX_HEALTHY);
+  mx_health_event ev[16];
+  const int ne = mx_hm_events(m, 0, ev, 16);
+  CHECK(ne == 1 && ev[0].kind == MX_EVT_HEALTH_CHANGE && ev[0].index == 6 &&
+        ev[0].value == MX_UNHEALTHY_FAULT_INJECTED);
+  CHECK(mx_hm_events(m, ev[0].seq, ev, 16) == 0);
+  const std::string state = dir + "/health.json";
+  CHECK(mx_hm_write_state(m, state.c_str()) == 0);
+  std::string text;
+  { FILE* f = std::fopen(state.c_str(), "r"); char b[8192]; size_t k = std::fread(b, 1, sizeof b, f); std::fclose(f); text.assign(b, k); }
+  CHECK(text.find("\"index\":6,\"bdf\":\"0000:e5:00.0\"") != std::string::npos);
+  CHECK(text.find("\"reason\":\"fault injected\"") != std::string::npos);
+  { FILE* f = std::fopen(fault.c_str(), "w"); std::fclose(f); }
+  CHECK(mx_hm_step(m, 0) == 1);
+  mx_hm_status(m, st, MX_MAX_GPUS);
+  CHECK(st[6].code == MX_HEALTHY);
+  mx_hm_destroy(m);
+  CHECK(mx_hm_create(nullptr, err, sizeof err) == nullptr);
+}
+
 int main(int argc, char** argv) {
   const std::string fx = argc > 1 ? argv[1] : "tests/fixtures/sysfs";
   test_enumerate(fx);
@@ -125,6 +171,7 @@ int main(int argc, char** argv) {
   test_cdi(fx);
   test_alloc(fx);
   test_health(fx);
+  test_monitor(fx);
   if (failures) {
     std::fprintf(stderr, "%d check(s) failed\n", failures);
     return 1;

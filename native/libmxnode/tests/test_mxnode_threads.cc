@@ -107,6 +107,32 @@ int main(int argc, char** argv) {
   CHECK(!b.cdi.empty());
   std::vector<std::thread> ts;
   for (int t = 0; t < 8; ++t) ts.emplace_back(worker, std::cref(root), std::cref(b), t, 200);
+  // the N02 monitor: the plugin's health thread steps it while gRPC threads
+  // and the state writer read it
+  mx_health_opts o{};
+  o.root = root.c_str();
+  o.event_quarantine_ms = 100;
+  char err[256];
+  mx_health_monitor* m = mx_hm_create(&o, err, sizeof err);
+  CHECK(m != nullptr);
+  std::atomic<bool> stop{false};
+  std::thread stepper([&] { for (int i = 0; i < 200; ++i) CHECK(mx_hm_step(m, 0) >= 0); stop = true; });
+  std::vector<std::thread> readers;
+  for (int t = 0; t < 3; ++t)
+    readers.emplace_back([&, t] {
+      mx_health_status st[MX_MAX_GPUS];
+      mx_health_event ev[8];
+      const std::string path = "/tmp/mxk_tsan_health_" + std::to_string(t) + ".json";
+      while (!stop) {
+        CHECK(mx_hm_status(m, st, MX_MAX_GPUS) == 8);
+        CHECK(mx_hm_events(m, 0, ev, 8) >= 0);
+        CHECK(mx_hm_write_state(m, path.c_str()) == 0);
+      }
+      std::remove(path.c_str());
+    });
+  stepper.join();
+  for (auto& t : readers) t.join();
+  mx_hm_destroy(m);
   for (auto& t : ts) t.join();
   if (failures.load()) {
     std::fprintf(stderr, "%d failures\n", failures.load());

@@ -18,11 +18,18 @@
 //   busbw = algbw * (n-1)/n     (reduce-scatter, all-gather, all-to-all)
 // (n = 1: busbw = 0 by definition; the RESULT keeps algbw.)
 // Correctness: rank r contributes (r+1) everywhere; sums must equal
-// n(n+1)/2, gathered / exchanged chunk j must equal j+1.
+// n(n+1)/2, gathered / exchanged chunk j must equal j+1 — checked over the
+// WHOLE receive buffer by a device kernel that counts mismatches.
+// Multi-process: the ncclUniqueId file carries a per-job nonce
+// (MXK_RUN_NONCE, else TORCHELASTIC_RUN_ID:MASTER_PORT); rank 0 deletes any
+// old file first and the other ranks ignore a file whose nonce is not theirs,
+// so a stale id from an earlier run can neither hang nor mis-wire this one.
+// Times are max-reduced over ranks (ncclMax) before they are reported.
 //
 //   mx-allreduce-perf [-b 8] [-e 8G] [-f 2] [-g N] [--scaling 1,2,4,8]
 //                     [--op allreduce|reducescatter|allgather|alltoall|all]
 //                     [--dtype float|bf16] [--iters 20] [--warmup 5] [--id-file F]
+//                     [--nonce S]
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -39,6 +46,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 namespace {
 
@@ -111,22 +120,39 @@ struct Opts {
   bool bf16 = false;
   int iters = 20, warmup = 5;
   std::string id_file;
+  std::string nonce;
   size_t esz() const { return bf16 ? 2 : 4; }
   ncclDataType_t dt() const { return bf16 ? ncclBfloat16 : ncclFloat; }
 };
 
-float read_elem(const void* dptr, size_t idx, bool bf16) {
-  if (bf16) {
-    uint16_t h = 0;
-    CHECK_HIP(hipMemcpy(&h, static_cast<const uint16_t*>(dptr) + idx, 2, hipMemcpyDeviceToHost));
-    uint32_t u = uint32_t(h) << 16;
-    float f;
-    std::memcpy(&f, &u, 4);
-    return f;
+// Mismatch count over the whole receive buffer: element i must equal `sum`
+// (chunk == 0: reductions) or (i / chunk) + 1 (gather / all-to-all).
+__global__ void count_mismatch(const void* p, size_t n, size_t chunk, float sum, int is_bf16,
+                               unsigned long long* bad) {
+  unsigned long long local = 0;
+  for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+    const float want = chunk ? float(i / chunk + 1) : sum;
+    const float got = is_bf16 ? __uint_as_float(uint32_t(static_cast<const uint16_t*>(p)[i]) << 16)
+                              : static_cast<const float*>(p)[i];
+    local += got != want;
   }
-  float f = 0;
-  CHECK_HIP(hipMemcpy(&f, static_cast<const float*>(dptr) + idx, 4, hipMemcpyDeviceToHost));
-  return f;
+  if (local) atomicAdd(bad, local);
+}
+
+unsigned long long mismatches(Op op, const void* rb, size_t recv, size_t count, int n, bool bf16,
+                              hipStream_t st) {
+  unsigned long long* d = nullptr;
+  unsigned long long h = 0;
+  CHECK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(h), st));
+  CHECK_HIP(hipMemsetAsync(d, 0, sizeof(h), st));
+  const size_t chunk = (op == Op::AllReduce || op == Op::ReduceScatter) ? 0 : count;
+  hipLaunchKernelGGL(count_mismatch, dim3(1024), dim3(256), 0, st, rb, recv, chunk,
+                     n * (n + 1) / 2.0f, int(bf16), d);
+  CHECK_HIP(hipGetLastError());
+  CHECK_HIP(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, st));
+  CHECK_HIP(hipFreeAsync(d, st));
+  CHECK_HIP(hipStreamSynchronize(st));
+  return h;
 }
 
 int iters_for(size_t bytes, int base) {
@@ -163,16 +189,9 @@ void issue(Op op, const void* sb, void* rb, const Shape& s, ncclDataType_t dt, n
   }
 }
 
-// Sampled correctness check of one rank's receive buffer.
-bool check_recv(Op op, const void* rb, const Shape& s, int n, bool bf16) {
-  const float sum = n * (n + 1) / 2.0f;
-  if (op == Op::AllReduce || op == Op::ReduceScatter)
-    return read_elem(rb, 0, bf16) == sum && read_elem(rb, s.recv - 1, bf16) == sum;
-  for (int j = 0; j < n; ++j) {   // chunk j came from rank j, which sent (j+1)
-    if (read_elem(rb, j * s.count, bf16) != float(j + 1)) return false;
-    if (read_elem(rb, j * s.count + s.count - 1, bf16) != float(j + 1)) return false;
-  }
-  return true;
+// Whole-buffer correctness check of one rank's receive buffer.
+bool check_recv(Op op, const void* rb, const Shape& s, int n, bool bf16, hipStream_t st) {
+  return mismatches(op, rb, s.recv, s.count, n, bf16, st) == 0;
 }
 
 void print_point(Op op, int n, const char* mode, size_t bytes, const Opts& o, double t, bool good) {
@@ -234,7 +253,7 @@ bool sweep_single(const Opts& o, Op op, int n, double* peak_busbw) {
     bool good = true;
     for (int g = 0; g < n; ++g) {
       CHECK_HIP(hipSetDevice(g));
-      good &= check_recv(op, rb[g], s, n, o.bf16);
+      good &= check_recv(op, rb[g], s, n, o.bf16, st[g]);
     }
     ok &= good;
     const size_t sbytes = std::max(s.send, s.recv) * esz;
@@ -255,25 +274,79 @@ bool sweep_single(const Opts& o, Op op, int n, double* peak_busbw) {
 // -------------------------------------------------------------------------
 // one process per GPU (torchrun env); unique id through a shared file
 // -------------------------------------------------------------------------
+// Per-job nonce that binds the id file to this launch.
+std::string run_nonce() {
+  if (const char* n = std::getenv("MXK_RUN_NONCE")) return n;
+  const char* run = std::getenv("TORCHELASTIC_RUN_ID");
+  const char* port = std::getenv("MASTER_PORT");
+  if (!run && !port) return "";
+  return std::string(run ? run : "") + ":" + (port ? port : "");
+}
+
+constexpr char kIdMagic[8] = {'M', 'X', 'K', 'N', 'C', 'C', 'L', '1'};
+
+// Rank 0 publishes (magic, nonce, id) atomically after removing any old file;
+// the other ranks wait for a file whose magic and nonce match.
+bool exchange_id(const std::string& path, const std::string& nonce, int rank, ncclUniqueId* id) {
+  if (rank == 0) {
+    std::remove(path.c_str());
+    CHECK_NCCL(ncclGetUniqueId(id));
+    const std::string tmp = path + ".tmp." + std::to_string(::getpid());
+    {
+      std::ofstream f(tmp, std::ios::binary);
+      const uint32_t len = static_cast<uint32_t>(nonce.size());
+      f.write(kIdMagic, sizeof(kIdMagic));
+      f.write(reinterpret_cast<const char*>(&len), sizeof(len));
+      f.write(nonce.data(), len);
+      f.write(reinterpret_cast<const char*>(id), sizeof(*id));
+      if (!f) return false;
+    }
+    return std::rename(tmp.c_str(), path.c_str()) == 0;
+  }
+  const char* ws = std::getenv("MXK_ID_WAIT_S");
+  const int polls = (ws ? std::max(1, std::atoi(ws)) : 60) * 100;
+  for (int i = 0; i <= polls; ++i) {   // 10 ms polls
+    std::ifstream f(path, std::ios::binary);
+    char magic[8];
+    uint32_t len = 0;
+    if (f && f.read(magic, 8) && !std::memcmp(magic, kIdMagic, 8) &&
+        f.read(reinterpret_cast<char*>(&len), sizeof(len)) && len < 4096) {
+      std::string got(len, '\0');
+      if (f.read(&got[0], len) && got == nonce &&
+          f.read(reinterpret_cast<char*>(id), sizeof(*id)))
+        return true;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
+  std::fprintf(stderr, "rank %d: timed out waiting for %s with nonce '%s'\n", rank, path.c_str(),
+               nonce.c_str());
+  return false;
+}
+
+// Slowest rank's time (every rank gets it).
+double max_over_ranks(double t, ncclComm_t comm, hipStream_t st) {
+  double* d = nullptr;
+  CHECK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(double), st));
+  CHECK_HIP(hipMemcpyAsync(d, &t, sizeof(double), hipMemcpyHostToDevice, st));
+  CHECK_NCCL(ncclAllReduce(d, d, 1, ncclFloat64, ncclMax, comm, st));
+  CHECK_HIP(hipMemcpyAsync(&t, d, sizeof(double), hipMemcpyDeviceToHost, st));
+  CHECK_HIP(hipFreeAsync(d, st));
+  CHECK_HIP(hipStreamSynchronize(st));
+  return t;
+}
+
 bool sweep_multiproc(const Opts& o, int rank, int world, int local) {
   ncclUniqueId id;
   if (o.id_file.empty()) {
     std::fprintf(stderr, "--id-file is required with WORLD_SIZE > 1\n");
     return false;
   }
-  if (rank == 0) {
-    CHECK_NCCL(ncclGetUniqueId(&id));
-    const std::string tmp = o.id_file + ".tmp";
-    std::ofstream(tmp, std::ios::binary).write(reinterpret_cast<const char*>(&id), sizeof(id));
-    std::rename(tmp.c_str(), o.id_file.c_str());
-  } else {
-    for (int i = 0;; ++i) {
-      std::ifstream f(o.id_file, std::ios::binary);
-      if (f && f.read(reinterpret_cast<char*>(&id), sizeof(id))) break;
-      if (i > 6000) { std::fprintf(stderr, "timed out waiting for %s\n", o.id_file.c_str()); return false; }
-      std::this_thread::sleep_for(std::chrono::milliseconds(10));
-    }
+  const std::string nonce = o.nonce.empty() ? run_nonce() : o.nonce;
+  if (nonce.empty()) {
+    std::fprintf(stderr, "no job nonce: set MXK_RUN_NONCE (or run under torchrun) or --nonce\n");
+    return false;
   }
+  if (!exchange_id(o.id_file, nonce, rank, &id)) return false;
   CHECK_HIP(hipSetDevice(local));
   ncclComm_t comm;
   CHECK_NCCL(ncclCommInitRank(&comm, world, id, rank));
@@ -299,9 +372,21 @@ bool sweep_multiproc(const Opts& o, int rank, int world, int local) {
       auto t0 = std::chrono::steady_clock::now();
       for (int i = 0; i < it; ++i) issue(op, sb, rb, s, o.dt(), comm, st);
       CHECK_HIP(hipStreamSynchronize(st));
-      const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / it;
+      double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / it;
       roctxRangePop();
-      const bool good = check_recv(op, rb, s, world, o.bf16);
+      t = max_over_ranks(t, comm, st);
+      unsigned long long bad = mismatches(op, rb, s.recv, s.count, world, o.bf16, st);
+      // every rank's verdict: total mismatches over the job
+      {
+        unsigned long long* d = nullptr;
+        CHECK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(bad), st));
+        CHECK_HIP(hipMemcpyAsync(d, &bad, sizeof(bad), hipMemcpyHostToDevice, st));
+        CHECK_NCCL(ncclAllReduce(d, d, 1, ncclUint64, ncclSum, comm, st));
+        CHECK_HIP(hipMemcpyAsync(&bad, d, sizeof(bad), hipMemcpyDeviceToHost, st));
+        CHECK_HIP(hipFreeAsync(d, st));
+        CHECK_HIP(hipStreamSynchronize(st));
+      }
+      const bool good = bad == 0;
       ok &= good;
       const size_t sbytes = std::max(s.send, s.recv) * esz;
       peak = std::max(peak, double(sbytes) / t / 1e9 * bus_factor(op, world));
@@ -315,6 +400,7 @@ bool sweep_multiproc(const Opts& o, int rank, int world, int local) {
   CHECK_HIP(hipFree(sb));
   CHECK_HIP(hipFree(rb));
   CHECK_NCCL(ncclCommDestroy(comm));
+  if (rank == 0) std::remove(o.id_file.c_str());
   return ok;
 }
 
@@ -350,6 +436,7 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[i], "--iters") && i + 1 < argc) o.iters = std::max(1, std::atoi(argv[++i]));
     else if (!std::strcmp(argv[i], "--warmup") && i + 1 < argc) o.warmup = std::max(0, std::atoi(argv[++i]));
     else if (!std::strcmp(argv[i], "--id-file") && i + 1 < argc) o.id_file = argv[++i];
+    else if (!std::strcmp(argv[i], "--nonce") && i + 1 < argc) o.nonce = argv[++i];
     else if (!std::strcmp(argv[i], "--op") && i + 1 < argc) {
       if (!parse_ops(argv[++i], &o.ops)) { std::fprintf(stderr, "bad --op %s\n", argv[i]); return 2; }
     } else { std::fprintf(stderr, "unknown argument %s\n", argv[i]); return 2; }

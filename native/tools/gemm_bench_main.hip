@@ -60,6 +60,31 @@ __global__ void diff_norms(const uint16_t* c, const uint16_t* r, size_t n, doubl
   atomicAdd(&out[1], s);
 }
 
+// JSON has no inf / NaN
+std::string json_num(double v) {
+  if (!std::isfinite(v)) return "null";
+  char b[32];
+  std::snprintf(b, sizeof(b), "%.4g", v);
+  return b;
+}
+
+// fp32 reference of one 256x256 block of C = A * B^T (row-major, K-contiguous
+// operands) at (r0, c0), compared with the kernel's bf16 output: max |diff|
+// and max |ref| (atomicMax on the float bits: both are non-negative).
+__global__ void spot_check(const uint16_t* A, const uint16_t* B, const uint16_t* C, int n, int r0,
+                           int c0, unsigned* max_err, unsigned* max_ref) {
+  const int r = r0 + blockIdx.x, c = c0 + threadIdx.x;
+  const uint16_t* a = A + size_t(r) * n;
+  const uint16_t* b = B + size_t(c) * n;
+  float acc = 0.f;
+  for (int k = 0; k < n; ++k)
+    acc = fmaf(__uint_as_float(uint32_t(a[k]) << 16), __uint_as_float(uint32_t(b[k]) << 16), acc);
+  const float got = __uint_as_float(uint32_t(C[size_t(r) * n + c]) << 16);
+  const float err = fabsf(got - acc);
+  atomicMax(max_err, __float_as_uint(err == err ? err : INFINITY));   // NaN -> inf
+  atomicMax(max_ref, __float_as_uint(fabsf(acc)));
+}
+
 struct Opts {
   std::vector<int> sizes{4096, 8192, 16384};
   int iters = 50;
@@ -92,7 +117,36 @@ bool run_device(int dev, const Opts& o) {
     hipLaunchKernelGGL(fill_uniform_bf16, dim3(2048), dim3(256), 0, st, A, elems, 0x1234u + dev);
     hipLaunchKernelGGL(fill_uniform_bf16, dim3(2048), dim3(256), 0, st, B, elems, 0x9876u + dev);
     double rel = -1;
-    mxk_gemm_bf16_tn(A, B, C, n, n, n, n, n, n, st);
+    std::string err_msg;
+    // poison C first: a launch that silently did nothing cannot pass
+    CK(hipMemsetAsync(C, 0xff, elems * 2, st));
+    const char* skip = std::getenv("MXK_GEMM_BENCH_SKIP_KERNEL");   // fault-injection hook
+    int launch_st = 0;
+    if (!(skip && *skip == '1')) launch_st = mxk_gemm_bf16_tn(A, B, C, n, n, n, n, n, n, st);
+    const hipError_t le = hipGetLastError();
+    if (launch_st != 0 || le != hipSuccess)
+      err_msg = std::string("kernel launch failed: ") +
+                hipGetErrorString(launch_st ? static_cast<hipError_t>(launch_st) : le);
+    // fp32 spot check of a random 256x256 block
+    unsigned* dmax = nullptr;
+    unsigned hmax[2] = {0, 0};
+    CK(hipMalloc(&dmax, 8));
+    CK(hipMemsetAsync(dmax, 0, 8, st));
+    const uint32_t h32 = (0x9E3779B1u * uint32_t(n)) ^ (0x85EBCA6Bu * uint32_t(dev + 1));
+    const int blocks = n / 256;
+    const int r0 = int(h32 % uint32_t(blocks)) * 256, c0 = int((h32 >> 16) % uint32_t(blocks)) * 256;
+    hipLaunchKernelGGL(spot_check, dim3(256), dim3(256), 0, st, A, B, C, n, r0, c0, dmax, dmax + 1);
+    CK(hipGetLastError());
+    CK(hipMemcpyAsync(hmax, dmax, 8, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    CK(hipFree(dmax));
+    float max_abs_err, max_ref;
+    std::memcpy(&max_abs_err, &hmax[0], 4);
+    std::memcpy(&max_ref, &hmax[1], 4);
+    const float spot_tol = 0.0078125f * max_ref;   // 2^-7 max|ref|: bf16 output rounding is 2^-8
+    const bool spot_ok = max_ref > 0.f && max_abs_err <= spot_tol;
+    if (err_msg.empty() && !spot_ok)
+      err_msg = max_ref > 0.f ? "fp32 spot check failed" : "fp32 spot check: reference block is zero";
     if (o.ref) {
       CK(hipMalloc(&R, elems * 2));
       const float alpha = 1.f, beta = 0.f;
@@ -111,7 +165,13 @@ bool run_device(int dev, const Opts& o) {
       double h[2];
       CK(hipMemcpyAsync(h, nrm, 16, hipMemcpyDeviceToHost, st));
       CK(hipStreamSynchronize(st));
-      rel = std::sqrt(h[0] / std::max(h[1], 1e-30));
+      if (!(h[1] > 0.0)) {
+        if (err_msg.empty()) err_msg = "rocBLAS reference norm is 0 (reference did not run)";
+        rel = -1;
+      } else {
+        rel = std::sqrt(h[0] / h[1]);
+        if (!(rel == rel) && err_msg.empty()) err_msg = "NaN in the output";
+      }
       CK(hipFree(R));
     }
     // warm-up: clocks settle under load on random data
@@ -143,14 +203,18 @@ bool run_device(int dev, const Opts& o) {
     std::sort(t.begin(), t.end());
     const double med = t[t.size() / 2] * 1e-3;
     const double tflops = 2.0 * n * double(n) * n / med / 1e12;
-    const bool pass = !o.ref || rel < 1e-2;
+    const bool pass = err_msg.empty() && (!o.ref || (rel >= 0 && rel < 1e-2));
     all_ok &= pass;
     {
       std::lock_guard<std::mutex> lk(g_print);
       std::printf("RESULT {\"test\":\"gemm\",\"gpu\":%d,\"M\":%d,\"N\":%d,\"K\":%d,\"dtype\":\"bf16\","
-                  "\"median_ms\":%.4f,\"min_ms\":%.4f,\"tflops\":%.1f,\"rel_err_vs_rocblas\":%.3g,"
-                  "\"pass\":%s}\n",
-                  dev, n, n, n, med * 1e3, t[0], tflops, rel, pass ? "true" : "false");
+                  "\"median_ms\":%.4f,\"min_ms\":%.4f,\"tflops\":%.1f,\"rel_err_vs_rocblas\":%s,"
+                  "\"spot_block\":[%d,%d],\"max_abs_err\":%s,\"spot_tolerance\":%.4g,"
+                  "\"pass\":%s%s%s%s}\n",
+                  dev, n, n, n, med * 1e3, t[0], tflops, json_num(rel).c_str(), r0, c0, json_num(max_abs_err).c_str(),
+                  spot_tol,
+                  pass ? "true" : "false", err_msg.empty() ? "" : ",\"error\":\"",
+                  err_msg.c_str(), err_msg.empty() ? "" : "\"");
       std::fflush(stdout);
     }
     CK(hipEventDestroy(e0));

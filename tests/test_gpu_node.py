@@ -80,6 +80,18 @@ def test_gemm_bench_binary_self_checks():
     r = res[-1]
     assert r["test"] == "gemm" and r["pass"], r
     assert r["tflops"] > 500, r
+    assert 0 < r["max_abs_err"] <= r["spot_tolerance"] and r["rel_err_vs_rocblas"] is not None, r
+
+
+def test_gemm_bench_binary_fails_when_kernel_skipped():
+    """Fault injection: the checked launch is skipped, the poisoned output
+    must fail both the fp32 spot check and the rocBLAS comparison."""
+    env = dict(os.environ, MXK_GEMM_BENCH_SKIP_KERNEL="1")
+    p = subprocess.run([os.path.join(BIN, "mx-gemm-bench"), "--sizes", "1024", "--iters", "3",
+                        "--warmup-ms", "20"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode != 0, p.stdout[-2000:]
+    r = _results(p.stdout)[-1]
+    assert r["pass"] is False and "error" in r, r
 
 
 def test_allreduce_binary_single_gpu():
