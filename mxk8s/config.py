@@ -82,6 +82,8 @@ VALUES: dict = {
                                                maximum=86400 * 30),
                      "reconcileSeconds": F("integer", "GPU-set / CDI-spec resync, 0 = off",
                                            minimum=0, maximum=86400),
+                     "partitionNaming": F("string", "compute-partition resource naming",
+                                          enum=["single", "mixed"]),
                      "sharing": {"timeSlicing": {
                          "replicas": F("integer", "advertise each GPU this many times",
                                        minimum=1, maximum=64),
@@ -90,6 +92,16 @@ VALUES: dict = {
                                                          "refuse requests for >1 replica")}},
                      "privileged": F("boolean"), "priorityClassName": F("string"),
                      "resources": RESOURCES},
+    "partitionManager": {"enabled": F("boolean"),
+                         "interval": F("integer", "seconds", minimum=5, maximum=86400),
+                         "settleTimeout": F("integer", "seconds", minimum=10, maximum=3600),
+                         "profiles": F("object", "profile name -> {compute, memory}",
+                                       items={"type": "object", "additionalProperties": {
+                                           "type": "object", "required": ["compute", "memory"],
+                                           "properties": {
+                                               "compute": {"enum": ["SPX", "DPX", "QPX", "CPX"]},
+                                               "memory": {"enum": ["NPS1", "NPS2", "NPS4"]}}}}),
+                         "resources": RESOURCES},
     "labeller": {"enabled": F("boolean"), "nfdFeatureFile": F("boolean"),
                  "interval": F("integer", "seconds", minimum=10, maximum=86400),
                  "resources": RESOURCES},

@@ -38,6 +38,8 @@ def main(argv=None) -> int:
                    help="CDI spec file to keep in sync with the live render nodes")
     p.add_argument("--reconcile-interval", type=float, default=30.0,
                    help="seconds between GPU-set / CDI-spec reconciliations (0 = off)")
+    p.add_argument("--partition-naming", choices=["single", "mixed"], default="single",
+                   help="compute partitions as <resource> or <resource>-<mode>")
     p.add_argument("--log-format", choices=["json", "text"], default="json")
     a = p.parse_args(argv)
     setup_logging(a.log_format)
@@ -49,7 +51,8 @@ def main(argv=None) -> int:
                        fail_requests_greater_than_one=a.fail_requests_greater_than_one,
                        rename_shared=a.rename_shared, ecc_quarantine_s=a.ecc_quarantine,
                        state_dir=a.state_dir, cdi_spec_path=a.cdi_spec,
-                       reconcile_interval=a.reconcile_interval)
+                       reconcile_interval=a.reconcile_interval,
+                       partition_naming=a.partition_naming)
     if a.fault_file:
         cfg.fault_file = a.fault_file
     run_forever(cfg)

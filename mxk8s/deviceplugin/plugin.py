@@ -57,6 +57,7 @@ log = logging.getLogger("mxk8s.deviceplugin")
 
 RESOURCE_NAME = "amd.com/gpu"
 CDI_KIND = "amd.com/gpu"
+PARTITION_MODES = {2: "dpx", 4: "qpx", 8: "cpx"}   # partitions per device -> compute mode
 
 
 @dataclasses.dataclass
@@ -82,6 +83,20 @@ class PluginConfig:
     state_dir: Optional[str] = None          # ECC baseline + health.json (hostPath /var/lib/mxk8s)
     cdi_spec_path: Optional[str] = None      # reconcile this CDI spec file (None: don't)
     reconcile_interval: float = 30.0
+    # compute partitions (DPX/QPX/CPX): "single" advertises every partition as
+    # <resource_name>; "mixed" advertises <resource_name>-<mode> (e.g.
+    # amd.com/gpu-cpx), the GPU Operator's MIG "mixed strategy" counterpart
+    partition_naming: str = "single"
+
+    def effective_resource(self, gpus) -> str:
+        if self.partition_naming != "mixed" or not gpus:
+            return self.resource_name
+        parts = {g.partitions for g in gpus}
+        if len(parts) != 1 or parts == {1}:
+            return self.resource_name     # SPX, or heterogeneous: plain name
+        mode = PARTITION_MODES.get(parts.pop(), "xpx")
+        base, dot, shared = self.resource_name.partition(".shared")
+        return f"{base}-{mode}{dot}{shared}"
 
     def __post_init__(self):
         if self.replicas < 1:
@@ -176,6 +191,7 @@ class AmdGpuDevicePlugin:
                  gpus: Optional[list[node.GpuInfo]] = None):
         self.cfg = config or PluginConfig()
         self.gpus = gpus if gpus is not None else node.enumerate_gpus(self.cfg.sysfs_root)
+        self.resource_name = self.cfg.effective_resource(self.gpus)
         self.state = DeviceState(self.gpus, self.cfg.replicas)
         self._server: Optional[grpc.Server] = None
         self._stop = threading.Event()
@@ -233,7 +249,7 @@ class AmdGpuDevicePlugin:
             if (self.cfg.replicas > 1 and self.cfg.fail_requests_greater_than_one
                     and len(requested) > 1):
                 context.abort(grpc.StatusCode.INVALID_ARGUMENT,
-                              f"time-sliced {self.cfg.resource_name}: request for "
+                              f"time-sliced {self.resource_name}: request for "
                               f"{len(requested)} replicas refused (limit 1 per container)")
             ids: list[str] = []
             for did in requested:
@@ -339,15 +355,24 @@ class AmdGpuDevicePlugin:
         with self._mon_lock:
             mon = self.monitor
         mon.step(wait_ms)
-        by_bdf = {g.bdf: str(g.index) for g in self.state.gpus.values()}
+        # the monitor enumerates the same root: its index i is GPU i (checked
+        # against the BDF; partitions of one device share it)
+        gpus = self.state.gpus
+
+        def dev_of(index: int, bdf: str) -> Optional[str]:
+            g = gpus.get(str(index))
+            return str(index) if g is not None and g.bdf == bdf else None
+
+        status = mon.status()
+        bdf_of = {st.index: st.bdf for st in status}
         for ev in mon.new_events():
-            dev = by_bdf.get(mon_bdf(mon, ev.index)) if ev.index >= 0 else None
+            dev = dev_of(ev.index, bdf_of.get(ev.index, "")) if ev.index >= 0 else None
             level = logging.INFO if ev.kind in (node.EVT_GPU_POST_RESET,
                                                 node.EVT_THERMAL_THROTTLE) else logging.WARNING
             log.log(level, "device %s: %s", dev, ev.message,
                     extra={"device": dev, "event": ev.name, "value": ev.value})
-        for st in mon.status():
-            dev = by_bdf.get(st.bdf)
+        for st in status:
+            dev = dev_of(st.index, st.bdf)
             if dev is None:
                 continue
             if self.state.set_health(dev, st.healthy, st.reason):
@@ -374,6 +399,16 @@ class AmdGpuDevicePlugin:
             self.state.replace_gpus(gpus)
             out["gpus_changed"] = True
             self.reconciles["gpus_changed"] += 1
+            name = self.cfg.effective_resource(gpus)
+            if name != self.resource_name:
+                # a partition-mode change under "mixed" naming: a new resource
+                log.warning("resource %s -> %s after the partition change; re-registering",
+                            self.resource_name, name, extra={"event": "resource_renamed",
+                                                             "resource": name})
+                self.resource_name = name
+                if self.cfg.register:
+                    self.register()
+                out["resource_renamed"] = name
         if self.cfg.cdi_spec_path:
             text = node.cdi_spec_text(self.cfg.sysfs_root, self.cfg.cdi_kind)
             try:
@@ -408,7 +443,7 @@ class AmdGpuDevicePlugin:
         server.start()
         self._server = server
         self._socket_ino = _inode(self.cfg.socket_path)
-        log.info("serving %s on %s (%d GPUs)", self.cfg.resource_name, self.cfg.socket_path,
+        log.info("serving %s on %s (%d GPUs)", self.resource_name, self.cfg.socket_path,
                  len(self.gpus))
 
     def register(self, timeout: float = 10.0) -> None:
@@ -417,13 +452,13 @@ class AmdGpuDevicePlugin:
             stub = api.Stub(ch, "Registration")
             stub.Register(api.RegisterRequest(
                 version=api.API_VERSION, endpoint=self.cfg.socket_name,
-                resource_name=self.cfg.resource_name,
+                resource_name=self.resource_name,
                 options=api.DevicePluginOptions(pre_start_required=False,
                                                 get_preferred_allocation_available=True)),
                 timeout=timeout)
         self.registrations += 1
         self._kubelet_ino = _inode(self.cfg.kubelet_socket)
-        log.info("registered %s with kubelet (%d)", self.cfg.resource_name, self.registrations)
+        log.info("registered %s with kubelet (%d)", self.resource_name, self.registrations)
 
     def start(self) -> "AmdGpuDevicePlugin":
         self.serve()
@@ -488,13 +523,6 @@ class AmdGpuDevicePlugin:
             except Exception:
                 log.exception("re-registration failed; retrying")
                 self._socket_ino = None
-
-
-def mon_bdf(mon: node.HealthMonitor, index: int) -> Optional[str]:
-    for st in mon.status():
-        if st.index == index:
-            return st.bdf
-    return None
 
 
 def _inode(path: str) -> Optional[int]:

@@ -93,16 +93,16 @@ class SmiBackend:
         for i in range(max(0, node.smi_count())):
             s = node.smi_sample(i)
             if s.valid:
-                out[s.bdf] = s
-                self._smi_index[s.bdf] = i
+                out[s.key] = s
+                self._smi_index[s.key] = i
         return out
 
-    def xgmi(self, bdf: str) -> Optional[list]:
-        i = self._smi_index.get(bdf)
+    def xgmi(self, key: str) -> Optional[list]:
+        i = self._smi_index.get(key)
         return None if i is None else node.smi_xgmi_links(i)
 
-    def processes(self, bdf: str) -> list:
-        i = self._smi_index.get(bdf)
+    def processes(self, key: str) -> list:
+        i = self._smi_index.get(key)
         return [] if i is None else node.smi_processes(i)
 
     def health(self, index: int) -> int:
@@ -140,7 +140,8 @@ def load_health_state(path: Optional[str], max_age_s: float = 120.0) -> Optional
         return None
     if time.time() * 1000 - float(doc.get("unix_ms", 0)) > max_age_s * 1000:
         return None
-    return {g["bdf"]: g for g in doc.get("gpus", [])}
+    return {(g["bdf"] if not g.get("partition") else f'{g["bdf"]}#{g["partition"]}'): g
+            for g in doc.get("gpus", [])}
 
 
 def _owner_list(v) -> list:
@@ -161,6 +162,8 @@ def render_metrics(gpus, samples: dict, health: Callable[[int], int], owners: di
         by_gpu.setdefault(l.from_index, []).append(l)
     for g in gpus:
         base = {"gpu": str(g.index), "bdf": g.bdf, "uuid": g.uuid}
+        if g.partitions > 1:
+            base["partition"] = str(g.partition)
         own = _owner_list(owners.get(str(g.index)))
         if len(own) == 1:     # unambiguous: label every series (dcgm-exporter style)
             base.update(namespace=own[0][0], pod=own[0][1], container=own[0][2])
@@ -173,7 +176,7 @@ def render_metrics(gpus, samples: dict, health: Callable[[int], int], owners: di
         w.add("amd_gpu_info", "gauge", "Static GPU facts (value is always 1).", 1,
               {**base, "arch": g.arch, "product": g.product, "device_id": f"0x{g.device_id:04x}",
                "driver_version": driver, "numa_node": str(g.numa_node)})
-        ph = (plugin_health or {}).get(g.bdf)
+        ph = (plugin_health or {}).get(g.key)
         if ph is not None:
             w.add("amd_gpu_device_healthy", "gauge",
                   "1 if the device plugin reports the GPU Healthy in ListAndWatch.",
@@ -202,7 +205,7 @@ def render_metrics(gpus, samples: dict, health: Callable[[int], int], owners: di
                 w.add("amd_gpu_link_max_bandwidth_bytes", "gauge",
                       "Link bandwidth advertised by KFD (bytes/s).",
                       int(l.max_bandwidth_mbps) * 125000, lab)
-        live = xgmi(g.bdf) if xgmi else None
+        live = xgmi(g.key) if xgmi else None
         for x in live or []:
             lab = {**base, "link": str(x.link), "peer_bdf": x.peer_bdf}
             if x.status != "unknown":
@@ -217,14 +220,14 @@ def render_metrics(gpus, samples: dict, health: Callable[[int], int], owners: di
             if x.bit_rate_gbps:
                 w.add("amd_gpu_xgmi_link_bitrate_gbps", "gauge", "Current xGMI link speed (Gb/s).",
                       x.bit_rate_gbps, lab)
-        for pr in (processes(g.bdf) if processes else []):
+        for pr in (processes(g.key) if processes else []):
             lab = {**base, "pid": str(pr.pid), "process": pr.name}
             uid = pod_uid(pr.pid)
             if uid:
                 lab["pod_uid"] = uid
             w.add("amd_gpu_process_memory_bytes", "gauge", "VRAM held by a process (bytes).",
                   pr.vram_bytes, lab)
-        s = samples.get(g.bdf)
+        s = samples.get(g.key)
         if s is None:
             continue
         w.add("amd_gpu_utilization_percent", "gauge", "GFX engine activity (%).", s.gfx_activity_pct, base)

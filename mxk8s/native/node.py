@@ -42,6 +42,7 @@ class _GpuInfo(ctypes.Structure):
         ("unique_id", ctypes.c_uint64), ("hive_id", ctypes.c_uint64),
         ("max_engine_clk_mhz", ctypes.c_uint32), ("num_xgmi_links", ctypes.c_int),
         ("product", ctypes.c_char * 48), ("uuid", ctypes.c_char * 40),
+        ("partition", ctypes.c_int), ("partitions", ctypes.c_int), ("num_xcc", ctypes.c_uint32),
     ]
 
 
@@ -61,7 +62,7 @@ class _Sample(ctypes.Structure):
         ("power_limit_w", ctypes.c_uint32), ("sclk_mhz", ctypes.c_uint32),
         ("mclk_mhz", ctypes.c_uint32), ("ecc_correctable", ctypes.c_uint64),
         ("ecc_uncorrectable", ctypes.c_uint64), ("num_processes", ctypes.c_uint32),
-        ("bdf", ctypes.c_char * 20),
+        ("bdf", ctypes.c_char * 20), ("partition_id", ctypes.c_int),
     ]
 
 
@@ -121,6 +122,14 @@ class GpuInfo:
     xgmi_links: int
     product: str
     uuid: str
+    partition: int = 0          # compute partition of its PCI device (DPX..CPX), 0 in SPX
+    partitions: int = 1         # partitions the PCI device is split into
+    num_xcc: int = 0
+
+    @property
+    def key(self) -> str:
+        """Stable per-device key: the BDF, plus the partition in DPX..CPX mode."""
+        return self.bdf if self.partition == 0 else f"{self.bdf}#{self.partition}"
 
     @property
     def render_path(self) -> str:
@@ -166,6 +175,11 @@ class GpuSample:
     ecc_uncorrectable: int
     num_processes: int
     bdf: str
+    partition_id: int = 0
+
+    @property
+    def key(self) -> str:
+        return self.bdf if self.partition_id == 0 else f"{self.bdf}#{self.partition_id}"
 
 
 class NodeLibraryMissing(RuntimeError):
@@ -259,7 +273,8 @@ def enumerate_gpus(root: Optional[str] = None) -> list[GpuInfo]:
             device_id=g.device_id, bdf=g.pci_bdf.decode(), numa_node=g.numa_node,
             simd_count=g.simd_count, cu_count=g.cu_count, vram_bytes=g.vram_bytes,
             unique_id=g.unique_id, hive_id=g.hive_id, max_sclk_mhz=g.max_engine_clk_mhz,
-            xgmi_links=g.num_xgmi_links, product=g.product.decode(), uuid=g.uuid.decode()))
+            xgmi_links=g.num_xgmi_links, product=g.product.decode(), uuid=g.uuid.decode(),
+            partition=g.partition, partitions=g.partitions, num_xcc=g.num_xcc))
     return out
 
 
@@ -363,7 +378,7 @@ def smi_sample(i: int) -> GpuSample:
                      power_w=s.power_w, power_limit_w=s.power_limit_w, sclk_mhz=s.sclk_mhz,
                      mclk_mhz=s.mclk_mhz, ecc_correctable=s.ecc_correctable,
                      ecc_uncorrectable=s.ecc_uncorrectable, num_processes=s.num_processes,
-                     bdf=s.bdf.decode())
+                     bdf=s.bdf.decode(), partition_id=s.partition_id)
 
 
 def smi_wait_events(timeout_ms: int, max_events: int = 32) -> list[tuple[int, int]]:

@@ -148,12 +148,15 @@ extern "C" mx_health_monitor* mx_hm_create(const mx_health_opts* o, char* err, s
     char serr[256] = {0};
     if (mx_smi_open(serr, sizeof(serr))) {
       m->smi = true;
+      // match amd-smi handles to KFD GPUs by BDF; partitions of one device
+      // share the BDF and pair up by partition id
       const int ns = mx_smi_count();
       for (int k = 0; k < ns; ++k) {
         mx_gpu_sample s;
         mx_smi_sample(k, &s);
         for (auto& g : m->gpus)
-          if (std::strcmp(s.bdf, g.info.pci_bdf) == 0) g.smi_index = k;
+          if (std::strcmp(s.bdf, g.info.pci_bdf) == 0 && s.partition_id == g.info.partition)
+            g.smi_index = k;
       }
     } else {
       m->event(-1, MX_EVT_HEALTH_CHANGE, 0, std::string("amd-smi unavailable: ") + serr);
@@ -309,7 +312,8 @@ extern "C" int mx_hm_write_state(mx_health_monitor* m, const char* path) {
     for (size_t i = 0; i < m->gpus.size(); ++i) {
       const auto& g = m->gpus[i];
       j << (i ? "," : "") << "{\"index\":" << i << ",\"bdf\":\"" << g.info.pci_bdf
-        << "\",\"uuid\":\"" << g.info.uuid << "\",\"healthy\":"
+        << "\",\"partition\":" << g.info.partition << ",\"uuid\":\"" << g.info.uuid
+        << "\",\"healthy\":"
         << (g.code == MX_HEALTHY ? "true" : "false") << ",\"code\":" << g.code
         << ",\"reason\":\"" << mx_health_reason(g.code) << "\",\"ecc_uncorrectable\":"
         << g.ecc_ue << ",\"ecc_baseline\":" << g.ecc_base << ",\"vm_faults\":" << g.vm_faults

@@ -45,7 +45,13 @@ typedef struct mx_gpu_info {
   uint32_t max_engine_clk_mhz;
   int num_xgmi_links;
   char product[48];             // "MI355X", from the device-id table
-  char uuid[40];                // "GPU-<unique_id hex>"
+  char uuid[40];                // "GPU-<unique_id hex>" (+ "-p<k>" for a partition)
+  // Compute partitioning (SPX/DPX/QPX/CPX): in DPX..CPX mode amdgpu exposes
+  // each partition of one PCI device as its own KFD node + render node; they
+  // share the BDF.  partition = 0..partitions-1 in render-minor order.
+  int partition;
+  int partitions;               // KFD nodes sharing this PCI device (1 = SPX)
+  uint32_t num_xcc;             // XCDs in this (partition of the) device
 } mx_gpu_info;
 
 typedef struct mx_link {
@@ -188,6 +194,7 @@ typedef struct mx_gpu_sample {
   uint64_t ecc_uncorrectable;
   uint32_t num_processes;
   char bdf[20];
+  int partition_id;                 // amd-smi BDFID bits 31:28 (0 in SPX mode)
 } mx_gpu_sample;
 
 // 1 if amd-smi could be loaded and initialised, 0 otherwise (msg in err).

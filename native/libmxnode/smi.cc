@@ -174,7 +174,10 @@ extern "C" int mx_smi_sample(int i, mx_gpu_sample* o) {
   SmiApi& a = *g_api;
   amdsmi_processor_handle h = a.gpus[i];
   uint64_t bdf = 0;
-  if (a.amdsmi_get_gpu_bdf_id(h, &bdf) == AMDSMI_STATUS_SUCCESS) fmt_bdf(bdf, o->bdf, sizeof(o->bdf));
+  if (a.amdsmi_get_gpu_bdf_id(h, &bdf) == AMDSMI_STATUS_SUCCESS) {
+    fmt_bdf(bdf, o->bdf, sizeof(o->bdf));
+    o->partition_id = static_cast<int>((bdf >> 28) & 0xf);
+  }
   amdsmi_engine_usage_t u;
   std::memset(&u, 0, sizeof(u));
   if (a.amdsmi_get_gpu_activity(h, &u) == AMDSMI_STATUS_SUCCESS) {

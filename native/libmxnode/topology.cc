@@ -129,6 +129,46 @@ void fill_info(const std::string& root, const RawNode& n, int index, mx_gpu_info
     if (mx::prop_u64(mx::parse_properties(text), "type") == 11) ++xg;
   }
   g->num_xgmi_links = xg;
+  g->num_xcc = static_cast<uint32_t>(mx::prop_u64(p, "num_xcc", 0));
+  g->partition = 0;
+  g->partitions = 1;
+}
+
+// Partitions of one PCI device (shared domain + location_id): number them in
+// render-minor order and make their UUIDs distinct.
+void mark_partitions(const std::string& root, mx_gpu_info* g, int n) {
+  for (int i = 0; i < n; ++i) {
+    int count = 0, rank = 0;
+    for (int j = 0; j < n; ++j) {
+      if (g[j].domain != g[i].domain || g[j].location_id != g[i].location_id) continue;
+      ++count;
+      if (g[j].drm_render_minor < g[i].drm_render_minor ||
+          (g[j].drm_render_minor == g[i].drm_render_minor && j < i))
+        ++rank;
+    }
+    g[i].partitions = count;
+    g[i].partition = rank;
+  }
+  for (int i = 0; i < n; ++i) {
+    if (g[i].partitions <= 1) continue;
+    const size_t len = std::strlen(g[i].uuid);
+    std::snprintf(g[i].uuid + len, sizeof(g[i].uuid) - len, "-p%d", g[i].partition);
+    // each partition has its own DRM card: the PCI device's drm/ directory
+    // lists all of them; pair the k-th card with the k-th render node
+    std::vector<int> cards, renders;
+    for (const std::string& e :
+         mx::list_dir(mx::rooted(root, std::string("/sys/bus/pci/devices/") + g[i].pci_bdf + "/drm"))) {
+      if (e.rfind("card", 0) == 0) cards.push_back(static_cast<int>(std::strtol(e.c_str() + 4, nullptr, 10)));
+      else if (e.rfind("renderD", 0) == 0)
+        renders.push_back(static_cast<int>(std::strtol(e.c_str() + 7, nullptr, 10)));
+    }
+    std::sort(cards.begin(), cards.end());
+    std::sort(renders.begin(), renders.end());
+    g[i].drm_card = -1;
+    if (cards.size() == renders.size())
+      for (size_t k = 0; k < renders.size(); ++k)
+        if (renders[k] == g[i].drm_render_minor) g[i].drm_card = cards[k];
+  }
 }
 
 }  // namespace
@@ -145,14 +185,17 @@ int mx_enumerate(const char* root_c, mx_gpu_info* out, int max, char* err, size_
     mx::set_err(err, errlen, e);
     return -1;
   }
-  int idx = 0;
+  std::vector<mx_gpu_info> all;
   for (const RawNode& n : nodes) {
     if (!is_gpu(n)) continue;
     if (mx::prop_u64(n.props, "vendor_id") != 0x1002) continue;   // AMD only
-    if (out && idx < max) fill_info(root, n, idx, &out[idx]);
-    ++idx;
+    all.emplace_back();
+    fill_info(root, n, static_cast<int>(all.size()) - 1, &all.back());
   }
-  return idx;
+  mark_partitions(root, all.data(), static_cast<int>(all.size()));
+  if (out)
+    for (int i = 0; i < static_cast<int>(all.size()) && i < max; ++i) out[i] = all[i];
+  return static_cast<int>(all.size());
 }
 
 int mx_links(const char* root_c, mx_link* out, int max, char* err, size_t errlen) {

@@ -126,6 +126,50 @@ def tree_8gpu(root: str, missing_render: int | None = None, ngpu: int = 8) -> No
     _w(root, "dev/kfd", "")
 
 
+PARTS = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}
+NPS = {"NPS1": 1, "NPS2": 2, "NPS4": 4}
+
+
+def write_partition_files(root: str, bdf: str, compute: str, memory: str) -> None:
+    pci = f"sys/bus/pci/devices/{bdf}"
+    _w(root, f"{pci}/current_compute_partition", compute + "\n")
+    _w(root, f"{pci}/available_compute_partition", "SPX, DPX, QPX, CPX\n")
+    _w(root, f"{pci}/current_memory_partition", memory + "\n")
+    _w(root, f"{pci}/available_memory_partition", "NPS1, NPS2\n")
+
+
+def tree_partitioned(root: str, compute: str = "CPX", memory: str = "NPS2", ngpu: int = 8) -> None:
+    """An MI355X node in a DPX/QPX/CPX compute mode: every PCI device shows up
+    as `parts` KFD nodes (num_xcc 8/parts, simd_count 1024/parts, the same BDF),
+    each with its own render node and card; local memory split by the NPS mode.
+    The partition sysfs files reflect the modes (tests use this as the state a
+    driver would reach after a partition change)."""
+    parts = PARTS[compute]
+    nodes = list(range(2, 2 + ngpu * parts))
+    cpu_node(root, 0, [(n, 2) for i, n in enumerate(nodes) if i // parts < 4])
+    cpu_node(root, 1, [(n, 2) for i, n in enumerate(nodes) if i // parts >= 4])
+    for gi in range(ngpu):
+        numa = 0 if gi < 4 else 1
+        bdf = MI355X_BDFS[gi]
+        peers = [nodes[pg * parts] for pg in range(ngpu) if pg != gi]
+        for k in range(parts):
+            idx = gi * parts + k
+            n = nodes[idx]
+            gpu_node(root, n, idx, bdf, numa, numa, peers if k == 0 else [])
+            props_path = os.path.join(root, TOPO, str(n), "properties")
+            text = open(props_path).read()
+            text = text.replace("simd_count 1024\n", f"simd_count {1024 // parts}\n")
+            text = text.replace("num_xcc 8\n", f"num_xcc {8 // parts}\n")
+            text = text.replace("array_count 32\n", f"array_count {32 // parts}\n")
+            text = text.replace("hive_id 0\n", f"hive_id {HIVE}\n")   # one hive, every partition
+            open(props_path, "w").write(text)
+            _w(root, f"{TOPO}/{n}/mem_banks/0/properties",
+               _props({"heap_type": 1, "size_in_bytes": VRAM // NPS[memory], "flags": 0,
+                       "width": 8192, "mem_clk_max": 2000}))
+        write_partition_files(root, bdf, compute, memory)
+    _w(root, "dev/kfd", "")
+
+
 def tree_1gpu(root: str) -> None:
     # the 1-GPU container view: one CPU node + the visible GPU at KFD node 8
     cpu_node(root, 1, [(8, 2)])

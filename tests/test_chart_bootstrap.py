@@ -151,6 +151,25 @@ def test_chart_plugin_health_and_reconcile_args():
     assert any(m["name"] == "state" and m.get("readOnly") for m in ec["volumeMounts"])
 
 
+def test_chart_partition_manager():
+    names = {d["metadata"]["name"] for d in _docs(render.load_values())}
+    assert "amd-gpu-stack-partition-manager" not in names          # opt-in, like the MIG manager
+    v = render.load_values(sets=["partitionManager.enabled=true", "devicePlugin.partitionNaming=mixed"])
+    docs = _docs(v)
+    pm = next(d for d in docs if d["metadata"]["name"] == "amd-gpu-stack-partition-manager")
+    c = pm["spec"]["template"]["spec"]["containers"][0]
+    assert c["command"] == ["python3", "-m", "mxk8s.partition"] and c["securityContext"]["privileged"]
+    assert {m["name"] for m in c["volumeMounts"]} >= {"sys", "profiles", "pod-resources"}
+    cm = next(d for d in docs if d["kind"] == "ConfigMap" and "partition" in d["metadata"]["name"])
+    import json as _json
+    assert _json.loads(cm["data"]["profiles.json"])["cpx-nps2"] == {"compute": "CPX", "memory": "NPS2"}
+    dp = next(d for d in docs if d["metadata"]["name"] == "amd-gpu-stack-device-plugin")
+    assert "--partition-naming=mixed" in dp["spec"]["template"]["spec"]["containers"][0]["args"]
+    from mxk8s.config import validate_values
+    assert validate_values(render.load_values(sets=["partitionManager.profiles.x.compute=XPX",
+                                                    "partitionManager.profiles.x.memory=NPS1"]))
+
+
 def test_deploy_files_are_up_to_date():
     """deploy/ must equal what the generators produce (single source of truth)."""
     with open(os.path.join(REPO, "deploy", "amd-gpu-stack.yaml")) as f:
