@@ -96,19 +96,39 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
+class _StdoutToStderr:
+    """RCCL prints a version banner on stdout when a communicator is built;
+    the driver reads rank 0's stdout for the ONE JSON line, so the banner goes
+    to stderr (fd-level: it is written by the C library)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def _init_group(backend, dev, world, rank):
     """Default process group at every N.  At N = 1 a 1-rank group on an
     in-process store: RCCL builds a real 1-rank communicator."""
     import torch.distributed as dist
     from mxk8s.parallel.dist import init_distributed
 
-    if world > 1:
-        init_distributed(backend=backend, device=dev if backend == "nccl" else None)
-    elif not dist.is_initialized():
-        kw = {}
-        if backend == "nccl":
-            kw["device_id"] = dev
-        dist.init_process_group(backend=backend, store=dist.HashStore(), rank=0, world_size=1, **kw)
+    with _StdoutToStderr():
+        if world > 1:
+            init_distributed(backend=backend, device=dev if backend == "nccl" else None)
+        elif not dist.is_initialized():
+            kw = {}
+            if backend == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(backend=backend, store=dist.HashStore(), rank=0, world_size=1,
+                                    **kw)
+        _barrier(dev)     # the communicator exists (and has printed) by now
     return dist.group.WORLD
 
 

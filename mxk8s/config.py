@@ -92,6 +92,9 @@ VALUES: dict = {
                                                          "refuse requests for >1 replica")}},
                      "privileged": F("boolean"), "priorityClassName": F("string"),
                      "resources": RESOURCES},
+    "operator": {"enabled": F("boolean", "GPUStackPolicy operator instead of helm-managed operands"),
+                 "interval": F("integer", "seconds", minimum=5, maximum=86400),
+                 "resources": RESOURCES},
     "partitionManager": {"enabled": F("boolean"),
                          "interval": F("integer", "seconds", minimum=5, maximum=86400),
                          "settleTimeout": F("integer", "seconds", minimum=10, maximum=3600),

@@ -1,13 +1,15 @@
 """Minimal Kubernetes API client (in-cluster service account or kubeconfig
-token), enough for the node labeller and ``mxk8s doctor``: GET and JSON
-merge-PATCH over HTTPS with the cluster CA.  No kubernetes Python package is
-needed (none is installed in the image)."""
+token), enough for the node labeller, the partition manager, the operator and
+``mxk8s doctor``: GET / LIST, POST, PUT, DELETE and JSON merge-PATCH over HTTPS
+with the cluster CA, plus the REST path of any manifest.  No kubernetes Python
+package is needed (none is installed in the image)."""
 from __future__ import annotations
 
 import json
 import os
 import ssl
 import urllib.error
+import urllib.parse
 import urllib.request
 from typing import Optional
 
@@ -73,3 +75,43 @@ class KubeClient:
     def patch_node_labels(self, name: str, labels: dict) -> dict:
         """labels: value None deletes the label (JSON merge patch)."""
         return self.merge_patch(f"/api/v1/nodes/{name}", {"metadata": {"labels": labels}})
+
+    def list(self, path: str, label_selector: Optional[str] = None) -> list:
+        q = "?labelSelector=" + urllib.parse.quote(label_selector) if label_selector else ""
+        return self._req("GET", path + q).get("items", [])
+
+    def create(self, collection: str, obj: dict) -> dict:
+        return self._req("POST", collection, obj)
+
+    def replace(self, path: str, obj: dict) -> dict:
+        return self._req("PUT", path, obj)
+
+    def delete(self, path: str) -> dict:
+        return self._req("DELETE", path)
+
+    def patch_status(self, path: str, status: dict) -> dict:
+        return self.merge_patch(path + "/status", {"status": status})
+
+
+# kinds whose objects are not namespaced (the ones this stack manages)
+CLUSTER_SCOPED = {"Namespace", "Node", "ClusterRole", "ClusterRoleBinding",
+                  "CustomResourceDefinition", "GPUStackPolicy", "RuntimeClass", "PriorityClass"}
+_PLURALS = {"GPUStackPolicy": "gpustackpolicies", "PriorityClass": "priorityclasses"}
+
+
+def plural(kind: str) -> str:
+    return _PLURALS.get(kind, kind.lower() + ("es" if kind.endswith("s") else "s"))
+
+
+def collection_path(api_version: str, kind: str, namespace: Optional[str] = None) -> str:
+    """REST collection path of ``kind`` (namespaced kinds need ``namespace``)."""
+    base = "/api/v1" if api_version == "v1" else f"/apis/{api_version}"
+    if kind in CLUSTER_SCOPED or not namespace:
+        return f"{base}/{plural(kind)}"
+    return f"{base}/namespaces/{namespace}/{plural(kind)}"
+
+
+def object_path(obj: dict, default_namespace: Optional[str] = None) -> str:
+    md = obj.get("metadata", {})
+    ns = None if obj["kind"] in CLUSTER_SCOPED else (md.get("namespace") or default_namespace)
+    return collection_path(obj["apiVersion"], obj["kind"], ns) + "/" + md["name"]

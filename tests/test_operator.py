@@ -1,0 +1,151 @@
+"""GPUStackPolicy operator (ClusterPolicy-controller counterpart) against an
+in-process fake API server: create from the policy, readiness in status,
+drift repair, garbage collection on spec change, invalid specs rejected
+without touching the operands."""
+import copy
+
+import pytest
+import yaml
+
+from mxk8s import operator as op
+from mxk8s.chart import render
+from mxk8s.operator.fake_apiserver import FakeApiServer
+from mxk8s.utils.kube import KubeClient
+
+NS = "amd-gpu"
+DS = f"/apis/apps/v1/namespaces/{NS}/daemonsets"
+POL = op.POLICIES + "/default"
+
+
+@pytest.fixture
+def api():
+    srv = FakeApiServer().start()
+    yield srv
+    srv.stop()
+
+
+def _policy(api, spec=None, name="default"):
+    api.put_object(f"{op.POLICIES}/{name}", {"apiVersion": op.GROUP_VERSION, "kind": op.KIND,
+                                             "metadata": {"name": name}, "spec": spec or {}})
+
+
+def _names(api, prefix):
+    return sorted(p.rsplit("/", 1)[1] for p in api.objects if p.rsplit("/", 1)[0] == prefix)
+
+
+def _ready(api, name, n=1):
+    api.objects[f"{DS}/{name}"]["status"] = {"desiredNumberScheduled": n, "numberReady": n}
+
+
+def test_creates_operands_and_reports_readiness(api):
+    _policy(api)
+    ctl = op.Controller(KubeClient(api.url), NS)
+    r = ctl.reconcile_once()
+    assert _names(api, DS) == ["amd-gpu-stack-device-plugin", "amd-gpu-stack-metrics-exporter",
+                               "amd-gpu-stack-node-labeller"]
+    assert f"/api/v1/namespaces/{NS}/services/amd-gpu-stack-metrics" in api.objects
+    assert f"/apis/batch/v1/namespaces/{NS}/jobs/amd-gpu-stack-validator" in api.objects
+    assert "/apis/rbac.authorization.k8s.io/v1/clusterroles/amd-gpu-stack-node-labeller" in api.objects
+    ds = api.objects[f"{DS}/amd-gpu-stack-device-plugin"]
+    assert ds["metadata"]["labels"][op.MANAGED_BY] == op.MANAGER
+    assert ds["metadata"]["labels"][op.POLICY_LABEL] == "default"
+    assert r.state == "notReady" and len(r.created) >= 8
+    st = api.objects[POL]["status"]
+    assert st["state"] == "notReady" and "device-plugin" in st["message"]
+    # pods come up, the validator Job succeeds -> ready; nothing is re-applied
+    for n in _names(api, DS):
+        _ready(api, n)
+    api.objects[f"/apis/batch/v1/namespaces/{NS}/jobs/amd-gpu-stack-validator"]["status"] = {"succeeded": 1}
+    r = ctl.reconcile_once()
+    assert r.state == "ready" and not (r.created or r.updated or r.deleted), r
+    assert api.objects[POL]["status"]["state"] == "ready"
+    assert all(o["ready"] for o in api.objects[POL]["status"]["operands"])
+    assert api.objects[POL]["status"]["observedGeneration"] == 1
+
+
+def test_repairs_drift_and_recreates_deleted(api):
+    _policy(api)
+    ctl = op.Controller(KubeClient(api.url), NS)
+    ctl.reconcile_once()
+    path = f"{DS}/amd-gpu-stack-device-plugin"
+    live = api.objects[path]
+    good = copy.deepcopy(live["spec"]["template"]["spec"]["containers"][0]["args"])
+    live["spec"]["template"]["spec"]["containers"][0]["args"].append("--replicas=9")
+    del api.objects[f"{DS}/amd-gpu-stack-node-labeller"]
+    r = ctl.reconcile_once()
+    assert "DaemonSet/amd-gpu-stack-device-plugin" in r.updated
+    assert "DaemonSet/amd-gpu-stack-node-labeller" in r.created
+    assert api.objects[path]["spec"]["template"]["spec"]["containers"][0]["args"] == good
+    # server-side additions (defaults, status) are not drift
+    api.objects[path]["spec"]["revisionHistoryLimit"] = 10
+    api.objects[path]["status"] = {"numberReady": 1}
+    assert not ctl.reconcile_once().updated
+
+
+def test_spec_change_reconfigures_and_garbage_collects(api):
+    _policy(api)
+    ctl = op.Controller(KubeClient(api.url), NS)
+    ctl.reconcile_once()
+    api.objects[POL]["spec"] = {"exporter": {"enabled": False},
+                                "devicePlugin": {"sharing": {"timeSlicing": {"replicas": 4}}}}
+    api.objects[POL]["metadata"]["generation"] = 2
+    r = ctl.reconcile_once()
+    assert "DaemonSet/amd-gpu-stack-metrics-exporter" in r.deleted
+    assert "Service/amd-gpu-stack-metrics" in r.deleted
+    assert "amd-gpu-stack-metrics-exporter" not in _names(api, DS)
+    args = api.objects[f"{DS}/amd-gpu-stack-device-plugin"]["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert "--replicas=4" in args
+    assert api.objects[POL]["status"]["observedGeneration"] == 2
+    # objects it did not create are never collected
+    api.put_object(f"{DS}/someone-elses", {"apiVersion": "apps/v1", "kind": "DaemonSet",
+                                           "metadata": {"name": "someone-elses", "namespace": NS}})
+    ctl.reconcile_once()
+    assert f"{DS}/someone-elses" in api.objects
+
+
+@pytest.mark.parametrize("spec,why", [({"driver": {"enabled": True}}, "driver.enabled"),
+                                      ({"exporter": {"port": 70000}}, "exporter.port")])
+def test_invalid_policy_is_reported_not_applied(api, spec, why):
+    _policy(api)
+    ctl = op.Controller(KubeClient(api.url), NS)
+    ctl.reconcile_once()
+    before = {p: copy.deepcopy(o) for p, o in api.objects.items() if p != POL}
+    api.objects[POL]["spec"] = spec
+    r = ctl.reconcile_once()
+    assert r.state == "error" and why in r.message
+    assert api.objects[POL]["status"]["state"] == "error"
+    after = {p: o for p, o in api.objects.items() if p != POL}
+    assert after == before            # operands untouched
+
+
+def test_only_one_policy_is_reconciled(api):
+    _policy(api, name="a-main")
+    _policy(api, name="b-other")
+    op.Controller(KubeClient(api.url), NS).reconcile_once()
+    assert api.objects[op.POLICIES + "/b-other"]["status"]["state"] == "ignored"
+    assert api.objects[op.POLICIES + "/a-main"]["status"]["state"] in ("ready", "notReady")
+
+
+def test_chart_operator_mode_renders_crd_controller_and_policy():
+    v = render.load_values(sets=["operator.enabled=true"])
+    docs = render.manifests(render.render(v))
+    kinds = [(d["kind"], d["metadata"]["name"]) for d in docs]
+    assert ("DaemonSet", "amd-gpu-stack-device-plugin") not in kinds    # the operator owns them
+    assert ("Deployment", "amd-gpu-stack-operator") in kinds
+    crd = next(d for d in docs if d["kind"] == "CustomResourceDefinition")
+    assert crd == op.crd()
+    pol = next(d for d in docs if d["kind"] == op.KIND)
+    assert pol["spec"]["devicePlugin"]["enabled"] is True and pol["spec"]["driver"]["enabled"] is False
+    # the operator renders the same operands helm would have rendered
+    want = render.manifests(render.render(render.load_values()))
+    got = op.Controller(None, "amd-gpu").desired(pol["spec"])
+    assert [(d["kind"], d["metadata"]["name"]) for d in got] == \
+        [(d["kind"], d["metadata"]["name"]) for d in want]
+    yaml.safe_dump(docs)
+
+
+def test_is_subset():
+    assert op.is_subset({"a": 1, "b": [{"c": "x"}]}, {"a": 1, "b": [{"c": "x", "d": 2}], "e": 3})
+    assert not op.is_subset({"a": 1}, {"a": 2})
+    assert not op.is_subset({"b": [1, 2]}, {"b": [1]})
+    assert op.is_subset({"port": 9400}, {"port": "9400"})
