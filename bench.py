@@ -212,6 +212,52 @@ def run_allreduce(args, dev, world, rank) -> dict:
     }
 
 
+def ab_other_sizes(args, dev, timer) -> list:
+    """The protocol's other square sizes (context for the headline shape):
+    hand-written kernel vs hipBLASLt, A/B-interleaved hipEvent medians after a
+    short warm-up on the warm chip, output checked against fp32."""
+    import torch
+
+    from mxk8s.ops import gemm_bf16_tn
+    out = []
+    for n in [int(x) for x in args.ab_sizes.split(",") if x]:
+        if dev.type != "cuda" and n > 1024:
+            continue
+        g = torch.Generator(device=dev)
+        g.manual_seed(n)
+        A = (torch.rand((n, n), device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+        Bt = (torch.rand((n, n), device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+        C = torch.empty((n, n), device=dev, dtype=torch.bfloat16)
+        C2 = torch.empty_like(C)
+        gemm_bf16_tn(A, Bt, C)
+        _sync(dev)
+        err, tol = _full_check(A, Bt, C)
+        fns = {"mxk": lambda: gemm_bf16_tn(A, Bt, C), "hipblaslt": lambda: torch.mm(A, Bt.t(), out=C2)}
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.5:
+            for f in fns.values():
+                f()
+            _sync(dev)
+        ts = {k: [] for k in fns}
+        reps = max(8, min(40, int(40 * (8192 / n) ** 3)))
+        for r in range(4):
+            for k in (("mxk", "hipblaslt") if r % 2 == 0 else ("hipblaslt", "mxk")):
+                mk = timer.marks(reps + 1)
+                for i in range(reps):
+                    timer.record(mk, i)
+                    fns[k]()
+                timer.record(mk, reps)
+                ts[k] += timer.elapsed_ms(mk)
+        med = {k: statistics.median(v) for k, v in ts.items()}
+        fl = 2.0 * n ** 3
+        out.append({"M": n, "N": n, "K": n, "check_ok": bool(err <= tol),
+                    "mxk_tflops": round(fl / med["mxk"] / 1e9, 2),
+                    "hipblaslt_tflops": round(fl / med["hipblaslt"] / 1e9, 2),
+                    "mxk_over_hipblaslt": round(med["hipblaslt"] / med["mxk"], 4)})
+        del A, Bt, C, C2
+    return out
+
+
 def run_validator(args) -> dict:
     import torch
 
@@ -317,6 +363,7 @@ def run_validator(args) -> dict:
               "hipblaslt_tflops": round(flops / m_blas / 1e9, 2),
               "mxk_over_hipblaslt": round(m_blas / m_mxk, 4)}
 
+    sizes_ab = [] if args.no_reference else ab_other_sizes(args, dev, timer)
     ar = None if args.no_allreduce else run_allreduce(args, dev, world, rank)
 
     return {
@@ -345,6 +392,7 @@ def run_validator(args) -> dict:
                        "tolerance": tol, "elements": M * N, "reference": "fp32 torch.matmul"},
         "hipblaslt_ab": ab,
         "hipblaslt_tflops_same_shape": None if ab is None else ab["hipblaslt_tflops"],
+        "ab_other_sizes": sizes_ab,
         "launch": "eager",
         "allreduce": ar,
     }
@@ -363,6 +411,8 @@ def main(argv=None) -> int:
     p.add_argument("--allreduce-sizes", default="1,4,16,64,256,1024",
                    help="all-reduce sweep sizes in MiB (comma list)")
     p.add_argument("--ab-rounds", type=int, default=6, help="A/B-interleaved hipBLASLt rounds")
+    p.add_argument("--ab-sizes", default="4096,16384",
+                   help="other square sizes A/B'd against hipBLASLt for context (not the metric)")
     p.add_argument("--no-reference", action="store_true")
     p.add_argument("--no-allreduce", action="store_true")
     p.add_argument("--seq-len", type=int, default=2048, help="ddp mode")

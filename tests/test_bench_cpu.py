@@ -18,7 +18,7 @@ def _run_bench(*extra, timeout=240):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--size", "256", "--steps", "3",
            "--warmup", "1", "--warmup-s", "0", "--allreduce-sizes", "1,2", "--allreduce-mib", "2",
-           "--ab-rounds", "2", *extra]
+           "--ab-rounds", "2", "--ab-sizes", "128", *extra]
     p = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
@@ -46,6 +46,7 @@ def _check_contract(out, n):
     for s in ar["sweep"]:
         assert s["busbw_GBps"] == pytest.approx(s["algbw_GBps"] * 2 * (n - 1) / n, rel=0.02, abs=0.011)
     assert out["hipblaslt_ab"]["launches_each"] == 2 * 20
+    assert [x["M"] for x in out["ab_other_sizes"]] == [128] and out["ab_other_sizes"][0]["check_ok"]
 
 
 def test_bench_single_rank_contract():
