@@ -12,9 +12,9 @@ driver:
   amd_gpu_clock_mhz{type=sclk|mclk}      amd_gpu_ecc_errors_total{type}
   amd_gpu_processes                      amd_gpu_xgmi_links
   amd_gpu_topology_link{peer,type}       amd_gpu_link_max_bandwidth_bytes{peer,type}
-  amd_gpu_xgmi_link_up{link,peer_bdf}    (live amd-smi xGMI link state)
-  amd_gpu_xgmi_read_bytes_total / _write_bytes_total{link,peer_bdf}
-  amd_gpu_xgmi_link_bitrate_gbps{link,peer_bdf}
+  amd_gpu_xgmi_link_up{link,status}     (live amd-smi xGMI link state)
+  amd_gpu_xgmi_read_bytes_total / _write_bytes_total{peer_bdf}
+  amd_gpu_xgmi_link_bitrate_gbps{peer_bdf}
   amd_gpu_process_memory_bytes{pid,process,pod_uid,...}  (per-process VRAM)
   amd_gpu_pod_info{namespace,pod,container}  amd_gpu_pods (time-sliced owners)
   amd_gpu_device_healthy{source,reason}  (the device plugin's own verdict)
@@ -206,17 +206,21 @@ def render_metrics(gpus, samples: dict, health: Callable[[int], int], owners: di
                       "Link bandwidth advertised by KFD (bytes/s).",
                       int(l.max_bandwidth_mbps) * 125000, lab)
         live = xgmi(g.key) if xgmi else None
+        # amd-smi reports link state per link slot and traffic per peer; the
+        # two lists are not aligned (a slot can be disabled, the metrics can
+        # carry an all-ones placeholder peer), so each series keeps its own key
         for x in live or []:
-            lab = {**base, "link": str(x.link), "peer_bdf": x.peer_bdf}
             if x.status != "unknown":
                 w.add("amd_gpu_xgmi_link_up", "gauge",
                       "Live xGMI link state from amd-smi (1 up, 0 down or disabled).",
-                      1 if x.status == "up" else 0, {**lab, "status": x.status})
-            if x.read_bytes is not None:
-                w.add("amd_gpu_xgmi_read_bytes_total", "counter",
-                      "Bytes received on the xGMI link (amd-smi link metrics).", x.read_bytes, lab)
-                w.add("amd_gpu_xgmi_write_bytes_total", "counter",
-                      "Bytes sent on the xGMI link (amd-smi link metrics).", x.write_bytes, lab)
+                      1 if x.status == "up" else 0, {**base, "link": str(x.link), "status": x.status})
+            if x.read_bytes is None or not x.peer_bdf or x.peer_bdf.startswith("ffff"):
+                continue
+            lab = {**base, "peer_bdf": x.peer_bdf}
+            w.add("amd_gpu_xgmi_read_bytes_total", "counter",
+                  "Bytes received from the peer over xGMI (amd-smi link metrics).", x.read_bytes, lab)
+            w.add("amd_gpu_xgmi_write_bytes_total", "counter",
+                  "Bytes sent to the peer over xGMI (amd-smi link metrics).", x.write_bytes, lab)
             if x.bit_rate_gbps:
                 w.add("amd_gpu_xgmi_link_bitrate_gbps", "gauge", "Current xGMI link speed (Gb/s).",
                       x.bit_rate_gbps, lab)

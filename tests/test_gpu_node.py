@@ -152,3 +152,56 @@ def test_exporter_on_live_box_serves_amd_smi_metrics():
     assert any(line.startswith("amd_gpu_power_watts{") for line in body.splitlines())
     assert any(line.startswith("amd_gpu_device_healthy{") and line.endswith(" 1")
                for line in body.splitlines())
+
+
+def test_live_xgmi_link_metrics_and_process_vram():
+    """amd-smi's xGMI link state / traffic and the per-process VRAM list on the
+    live MI355X, and the exporter series built from them.  A GPU process (this
+    test's own torch context) must show up with non-zero VRAM."""
+    import json as _json
+
+    import torch
+
+    from mxk8s.exporter import Exporter, ExporterConfig, SmiBackend
+
+    ok, err = node.smi_open()
+    assert ok, err
+    x = torch.ones(64 << 20, device="cuda")       # 256 MiB held by this process
+    torch.cuda.synchronize()
+    be = SmiBackend("")
+    text = Exporter(ExporterConfig(pod_resources=False), backend=be).sample_once()
+    links = node.smi_xgmi_links(0)
+    report = {"links": None if links is None else [l.__dict__ for l in links],
+              "procs": [p.__dict__ for p in node.smi_processes(0)]}
+    print("RESULT " + _json.dumps({"test": "live_xgmi_procs", **report}))
+    if links is not None:                           # amd-smi supports the queries here
+        assert links, "an MI355X has xGMI links"
+        assert all(l.status in ("up", "down", "disabled", "unknown") for l in links)
+        assert "amd_gpu_xgmi_link_up{" in text or "amd_gpu_xgmi_read_bytes_total{" in text
+    # amd-smi reports host PIDs (the container's PID namespace differs), so
+    # look for a process holding at least this test's 256 MiB
+    procs = node.smi_processes(0)
+    assert any(p.vram_bytes >= 256 << 20 for p in procs), report["procs"]
+    assert "amd_gpu_process_memory_bytes{" in text
+    del x
+
+
+def test_health_monitor_on_live_box():
+    """The N02 monitor with live amd-smi: every GPU matched to its amd-smi
+    handle, the ECC baseline taken, healthy, and the state file written."""
+    import json as _json
+    import tempfile
+
+    d = tempfile.mkdtemp()
+    m = node.HealthMonitor(root="", state_dir=d, use_smi=True)
+    try:
+        assert m.smi_active
+        m.step(100)
+        st = m.status()
+        assert st and all(s.smi_index >= 0 and s.ecc_valid and s.healthy for s in st), st
+        assert m.write_state(os.path.join(d, "health.json"))
+        doc = _json.load(open(os.path.join(d, "health.json")))
+        assert doc["smi"] and all(g["healthy"] for g in doc["gpus"])
+        assert open(os.path.join(d, "ecc-baseline")).read().startswith("boot ")
+    finally:
+        m.close()

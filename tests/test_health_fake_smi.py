@@ -251,6 +251,7 @@ def test_exporter_reads_plugin_health_state(fake_smi, plugin_dir, tmp_path):
         assert len(up) == 7 and all(l.endswith(" 1") for l in up)
         rd = [l for l in text.splitlines() if l.startswith('amd_gpu_xgmi_read_bytes_total{gpu="0"')]
         assert len(rd) == 7 and rd[0].endswith(f" {100 * 1024}") and 'peer_bdf="0000:15:00.0"' in rd[0]
+        assert 'link="0"' not in rd[0]      # traffic is keyed by peer, state by link slot
         # a stale state file (plugin gone) falls back to the sysfs verdict
         doc = json.load(open(os.path.join(state, "health.json")))
         doc["unix_ms"] = 0
