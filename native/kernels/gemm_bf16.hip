@@ -54,6 +54,8 @@
 //  16 w4j   schedule 6 under s_setprio 1
 //  17 w4j   schedule 6, K loop rotated per XCD (different K-slices per XCD)
 //  18 w4j   schedule 6, K loop rotated per workgroup
+//  19 pp8   8 waves, two per SIMD, compute / load ping-pong (mxk_gemm_bf16_tn_pp8)
+//  20 pp8   19 with the second group at s_setprio 1
 // The earlier schedules (one-barrier w4b, 8-wave, 4-deep ring, w4h, ...)
 // were retired when an ISA audit (tests/test_isa_hazards.py) found their
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
@@ -514,6 +516,146 @@ mxk_gemm_bf16_tn_w4ip(const uint16_t* __restrict__ A, const uint16_t* __restrict
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+
+// ---------------------------------------------------------------------------
+// pp8 (schedule 19): 8 waves, two per SIMD, in a compute / load ping-pong.
+// The 4-wave kernel above runs one wave per SIMD, so every barrier, LDS
+// latency and DMA wait of that wave leaves the SIMD's matrix pipe idle (PMC:
+// MFMA busy 83.5 %).  Here a 512-thread workgroup keeps the 256x256 tile but
+// splits it over two groups of four waves (group g = waves 4g..4g+3, one wave
+// of each group per SIMD); each wave owns 128 x 64 of C (32 16x16x32 tiles,
+// 128 AGPR accumulators) and ONE K-tile of fragments (96 VGPRs).  Every wave
+// runs the same straight-line sequence per K-tile t
+//     L_t: read K-tile t's fragments from LDS  | barrier
+//     C_t: its 64 MFMAs                        | barrier
+// and group 1 runs it one phase behind group 0 (one extra barrier first), so
+// in every phase one wave per SIMD issues MFMAs while its partner reads LDS.
+// Group 0 also moves the data: in L_t it issues the LDS-DMA of stage t+1 into
+// the buffer both groups finished reading in the two phases before, and waits
+// for it at the end of C_t.  No branch touches fragments or accumulators, so
+// the register allocation is the single-K-tile one.  Same LDS image, swizzle,
+// DMA piece map (group 0 plays the 4 waves of make_dmak) and store tail as the
+// 4-wave kernel.
+constexpr int PP_THREADS = 512;
+
+__device__ __forceinline__ void pp_fence() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int PAR>
+__device__ __forceinline__ void pp_load(bf16x8_t (&fa)[2][8], bf16x8_t (&fb)[2][4],
+                                        const char* smem, int a_base, int b_base, int off_k0,
+                                        int off_k1) {
+  constexpr int SUB = 2048;
+  const char* X = smem + PAR * W4B_STAGE_BYTES;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[0][j] = lds_read_b128(X + b_base + j * SUB + off_k0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa[0][i] = lds_read_b128(X + a_base + i * SUB + off_k0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[1][j] = lds_read_b128(X + b_base + j * SUB + off_k1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa[1][i] = lds_read_b128(X + a_base + i * SUB + off_k1);
+}
+
+__device__ __forceinline__ void pp_compute(f32x4_t (&acc)[8][4], const bf16x8_t (&fa)[2][8],
+                                           const bf16x8_t (&fb)[2][4]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mfma_16x16x32_agpr(acc[i][j], fb[h][j], fa[h][i]);
+}
+
+template <int PAR>
+__device__ __forceinline__ void pp_dma(char* smem, const DmaK& dma_a, const DmaK& dma_b, int kb,
+                                       int wl) {
+  char* X = smem + PAR * W4B_STAGE_BYTES;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_a.issue(X, p, kb, wl);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_b.issue(X + W4B_OP_BYTES, p, kb, wl);
+}
+
+// K-tile t with buffer parity PAR = t & 1: L_t | barrier | C_t | barrier
+template <int PAR>
+__device__ __forceinline__ void pp_ktile(f32x4_t (&acc)[8][4], bf16x8_t (&fa)[2][8],
+                                         bf16x8_t (&fb)[2][4], char* smem, int a_base, int b_base,
+                                         int off_k0, int off_k1, const DmaK& dma_a,
+                                         const DmaK& dma_b, int g, int wl, int t, int ns) {
+  pp_load<PAR>(fa, fb, smem, a_base, b_base, off_k0, off_k1);
+  // stage t+1 into the other buffer (read by group 0 in L_{t-1}, group 1 in
+  // L_{t-1} one phase later: both done); stage 1 came with the prologue
+  if (g == 0 && t >= 1 && t + 1 < ns) pp_dma<PAR ^ 1>(smem, dma_a, dma_b, (t + 1) * BK * 2, wl);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  pp_fence();
+  __builtin_amdgcn_s_barrier();
+  pp_fence();
+  pp_compute(acc, fa, fb);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // group 0: stage t+1 landed
+  pp_fence();
+  __builtin_amdgcn_s_barrier();
+  pp_fence();
+}
+
+template <int MAP, int PRIO>
+__global__ void __launch_bounds__(PP_THREADS, 1)
+mxk_gemm_bf16_tn_pp8(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = wave >> 2;          // group
+  const int wl = wave & 3;          // wave within the group (DMA piece map)
+  const int wm = wl & 1;            // 128-row half of the tile
+  const int wn = (wl >> 1) + 2 * g; // 64-column quarter
+  if constexpr (PRIO) {
+    if (g == 1) __builtin_amdgcn_s_setprio(1);   // the younger half loses arbitration otherwise
+  }
+  int m0, n0;
+  w4b_tile<MAP>(blockIdx.x, gridDim.x, M / BM, N / BN, &m0, &n0);
+  const DmaK dma_a = make_dmak(A, lda, m0, lane, wl);
+  const DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wl);
+
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 4 * SUB;
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t fa[2][8], fb[2][4];
+
+  const int ns = K / BK;
+  // prologue: group 0 moves stage 0, group 1 stage 1 (each as the 4-wave map)
+  if (g == 0) pp_dma<0>(smem, dma_a, dma_b, 0, wl);
+  else if (ns > 1) pp_dma<1>(smem, dma_a, dma_b, BK * 2, wl);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (g == 1) __builtin_amdgcn_s_barrier();      // group 1 runs one phase behind
+  pp_fence();
+  int t = 0;
+  for (; t + 2 <= ns; t += 2) {
+    pp_ktile<0>(acc, fa, fb, smem, a_base, b_base, off_k0, off_k1, dma_a, dma_b, g, wl, t, ns);
+    pp_ktile<1>(acc, fa, fb, smem, a_base, b_base, off_k0, off_k1, dma_a, dma_b, g, wl, t + 1, ns);
+  }
+  if (t < ns)
+    pp_ktile<0>(acc, fa, fb, smem, a_base, b_base, off_k0, off_k1, dma_a, dma_b, g, wl, t, ns);
+  mxk::mfma_drain(acc);
+  store_block_wide<true, 8, 4>(acc, C, ldc, m0 + wm * 128, n0 + wn * 64, lane);
+  if (g == 0) __builtin_amdgcn_s_barrier();      // same barrier count as group 1
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ---------------------------------------------------------------------------
 // Generic bounds-checked MFMA GEMM (any M, N, K; K-contiguous operands).
 // 64x64 tile, 256 threads (2x2 waves of 32x32), register-staged through LDS.
@@ -588,13 +730,14 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                                      int variant, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 19;
+constexpr int kNumVariants = 21;
 constexpr int kDefaultVariant = 6;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
     "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar",
     "w4j_hb_st", "x2_hb", "diag_nostore", "w4ip_hb_st", "w4ip_hb_nt", "w4j_earlyb",
-    "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg"};
+    "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg", "pp8",
+    "pp8_prio"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -647,6 +790,14 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 16: launch_w4i<1, 2, 1, 0, 6>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 17: launch_w4i<1, 2, 1, 0, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 18: launch_w4i<1, 2, 1, 0, 1, 2>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 19:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_pp8<1, 0>), dim3(nwg), dim3(PP_THREADS), 0, stream, a, b,
+                         c, M, N, K, lda, ldb, ldc);
+      break;
+    case 20:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_pp8<1, 1>), dim3(nwg), dim3(PP_THREADS), 0, stream, a, b,
+                         c, M, N, K, lda, ldb, ldc);
+      break;
     case 11:
     case 12: {
       const int grid = nwg < num_cus() ? nwg : num_cus();

@@ -165,17 +165,17 @@ __device__ __forceinline__ void w4b_tile(int bid, int nwg, int tiles_m, int tile
 // bf16 store of a wave's 128x128 accumulator block, widened to dwordx4 by
 // v_permlane16_swap (w4b EPI 1).  NT: non-temporal stores (C is written once
 // and not re-read by this kernel; keeps it from displacing A/B panels).
-template <bool NT = false>
-__device__ __forceinline__ void store_block_wide(const f32x4_t (&acc)[8][8], uint16_t* C, int ldc,
+template <bool NT = false, int NI = 8, int NJ = 8>
+__device__ __forceinline__ void store_block_wide(const f32x4_t (&acc)[NI][NJ], uint16_t* C, int ldc,
                                                  int row0, int col0, int lane) {
   const int crow = lane & 15;
   const int q = lane >> 4;
   const int ccol = (q & 1) * 16 + (q >> 1) * 8;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < NI; ++i) {
     uint16_t* cp = C + static_cast<size_t>(row0 + i * 16 + crow) * ldc + col0 + ccol;
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) {
+    for (int j = 0; j < NJ; j += 2) {
       const uint32_t x0 = pack2bf(acc[i][j][0], acc[i][j][1]);
       const uint32_t x1 = pack2bf(acc[i][j][2], acc[i][j][3]);
       const uint32_t y0 = pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
