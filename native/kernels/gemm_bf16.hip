@@ -535,7 +535,12 @@ mxk_gemm_bf16_tn_w4ip(const uint16_t* __restrict__ A, const uint16_t* __restrict
 // for it at the end of C_t.  No branch touches fragments or accumulators, so
 // the register allocation is the single-K-tile one.  Same LDS image, swizzle,
 // DMA piece map (group 0 plays the 4 waves of make_dmak) and store tail as the
-// 4-wave kernel.
+// 4-wave kernel.  Measured (profiles/r2_gemm_ab/pp8_pingpong_ab.log): correct
+// (bit-identical to schedule 6) but 6 % slower at 8192^3 and 11 % at 16384^3:
+// with two 64 KiB stages the DMA of stage t+1 can only start when both groups
+// have left buffer t-1, so it gets ~1 phase (~1000 cycles) to land against
+// ~100-200 MFMAs (1500-3000 cycles) in schedule 6, and every K-tile pays two
+// workgroup barriers.  Kept as an A/B variant, not the default.
 constexpr int PP_THREADS = 512;
 
 __device__ __forceinline__ void pp_fence() {

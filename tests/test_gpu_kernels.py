@@ -60,7 +60,8 @@ def test_gemm_narrow_c_stride(cuda_device):
     assert torch.count_nonzero(buf[:, N:]) == 0   # nothing written past N
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 4096, 256), (1024, 768, 512)])
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 256), (1024, 768, 512), (512, 512, 64),
+                                   (512, 768, 128), (768, 512, 192)])
 def test_gemm_every_schedule_vs_fp32(cuda_device, M, N, K):
     """Every non-ablation schedule of the 256x256 kernel; 4096^2 puts the
     XCD super-block map (16x16 tiles) in play, 1024x768 its MAP-0 fallback."""
@@ -79,6 +80,26 @@ def test_gemm_every_schedule_vs_fp32(cuda_device, M, N, K):
         _lib.check(st, f"variant {v}")
         err = (c.float() - ref).abs().max().item()
         assert err <= tol, (v, err)
+
+
+@pytest.mark.parametrize("M,N,K,variants", [(8192, 8192, 8192, (6, 19)), (16384, 16384, 512, (6,)),
+                                            (16384, 6144, 4096, (6, 19))])
+def test_gemm_headline_shapes_full_output_vs_fp32(cuda_device, M, N, K, variants):
+    """The long-K headline shape and the XCD super-block map at 64x64 tiles,
+    the WHOLE output against an fp32 GEMM (tolerance 2^-7 max|ref|)."""
+    from mxk8s.ops import _lib
+    L = _lib.lib()
+    a = _rand((M, K), cuda_device, 31).bfloat16()
+    bt = _rand((N, K), cuda_device, 32).bfloat16()
+    ref = a.float() @ bt.float().t()
+    tol = ref.abs().max().item() * 2 ** -7
+    for v in variants:
+        c = torch.full((M, N), float("nan"), device=cuda_device, dtype=torch.bfloat16)
+        st = L.mxk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
+                                        v, _lib.stream_ptr(cuda_device))
+        _lib.check(st, f"variant {v}")
+        err = (c.float() - ref).abs().max().item()
+        assert err <= tol, (v, err, tol)
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (17, 33, 65), (100, 300, 200), (255, 257, 63)])
