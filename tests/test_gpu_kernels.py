@@ -314,3 +314,18 @@ def test_qkv_rope_matches_split_rope(cuda_device):
     torch.autograd.backward((q, k, v), (gq, gk, gv))
     torch.autograd.backward((rq, rk, rv), (gq, gk, gv))
     assert torch.equal(qkv.grad, ref_in.grad)
+    # ... and both against an independent fp32 PyTorch reference (rotate-half
+    # RoPE in fp32; its gradient is the inverse rotation of the incoming grad)
+    from mxk8s.ops.fused import rope_ref
+    x32 = qkv.detach().float()
+    fq, fk, fv = x32.split([hq * hd, hkv * hd, hkv * hd], dim=-1)
+    want_q = rope_ref(fq.reshape(B, S, hq, hd), cos, sin)
+    want_k = rope_ref(fk.reshape(B, S, hkv, hd), cos, sin)
+    tol = 2 ** -7 * 4.0                        # bf16 output of |x| <= 2 rotated values
+    assert (q.float() - want_q).abs().max().item() <= tol
+    assert (k.float() - want_k).abs().max().item() <= tol
+    assert torch.equal(v.float(), fv.reshape(B, S, hkv, hd))
+    dq32 = rope_ref(gq.float(), cos, sin, sign=-1.0)
+    dk32 = rope_ref(gk.float(), cos, sin, sign=-1.0)
+    want_g = torch.cat([dq32.reshape(B, S, -1), dk32.reshape(B, S, -1), gv.float().reshape(B, S, -1)], -1)
+    assert (qkv.grad.float() - want_g).abs().max().item() <= 2 ** -7 * 2.0
