@@ -53,11 +53,13 @@ def attention_ref(q, k, v, causal: bool = True, scale: float | None = None) -> t
     return o.transpose(1, 2).to(q.dtype)
 
 
-def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None, variant: int = 2):
+def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None, variant: int = 3):
     """HIP forward: returns (o [B,S,Hq,D] bf16, lse [B,Hq,S] fp32).
 
-    ``variant`` 2 (default) feeds K/V by LDS-DMA, 1 is the same with the
-    loop unrolled by two, 0 stages K/V through registers (A/B runs)."""
+    ``variant`` 3 (default) feeds K/V by LDS-DMA with the software-pipelined
+    body (exp of one P chunk under the PV MFMAs of the previous one), 2 is the
+    plain DMA body, 1 the same unrolled by two, 0 stages K/V through
+    registers (A/B runs)."""
     B, S, Hq, D = q.shape
     Hkv = k.shape[2]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -71,7 +73,7 @@ def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None, variant: 
     return o, lse
 
 
-_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "2"))
+_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "3"))
 
 
 def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = None,
@@ -80,9 +82,12 @@ def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = N
 
     ``dk``/``dv`` may be preallocated views (e.g. slices of a fused dQKV
     buffer) with a token stride; by default they are fresh contiguous tensors.
-    ``variant`` 2 (default): dK/dV accumulated over the query-head group in
-    one workgroup, bf16 out, K/V and Q/dO tiles by LDS-DMA (1.21 vs 1.31-1.36
-    ms per Llama-3-8B layer at B 8, bit-identical: profiles/r1_attention/);
+    ``variant`` 3 (default): variant 2 with explicitly software-pipelined
+    dK/dV and dQ bodies (LDS operands read a group ahead instead of one
+    lgkmcnt(0) per MFMA), bit-identical to 2 and 15 % faster (1.070 vs 1.262
+    ms per Llama-3-8B layer at B 8: profiles/r2_attention/); 2: dK/dV
+    accumulated over the query-head group in one workgroup, bf16 out, K/V and
+    Q/dO tiles by LDS-DMA (1.21 vs 1.31-1.36 ms, profiles/r1_attention/);
     1: the same with register-staged tiles; 0: per-query-head fp32 partials
     + GQA reduce."""
     B, S, Hq, D = q.shape

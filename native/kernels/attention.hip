@@ -324,7 +324,7 @@ namespace {
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 }
 
-template <bool CAUSAL, bool UNROLL>
+template <bool CAUSAL, bool UNROLL, bool PIPE = false>
 __global__ void __launch_bounds__(NT, 2)
 mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                         const uint16_t* __restrict__ v, uint16_t* __restrict__ o,
@@ -434,12 +434,48 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
       f32x16_t s0, s1;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
+      bf16x8_t vop[16];   // V^T operands [4 db + ks] (PIPE)
+      auto read_v = [&](int x) {
+        vop[x] = cat8(lds_tr_b64(vt + voff[x >> 2][0] + (x & 3) * 4096),
+                      lds_tr_b64(vt + voff[x >> 2][1] + (x & 3) * 4096));
+      };
+      if constexpr (PIPE) {
+        // K operands a k-step pair ahead (two-slot ring), the first V^T
+        // operands under the last S MFMAs and the softmax, the rest one db
+        // ahead of the PV MFMAs; sched_barrier fences keep the order (the
+        // plain loop below gets read -> lgkmcnt(0) -> MFMA per instruction)
+        bf16x8_t ka[2][4];
+        auto read_k = [&](int pr, int slot) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const bf16x8_t a0 = lds_b128(kt + koff[s]);
-        const bf16x8_t a1 = lds_b128(kt + koff[s] + 32 * 256);
-        s0 = mfma32(a0, qf[s], s0);
-        s1 = mfma32(a1, qf[s], s1);
+          for (int e = 0; e < 2; ++e) {
+            ka[slot][2 * e] = lds_b128(kt + koff[2 * pr + e]);
+            ka[slot][2 * e + 1] = lds_b128(kt + koff[2 * pr + e] + 32 * 256);
+          }
+        };
+        read_k(0, 0);
+#pragma unroll
+        for (int pr = 0; pr < 4; ++pr) {
+          if (pr < 3) read_k(pr + 1, (pr + 1) & 1);
+          else
+#pragma unroll
+            for (int x = 0; x < 4; ++x) read_v(x);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            s0 = mfma32(ka[pr & 1][2 * e], qf[2 * pr + e], s0);
+            s1 = mfma32(ka[pr & 1][2 * e + 1], qf[2 * pr + e], s1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int x = 4; x < 8; ++x) read_v(x);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8_t a0 = lds_b128(kt + koff[s]);
+          const bf16x8_t a1 = lds_b128(kt + koff[s] + 32 * 256);
+          s0 = mfma32(a0, qf[s], s0);
+          s1 = mfma32(a1, qf[s], s1);
+        }
       }
       if (CAUSAL && kv0 + BKV - 1 > qw0) {
 #pragma unroll
@@ -459,42 +495,83 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
       const float alpha = fexp2((m - m_new) * c);
       m = m_new;
       const f32x2_t nmc = {-m_new * c, -m_new * c};
-      f32x2_t ls2 = {0.f, 0.f};
+      if constexpr (PIPE) {
+        // P in four 16-key chunks: the exp of chunk ks + 1 runs on the VALU
+        // while the four PV MFMAs of chunk ks run on the matrix core (one
+        // wave overlaps its own softmax with its own MFMAs)
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        f32x2_t x0 = {s0[r], s0[r + 1]};
-        f32x2_t x1 = {s1[r], s1[r + 1]};
-        x0 = __builtin_elementwise_fma(x0, cc, nmc);
-        x1 = __builtin_elementwise_fma(x1, cc, nmc);
-        x0[0] = fexp2(x0[0]);
-        x0[1] = fexp2(x0[1]);
-        x1[0] = fexp2(x1[0]);
-        x1[1] = fexp2(x1[1]);
-        ls2 += x0 + x1;
-        s0[r] = x0[0];
-        s0[r + 1] = x0[1];
-        s1[r] = x1[0];
-        s1[r + 1] = x1[1];
-      }
-      l = l * alpha + (ls2[0] + ls2[1]);
-      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+        for (int x = 8; x < 16; ++x) read_v(x);
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
 #pragma unroll
-        for (int db = 0; db < 4; ++db)
+          for (int db = 0; db < 4; ++db)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[db][r] *= alpha;
-      }
-      bf16x8_t pf[4];
-      pf[0] = pack8(s0, 0);
-      pf[1] = pack8(s0, 8);
-      pf[2] = pack8(s1, 0);
-      pf[3] = pack8(s1, 8);
+            for (int r = 0; r < 16; ++r) acc[db][r] *= alpha;
+        }
+        f32x2_t ls2 = {0.f, 0.f};
+        auto chunk = [&](int ks) {
+          f32x16_t& x = ks < 2 ? s0 : s1;
+          const int base = (ks & 1) * 8;
 #pragma unroll
-      for (int db = 0; db < 4; ++db) {
+          for (int r = 0; r < 8; r += 2) {
+            f32x2_t y = {x[base + r], x[base + r + 1]};
+            y = __builtin_elementwise_fma(y, cc, nmc);
+            y[0] = fexp2(y[0]);
+            y[1] = fexp2(y[1]);
+            ls2 += y;
+            x[base + r] = y[0];
+            x[base + r + 1] = y[1];
+          }
+          return pack8(x, base);
+        };
+        bf16x8_t pf[4];
+        pf[0] = chunk(0);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-          const bf16x4_t lo = lds_tr_b64(vt + voff[db][0] + ks * 4096);
-          const bf16x4_t hi = lds_tr_b64(vt + voff[db][1] + ks * 4096);
-          acc[db] = mfma32(cat8(lo, hi), pf[ks], acc[db]);
+#pragma unroll
+          for (int db = 0; db < 4; ++db) acc[db] = mfma32(vop[4 * db + ks], pf[ks], acc[db]);
+          if (ks < 3) pf[ks + 1] = chunk(ks + 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        l = l * alpha + (ls2[0] + ls2[1]);
+      } else {
+        f32x2_t ls2 = {0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          f32x2_t x0 = {s0[r], s0[r + 1]};
+          f32x2_t x1 = {s1[r], s1[r + 1]};
+          x0 = __builtin_elementwise_fma(x0, cc, nmc);
+          x1 = __builtin_elementwise_fma(x1, cc, nmc);
+          x0[0] = fexp2(x0[0]);
+          x0[1] = fexp2(x0[1]);
+          x1[0] = fexp2(x1[0]);
+          x1[1] = fexp2(x1[1]);
+          ls2 += x0 + x1;
+          s0[r] = x0[0];
+          s0[r + 1] = x0[1];
+          s1[r] = x1[0];
+          s1[r + 1] = x1[1];
+        }
+        l = l * alpha + (ls2[0] + ls2[1]);
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+          for (int db = 0; db < 4; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[db][r] *= alpha;
+        }
+        bf16x8_t pf[4];
+        pf[0] = pack8(s0, 0);
+        pf[1] = pack8(s0, 8);
+        pf[2] = pack8(s1, 0);
+        pf[3] = pack8(s1, 8);
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            const bf16x4_t lo = lds_tr_b64(vt + voff[db][0] + ks * 4096);
+            const bf16x4_t hi = lds_tr_b64(vt + voff[db][1] + ks * 4096);
+            acc[db] = mfma32(cat8(lo, hi), pf[ks], acc[db]);
+          }
         }
       }
     }
@@ -531,15 +608,17 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
 
 // ---------------------------------------------------------------------------
 // variant: 0 = register-staged K/V, 1 = LDS-DMA with the loop unrolled by 2
-// (static LDS buffer), 2 = LDS-DMA (default).  1 and 2 fall back to 0 when a
-// K/V panel exceeds the 32-bit buffer range.  B=8 Llama shape: 0.42 / 0.43 /
-// 0.38 ms (profiles/r1_attention/).
+// (static LDS buffer), 2 = LDS-DMA, 3 = 2 with the PIPE body (operands read a
+// group ahead, exp of P chunk ks+1 under the PV MFMAs of chunk ks; default).
+// 1-3 fall back to 0 when a K/V panel exceeds the 32-bit buffer range.  B=8
+// Llama shape: 0.42 / 0.43 / 0.38 ms (profiles/r1_attention/); 2 -> 3:
+// 0.3385 -> 0.3312 ms (profiles/r2_attention/).
 MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, void* o, float* lse,
                                  int B, int S, int Hq, int Hkv, int head_dim, long q_tok,
                                  long k_tok, long v_tok, float scale, int causal, int variant,
                                  hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv ||
-      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 2 ||
+      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 3 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) % 16)
     return static_cast<int>(hipErrorInvalidValue);
@@ -550,7 +629,14 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
   const auto* kp = static_cast<const uint16_t*>(k);
   const auto* vp = static_cast<const uint16_t*>(v);
   auto* op = static_cast<uint16_t*>(o);
-  if (variant == 1) {
+  if (variant == 3) {
+    if (causal)
+      hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<true, false, true>), dim3(nwg), dim3(NT), 0, stream,
+                         qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    else
+      hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<false, false, true>), dim3(nwg), dim3(NT), 0,
+                         stream, qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  } else if (variant == 1) {
     if (causal)
       hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<true, true>), dim3(nwg), dim3(NT), 0, stream, qp,
                          kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
@@ -638,7 +724,7 @@ mxk_attn_bwd_delta_kernel(const uint16_t* __restrict__ o, const uint16_t* __rest
 // kernel's piece mapping, destinations bound to M0) instead of register
 // staging - frees the 32 staging VGPRs that made this kernel spill at two
 // waves per SIMD, and the ds_writes.  Requires S * token_stride * 2 < 2^32.
-template <bool CAUSAL, bool DMA = false>
+template <bool CAUSAL, bool DMA = false, bool PIPE = false>
 __global__ void __launch_bounds__(NT, 2)
 mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                        const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
@@ -759,6 +845,69 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
       const char* kt = smem[buf];
       const char* vt = smem[buf] + TILE_BYTES;
       const bool diag = CAUSAL && kv0 + BKV - 1 > qw0;
+      if constexpr (PIPE) {
+        // software-pipelined as the dK/dV kernel's PIPE body: S / dP operands
+        // read a half (4 k-steps) ahead, dS-side transposed reads issued
+        // under the exp, the next half's first operands under the dQ MFMAs
+        bf16x8_t ka[2][2], va[2][2];    // ring of two k-step pairs
+        auto read_p = [&](int kh, int pr, int slot) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int s = 2 * pr + e;
+            ka[slot][e] = lds_b128(kt + swz(32 * kh + r32, 2 * s + h));
+            va[slot][e] = lds_b128(vt + swz(32 * kh + r32, 2 * s + h));
+          }
+        };
+        auto read_t = [&](int kh, int db, int kk) {
+          const int key = 32 * kh + 16 * kk + tr_key;
+          const int ch = 4 * db + tr_ch;
+          return cat8(lds_tr_b64(kt + swz(key, ch) + tr_byte), lds_tr_b64(kt + swz(key + 8, ch) + tr_byte));
+        };
+        read_p(0, 0, 0);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          __builtin_amdgcn_sched_barrier(0);
+          f32x16_t s0, p0;
+          zero16(s0);
+          zero16(p0);
+          bf16x8_t ta[8];
+#pragma unroll
+          for (int pr = 0; pr < 4; ++pr) {
+            if (pr < 3) {
+              read_p(kh, pr + 1, (pr + 1) & 1);
+            } else {
+#pragma unroll
+              for (int x = 0; x < 4; ++x) ta[x] = read_t(kh, x >> 1, x & 1);
+            }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              s0 = mfma32(ka[pr & 1][e], qf[2 * pr + e], s0);
+              p0 = mfma32(va[pr & 1][e], dof[2 * pr + e], p0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#pragma unroll
+          for (int x = 4; x < 8; ++x) ta[x] = read_t(kh, x >> 1, x & 1);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float e0 = fexp2(fmaf(s0[r], c, -lse2));
+            if (diag && kv0 + 32 * kh + crow(r, h) > myq) e0 = 0.f;
+            s0[r] = e0 * (p0[r] - dlt);   // dS^T
+          }
+          bf16x8_t df[2];
+          df[0] = pack8(s0, 0);
+          df[1] = pack8(s0, 8);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int x = 0; x < 8; ++x) {
+            acc[x >> 1] = mfma32(ta[x], df[x & 1], acc[x >> 1]);
+            if (kh == 0 && x == 5) {
+              read_p(1, 0, 0);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
+      } else {
       // one 32-key half at a time keeps S^T / dP^T to 32 registers
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
@@ -794,6 +943,7 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
             acc[db] = mfma32(a, df[kk], acc[db]);
           }
         }
+      }
       }
     }
     if constexpr (DMA) {
@@ -1027,7 +1177,7 @@ constexpr int NT16 = 512;
 // ~1.1 GB more HBM traffic per Llama-3-8B layer at B = 8).
 // DMA: Q / dO slices by LDS-DMA (wave w moves the 1-KiB pieces 2w, 2w + 1 of
 // each), as in the dQ kernel; the lse / delta rows stay register-staged.
-template <bool CAUSAL, bool GQA = false, bool DMA = false>
+template <bool CAUSAL, bool GQA = false, bool DMA = false, bool PIPE = false>
 __global__ void __launch_bounds__(NT16, 1)
 mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                            const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
@@ -1090,43 +1240,56 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
   const int tr_byte = 8 * (c16 & 1);
   const int q_begin = CAUSAL ? k0 : 0;
   const int nsl = (S - q_begin) / BQB;
-  for (int gq = 0; gq < (GQA ? grp : 1); ++gq) {
-  const int hq = hq0 + gq;
-  const uint16_t* qb_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
-  const uint16_t* dob_ptr = dout + static_cast<long>(b) * S * Hq * D + static_cast<long>(hq) * D;
-  const float* lse_b = lse + (static_cast<long>(b) * Hq + hq) * S;
-  const float* dl_b = delta + (static_cast<long>(b) * Hq + hq) * S;
+  // Work items i = (query slice t, head gq of the group), head-outer, slices
+  // ascending from the diagonal; pipelined across head boundaries.  (A
+  // slice-outer walk from the last slice down, heads inner, which keeps the
+  // key blocks of a group in lockstep on the same Q / dO slice, measured
+  // neutral: 1.2417 vs 1.2468 ms per Llama-3-8B layer, profiles/r2_attention.)
+  const int ngq = GQA ? grp : 1;
+  const int niter = nsl * ngq;
+  auto item = [&](int i, int* t, int* gq) {
+    *gq = i / nsl;
+    *t = i - *gq * nsl;
+  };
+  const uint16_t* qg_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq0) * D;
+  const uint16_t* dog_ptr = dout + static_cast<long>(b) * S * Hq * D + static_cast<long>(hq0) * D;
+  const float* lse_g = lse + (static_cast<long>(b) * Hq + hq0) * S;
+  const float* dl_g = delta + (static_cast<long>(b) * Hq + hq0) * S;
   // loader: 512 threads x 2 chunks per tile (64 rows x 16 chunks)
   const int ld_row = tid >> 4, ld_ch = tid & 15;
   bf16x8_t qst[2], dst[2];
   float rst = 0.f;
-  auto load_slice = [&](int t) {
+  auto load_slice = [&](int i) {
+    int t, gq;
+    item(i, &t, &gq);
     const long r0 = q_begin + static_cast<long>(t) * BQB + ld_row;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      qst[i] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + (r0 + 32 * i) * q_tok + ld_ch * 8);
-      dst[i] = *reinterpret_cast<const bf16x8_t*>(dob_ptr + (r0 + 32 * i) * Hq * D + ld_ch * 8);
+    for (int j = 0; j < 2; ++j) {
+      qst[j] = *reinterpret_cast<const bf16x8_t*>(qg_ptr + (r0 + 32 * j) * q_tok + gq * D + ld_ch * 8);
+      dst[j] = *reinterpret_cast<const bf16x8_t*>(dog_ptr + (r0 + 32 * j) * Hq * D + gq * D + ld_ch * 8);
     }
     if (tid < 2 * BQB) {
       const long qi = q_begin + static_cast<long>(t) * BQB + (tid & (BQB - 1));
-      rst = tid < BQB ? -lse_b[qi] * 1.4426950408889634f * inv_c : -dl_b[qi];
+      rst = tid < BQB ? -lse_g[gq * S + qi] * 1.4426950408889634f * inv_c : -dl_g[gq * S + qi];
     }
   };
   auto store_slice = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int off = swz16(ld_row + 32 * i, ld_ch);
-      *reinterpret_cast<bf16x8_t*>(smem[buf] + off) = qst[i];
-      *reinterpret_cast<bf16x8_t*>(smem[buf] + BQB * 256 + off) = dst[i];
+    for (int j = 0; j < 2; ++j) {
+      const int off = swz16(ld_row + 32 * j, ld_ch);
+      *reinterpret_cast<bf16x8_t*>(smem[buf] + off) = qst[j];
+      *reinterpret_cast<bf16x8_t*>(smem[buf] + BQB * 256 + off) = dst[j];
     }
     if (tid < 2 * BQB) srow[buf][tid / BQB][tid & (BQB - 1)] = rst;
   };
   // raw load at the top, arithmetic at the store: math right after the load
   // would put a vmcnt(0) there, which also waits for the slice DMA just issued
-  auto load_row = [&](int t) {
+  auto load_row = [&](int i) {
     if (tid < 2 * BQB) {
+      int t, gq;
+      item(i, &t, &gq);
       const long qi = q_begin + static_cast<long>(t) * BQB + (tid & (BQB - 1));
-      rst = (tid < BQB ? lse_b : dl_b)[qi];
+      rst = (tid < BQB ? lse_g : dl_g)[gq * S + qi];
     }
   };
   auto store_row = [&](int buf) {
@@ -1137,8 +1300,9 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
   uint32_t qvo[2] = {}, dvo[2] = {};
   const uint32_t sm32 = mxk::lds_addr32(&smem[0][0]);
   if constexpr (DMA) {
-    rq = mxk::make_rsrc(qb_ptr, static_cast<unsigned>(S * q_tok * 2));
-    rd = mxk::make_rsrc(dob_ptr, static_cast<unsigned>(static_cast<long>(S) * Hq * D * 2));
+    // base at the group's first head; head gq is + 2 D gq bytes of soffset
+    rq = mxk::make_rsrc(qg_ptr, static_cast<unsigned>(S * q_tok * 2));
+    rd = mxk::make_rsrc(dog_ptr, static_cast<unsigned>(static_cast<long>(S) * Hq * D * 2));
     // lane i lands at row 4g + (i >> 4), slot i & 15 = chunk ^ 2 (row & 7)
     const int prow = lane >> 4, pslot = lane & 15;
 #pragma unroll
@@ -1149,13 +1313,15 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
       dvo[p] = static_cast<uint32_t>(r * Hq * D * 2 + ch * 16);
     }
   }
-  auto issue = [&](int t, int buf) {
+  auto issue = [&](int i, int buf) {
+    int t, gq;
+    item(i, &t, &gq);
     const long row0 = q_begin + static_cast<long>(t) * BQB;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const uint32_t d = sm32 + buf * (2 * BQB * 256) + (2 * wave + p) * 1024;
-      mxk::dma16m(rq, d, qvo[p], static_cast<uint32_t>(row0 * q_tok * 2));
-      mxk::dma16m(rd, d + BQB * 256, dvo[p], static_cast<uint32_t>(row0 * Hq * D * 2));
+      mxk::dma16m(rq, d, qvo[p], static_cast<uint32_t>(row0 * q_tok * 2 + gq * D * 2));
+      mxk::dma16m(rd, d + BQB * 256, dvo[p], static_cast<uint32_t>(row0 * Hq * D * 2 + gq * D * 2));
     }
   };
   if constexpr (DMA) {
@@ -1169,22 +1335,108 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
   }
   __syncthreads();
 
-
-  for (int t = 0; t < nsl; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nsl) {
+  for (int i = 0; i < niter; ++i) {
+    const int buf = i & 1;
+    if (i + 1 < niter) {
       if constexpr (DMA) {
-        issue(t + 1, buf ^ 1);   // buf ^ 1 last read in slice t - 1 (barrier-certified)
-        load_row(t + 1);
+        issue(i + 1, buf ^ 1);   // buf ^ 1 last read in item i - 1 (barrier-certified)
+        load_row(i + 1);
       } else {
-        load_slice(t + 1);
+        load_slice(i + 1);
       }
     }
+    int t, gq_unused;
+    item(i, &t, &gq_unused);
     const int qs0 = q_begin + t * BQB;
     if (!CAUSAL || qs0 + BQB - 1 >= kw0) {
       const char* qt = smem[buf];
       const char* dt = smem[buf] + BQB * 256;
       const bool diag = CAUSAL && qs0 < kw0 + 15;
+      if constexpr (PIPE) {
+        // Explicitly software-pipelined: every LDS operand is read one MFMA
+        // group ahead of its use, and sched_barrier fences keep the compiler
+        // from re-serialising read -> lgkmcnt(0) -> MFMA per instruction
+        // (what it emits for the plain loop below: 64 waits per slice, each
+        // exposing a full LDS latency).  The waitcnt pass then counts
+        // lgkmcnt down through each group.
+        bf16x8_t qa[8], da[8];          // S / dP A operands, [2 s + h]
+        float4 l4[2], d4[2];            // -lse / -delta rows of the two halves
+        auto read_a = [&](int ks) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int qr = 32 * ks + 16 * h + 4 * G;
+            l4[h] = *reinterpret_cast<const float4*>(&srow[buf][0][qr]);
+            d4[h] = *reinterpret_cast<const float4*>(&srow[buf][1][qr]);
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int row = 32 * ks + 16 * h + c16;
+              qa[2 * s + h] = *reinterpret_cast<const bf16x8_t*>(qt + swz16(row, 4 * s + G));
+              da[2 * s + h] = *reinterpret_cast<const bf16x8_t*>(dt + swz16(row, 4 * s + G));
+            }
+          }
+        };
+        auto read_b = [&](int ks, int db, bf16x8_t* ao, bf16x8_t* aq) {
+          const int row = 32 * ks + tr_row;
+          const int ch = 2 * db + tr_chb;
+          *ao = cat8(lds_tr_b64(dt + swz16(row, ch) + tr_byte),
+                     lds_tr_b64(dt + swz16(row + 16, ch) + tr_byte));
+          *aq = cat8(lds_tr_b64(qt + swz16(row, ch) + tr_byte),
+                     lds_tr_b64(qt + swz16(row + 16, ch) + tr_byte));
+        };
+        read_a(0);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          __builtin_amdgcn_sched_barrier(0);
+          f32x4_t st[2], pt[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            st[h] = f32x4_t{l4[h].x, l4[h].y, l4[h].z, l4[h].w};
+            pt[h] = f32x4_t{d4[h].x, d4[h].y, d4[h].z, d4[h].w};
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              st[h] = mfma16(qa[2 * s + h], kf[s], st[h]);
+              pt[h] = mfma16(da[2 * s + h], vf[s], pt[h]);
+            }
+          }
+          // first half of the dV / dK operands in flight under the exp
+          bf16x8_t ob[8], qb[8];
+#pragma unroll
+          for (int db = 0; db < 4; ++db) read_b(ks, db, &ob[db], &qb[db]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float e = fexp2(st[h][r] * c);
+              if (diag && mykey > qs0 + 32 * ks + 16 * h + 4 * G + r) e = 0.f;
+              st[h][r] = e;                  // P
+              pt[h][r] = e * pt[h][r];       // dS
+            }
+          }
+          const bf16x8_t pf = pack2x4(st[0], st[1]);
+          const bf16x8_t sf = pack2x4(pt[0], pt[1]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int db = 0; db < 4; ++db) {
+            dva[db] = mfma16(ob[db], pf, dva[db]);
+            dka[db] = mfma16(qb[db], sf, dka[db]);
+            read_b(ks, db + 4, &ob[db + 4], &qb[db + 4]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (ks == 0) read_a(1);       // next half's S / dP operands under the last MFMAs
+#pragma unroll
+          for (int db = 4; db < 8; ++db) {
+            dva[db] = mfma16(ob[db], pf, dva[db]);
+            dka[db] = mfma16(qb[db], sf, dka[db]);
+          }
+        }
+      } else {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         f32x4_t st[2], pt[2];
@@ -1229,16 +1481,16 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
           dka[db] = mfma16(aq, sf, dka[db]);
         }
       }
+      }
     }
     if constexpr (DMA) {
-      vm_wait0();   // own pieces of slice t+1
-      if (t + 1 < nsl) store_row(buf ^ 1);
+      vm_wait0();   // own pieces of item i+1
+      if (i + 1 < niter) store_row(buf ^ 1);
     } else {
-      if (t + 1 < nsl) store_slice(buf ^ 1);
+      if (i + 1 < niter) store_slice(buf ^ 1);
     }
     __syncthreads();
   }
-  }   // query heads of the group
   // lane = key, registers r: d = 16 db + 4 G + r
   if constexpr (GQA) {
     uint16_t* dkr = dk + (static_cast<long>(b) * S + mykey) * dk_tok + static_cast<long>(hkv) * D;
@@ -1310,14 +1562,17 @@ MXK_API long mxk_attn_bwd_workspace(int B, int S, int Hq) {
 // variant 1: dK/dV per (batch, KV head, key block) over the whole query-head
 // group, bf16 out; 2: variant 1 with LDS-DMA tile loads in the dQ and dK/dV
 // kernels (register-staged when a panel exceeds the 32-bit buffer range);
-// 0: per query head + fp32 partials + GQA reduce.
+// 3: variant 2 with the explicitly software-pipelined (PIPE) dK/dV and dQ
+// bodies, bit-identical to 2 (default; 1.262 -> 1.070 ms per Llama-3-8B
+// layer, profiles/r2_attention/); 0: per query head + fp32 partials + GQA
+// reduce.
 MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, const void* o,
                                  const void* dout, const float* lse, void* dq, void* dk, void* dv,
                                  void* workspace, int B, int S, int Hq, int Hkv, int head_dim,
                                  long q_tok, long k_tok, long v_tok, long dk_tok, long dv_tok,
                                  float scale, int causal, int variant, hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv || q_tok % 8 ||
-      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 2 ||
+      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 3 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
        reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
@@ -1339,11 +1594,19 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
   const int nwg = B * Hq * (S / BQ);
   const int nwg_kv = B * Hkv * (S / BQ);
   const long qspan = static_cast<long>(S) * (q_tok > static_cast<long>(Hq) * D ? q_tok : Hq * D) * 2;
-  if (variant == 2 && causal && qspan < (1L << 32)) {
+  if (variant == 3 && causal && qspan < (1L << 32)) {
+    hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<true, true, true, true>), dim3(nwg_kv),
+                       dim3(NT16), 0, stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok,
+                       k_tok, v_tok, scale, dK, dV, dk_tok, dv_tok);
+  } else if (variant == 3 && qspan < (1L << 32)) {
+    hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<false, true, true, true>), dim3(nwg_kv),
+                       dim3(NT16), 0, stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok,
+                       k_tok, v_tok, scale, dK, dV, dk_tok, dv_tok);
+  } else if (variant == 2 && causal && qspan < (1L << 32)) {
     hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<true, true, true>), dim3(nwg_kv), dim3(NT16), 0,
                        stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok,
                        v_tok, scale, dK, dV, dk_tok, dv_tok);
-  } else if (variant == 2 && qspan < (1L << 32)) {
+  } else if (variant >= 2 && qspan < (1L << 32)) {
     hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<false, true, true>), dim3(nwg_kv), dim3(NT16),
                        0, stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok, k_tok,
                        v_tok, scale, dK, dV, dk_tok, dv_tok);
@@ -1366,9 +1629,15 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
                        v_tok, scale, nullptr, nullptr, 0L, 0L);
   }
   const long span = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
-  const bool dq_dma = variant == 2 && span < (1L << 32);
+  const bool dq_dma = variant >= 2 && span < (1L << 32);
   auto* dQ = static_cast<uint16_t*>(dq);
-  if (causal && dq_dma)
+  if (causal && dq_dma && variant == 3)
+    hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<true, true, true>), dim3(nwg), dim3(NT), 0, stream,
+                       Q, K, V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  else if (dq_dma && variant == 3)
+    hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<false, true, true>), dim3(nwg), dim3(NT), 0, stream,
+                       Q, K, V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  else if (causal && dq_dma)
     hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<true, true>), dim3(nwg), dim3(NT), 0, stream, Q, K,
                        V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
   else if (causal)

@@ -27,8 +27,9 @@ def _qkv(B, S, Hq, Hkv, dev, seed=0, fused=False):
     (1, 512, 8, 2, True, True),
     (1, 384, 4, 4, False, False),
     (1, 256, 4, 1, False, True),
+    (1, 2048, 32, 8, True, True),     # the Llama-3-8B step's attention shape (B = 1)
 ])
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_attn_fwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused, variant):
     q, k, v = _qkv(B, S, Hq, Hkv, cuda_device, fused=fused)
     assert A.supported(q, k, v)
@@ -50,6 +51,7 @@ def test_attn_fwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused, v
     (2, 256, 4, 2, True, True),
     (1, 512, 8, 2, True, False),
     (1, 256, 4, 4, False, False),
+    (1, 2048, 32, 8, True, True),     # the Llama-3-8B step's attention shape (B = 1)
 ])
 def test_attn_bwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
     q, k, v = _qkv(B, S, Hq, Hkv, cuda_device, seed=1, fused=fused)
@@ -68,11 +70,12 @@ def test_attn_bwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
         assert err < tol, (name, err, tol)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
     (1, 256, 8, 2, True),
     (2, 384, 4, 1, True),
     (1, 256, 4, 4, False),
+    (1, 2048, 32, 8, True),
 ])
 def test_attn_bwd_variants_into_strided_dkdv(cuda_device, B, S, Hq, Hkv, causal, variant):
     """Both dK/dV schedules (per-q-head partials + reduce, GQA-fused), writing
