@@ -1139,6 +1139,13 @@ mxk_attn_bwd_dkdv_kernel(const uint16_t* __restrict__ q, const uint16_t* __restr
   }
 }
 
+// Round-2 alternatives measured against the PIPE body of this kernel
+// (profiles/r2_attention/): a four-buffer LDS ring with every load three
+// items ahead (lse / delta rows by DMA too) 1.129 vs 1.099 ms per layer, and
+// a pipelined 32-key-per-wave kernel (4 waves, one per SIMD, half the LDS
+// operand traffic, dK / dV pinned to AGPRs, softmax overlapped in-wave)
+// 1.182 vs 1.107 ms - two waves per SIMD hide more than the halved LDS
+// traffic saves.
 // dK/dV with 16x16x32 MFMAs: one workgroup = 8 waves x 16 keys (128 keys of
 // one (batch, q-head)), so a wave holds dK^T / dV^T of its keys in 64
 // registers (32x32 tiles need 128) and two waves share each SIMD - the
