@@ -1145,7 +1145,11 @@ mxk_attn_bwd_dkdv_kernel(const uint16_t* __restrict__ q, const uint16_t* __restr
 // a pipelined 32-key-per-wave kernel (4 waves, one per SIMD, half the LDS
 // operand traffic, dK / dV pinned to AGPRs, softmax overlapped in-wave)
 // 1.182 vs 1.107 ms - two waves per SIMD hide more than the halved LDS
-// traffic saves.
+// traffic saves.  Also neutral: 128-query slices (half the barriers and
+// pipeline drains; 1.1249 vs 1.1215 ms, bit-identical).  A staggered order
+// for waves 4-7 (both S / dP groups first, so the SIMD partners' exp phases
+// do not coincide) needs ~16 more VGPRs than the 223 of this body and
+// spilled (119 VGPRs, 4.17 ms).
 // dK/dV with 16x16x32 MFMAs: one workgroup = 8 waves x 16 keys (128 keys of
 // one (batch, q-head)), so a wave holds dK^T / dV^T of its keys in 64
 // registers (32x32 tiles need 128) and two waves share each SIMD - the
