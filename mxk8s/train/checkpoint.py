@@ -69,6 +69,8 @@ def save(ckpt_dir: str, ddp, opt, step: int) -> None:
     sharded = bool(getattr(ddp, "sharded", False))
     os.makedirs(ckpt_dir, exist_ok=True)
     fp = layout_fingerprint(ddp.space)
+    if hasattr(opt, "synchronize"):
+        opt.synchronize()      # pending side-stream updates (FlatAdamW overlap)
     if sharded or rank == 0:
         _atomic_save({"master": opt.master, "exp_avg": opt.exp_avg, "exp_avg_sq": opt.exp_avg_sq},
                       os.path.join(ckpt_dir, f"optim-rank{rank if sharded else 0}.safetensors"),
@@ -92,6 +94,8 @@ def save(ckpt_dir: str, ddp, opt, step: int) -> None:
 def load(ckpt_dir: str, ddp, opt) -> int:
     """Restore parameters and optimizer state; returns the saved step."""
     world, rank, _ = mxdist.world_info()
+    if hasattr(opt, "synchronize"):
+        opt.synchronize()      # no side-stream update may land after the restore
     with open(os.path.join(ckpt_dir, "meta.json")) as f:
         meta = json.load(f)
     if meta.get("format") != "mxk8s-flat-v1":

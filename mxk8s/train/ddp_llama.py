@@ -48,10 +48,17 @@ def use_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
 
 
 def build(cfg: LlamaConfig, device: torch.device, bucket_mb: float, lr: float = 3e-4,
-          zero: bool = True):
+          zero: bool = True, overlap: bool | None = None):
     """Model + DDP + optimizer.  ``zero`` shards the AdamW state and step over
     the ranks (ZeRO-1, reduce-scatter + all-gather); it only applies with
-    more than one rank."""
+    more than one rank.  ``overlap`` (``MXK_OPT_OVERLAP=1``) runs the
+    unsharded AdamW on a side stream under the next forward
+    (``FlatAdamW.enable_overlap``); bit-identical, but measured neutral on
+    one MI355X (617-618 ms per step either way, profiles/r2_ddp/
+    opt_overlap_ab.log: the forward GEMMs leave no CU slots for the update
+    kernels), so off by default."""
+    if overlap is None:
+        overlap = os.environ.get("MXK_OPT_OVERLAP", "0") == "1"
     with torch.device(device):
         model = Llama(cfg)
     model = model.to(torch.bfloat16)
@@ -60,7 +67,21 @@ def build(cfg: LlamaConfig, device: torch.device, bucket_mb: float, lr: float = 
         opt = ShardedFlatAdamW(ddp, lr=lr)
     else:
         opt = FlatAdamW(ddp.space, lr=lr, grad_scale=ddp.grad_scale)
+        if overlap and device.type == "cuda":
+            opt.enable_overlap(overlap_stages(model))
     return model, ddp, opt
+
+
+def overlap_stages(model: Llama):
+    """AdamW stages in the order the forward reads parameters: the embedding
+    with every 1-D weight (the fused norms read the next layer's weight one
+    layer early), then each block's matrices, then the LM head."""
+    one_d = [p for p in model.parameters() if p.requires_grad and p.dim() < 2]
+    stages = [([model.embed.weight] + one_d, model.embed)]
+    for layer in model.layers:
+        stages.append(([p for p in layer.parameters() if p.dim() >= 2], layer))
+    stages.append(([model.lm_head.weight], model.lm_head))
+    return stages
 
 
 def train_step(model, ddp, opt, tokens) -> torch.Tensor:

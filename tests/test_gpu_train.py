@@ -88,3 +88,27 @@ def test_sharded_clip_kernels_vs_torch(cuda_device):
         clip = max_norm / (norm + 1e-6) if norm > max_norm else 1.0
         assert abs(out[1].item() - norm) <= 1e-4 * norm
         assert abs(out[0].item() - clip / world) <= 1e-4 * clip / world
+
+
+def test_overlapped_adamw_bit_identical(cuda_device):
+    """FlatAdamW.enable_overlap (AdamW on a side stream, each block's forward
+    waits for its own stage) gives bit-identical parameters, moments and
+    losses to the serial step, and covers every parameter."""
+    from mxk8s.train.ddp_llama import build, train_step
+    cfg = LlamaConfig.tiny()
+    tok = torch.randint(0, cfg.vocab_size, (2, 129), device=cuda_device,
+                        generator=torch.Generator(device=cuda_device).manual_seed(1))
+    runs = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        model, ddp, opt = build(cfg, cuda_device, bucket_mb=1.0, overlap=overlap)
+        assert (opt._stages is not None) == overlap
+        losses = [train_step(model, ddp, opt, tok) for _ in range(4)]
+        opt_sync = getattr(opt, "synchronize", None)
+        if opt_sync:
+            opt_sync()
+        torch.cuda.synchronize()
+        runs.append((torch.stack(losses).cpu(), ddp.space.param_buf.clone(), opt.exp_avg.clone(),
+                     opt.exp_avg_sq.clone(), opt.master.clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
