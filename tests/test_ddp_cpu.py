@@ -299,3 +299,21 @@ def test_checkpoint_rejects_interrupted_overwrite(tmp_path):
                              "save_step": 8})
     with pytest.raises(ValueError, match="shard does not match meta.json"):
         checkpoint.load(ck, ddp, opt)
+
+
+def test_overlap_stages_cover_every_parameter_once():
+    """The AdamW overlap plan (forward-need order) names every trainable
+    parameter exactly once, and each stage's ranges stay on one side of the
+    weight-decay boundary; on the CPU the overlap stays off."""
+    from mxk8s.train.ddp_llama import overlap_stages
+    model = Llama(LlamaConfig.tiny())
+    stages = overlap_stages(model)
+    ids = [id(p) for params, _ in stages for p in params]
+    assert len(ids) == len(set(ids)) == len([p for p in model.parameters() if p.requires_grad])
+    assert stages[0][1] is model.embed and stages[-1][1] is model.lm_head
+    assert [m for _, m in stages[1:-1]] == list(model.layers)
+    space = FlatParamSpace(model)
+    opt = FlatAdamW(space)
+    assert opt.enable_overlap(stages) is False and opt._stages is None
+    merged = opt._merge_ranges([(0, 10), (64, 100), (space.n_decay, space.n_decay + 4)])
+    assert all((a < space.n_decay) == (b <= space.n_decay) for a, b in merged)
