@@ -491,8 +491,19 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s1[r]);
       mx = half_max(mx);
-      const float m_new = fmaxf(m, mx);
-      const float alpha = fexp2((m - m_new) * c);
+      float m_new = fmaxf(m, mx);
+      bool grow = true;
+      if constexpr (PIPE) {
+        // Lazy rescale: keep the stale row max unless the new one exceeds it
+        // by more than 2^8 (log2 units).  P = exp2((s - m) c) then stays
+        // <= 256 - exact in bf16's exponent range - and l / acc stay
+        // consistent with the m they were built with (final o = acc / l,
+        // lse = m scale + ln l).  On random data almost every block after the
+        // first skips the 32 v_pk_mul of the accumulator rescale.
+        grow = (m_new - m) * c > 8.f;
+        if (!grow) m_new = m;
+      }
+      const float alpha = grow ? fexp2((m - m_new) * c) : 1.f;
       m = m_new;
       const f32x2_t nmc = {-m_new * c, -m_new * c};
       if constexpr (PIPE) {
@@ -501,7 +512,7 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
         // wave overlaps its own softmax with its own MFMAs)
 #pragma unroll
         for (int x = 8; x < 16; ++x) read_v(x);
-        if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+        if (__builtin_amdgcn_ballot_w64(grow)) {
 #pragma unroll
           for (int db = 0; db < 4; ++db)
 #pragma unroll
@@ -609,16 +620,18 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
 // ---------------------------------------------------------------------------
 // variant: 0 = register-staged K/V, 1 = LDS-DMA with the loop unrolled by 2
 // (static LDS buffer), 2 = LDS-DMA, 3 = 2 with the PIPE body (operands read a
-// group ahead, exp of P chunk ks+1 under the PV MFMAs of chunk ks; default).
-// 1-3 fall back to 0 when a K/V panel exceeds the 32-bit buffer range.  B=8
-// Llama shape: 0.42 / 0.43 / 0.38 ms (profiles/r1_attention/); 2 -> 3:
-// 0.3385 -> 0.3312 ms (profiles/r2_attention/).
+// group ahead, exp of P chunk ks+1 under the PV MFMAs of chunk ks, lazy
+// rescale), 4 = 3 unrolled by 2 (default: the per-iteration v_or of the
+// buffer base into 22 LDS addresses disappears).  1-4 fall back to 0 when a
+// K/V panel exceeds the 32-bit buffer range.  B=8 Llama shape: 0.42 / 0.43 /
+// 0.38 ms (profiles/r1_attention/); round 2: 2 / 3 / 4 = 0.3387 / 0.3218 /
+// 0.3133 ms (profiles/r2_attention/fwd_lazy_rescale_unroll_ab.log).
 MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, void* o, float* lse,
                                  int B, int S, int Hq, int Hkv, int head_dim, long q_tok,
                                  long k_tok, long v_tok, float scale, int causal, int variant,
                                  hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv ||
-      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 3 ||
+      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 4 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) % 16)
     return static_cast<int>(hipErrorInvalidValue);
@@ -629,7 +642,14 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
   const auto* kp = static_cast<const uint16_t*>(k);
   const auto* vp = static_cast<const uint16_t*>(v);
   auto* op = static_cast<uint16_t*>(o);
-  if (variant == 3) {
+  if (variant == 4) {
+    if (causal)
+      hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<true, true, true>), dim3(nwg), dim3(NT), 0, stream,
+                         qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    else
+      hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<false, true, true>), dim3(nwg), dim3(NT), 0,
+                         stream, qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  } else if (variant == 3) {
     if (causal)
       hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<true, false, true>), dim3(nwg), dim3(NT), 0, stream,
                          qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
@@ -724,7 +744,7 @@ mxk_attn_bwd_delta_kernel(const uint16_t* __restrict__ o, const uint16_t* __rest
 // kernel's piece mapping, destinations bound to M0) instead of register
 // staging - frees the 32 staging VGPRs that made this kernel spill at two
 // waves per SIMD, and the ds_writes.  Requires S * token_stride * 2 < 2^32.
-template <bool CAUSAL, bool DMA = false, bool PIPE = false>
+template <bool CAUSAL, bool DMA = false, bool PIPE = false, bool UNROLL = false>
 __global__ void __launch_bounds__(NT, 2)
 mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                        const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
@@ -833,6 +853,7 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   const int tr_ch = 2 * (G & 1) + ((i16 & 3) >> 1);
   const int tr_byte = 8 * (i16 & 1);
 
+  if constexpr (!UNROLL) {
   for (int j = 0; j < nkv; ++j) {
     const int buf = j & 1;
     // DMA: buffer buf^1 was last read in iteration j-1 (barrier-certified)
@@ -952,6 +973,133 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
       if (j + 1 < nkv) store_tile(buf ^ 1);
     }
     __syncthreads();
+  }
+  } else {
+  // UNROLL: the loop body as a lambda called with a compile-time buffer, so
+  // the LDS read addresses are loop invariants (as in the forward's variant 4)
+  auto step = [&](int j, int buf) {
+    // DMA: buffer buf^1 was last read in iteration j-1 (barrier-certified)
+    if (j + 1 < nkv) {
+      if constexpr (DMA) issue(j + 1, buf ^ 1);
+      else load_tile(j + 1);
+    }
+    const int kv0 = j * BKV;
+    if (!CAUSAL || kv0 <= qw0 + 31) {
+      const char* kt = smem[buf];
+      const char* vt = smem[buf] + TILE_BYTES;
+      const bool diag = CAUSAL && kv0 + BKV - 1 > qw0;
+      if constexpr (PIPE) {
+        // software-pipelined as the dK/dV kernel's PIPE body: S / dP operands
+        // read a half (4 k-steps) ahead, dS-side transposed reads issued
+        // under the exp, the next half's first operands under the dQ MFMAs
+        bf16x8_t ka[2][2], va[2][2];    // ring of two k-step pairs
+        auto read_p = [&](int kh, int pr, int slot) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int s = 2 * pr + e;
+            ka[slot][e] = lds_b128(kt + swz(32 * kh + r32, 2 * s + h));
+            va[slot][e] = lds_b128(vt + swz(32 * kh + r32, 2 * s + h));
+          }
+        };
+        auto read_t = [&](int kh, int db, int kk) {
+          const int key = 32 * kh + 16 * kk + tr_key;
+          const int ch = 4 * db + tr_ch;
+          return cat8(lds_tr_b64(kt + swz(key, ch) + tr_byte), lds_tr_b64(kt + swz(key + 8, ch) + tr_byte));
+        };
+        read_p(0, 0, 0);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          __builtin_amdgcn_sched_barrier(0);
+          f32x16_t s0, p0;
+          zero16(s0);
+          zero16(p0);
+          bf16x8_t ta[8];
+#pragma unroll
+          for (int pr = 0; pr < 4; ++pr) {
+            if (pr < 3) {
+              read_p(kh, pr + 1, (pr + 1) & 1);
+            } else {
+#pragma unroll
+              for (int x = 0; x < 4; ++x) ta[x] = read_t(kh, x >> 1, x & 1);
+            }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              s0 = mfma32(ka[pr & 1][e], qf[2 * pr + e], s0);
+              p0 = mfma32(va[pr & 1][e], dof[2 * pr + e], p0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#pragma unroll
+          for (int x = 4; x < 8; ++x) ta[x] = read_t(kh, x >> 1, x & 1);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float e0 = fexp2(fmaf(s0[r], c, -lse2));
+            if (diag && kv0 + 32 * kh + crow(r, h) > myq) e0 = 0.f;
+            s0[r] = e0 * (p0[r] - dlt);   // dS^T
+          }
+          bf16x8_t df[2];
+          df[0] = pack8(s0, 0);
+          df[1] = pack8(s0, 8);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int x = 0; x < 8; ++x) {
+            acc[x >> 1] = mfma32(ta[x], df[x & 1], acc[x >> 1]);
+            if (kh == 0 && x == 5) {
+              read_p(1, 0, 0);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
+      } else {
+      // one 32-key half at a time keeps S^T / dP^T to 32 registers
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        f32x16_t s0, p0;
+        zero16(s0);
+        zero16(p0);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8_t kf = lds_b128(kt + swz(32 * kh + r32, 2 * s + h));
+          const bf16x8_t vf = lds_b128(vt + swz(32 * kh + r32, 2 * s + h));
+          s0 = mfma32(kf, qf[s], s0);
+          p0 = mfma32(vf, dof[s], p0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float e0 = fexp2(fmaf(s0[r], c, -lse2));
+          if (diag && kv0 + 32 * kh + crow(r, h) > myq) e0 = 0.f;
+          s0[r] = e0 * (p0[r] - dlt);   // dS^T
+        }
+        bf16x8_t df[2];
+        df[0] = pack8(s0, 0);
+        df[1] = pack8(s0, 8);
+        // dQ^T += K^T . dS^T  (K^T by transposed reads of the K image)
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const int key = 32 * kh + 16 * kk + tr_key;
+            const int ch = 4 * db + tr_ch;
+            const bf16x4_t lo = lds_tr_b64(kt + swz(key, ch) + tr_byte);
+            const bf16x4_t hi = lds_tr_b64(kt + swz(key + 8, ch) + tr_byte);
+            const bf16x8_t a = cat8(lo, hi);
+            acc[db] = mfma32(a, df[kk], acc[db]);
+          }
+        }
+      }
+      }
+    }
+    if constexpr (DMA) {
+      vm_wait0();   // own pieces of tile j+1
+    } else {
+      if (j + 1 < nkv) store_tile(buf ^ 1);
+    }
+    __syncthreads();
+  };
+  for (int j = 0; j < nkv; j += 2) {
+    step(j, 0);
+    if (j + 1 < nkv) step(j + 1, 1);
+  }
   }
   uint16_t* row = dq + (static_cast<long>(b) * S + myq) * Hq * D + static_cast<long>(hq) * D;
 #pragma unroll
@@ -1575,15 +1723,16 @@ MXK_API long mxk_attn_bwd_workspace(int B, int S, int Hq) {
 // kernels (register-staged when a panel exceeds the 32-bit buffer range);
 // 3: variant 2 with the explicitly software-pipelined (PIPE) dK/dV and dQ
 // bodies, bit-identical to 2 (default; 1.262 -> 1.070 ms per Llama-3-8B
-// layer, profiles/r2_attention/); 0: per query head + fp32 partials + GQA
-// reduce.
+// layer, profiles/r2_attention/); 4: 3 with the dQ loop unrolled by two
+// (compile-time LDS buffer), bit-identical and within noise (1.1487 vs
+// 1.1525 ms); 0: per query head + fp32 partials + GQA reduce.
 MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, const void* o,
                                  const void* dout, const float* lse, void* dq, void* dk, void* dv,
                                  void* workspace, int B, int S, int Hq, int Hkv, int head_dim,
                                  long q_tok, long k_tok, long v_tok, long dk_tok, long dv_tok,
                                  float scale, int causal, int variant, hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv || q_tok % 8 ||
-      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 3 ||
+      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 4 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
        reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
@@ -1605,11 +1754,11 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
   const int nwg = B * Hq * (S / BQ);
   const int nwg_kv = B * Hkv * (S / BQ);
   const long qspan = static_cast<long>(S) * (q_tok > static_cast<long>(Hq) * D ? q_tok : Hq * D) * 2;
-  if (variant == 3 && causal && qspan < (1L << 32)) {
+  if (variant >= 3 && causal && qspan < (1L << 32)) {
     hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<true, true, true, true>), dim3(nwg_kv),
                        dim3(NT16), 0, stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok,
                        k_tok, v_tok, scale, dK, dV, dk_tok, dv_tok);
-  } else if (variant == 3 && qspan < (1L << 32)) {
+  } else if (variant >= 3 && qspan < (1L << 32)) {
     hipLaunchKernelGGL((mxk_attn_bwd_dkdv16_kernel<false, true, true, true>), dim3(nwg_kv),
                        dim3(NT16), 0, stream, Q, K, V, dO, lse, delta, dk_p, dv_p, S, Hq, Hkv, q_tok,
                        k_tok, v_tok, scale, dK, dV, dk_tok, dv_tok);
@@ -1642,10 +1791,13 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
   const long span = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
   const bool dq_dma = variant >= 2 && span < (1L << 32);
   auto* dQ = static_cast<uint16_t*>(dq);
-  if (causal && dq_dma && variant == 3)
+  if (causal && dq_dma && variant == 4)
+    hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<true, true, true, true>), dim3(nwg), dim3(NT), 0,
+                       stream, Q, K, V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  else if (causal && dq_dma && variant == 3)
     hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<true, true, true>), dim3(nwg), dim3(NT), 0, stream,
                        Q, K, V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
-  else if (dq_dma && variant == 3)
+  else if (dq_dma && variant >= 3)
     hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<false, true, true>), dim3(nwg), dim3(NT), 0, stream,
                        Q, K, V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
   else if (causal && dq_dma)

@@ -29,7 +29,7 @@ def _qkv(B, S, Hq, Hkv, dev, seed=0, fused=False):
     (1, 256, 4, 1, False, True),
     (1, 2048, 32, 8, True, True),     # the Llama-3-8B step's attention shape (B = 1)
 ])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_attn_fwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused, variant):
     q, k, v = _qkv(B, S, Hq, Hkv, cuda_device, fused=fused)
     assert A.supported(q, k, v)
@@ -70,7 +70,7 @@ def test_attn_bwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
         assert err < tol, (name, err, tol)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
     (1, 256, 8, 2, True),
     (2, 384, 4, 1, True),
