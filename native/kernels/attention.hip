@@ -910,11 +910,14 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
 #pragma unroll
           for (int x = 4; x < 8; ++x) ta[x] = read_t(kh, x >> 1, x & 1);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float e0 = fexp2(fmaf(s0[r], c, -lse2));
-            if (diag && kv0 + 32 * kh + crow(r, h) > myq) e0 = 0.f;
-            s0[r] = e0 * (p0[r] - dlt);   // dS^T
+          for (int r = 0; r < 16; ++r) s0[r] = fexp2(fmaf(s0[r], c, -lse2));   // P^T
+          if (diag) {   // wave-uniform: only diagonal tiles pay for the mask
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (kv0 + 32 * kh + crow(r, h) > myq) s0[r] = 0.f;
           }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s0[r] *= p0[r] - dlt;   // dS^T
           bf16x8_t df[2];
           df[0] = pack8(s0, 0);
           df[1] = pack8(s0, 8);
@@ -1032,11 +1035,14 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
 #pragma unroll
           for (int x = 4; x < 8; ++x) ta[x] = read_t(kh, x >> 1, x & 1);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float e0 = fexp2(fmaf(s0[r], c, -lse2));
-            if (diag && kv0 + 32 * kh + crow(r, h) > myq) e0 = 0.f;
-            s0[r] = e0 * (p0[r] - dlt);   // dS^T
+          for (int r = 0; r < 16; ++r) s0[r] = fexp2(fmaf(s0[r], c, -lse2));   // P^T
+          if (diag) {   // wave-uniform: only diagonal tiles pay for the mask
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (kv0 + 32 * kh + crow(r, h) > myq) s0[r] = 0.f;
           }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s0[r] *= p0[r] - dlt;   // dS^T
           bf16x8_t df[2];
           df[0] = pack8(s0, 0);
           df[1] = pack8(s0, 8);
@@ -1569,15 +1575,20 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
           for (int db = 0; db < 4; ++db) read_b(ks, db, &ob[db], &qb[db]);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
+          for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float e = fexp2(st[h][r] * c);
-              if (diag && mykey > qs0 + 32 * ks + 16 * h + 4 * G + r) e = 0.f;
-              st[h][r] = e;                  // P
-              pt[h][r] = e * pt[h][r];       // dS
-            }
+            for (int r = 0; r < 4; ++r) st[h][r] = fexp2(st[h][r] * c);   // P
+          if (diag) {   // wave-uniform: only diagonal slices pay for the mask
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (mykey > qs0 + 32 * ks + 16 * h + 4 * G + r) st[h][r] = 0.f;
           }
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pt[h][r] *= st[h][r];   // dS
           const bf16x8_t pf = pack2x4(st[0], st[1]);
           const bf16x8_t sf = pack2x4(pt[0], pt[1]);
           __builtin_amdgcn_sched_barrier(0);
