@@ -909,15 +909,26 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
           }
 #pragma unroll
           for (int x = 4; x < 8; ++x) ta[x] = read_t(kh, x >> 1, x & 1);
+          // packed fp32 (v_pk_fma / v_pk_add / v_pk_mul): half the VALU issues
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s0[r] = fexp2(fmaf(s0[r], c, -lse2));   // P^T
+          for (int r = 0; r < 16; r += 2) {
+            f32x2_t x = {s0[r], s0[r + 1]};
+            x = __builtin_elementwise_fma(x, f32x2_t{c, c}, f32x2_t{-lse2, -lse2});
+            s0[r] = fexp2(x[0]);   // P^T
+            s0[r + 1] = fexp2(x[1]);
+          }
           if (diag) {   // wave-uniform: only diagonal tiles pay for the mask
 #pragma unroll
             for (int r = 0; r < 16; ++r)
               if (kv0 + 32 * kh + crow(r, h) > myq) s0[r] = 0.f;
           }
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s0[r] *= p0[r] - dlt;   // dS^T
+          for (int r = 0; r < 16; r += 2) {
+            const f32x2_t pp = f32x2_t{p0[r], p0[r + 1]} - f32x2_t{dlt, dlt};
+            const f32x2_t d = f32x2_t{s0[r], s0[r + 1]} * pp;   // dS^T
+            s0[r] = d[0];
+            s0[r + 1] = d[1];
+          }
           bf16x8_t df[2];
           df[0] = pack8(s0, 0);
           df[1] = pack8(s0, 8);
@@ -1034,15 +1045,26 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
           }
 #pragma unroll
           for (int x = 4; x < 8; ++x) ta[x] = read_t(kh, x >> 1, x & 1);
+          // packed fp32 (v_pk_fma / v_pk_add / v_pk_mul): half the VALU issues
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s0[r] = fexp2(fmaf(s0[r], c, -lse2));   // P^T
+          for (int r = 0; r < 16; r += 2) {
+            f32x2_t x = {s0[r], s0[r + 1]};
+            x = __builtin_elementwise_fma(x, f32x2_t{c, c}, f32x2_t{-lse2, -lse2});
+            s0[r] = fexp2(x[0]);   // P^T
+            s0[r + 1] = fexp2(x[1]);
+          }
           if (diag) {   // wave-uniform: only diagonal tiles pay for the mask
 #pragma unroll
             for (int r = 0; r < 16; ++r)
               if (kv0 + 32 * kh + crow(r, h) > myq) s0[r] = 0.f;
           }
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s0[r] *= p0[r] - dlt;   // dS^T
+          for (int r = 0; r < 16; r += 2) {
+            const f32x2_t pp = f32x2_t{p0[r], p0[r + 1]} - f32x2_t{dlt, dlt};
+            const f32x2_t d = f32x2_t{s0[r], s0[r + 1]} * pp;   // dS^T
+            s0[r] = d[0];
+            s0[r + 1] = d[1];
+          }
           bf16x8_t df[2];
           df[0] = pack8(s0, 0);
           df[1] = pack8(s0, 8);
@@ -1577,7 +1599,11 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
 #pragma unroll
           for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) st[h][r] = fexp2(st[h][r] * c);   // P
+            for (int r = 0; r < 4; r += 2) {
+              const f32x2_t x = f32x2_t{st[h][r], st[h][r + 1]} * f32x2_t{c, c};
+              st[h][r] = fexp2(x[0]);   // P
+              st[h][r + 1] = fexp2(x[1]);
+            }
           if (diag) {   // wave-uniform: only diagonal slices pay for the mask
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -1588,7 +1614,11 @@ mxk_attn_bwd_dkdv16_kernel(const uint16_t* __restrict__ q, const uint16_t* __res
 #pragma unroll
           for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) pt[h][r] *= st[h][r];   // dS
+            for (int r = 0; r < 4; r += 2) {
+              const f32x2_t d = f32x2_t{pt[h][r], pt[h][r + 1]} * f32x2_t{st[h][r], st[h][r + 1]};
+              pt[h][r] = d[0];   // dS
+              pt[h][r + 1] = d[1];
+            }
           const bf16x8_t pf = pack2x4(st[0], st[1]);
           const bf16x8_t sf = pack2x4(pt[0], pt[1]);
           __builtin_amdgcn_sched_barrier(0);
