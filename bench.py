@@ -214,8 +214,9 @@ def run_allreduce(args, dev, world, rank) -> dict:
 
 def ab_other_sizes(args, dev, timer) -> list:
     """The protocol's other square sizes (context for the headline shape):
-    hand-written kernel vs hipBLASLt, A/B-interleaved hipEvent medians after a
-    short warm-up on the warm chip, output checked against fp32."""
+    hand-written kernel vs hipBLASLt, A/B-interleaved blocks of back-to-back
+    launches (median of 8 blocks per kernel) after a short warm-up on the
+    warm chip, output checked against fp32."""
     import torch
 
     from mxk8s.ops import gemm_bf16_tn
@@ -238,16 +239,20 @@ def ab_other_sizes(args, dev, timer) -> list:
             for f in fns.values():
                 f()
             _sync(dev)
+        # blocks of back-to-back launches bracketed by one event pair: at
+        # 4096^3 a launch is ~0.1 ms, and an event record plus a Python call
+        # per launch let the host fall behind the GPU (per-launch events put
+        # both kernels ~4 % below their back-to-back rate, unevenly)
         ts = {k: [] for k in fns}
         reps = max(8, min(40, int(40 * (8192 / n) ** 3)))
-        for r in range(4):
+        for r in range(8):
             for k in (("mxk", "hipblaslt") if r % 2 == 0 else ("hipblaslt", "mxk")):
-                mk = timer.marks(reps + 1)
-                for i in range(reps):
-                    timer.record(mk, i)
+                mk = timer.marks(2)
+                timer.record(mk, 0)
+                for _ in range(reps):
                     fns[k]()
-                timer.record(mk, reps)
-                ts[k] += timer.elapsed_ms(mk)
+                timer.record(mk, 1)
+                ts[k].append(timer.elapsed_ms(mk)[0] / reps)
         med = {k: statistics.median(v) for k, v in ts.items()}
         fl = 2.0 * n ** 3
         out.append({"M": n, "N": n, "K": n, "check_ok": bool(err <= tol),

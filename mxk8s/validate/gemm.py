@@ -29,16 +29,20 @@ from ..utils import roctx
 
 
 def _events_time(fn, iters: int) -> list[float]:
-    times = []
+    """Seconds per launch over one block of ``iters`` back-to-back launches.
+
+    (Until round 2 each launch was timed alone with a synchronize after it:
+    every kernel then started on an idle GPU, which at 4096^3 (~0.1 ms)
+    costs hipBLASLt ~13 % and this kernel ~3 %, and made the hand-written
+    kernel look 9-10 % ahead there; back to back it is 3 % behind.)"""
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
     for _ in range(iters):
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
-        s.record()
         fn()
-        e.record()
-        e.synchronize()
-        times.append(s.elapsed_time(e) * 1e-3)
-    return times
+    e.record()
+    e.synchronize()
+    return [s.elapsed_time(e) * 1e-3 / iters]
 
 
 def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,

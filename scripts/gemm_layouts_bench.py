@@ -15,19 +15,29 @@ VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1").split(",")]
 SHAPES = [(4096, 6144, "wqkv"), (4096, 4096, "wo"), (4096, 28672, "w13"), (14336, 4096, "w2")]
 
 
-def timeit(fn, iters=30):
-    for _ in range(5):
-        fn()
+def timeit(fns, iters=30, rounds=6):
+    """Median seconds-per-launch of each fn over A/B-interleaved blocks of
+    back-to-back launches (one event pair per block: a synchronize after
+    every launch starts each kernel on an idle GPU and biases small and
+    medium GEMMs, hipBLASLt's more than this kernel's)."""
+    for f in fns:
+        for _ in range(5):
+            f()
     torch.cuda.synchronize()
-    ts = []
-    for _ in range(iters):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        fn()
-        e.record()
-        e.synchronize()
-        ts.append(s.elapsed_time(e))
-    return statistics.median(ts)
+    ts = [[] for _ in fns]
+    for r in range(rounds):
+        order = list(range(len(fns)))
+        if r % 2:
+            order.reverse()
+        for i in order:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(iters):
+                fns[i]()
+            e.record()
+            e.synchronize()
+            ts[i].append(s.elapsed_time(e) / iters)
+    return [statistics.median(t) for t in ts]
 
 
 def main():
@@ -49,6 +59,7 @@ def main():
             K = din if kind == "fwd" else (dout if kind == "dgrad" else T)
             flops = 2.0 * shp[0] * shp[1] * K
             res = {"gemm": f"{name}.{kind}", "M": shp[0], "N": shp[1], "K": K}
+            fns, names = [], []
             for v in VARIANTS:
                 out.zero_()
                 ok = gemm_bf16_ex(a, b, ak, bk, out, variant=v)
@@ -58,9 +69,16 @@ def main():
                 rel = ((out.float() - ref.float()).norm() / ref.float().norm()).item()
                 if not rel < 1e-2:
                     raise SystemExit(f"{name}.{kind} variant {v}: wrong result rel {rel}")
-                t = timeit(lambda: gemm_bf16_ex(a, b, ak, bk, out, variant=v))
-                res[f"mxk_v{v}_tflops"] = round(flops / t / 1e9, 1)
-            res["hipblaslt_tflops"] = round(flops / timeit(ref_fn) / 1e9, 1)
+                fns.append(lambda v=v: gemm_bf16_ex(a, b, ak, bk, out, variant=v))
+                names.append(f"mxk_v{v}_tflops")
+            out2 = torch.empty(shp, device=dev, dtype=torch.bfloat16)
+            blas = {"fwd": lambda: torch.matmul(x, w.t(), out=out2),
+                    "dgrad": lambda: torch.matmul(dy, w, out=out2),
+                    "wgrad": lambda: torch.matmul(dy.t(), x, out=out2)}[kind]
+            fns.append(blas)
+            names.append("hipblaslt_tflops")
+            for nm, t in zip(names, timeit(fns)):
+                res[nm] = round(flops / t / 1e9, 1)
             print("RESULT " + json.dumps(res), flush=True)
 
 
