@@ -112,6 +112,14 @@ VALUES: dict = {
                  "interval": F("integer", "seconds", minimum=1, maximum=3600),
                  "privileged": F("boolean"), "podResources": F("boolean"),
                  "service": {"type": F("string", "", enum=["ClusterIP", "NodePort", "LoadBalancer"])},
+                 "serviceMonitor": {
+                     "enabled": F("boolean", "create a Prometheus-operator ServiceMonitor "
+                                             "(dcgm-exporter serviceMonitor counterpart)"),
+                     "interval": F("string", "scrape interval", pattern=r"^[0-9]+(ms|s|m)$"),
+                     "honorLabels": F("boolean", "keep the exporter's gpu / pod labels on clashes"),
+                     "additionalLabels": F("object", "extra labels (e.g. the Prometheus selector)",
+                                           items={"type": "object",
+                                                  "additionalProperties": {"type": "string"}})},
                  "resources": RESOURCES},
     "validator": {"enabled": F("boolean"),
                   "gpus": F("integer", "amd.com/gpu requested by the validator pod", minimum=1,

@@ -50,7 +50,8 @@ POLICY_LABEL = "mxk8s.io/policy"
 OPERAND_KINDS = [("apps/v1", "DaemonSet"), ("v1", "Service"), ("v1", "ConfigMap"),
                  ("batch/v1", "Job"), ("v1", "ServiceAccount"),
                  ("rbac.authorization.k8s.io/v1", "ClusterRole"),
-                 ("rbac.authorization.k8s.io/v1", "ClusterRoleBinding")]
+                 ("rbac.authorization.k8s.io/v1", "ClusterRoleBinding"),
+                 ("monitoring.coreos.com/v1", "ServiceMonitor")]   # 404 without the CRD: skipped
 
 
 def is_subset(want, have) -> bool:

@@ -102,6 +102,29 @@ def test_chart_values_overrides():
         render.render(render.load_values(sets=["validator.gpus=9"]))
 
 
+def test_chart_service_monitor():
+    """exporter.serviceMonitor (dcgm-exporter serviceMonitor counterpart):
+    off by default; on, a ServiceMonitor selects the metrics Service's port."""
+    assert not [d for d in _docs(render.load_values()) if d["kind"] == "ServiceMonitor"]
+    v = render.load_values(sets=["exporter.serviceMonitor.enabled=true",
+                                 "exporter.serviceMonitor.interval=30s"])
+    v["exporter"]["serviceMonitor"]["additionalLabels"] = {"release": "kube-prometheus-stack"}
+    docs = _docs(v)
+    sm = next(d for d in docs if d["kind"] == "ServiceMonitor")
+    svc = next(d for d in docs if d["kind"] == "Service")
+    assert sm["apiVersion"] == "monitoring.coreos.com/v1"
+    assert sm["metadata"]["labels"]["release"] == "kube-prometheus-stack"
+    assert sm["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
+    ep = sm["spec"]["endpoints"][0]
+    assert ep["port"] == svc["spec"]["ports"][0]["name"] == "metrics"
+    assert ep["interval"] == "30s" and ep["honorLabels"] is False
+    assert sm["spec"]["namespaceSelector"]["matchNames"] == [svc["metadata"]["namespace"]]
+    # schema: a malformed interval is rejected
+    from mxk8s import config
+    errs = config.validate_values(render.load_values(sets=["exporter.serviceMonitor.interval=soon"]))
+    assert any("serviceMonitor.interval" in e for e in errs), errs
+
+
 def test_chart_time_slicing_args():
     v = render.load_values(sets=["devicePlugin.sharing.timeSlicing.replicas=4",
                                  "devicePlugin.sharing.timeSlicing.failRequestsGreaterThanOne=true"])

@@ -149,3 +149,18 @@ def test_is_subset():
     assert not op.is_subset({"a": 1}, {"a": 2})
     assert not op.is_subset({"b": [1, 2]}, {"b": [1]})
     assert op.is_subset({"port": 9400}, {"port": "9400"})
+
+
+def test_service_monitor_operand_created_and_collected(api):
+    """exporter.serviceMonitor in the policy: the operator applies the
+    ServiceMonitor (monitoring.coreos.com) and collects it when turned off."""
+    sm = f"/apis/monitoring.coreos.com/v1/namespaces/{NS}/servicemonitors/amd-gpu-stack-metrics"
+    _policy(api, {"exporter": {"serviceMonitor": {"enabled": True, "interval": "30s"}}})
+    ctl = op.Controller(KubeClient(api.url), NS)
+    r = ctl.reconcile_once()
+    assert "ServiceMonitor/amd-gpu-stack-metrics" in r.created
+    assert api.objects[sm]["spec"]["endpoints"][0]["interval"] == "30s"
+    api.objects[POL]["spec"] = {}
+    api.objects[POL]["metadata"]["generation"] = 2
+    r = ctl.reconcile_once()
+    assert "ServiceMonitor/amd-gpu-stack-metrics" in r.deleted and sm not in api.objects
