@@ -227,3 +227,15 @@ def test_pod_uid_from_cgroup(tmp_path):
         "12:memory:/kubepods/burstable/pod0b1c2d3e-aaaa-bbbb-cccc-0123456789ab/deadbeef\n")
     assert pod_uid_of(43, str(tmp_path)) == "0b1c2d3e-aaaa-bbbb-cccc-0123456789ab"
     assert pod_uid_of(44, str(tmp_path)) is None
+
+
+def test_metrics_doc_names_exist():
+    """Every exporter series named in docs/METRICS.md is one the exporter emits."""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    doc = open(os.path.join(root, "docs", "METRICS.md")).read()
+    src = open(os.path.join(root, "mxk8s", "exporter", "__init__.py")).read()
+    named = set(re.findall(r"\b(amd_gpu_[a-z_]+)", doc))
+    assert named
+    missing = sorted(n for n in named if f'"{n}"' not in src)
+    assert not missing, missing
