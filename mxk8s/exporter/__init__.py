@@ -245,6 +245,10 @@ def render_metrics(gpus, samples: dict, health: Callable[[int], int], owners: di
                       float(val), {**base, "sensor": sensor})
         w.add("amd_gpu_power_watts", "gauge", "Socket power (W).", s.power_w, base)
         w.add("amd_gpu_power_limit_watts", "gauge", "Power cap (W).", s.power_limit_w, base)
+        if getattr(s, "energy_j", None) is not None:
+            w.add("amd_gpu_energy_joules_total", "counter",
+                  "Energy consumed since the driver loaded (J, amd-smi accumulator).",
+                  round(s.energy_j, 3), base)
         w.add("amd_gpu_clock_mhz", "gauge", "Current clock (MHz).", s.sclk_mhz, {**base, "type": "sclk"})
         w.add("amd_gpu_clock_mhz", "gauge", "Current clock (MHz).", s.mclk_mhz, {**base, "type": "mclk"})
         w.add("amd_gpu_ecc_errors_total", "counter", "Accumulated ECC errors.", s.ecc_correctable,

@@ -63,6 +63,7 @@ class _Sample(ctypes.Structure):
         ("mclk_mhz", ctypes.c_uint32), ("ecc_correctable", ctypes.c_uint64),
         ("ecc_uncorrectable", ctypes.c_uint64), ("num_processes", ctypes.c_uint32),
         ("bdf", ctypes.c_char * 20), ("partition_id", ctypes.c_int),
+        ("energy_j", ctypes.c_double),
     ]
 
 
@@ -176,6 +177,7 @@ class GpuSample:
     num_processes: int
     bdf: str
     partition_id: int = 0
+    energy_j: Optional[float] = None    # accumulated since driver load; None if unsupported
 
     @property
     def key(self) -> str:
@@ -378,7 +380,8 @@ def smi_sample(i: int) -> GpuSample:
                      power_w=s.power_w, power_limit_w=s.power_limit_w, sclk_mhz=s.sclk_mhz,
                      mclk_mhz=s.mclk_mhz, ecc_correctable=s.ecc_correctable,
                      ecc_uncorrectable=s.ecc_uncorrectable, num_processes=s.num_processes,
-                     bdf=s.bdf.decode(), partition_id=s.partition_id)
+                     bdf=s.bdf.decode(), partition_id=s.partition_id,
+                     energy_j=s.energy_j if s.energy_j >= 0 else None)
 
 
 def smi_wait_events(timeout_ms: int, max_events: int = 32) -> list[tuple[int, int]]:

@@ -195,6 +195,7 @@ typedef struct mx_gpu_sample {
   uint32_t num_processes;
   char bdf[20];
   int partition_id;                 // amd-smi BDFID bits 31:28 (0 in SPX mode)
+  double energy_j;                  // accumulated energy (J) since driver load, < 0 if unsupported
 } mx_gpu_sample;
 
 // 1 if amd-smi could be loaded and initialised, 0 otherwise (msg in err).

@@ -46,6 +46,7 @@ struct SmiApi {
   MX_SMI_FN(amdsmi_stop_gpu_event_notification);
   MX_SMI_FN(amdsmi_get_gpu_xgmi_link_status);
   MX_SMI_FN(amdsmi_get_link_metrics);
+  MX_SMI_FN(amdsmi_get_energy_count);
   std::vector<amdsmi_processor_handle> gpus;
   bool events_on = false;
   std::string driver_version;
@@ -105,6 +106,8 @@ extern "C" int mx_smi_open(char* err, size_t errlen) {
   // xGMI link state / traffic: optional too (guest / older amd-smi)
   bind(h, "amdsmi_get_gpu_xgmi_link_status", &api->amdsmi_get_gpu_xgmi_link_status);
   bind(h, "amdsmi_get_link_metrics", &api->amdsmi_get_link_metrics);
+  // energy accumulator: optional (dcgm-exporter's total-energy counterpart)
+  bind(h, "amdsmi_get_energy_count", &api->amdsmi_get_energy_count);
   if (!ok) {
     mx::set_err(err, errlen, "libamd_smi.so lacks required symbols");
     dlclose(h);
@@ -170,6 +173,7 @@ extern "C" int mx_smi_sample(int i, mx_gpu_sample* o) {
   std::memset(o, 0, sizeof(*o));
   o->index = i;
   o->temp_edge_mc = o->temp_hotspot_mc = o->temp_mem_mc = INT64_MIN;
+  o->energy_j = -1.0;
   if (!g_api || i < 0 || i >= static_cast<int>(g_api->gpus.size())) return 0;
   SmiApi& a = *g_api;
   amdsmi_processor_handle h = a.gpus[i];
@@ -200,6 +204,12 @@ extern "C" int mx_smi_sample(int i, mx_gpu_sample* o) {
                                         : (p.socket_power ? p.socket_power : p.average_socket_power);
     // ROCm 7.2 amd-smi reports power_limit in microwatts on MI355X (1.4e9 = 1400 W)
     o->power_limit_w = p.power_limit > 100000u ? p.power_limit / 1000000u : p.power_limit;
+  }
+  if (a.amdsmi_get_energy_count) {
+    uint64_t acc = 0, ts = 0;
+    float res = 0.f;   // microjoules per count
+    if (a.amdsmi_get_energy_count(h, &acc, &res, &ts) == AMDSMI_STATUS_SUCCESS && res > 0.f)
+      o->energy_j = static_cast<double>(acc) * res * 1e-6;
   }
   amdsmi_clk_info_t c;
   std::memset(&c, 0, sizeof(c));

@@ -7,7 +7,7 @@
 //                                  key=value pairs (re-read on every call):
 //       bdf=0000:05:00.0 gfx=37 umc=12 vram_used=<B> vram_total=<B>
 //       temp_edge=41 temp_hotspot=55 temp_mem=48 power=612 power_limit=1400
-//       sclk=2100 mclk=1300 ecc_ce=0 ecc_ue=0
+//       sclk=2100 mclk=1300 ecc_ce=0 ecc_ue=0 energy=<uJ>
 //       xgmi_status=1,1,1,1,1,1,0      (per link: 0 down, 1 up, 2 disabled)
 //       xgmi_read_kb=10,20,...         (per link cumulative KB)
 //       xgmi_write_kb=...  xgmi_bitrate=32  xgmi_maxbw=64
@@ -197,6 +197,20 @@ amdsmi_status_t amdsmi_get_power_info(amdsmi_processor_handle h, amdsmi_power_in
   std::memset(p, 0, sizeof(*p));
   p->current_socket_power = static_cast<uint32_t>(num(g, "power"));
   p->power_limit = static_cast<uint32_t>(num(g, "power_limit", 1400));
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+// energy=<uJ> (absent: unsupported); the real library reports counts of
+// ~15.3 uJ, so the fake uses the same resolution
+amdsmi_status_t amdsmi_get_energy_count(amdsmi_processor_handle h, uint64_t* acc, float* res,
+                                        uint64_t* ts) {
+  Gpu g;
+  if (!get(h, &g)) return AMDSMI_STATUS_INVAL;
+  const uint64_t uj = num(g, "energy", ~0ull);
+  if (uj == ~0ull) return AMDSMI_STATUS_NOT_SUPPORTED;
+  *res = 15.259f;
+  *acc = static_cast<uint64_t>(static_cast<double>(uj) / 15.259);
+  *ts = 0;
   return AMDSMI_STATUS_SUCCESS;
 }
 

@@ -67,6 +67,24 @@ def test_live_smi_sample_is_sane():
     assert s.ecc_uncorrectable == 0
 
 
+def test_live_energy_counter_tracks_power():
+    """amd_gpu_energy_joules_total's source: the amd-smi accumulator advances
+    by about socket power x elapsed time (probe on MI355X: 278.7 J over 1 s
+    at 277 W)."""
+    import time
+    ok, err = node.smi_open()
+    assert ok, err
+    s1 = node.smi_sample(0)
+    assert s1.energy_j is not None and s1.energy_j > 0
+    t0 = time.perf_counter()
+    time.sleep(1.0)
+    s2 = node.smi_sample(0)
+    dt = time.perf_counter() - t0
+    de = s2.energy_j - s1.energy_j
+    p = max(1, (s1.power_w + s2.power_w) / 2)
+    assert 0.3 * p * dt <= de <= 3.0 * p * dt, (de, p, dt)
+
+
 def test_vector_add_binary_passes():
     res = _results(_run([os.path.join(BIN, "mx-vector-add"), "--n", "50000"]))
     assert res and res[-1]["test"] == "vectoradd" and res[-1]["pass"], res

@@ -342,3 +342,16 @@ def test_exporter_process_vram_and_link_down(fake_smi, tmp_path):
                for l in pm)
     down = [l for l in text.splitlines() if l.startswith('amd_gpu_xgmi_link_up{gpu="3"') and l.endswith(" 0")]
     assert len(down) == 2 and any('status="disabled"' in l for l in down)
+
+
+def test_exporter_energy_counter(fake_smi, tmp_path):
+    """amdsmi_get_energy_count (accumulator x resolution, uJ) becomes
+    amd_gpu_energy_joules_total; a GPU without the counter emits no series."""
+    from mxk8s.exporter import Exporter, ExporterConfig, SmiBackend
+    fake_smi.set(2, energy=1234567890)
+    exp = Exporter(ExporterConfig(sysfs_root=ROOT, pod_resources=False), backend=SmiBackend(ROOT))
+    text = exp.sample_once()
+    en = [l for l in text.splitlines() if l.startswith("amd_gpu_energy_joules_total{")]
+    assert len(en) == 1 and 'gpu="2"' in en[0]
+    assert abs(float(en[0].rsplit(" ", 1)[1]) - 1234.568) < 0.05
+    assert "# TYPE amd_gpu_energy_joules_total counter" in text
