@@ -293,7 +293,9 @@ def test_reconcile_rewrites_stale_cdi_and_readvertises(plugin_dir, tmp_path):
         assert len(resp.devices) == 8
         assert _wait(lambda: "/dev/dri/renderD199" in json.dumps(_read_json(cdi) or {}))
         assert "/dev/dri/renderD135" not in json.dumps(_read_json(cdi))
-        assert plugin.reconciles["cdi_rewritten"] >= 2 and plugin.reconciles["gpus_changed"] == 1
+        # the counters move just after the rename / resend the asserts above saw
+        assert _wait(lambda: plugin.reconciles["cdi_rewritten"] >= 2)
+        assert plugin.reconciles["gpus_changed"] == 1
         req = api.AllocateRequest()
         req.container_requests.add(devices_ids=["7"])
         c = stub.Allocate(req, timeout=5).container_responses[0]
