@@ -56,6 +56,9 @@
 //  18 w4j   schedule 6, K loop rotated per workgroup
 //  19 pp8   8 waves, two per SIMD, compute / load ping-pong (mxk_gemm_bf16_tn_pp8)
 //  20 pp8   19 with the second group at s_setprio 1
+//  21-24 w4j schedule 6 with a staggered first round (four CU groups start
+//           1/2/4/8 x ~1024 clocks apart, so C store bursts do not coincide)
+//  25 w4j   variant 23 with plain (temporal) widened stores
 // The earlier schedules (one-barrier w4b, 8-wave, 4-deep ring, w4h, ...)
 // were retired when an ISA audit (tests/test_isa_hazards.py) found their
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
@@ -298,11 +301,22 @@ __device__ __forceinline__ void ktile_sched(f32x4_t (&acc)[8][8], bf16x8_t (&f0a
                                    dma_a, dma_b, kb2, wave_s, par);
 }
 
-template <int MAP, int EPI, int LATE = 0, int R1 = 0, int SCHED = 0, int ROT = 0>
+template <int MAP, int EPI, int LATE = 0, int R1 = 0, int SCHED = 0, int ROT = 0, int STAG = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
   __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  if constexpr (STAG > 0) {
+    // STAG: staggered first round.  The first 256 workgroups (one per CU)
+    // start in four groups STAG x ~1024 clocks apart (group = CU slot within
+    // the XCD mod 4), so the workgroups of a round finish, and burst their C
+    // tiles to HBM, at four moments instead of one; later workgroups inherit
+    // the offset from the CU they land on.
+    if (blockIdx.x < 256) {
+      const int g = __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) & 3);
+      for (int i = 0; i < g * STAG; ++i) __builtin_amdgcn_s_sleep(16);
+    }
+  }
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -735,14 +749,14 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                                      int variant, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 21;
+constexpr int kNumVariants = 26;
 constexpr int kDefaultVariant = 6;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
     "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar",
     "w4j_hb_st", "x2_hb", "diag_nostore", "w4ip_hb_st", "w4ip_hb_nt", "w4j_earlyb",
     "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg", "pp8",
-    "pp8_prio"};
+    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -757,10 +771,10 @@ int num_cus() {
   return cus;
 }
 
-template <int MAP, int EPI, int LATE, int R1 = 0, int SCHED = 0, int ROT = 0>
+template <int MAP, int EPI, int LATE, int R1 = 0, int SCHED = 0, int ROT = 0, int STAG = 0>
 void launch_w4i(int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b, uint16_t* c,
                 int M, int N, int K, int lda, int ldb, int ldc) {
-  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4i<MAP, EPI, LATE, R1, SCHED, ROT>), dim3(nwg), dim3(W4_THREADS),
+  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4i<MAP, EPI, LATE, R1, SCHED, ROT, STAG>), dim3(nwg), dim3(W4_THREADS),
                      0, stream, a, b, c, M, N, K, lda, ldb, ldc);
 }
 
@@ -795,6 +809,11 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 16: launch_w4i<1, 2, 1, 0, 6>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 17: launch_w4i<1, 2, 1, 0, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 18: launch_w4i<1, 2, 1, 0, 1, 2>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 21: launch_w4i<1, 2, 1, 0, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 22: launch_w4i<1, 2, 1, 0, 1, 0, 2>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 23: launch_w4i<1, 2, 1, 0, 1, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 24: launch_w4i<1, 2, 1, 0, 1, 0, 8>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 25: launch_w4i<1, 1, 1, 0, 1, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 19:
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_pp8<1, 0>), dim3(nwg), dim3(PP_THREADS), 0, stream, a, b,
                          c, M, N, K, lda, ldb, ldc);
