@@ -34,6 +34,9 @@ _SIGNATURES = {
     "mxk_gemm_bf16_tn_is_fast": (_i, [_i, _i, _i]),
     "mxk_gemm_bf16_ex": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_ex_variant": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "mxk_gemm_bf16_ex_ws": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _l,
+                                 ctypes.POINTER(ctypes.c_int), _vp]),
+    "mxk_gemm_bf16_split_workspace": (_l, []),
     "mxk_gemm_bf16_dgrad_swiglu": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_tn_variant": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_tn_num_variants": (_i, []),

@@ -8,9 +8,27 @@ otherwise); CPU tensors use an fp32 PyTorch reference.
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import torch
 
 from . import _lib
+
+# Split tail (mxk_gemm_bf16_ex_ws): an output whose 256^2 tiles leave the
+# last round of the CUs at most half full (the Llama-3-8B wqkv / w2 weight
+# gradients: 384 / 896 tiles on 256 CUs) runs its tail tiles as two K halves
+# each; MXK_SPLIT_TAIL=0 turns it off (A/B).
+_USE_SPLIT_TAIL = os.environ.get("MXK_SPLIT_TAIL", "1") != "0"
+_split_ws: dict = {}
+
+
+def _split_workspace(device: torch.device) -> torch.Tensor:
+    ws = _split_ws.get(device)
+    if ws is None:
+        n = int(_lib.lib().mxk_gemm_bf16_split_workspace())
+        ws = _split_ws[device] = torch.empty(n, dtype=torch.uint8, device=device)
+    return ws
 
 
 def _check_operand(t: torch.Tensor, name: str) -> None:
@@ -77,10 +95,18 @@ def gemm_bf16_ex(a: torch.Tensor, b: torch.Tensor, a_kmajor: bool, b_kmajor: boo
     N, K2 = (b.shape if b_kmajor else (b.shape[1], b.shape[0]))
     if K != K2 or tuple(out.shape) != (M, N) or not is_fast_shape(M, N, K):
         return False
-    st = _lib.lib().mxk_gemm_bf16_ex_variant(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K,
-                                             a.stride(0), b.stride(0), out.stride(0),
-                                             int(a_kmajor), int(b_kmajor), int(variant),
-                                             _lib.stream_ptr(a.device))
+    if variant == 1 and _USE_SPLIT_TAIL and not (a_kmajor and b_kmajor):
+        ws = _split_workspace(a.device)
+        split = ctypes.c_int(0)
+        st = _lib.lib().mxk_gemm_bf16_ex_ws(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K,
+                                            a.stride(0), b.stride(0), out.stride(0),
+                                            int(a_kmajor), int(b_kmajor), ws.data_ptr(), ws.numel(),
+                                            ctypes.byref(split), _lib.stream_ptr(a.device))
+    else:
+        st = _lib.lib().mxk_gemm_bf16_ex_variant(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N,
+                                                 K, a.stride(0), b.stride(0), out.stride(0),
+                                                 int(a_kmajor), int(b_kmajor), int(variant),
+                                                 _lib.stream_ptr(a.device))
     if st == 1:   # hipErrorInvalidValue: layout/stride limits -> library GEMM
         return False
     _lib.check(st, "mxk_gemm_bf16_ex")

@@ -55,9 +55,9 @@ def _tail_heavy(M: int, N: int, cus: int = 256) -> bool:
 
 
 def _wgrad_into(sink: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
-    # no tail-heavy exception here: even the 384-tile wqkv wgrad (6144 x 4096,
-    # 1.5 rounds on 256 CUs) runs 1215 TF/s on the layout kernel against
-    # hipBLASLt's 1150 (profiles/r1_gemm_m0/llama_*.log)
+    # no tail-heavy exception here: even without its split tail the 384-tile
+    # wqkv wgrad (6144 x 4096, 1.5 rounds on 256 CUs) ran 1215 TF/s on the
+    # layout kernel against hipBLASLt's 1150 (profiles/r1_gemm_m0/llama_*.log)
     if _USE_MXK_WGRAD and sink.is_cuda and dy2.is_contiguous() and x2.is_contiguous() and \
             gemm_bf16_ex(dy2, x2, False, False, sink):
         return
@@ -65,10 +65,11 @@ def _wgrad_into(sink: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None
 
 
 def _dgrad(dy: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    # tail-heavy outputs take the kernel's split tail (gemm_bf16_ex)
     if _USE_MXK_DGRAD and dy.is_cuda and dy.is_contiguous() and weight.is_contiguous():
         dy2 = dy.reshape(-1, dy.shape[-1])
         out = torch.empty((dy2.shape[0], weight.shape[1]), device=dy.device, dtype=dy.dtype)
-        if not _tail_heavy(*out.shape) and gemm_bf16_ex(dy2, weight, True, False, out):
+        if gemm_bf16_ex(dy2, weight, True, False, out):
             return out.view(*dy.shape[:-1], weight.shape[1])
     return torch.matmul(dy, weight)
 

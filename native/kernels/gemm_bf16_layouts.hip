@@ -414,11 +414,18 @@ __device__ __forceinline__ void x2_ktile_s(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)
 // EPI 0: 8-B stores, 1: widened 16-B stores, 2: SwiGLU backward
 // (mxk::swiglu_bwd_block: C = d[g | u], aux = [g | u], both row stride ldc,
 // u at column offset N).
-template <bool AN, bool BN, int EPI, int SCHED = 0>
+// SPLIT (split tail): workgroups [0, q_full) run whole tiles; the last
+// T - q_full tiles (at most half a round) are split in two K halves, one
+// workgroup each (blockIdx q_full + 2t + h), dispatched last so that the
+// 2(T - q_full) halves fill the final round instead of leaving half the CUs
+// idle.  A half writes its fp32 partial tile to ws[2t + h] ([256][256]);
+// mxk_gemm_split_fixup sums the pair into C.
+template <bool AN, bool BN, int EPI, int SCHED = 0, bool SPLIT = false>
 __global__ void __launch_bounds__(XT, 1)
 mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                         uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc,
-                        const uint16_t* __restrict__ aux = nullptr) {
+                        const uint16_t* __restrict__ aux = nullptr, float* __restrict__ ws = nullptr,
+                        int q_full = 0) {
   constexpr int A_BYTES = XOp<AN>::BYTES;
   constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
@@ -427,13 +434,24 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1;
   const int wn = wave & 1;
+  int tile = blockIdx.x, unit = -1, kbeg = 0, klen = K;
+  if constexpr (SPLIT) {
+    if (tile >= q_full) {
+      unit = tile - q_full;
+      tile = q_full + (unit >> 1);
+      klen = K >> 1;
+      kbeg = (unit & 1) * klen;
+    }
+  }
   int m0, n0;
-  mxk::w4b_tile<1>(blockIdx.x, gridDim.x, M / XBM, N / XBM, &m0, &n0);
+  mxk::w4b_tile<1>(tile, (M / XBM) * (N / XBM), M / XBM, N / XBM, &m0, &n0);
 
   XOp<AN> oa;
   XOp<BN> ob;
-  oa.init(A, lda, m0, K, lane, wave);
-  ob.init(B, ldb, n0, K, lane, wave);
+  // the K range [kbeg, kbeg + klen): K-major operands start kbeg columns in,
+  // N/M-major ones kbeg rows down
+  oa.init(AN ? A + static_cast<size_t>(kbeg) * lda : A + kbeg, lda, m0, klen, lane, wave);
+  ob.init(BN ? B + static_cast<size_t>(kbeg) * ldb : B + kbeg, ldb, n0, klen, lane, wave);
   oa.set_lds(smem, mxk::lds_addr32(smem));
   ob.set_lds(smem, mxk::lds_addr32(smem));
 
@@ -443,7 +461,7 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int ns = K / XBK;
+  const int ns = klen / XBK;
   const uint32_t ka = oa.kstep(), kb = ob.kstep();
 #pragma unroll
   for (int p = 0; p < 8; ++p) oa.issue_s(smem, p, 0, wave);
@@ -487,12 +505,51 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   mxk::mfma_drain(acc);
 
+  if constexpr (SPLIT) {
+    if (unit >= 0) {
+      // fp32 partial: lane holds 4 consecutive columns of row i*16 + (lane & 15)
+      float* wp = ws + static_cast<size_t>(unit) * (XBM * XBM);
+      const int r0 = wm * 128 + (lane & 15), c0 = wn * 128 + (lane >> 4) * 4;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          *reinterpret_cast<f32x4_t*>(wp + (r0 + i * 16) * XBM + c0 + j * 16) = acc[i][j];
+      return;
+    }
+  }
   if constexpr (EPI == 2)
     mxk::swiglu_bwd_block(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane);
   else if constexpr (EPI == 1)
     mxk::store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else
     mxk::store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+}
+
+// C tile of split pair t = ws[2t] + ws[2t + 1]; grid (32, tail tiles), each
+// thread 8 consecutive columns of one row (two 8-B stores: ldc % 4 == 0).
+__global__ void __launch_bounds__(256)
+mxk_gemm_split_fixup(const float* __restrict__ ws, uint16_t* __restrict__ C, int M, int N, int ldc,
+                     int q_full) {
+  const int t = blockIdx.y;
+  int m0, n0;
+  mxk::w4b_tile<1>(q_full + t, (M / XBM) * (N / XBM), M / XBM, N / XBM, &m0, &n0);
+  const int e = (blockIdx.x * 256 + threadIdx.x) * 8;
+  const int r = e / XBM, c = e % XBM;
+  const float* p0 = ws + static_cast<size_t>(2 * t) * (XBM * XBM) + e;
+  const float* p1 = p0 + XBM * XBM;
+  const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(p0);
+  const f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(p0 + 4);
+  const f32x4_t b0 = *reinterpret_cast<const f32x4_t*>(p1);
+  const f32x4_t b1 = *reinterpret_cast<const f32x4_t*>(p1 + 4);
+  uint2 lo, hi;
+  lo.x = mxk::pack2bf(a0[0] + b0[0], a0[1] + b0[1]);
+  lo.y = mxk::pack2bf(a0[2] + b0[2], a0[3] + b0[3]);
+  hi.x = mxk::pack2bf(a1[0] + b1[0], a1[1] + b1[1]);
+  hi.y = mxk::pack2bf(a1[2] + b1[2], a1[3] + b1[3]);
+  uint16_t* cp = C + static_cast<size_t>(m0 + r) * ldc + n0 + c;
+  *reinterpret_cast<uint2*>(cp) = lo;
+  *reinterpret_cast<uint2*>(cp + 4) = hi;
 }
 
 template <bool AN, bool BN>
@@ -582,6 +639,94 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
                      static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
                      static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
                      static_cast<const uint16_t*>(gu));
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+namespace {
+int device_cus() {
+  static thread_local int dev_cached = -1, cus = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && dev != dev_cached) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      cus = n;
+    dev_cached = dev;
+  }
+  return cus;
+}
+
+template <bool AN, bool BN>
+void launch_split(int sched, bool wide, int nwg, int q_full, hipStream_t stream, const uint16_t* a,
+                  const uint16_t* b, uint16_t* c, int M, int N, int K, int lda, int ldb, int ldc,
+                  float* ws) {
+  const dim3 grid(q_full + 2 * (nwg - q_full));
+  if (sched == 1 && wide)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 1, 1, true>), grid, dim3(XT), 0, stream, a,
+                       b, c, M, N, K, lda, ldb, ldc, nullptr, ws, q_full);
+  else if (sched == 1)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 1, true>), grid, dim3(XT), 0, stream, a,
+                       b, c, M, N, K, lda, ldb, ldc, nullptr, ws, q_full);
+  else if (wide)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 1, 0, true>), grid, dim3(XT), 0, stream, a,
+                       b, c, M, N, K, lda, ldb, ldc, nullptr, ws, q_full);
+  else
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 0, true>), grid, dim3(XT), 0, stream, a,
+                       b, c, M, N, K, lda, ldb, ldc, nullptr, ws, q_full);
+  hipLaunchKernelGGL(mxk_gemm_split_fixup, dim3(XBM * XBM / (256 * 8), nwg - q_full), dim3(256), 0,
+                     stream, ws, c, M, N, ldc, q_full);
+}
+}  // namespace
+
+// Bytes of fp32 workspace the split tail of an (M, N) output needs at most
+// (half a round of tiles, two partial tiles each).
+MXK_API long mxk_gemm_bf16_split_workspace(void) {
+  return static_cast<long>(device_cus() / 2) * 2 * XBM * XBM * 4;
+}
+
+// mxk_gemm_bf16_ex (variant 1) with the split tail: when the output's 256^2
+// tiles fill q whole rounds of the CUs plus a last round at most half full
+// (e.g. 384 tiles on 256 CUs), the tail tiles run as K halves on twice as
+// many workgroups (fp32 partials in ws, summed by a fixup kernel) instead of
+// leaving half the chip idle for a whole round.  Layouts other than both
+// K-major only; every other case runs mxk_gemm_bf16_ex unchanged.  `ws`
+// holds >= ws_bytes (mxk_gemm_bf16_split_workspace()); sets *split to 1
+// when the split path ran.
+MXK_API int mxk_gemm_bf16_ex_ws(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                                int ldb, int ldc, int a_kmajor, int b_kmajor, void* ws,
+                                long ws_bytes, int* split, hipStream_t stream) {
+  if (split) *split = 0;
+  const int cus = device_cus();
+  const long nwg = M > 0 && N > 0 ? static_cast<long>(M / XBM) * (N / XBM) : 0;
+  const int tail = nwg > 0 ? static_cast<int>(nwg % cus) : 0;
+  const bool want = !(a_kmajor && b_kmajor) && tail > 0 && 2 * tail <= cus && K % (2 * XBK) == 0 &&
+                    K >= 16 * XBK && ws != nullptr &&
+                    ws_bytes >= static_cast<long>(2 * tail) * XBM * XBM * 4 &&
+                    reinterpret_cast<uintptr_t>(ws) % 16 == 0;
+  if (!want)
+    return mxk_gemm_bf16_ex_variant(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor, 1, stream);
+  const auto bytes = [](long rows, long ld) { return rows * ld * 2; };
+  const bool ok = M % XBM == 0 && N % XBM == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 &&
+                  (a_kmajor ? lda >= K : lda >= M) && (b_kmajor ? ldb >= K : ldb >= N) &&
+                  ldc >= N && (a_kmajor || bytes(K, lda) < (1L << 32)) &&
+                  (b_kmajor || bytes(K, ldb) < (1L << 32)) &&
+                  reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(C) % 8 == 0;
+  if (!ok) return static_cast<int>(hipErrorInvalidValue);
+  const int sched = (!a_kmajor && !b_kmajor) ? 1 : 0;
+  const bool wide = (ldc % 8 == 0) && (reinterpret_cast<uintptr_t>(C) % 16 == 0);
+  const int q_full = static_cast<int>(nwg) - tail;
+  auto a = static_cast<const uint16_t*>(A);
+  auto b = static_cast<const uint16_t*>(B);
+  auto c = static_cast<uint16_t*>(C);
+  auto w = static_cast<float*>(ws);
+  if (a_kmajor)
+    launch_split<false, true>(sched, wide, nwg, q_full, stream, a, b, c, M, N, K, lda, ldb, ldc, w);
+  else if (b_kmajor)
+    launch_split<true, false>(sched, wide, nwg, q_full, stream, a, b, c, M, N, K, lda, ldb, ldc, w);
+  else
+    launch_split<true, true>(sched, wide, nwg, q_full, stream, a, b, c, M, N, K, lda, ldb, ldc, w);
+  if (split) *split = 1;
   MXK_RETURN_LAUNCH_STATUS();
 }
 

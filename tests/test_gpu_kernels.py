@@ -276,6 +276,44 @@ def test_gemm_layouts_vs_fp32(cuda_device, layout, variant, M, N, K):
     assert not gemm_bf16_ex(a[:, :-64] if ak else a[:-64], b, ak, bk, out, variant=variant)
 
 
+@pytest.mark.parametrize("layout", ["nn", "nt_wgrad", "tt"])
+@pytest.mark.parametrize("M,N,K", [(2048, 2048, 1024), (6144, 4096, 1024), (4096, 14336, 2048)])
+def test_gemm_split_tail_vs_fp32(cuda_device, layout, M, N, K):
+    """Split tail of the layout kernel: 64 tiles (all split, no whole-tile
+    round), 384 and 896 tiles (the Llama-3-8B wqkv / w2 weight-gradient tile
+    counts: one / three whole rounds + 128 tiles as K halves, fp32 partials
+    summed by the fixup kernel).  The split path must actually run."""
+    import ctypes
+
+    from mxk8s.ops import _lib
+    from mxk8s.ops.gemm import _split_workspace
+    g = torch.Generator(device=cuda_device).manual_seed(5)
+    r = lambda *s: (torch.rand(*s, device=cuda_device, generator=g) * 2 - 1).bfloat16()  # noqa: E731
+    if layout == "nn":
+        a, b, ak, bk = r(M, K), r(K, N), True, False
+        ref = a.float() @ b.float()
+    elif layout == "tt":
+        a, b, ak, bk = r(K, M), r(N, K), False, True
+        ref = a.float().t() @ b.float().t()
+    else:
+        a, b, ak, bk = r(K, M), r(K, N), False, False
+        ref = a.float().t() @ b.float()
+    out = torch.full((M, N), float("nan"), device=cuda_device, dtype=torch.bfloat16)
+    ws = _split_workspace(cuda_device)
+    cus = torch.cuda.get_device_properties(cuda_device).multi_processor_count
+    tiles = (M // 256) * (N // 256)
+    split = ctypes.c_int(-1)
+    st = _lib.lib().mxk_gemm_bf16_ex_ws(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K,
+                                        a.stride(0), b.stride(0), out.stride(0), int(ak), int(bk),
+                                        ws.data_ptr(), ws.numel(), ctypes.byref(split),
+                                        _lib.stream_ptr(cuda_device))
+    _lib.check(st, "mxk_gemm_bf16_ex_ws")
+    torch.cuda.synchronize()
+    assert split.value == int(0 < tiles % cus <= cus // 2)
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 2 ** -7 * ref.abs().max().item() + 1e-3, err
+
+
 @pytest.mark.parametrize("T,V", [(4, 128256), (300, 1000), (7, 8)])
 def test_fused_cross_entropy_vs_fp32(cuda_device, T, V):
     from mxk8s.ops.xent import cross_entropy
