@@ -24,10 +24,14 @@ _split_ws: dict = {}
 
 
 def _split_workspace(device: torch.device) -> torch.Tensor:
-    ws = _split_ws.get(device)
+    """fp32 partial-tile workspace of the split tail, one per (device,
+    stream): GEMMs on one stream run in order, so they can share it; two
+    streams must not (their GEMMs may overlap)."""
+    key = (device, _lib.stream_ptr(device))
+    ws = _split_ws.get(key)
     if ws is None:
         n = int(_lib.lib().mxk_gemm_bf16_split_workspace())
-        ws = _split_ws[device] = torch.empty(n, dtype=torch.uint8, device=device)
+        ws = _split_ws[key] = torch.empty(n, dtype=torch.uint8, device=device)
     return ws
 
 
