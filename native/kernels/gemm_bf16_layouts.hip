@@ -414,12 +414,15 @@ __device__ __forceinline__ void x2_ktile_s(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)
 // EPI 0: 8-B stores, 1: widened 16-B stores, 2: SwiGLU backward
 // (mxk::swiglu_bwd_block: C = d[g | u], aux = [g | u], both row stride ldc,
 // u at column offset N).
-// SPLIT (split tail): workgroups [0, q_full) run whole tiles; the last
-// T - q_full tiles (at most half a round) are split in two K halves, one
-// workgroup each (blockIdx q_full + 2t + h), dispatched last so that the
-// 2(T - q_full) halves fill the final round instead of leaving half the CUs
-// idle.  A half writes its fp32 partial tile to ws[2t + h] ([256][256]);
-// mxk_gemm_split_fixup sums the pair into C.
+// SPLIT (split tail): the launch after the whole-tile one (grid q_full,
+// tiles [0, q_full) of the same map) covers the last T - q_full tiles (at
+// most half a round) as two K halves each, one workgroup per half
+// (blockIdx 2t + h), so the 2(T - q_full) halves fill the final round
+// instead of leaving half the CUs idle.  A half writes its fp32 partial
+// tile to ws[2t + h] ([256][256]); mxk_gemm_split_fixup sums the pair into
+// C.  A separate kernel (not a branch of the whole-tile one): with both
+// epilogues in one body the allocator spilled accumulators, and a spill
+// store of an AGPR right behind its inline-asm MFMA reads a stale value.
 template <bool AN, bool BN, int EPI, int SCHED = 0, bool SPLIT = false>
 __global__ void __launch_bounds__(XT, 1)
 mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
@@ -434,14 +437,11 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1;
   const int wn = wave & 1;
-  int tile = blockIdx.x, unit = -1, kbeg = 0, klen = K;
+  int tile = blockIdx.x, kbeg = 0, klen = K;
   if constexpr (SPLIT) {
-    if (tile >= q_full) {
-      unit = tile - q_full;
-      tile = q_full + (unit >> 1);
-      klen = K >> 1;
-      kbeg = (unit & 1) * klen;
-    }
+    tile = q_full + (static_cast<int>(blockIdx.x) >> 1);
+    klen = K >> 1;
+    kbeg = (blockIdx.x & 1) * klen;
   }
   int m0, n0;
   mxk::w4b_tile<1>(tile, (M / XBM) * (N / XBM), M / XBM, N / XBM, &m0, &n0);
@@ -506,19 +506,15 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
   mxk::mfma_drain(acc);
 
   if constexpr (SPLIT) {
-    if (unit >= 0) {
-      // fp32 partial: lane holds 4 consecutive columns of row i*16 + (lane & 15)
-      float* wp = ws + static_cast<size_t>(unit) * (XBM * XBM);
-      const int r0 = wm * 128 + (lane & 15), c0 = wn * 128 + (lane >> 4) * 4;
+    // fp32 partial: lane holds 4 consecutive columns of row i*16 + (lane & 15)
+    float* wp = ws + static_cast<size_t>(blockIdx.x) * (XBM * XBM);
+    const int r0 = wm * 128 + (lane & 15), c0 = wn * 128 + (lane >> 4) * 4;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          *reinterpret_cast<f32x4_t*>(wp + (r0 + i * 16) * XBM + c0 + j * 16) = acc[i][j];
-      return;
-    }
-  }
-  if constexpr (EPI == 2)
+      for (int j = 0; j < 8; ++j)
+        *reinterpret_cast<f32x4_t*>(wp + (r0 + i * 16) * XBM + c0 + j * 16) = acc[i][j];
+  } else if constexpr (EPI == 2)
     mxk::swiglu_bwd_block(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane);
   else if constexpr (EPI == 1)
     mxk::store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
@@ -659,15 +655,11 @@ template <bool AN, bool BN>
 void launch_split(int sched, bool wide, int nwg, int q_full, hipStream_t stream, const uint16_t* a,
                   const uint16_t* b, uint16_t* c, int M, int N, int K, int lda, int ldb, int ldc,
                   float* ws) {
-  const dim3 grid(q_full + 2 * (nwg - q_full));
-  if (sched == 1 && wide)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 1, 1, true>), grid, dim3(XT), 0, stream, a,
-                       b, c, M, N, K, lda, ldb, ldc, nullptr, ws, q_full);
-  else if (sched == 1)
+  // whole tiles [0, q_full) (the tile map is over all nwg tiles, not the grid)
+  if (q_full > 0) launch_x<AN, BN>(sched, wide, q_full, stream, a, b, c, M, N, K, lda, ldb, ldc);
+  const dim3 grid(2 * (nwg - q_full));
+  if (sched == 1)
     hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 1, true>), grid, dim3(XT), 0, stream, a,
-                       b, c, M, N, K, lda, ldb, ldc, nullptr, ws, q_full);
-  else if (wide)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 1, 0, true>), grid, dim3(XT), 0, stream, a,
                        b, c, M, N, K, lda, ldb, ldc, nullptr, ws, q_full);
   else
     hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 0, true>), grid, dim3(XT), 0, stream, a,

@@ -31,7 +31,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+  // one v_cvt_pk_bf16_f32 for the pair (two scalar casts cost two converts
+  // and an SDWA or)
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+  const b2_t b = __builtin_convertvector(f2_t{lo, hi}, b2_t);
+  return __builtin_bit_cast(uint32_t, b);
 }
 
 // Bijective XCD-aware remap of a 1-D block id: blocks b and b+8 share an
@@ -225,29 +230,33 @@ __device__ __forceinline__ void store_block_narrow(const f32x4_t (&acc)[8][8], u
 __device__ __forceinline__ void swiglu_bwd_rows(const f32x4_t (&acc)[8][8], int i,
                                                 const uint2 (&gw)[8], const uint2 (&uw)[8],
                                                 uint16_t* dgu, long off, int F) {
+  // element pairs in packed fp32 (v_pk_mul/fma_f32: two elements per VALU
+  // op); exp and rcp stay per element.  With 1 + g (1 - s) = (1 + g) - g s:
+  //   t = d s,  du = t g,  dg = t u ((1 + g) - g s)
+  typedef float f2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const uint32_t gp[2] = {gw[j].x, gw[j].y};
     const uint32_t up[2] = {uw[j].x, uw[j].y};
-    float dg[4], du[4];
+    uint32_t pg[2], pu[2];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t gbits = (e & 1) ? (gp[e >> 1] & 0xFFFF0000u) : (gp[e >> 1] << 16);
-      const uint32_t ubits = (e & 1) ? (up[e >> 1] & 0xFFFF0000u) : (up[e >> 1] << 16);
-      const float g = __uint_as_float(gbits);
-      const float u = __uint_as_float(ubits);
-      const float d = acc[i][j][e];
-      const float sg = 1.f / (1.f + __expf(-g));
-      du[e] = d * g * sg;
-      dg[e] = d * u * sg * (1.f + g * (1.f - sg));
+    for (int h = 0; h < 2; ++h) {
+      const f2_t g = {__uint_as_float(gp[h] << 16), __uint_as_float(gp[h] & 0xFFFF0000u)};
+      const f2_t u = {__uint_as_float(up[h] << 16), __uint_as_float(up[h] & 0xFFFF0000u)};
+      const f2_t d = {acc[i][j][2 * h], acc[i][j][2 * h + 1]};
+      const f2_t x = g * -1.44269504f;
+      // v_rcp_f32 (1 ulp) instead of the IEEE division sequence (~10 VALU
+      // ops per element); the result is rounded to bf16 anyway
+      const f2_t sg = {__builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[0])),
+                       __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[1]))};
+      const f2_t t = d * sg;
+      const f2_t du = t * g;
+      const f2_t dg = t * u * ((g + 1.f) - g * sg);
+      pg[h] = pack2bf(dg[0], dg[1]);
+      pu[h] = pack2bf(du[0], du[1]);
     }
-    uint2 pg, pu;
-    pg.x = pack2bf(dg[0], dg[1]);
-    pg.y = pack2bf(dg[2], dg[3]);
-    pu.x = pack2bf(du[0], du[1]);
-    pu.y = pack2bf(du[2], du[3]);
-    *reinterpret_cast<uint2*>(dgu + off + j * 16) = pg;
-    *reinterpret_cast<uint2*>(dgu + off + F + j * 16) = pu;
+    *reinterpret_cast<uint2*>(dgu + off + j * 16) = make_uint2(pg[0], pg[1]);
+    *reinterpret_cast<uint2*>(dgu + off + F + j * 16) = make_uint2(pu[0], pu[1]);
   }
 }
 

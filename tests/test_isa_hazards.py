@@ -55,6 +55,15 @@ def close_accumulator_reads(asm: str) -> dict[str, int]:
                 for m in re.finditer(r"\ba(\d+)\b", ops):
                     if int(m.group(1)) in pend and pend[int(m.group(1))] < 12:
                         n += 1
+            elif ln.startswith(("scratch_store", "global_store", "buffer_store", "flat_store")):
+                # a store straight from accumulators (e.g. a register-allocator
+                # spill of an AGPR) reads them just like v_accvgpr_read
+                ops = ln.split(" ", 1)[1] if " " in ln else ""
+                for m in re.finditer(r"\ba\[(\d+):(\d+)\]|\ba(\d+)\b", ops):
+                    lo = int(m.group(1) or m.group(3))
+                    hi = int(m.group(2) or m.group(3))
+                    if any(r in pend and pend[r] < 12 for r in range(lo, hi + 1)):
+                        n += 1
         if n:
             bad[name] = n
     return bad
@@ -74,3 +83,10 @@ def test_detector_flags_a_close_read():
     assert close_accumulator_reads(asm) == {"_Zfoo": 1}
     safe = asm.replace("\ts_add_u32 s0, s0, 1\n", "\ts_nop 7\n\ts_nop 7\n")
     assert close_accumulator_reads(safe) == {}
+
+
+def test_detector_flags_a_close_accumulator_spill():
+    asm = ("_Zbar:\n\tv_mfma_f32_16x16x32_bf16 a[252:255], v[0:3], v[4:7], a[252:255]\n"
+           "\ts_mov_b32 s0, 1\n\tscratch_store_dwordx4 off, a[252:255], off offset:4\n"
+           ".Lfunc_end0:\n")
+    assert close_accumulator_reads(asm) == {"_Zbar": 1}
