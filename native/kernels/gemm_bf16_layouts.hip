@@ -25,6 +25,8 @@
 // AGPR accumulators per wave, one barrier per 64-deep stage.
 #include "mx_common.h"
 
+#include <cstdlib>
+
 namespace {
 constexpr int XT = 256;          // threads (4 waves)
 constexpr int XBM = 256;         // macro tile M = N = 256
@@ -411,7 +413,8 @@ __device__ __forceinline__ void x2_ktile_s(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)
     x2_ktile<AN, BN, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, soa, sob, wave, par);
 }
 
-// EPI 0: 8-B stores, 1: widened 16-B stores, 2: SwiGLU backward
+// EPI 0: 8-B stores, 1: widened 16-B stores, 2: SwiGLU backward, 3: SwiGLU
+// backward with 16-B g / u accesses (mxk::swiglu_bwd_block_wide)
 // (mxk::swiglu_bwd_block: C = d[g | u], aux = [g | u], both row stride ldc,
 // u at column offset N).
 // SPLIT (split tail): the launch after the whole-tile one (grid q_full,
@@ -516,6 +519,8 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
         *reinterpret_cast<f32x4_t*>(wp + (r0 + i * 16) * XBM + c0 + j * 16) = acc[i][j];
   } else if constexpr (EPI == 2)
     mxk::swiglu_bwd_block(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane);
+  else if constexpr (EPI == 3)
+    mxk::swiglu_bwd_block_wide(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane);
   else if constexpr (EPI == 1)
     mxk::store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else
@@ -631,10 +636,23 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
                   reinterpret_cast<uintptr_t>(dgu) % 8 == 0;
   if (!ok) return static_cast<int>(hipErrorInvalidValue);
   const int nwg = (M / XBM) * (F / XBM);
-  hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<false, true, 2, 0>), dim3(nwg), dim3(XT), 0, stream,
-                     static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
-                     static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
-                     static_cast<const uint16_t*>(gu));
+  // EPI 3: 16-B g/u accesses (MXK_SWIGLU_WIDE=0 keeps the 8-B form, A/B)
+  static const bool wide_ok = [] {
+    const char* e = std::getenv("MXK_SWIGLU_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  const bool wide = wide_ok && reinterpret_cast<uintptr_t>(gu) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(dgu) % 16 == 0;
+  if (wide)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<false, true, 3, 0>), dim3(nwg), dim3(XT), 0, stream,
+                       static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
+                       static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
+                       static_cast<const uint16_t*>(gu));
+  else
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<false, true, 2, 0>), dim3(nwg), dim3(XT), 0, stream,
+                       static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
+                       static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
+                       static_cast<const uint16_t*>(gu));
   MXK_RETURN_LAUNCH_STATUS();
 }
 

@@ -284,6 +284,71 @@ __device__ __forceinline__ void swiglu_bwd_block(const f32x4_t (&acc)[8][8], con
   }
 }
 
+// Widened form of swiglu_bwd_block: v_permlane16_swap pairs the 16x16 tiles
+// j and j+1 (as store_block_wide does for bf16 C), so each lane owns 8
+// consecutive columns and every g / u load and dg / du store is 16 B (one
+// wave-instruction = 16 rows x 64 B instead of 16 rows x 32 B): half the
+// memory instructions.  Lanes q = lane >> 4: columns j*16 + (q&1)*16 +
+// (q>>1)*8 + 0..7; swap(a_e, b_e) of tile j / j+1 element e gives columns e
+// and 4 + e of that run.  Needs gu, dgu 16-B aligned and ld % 8 == 0.
+__device__ __forceinline__ void swiglu_bwd_block_wide(const f32x4_t (&acc)[8][8],
+                                                      const uint16_t* gu, uint16_t* dgu, long ld,
+                                                      int F, int row0, int col0, int lane) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  const int crow = lane & 15;
+  const int q = lane >> 4;
+  const int ccol = (q & 1) * 16 + (q >> 1) * 8;
+  const long off0 = static_cast<long>(row0 + crow) * ld + col0 + ccol;
+  const long step = 16 * ld;
+  uint4 gw[2][4], uw[2][4];
+  auto load = [&](int i, int b) {
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      gw[b][jp] = *reinterpret_cast<const uint4*>(gu + off0 + i * step + jp * 32);
+      uw[b][jp] = *reinterpret_cast<const uint4*>(gu + off0 + i * step + F + jp * 32);
+    }
+  };
+  load(0, 0);
+  load(1, 1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int b = i & 1;
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][e]),
+                                                        __float_as_uint(acc[i][2 * jp + 1][e]),
+                                                        false, false);
+        d[e] = __uint_as_float(p[0]);
+        d[4 + e] = __uint_as_float(p[1]);
+      }
+      const uint32_t gp[4] = {gw[b][jp].x, gw[b][jp].y, gw[b][jp].z, gw[b][jp].w};
+      const uint32_t up[4] = {uw[b][jp].x, uw[b][jp].y, uw[b][jp].z, uw[b][jp].w};
+      uint32_t pg[4], pu[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const f2_t g = {__uint_as_float(gp[h] << 16), __uint_as_float(gp[h] & 0xFFFF0000u)};
+        const f2_t u = {__uint_as_float(up[h] << 16), __uint_as_float(up[h] & 0xFFFF0000u)};
+        const f2_t dd = {d[2 * h], d[2 * h + 1]};
+        const f2_t x = g * -1.44269504f;
+        const f2_t sg = {__builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[0])),
+                         __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[1]))};
+        const f2_t t = dd * sg;
+        const f2_t du = t * g;
+        const f2_t dg = t * u * ((g + 1.f) - g * sg);
+        pg[h] = pack2bf(dg[0], dg[1]);
+        pu[h] = pack2bf(du[0], du[1]);
+      }
+      *reinterpret_cast<uint4*>(dgu + off0 + i * step + jp * 32) = make_uint4(pg[0], pg[1], pg[2], pg[3]);
+      *reinterpret_cast<uint4*>(dgu + off0 + i * step + F + jp * 32) =
+          make_uint4(pu[0], pu[1], pu[2], pu[3]);
+    }
+    if (i + 2 < 8) load(i + 2, b);
+  }
+}
+
 // Per-K-tile instruction positions of the three-barrier GEMM schedules (see
 // gemm_bf16.hip): for MFMA index m (0..127) the fragment read / DMA piece
 // index that follows it (-1: none), and the MFMA after which each wait and
