@@ -414,7 +414,8 @@ __device__ __forceinline__ void x2_ktile_s(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)
 }
 
 // EPI 0: 8-B stores, 1: widened 16-B stores, 2: SwiGLU backward, 3: SwiGLU
-// backward with 16-B g / u accesses (mxk::swiglu_bwd_block_wide)
+// backward with 16-B g / u accesses (mxk::swiglu_bwd_block_wide), 4: the same
+// staged through LDS so each access covers whole lines (swiglu_bwd_block_lds)
 // (mxk::swiglu_bwd_block: C = d[g | u], aux = [g | u], both row stride ldc,
 // u at column offset N).
 // SPLIT (split tail): the launch after the whole-tile one (grid q_full,
@@ -521,6 +522,14 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     mxk::swiglu_bwd_block(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane);
   else if constexpr (EPI == 3)
     mxk::swiglu_bwd_block_wide(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane);
+  else if constexpr (EPI == 4) {
+    static_assert(4 * mxk::kSwigluLdsWave <= 2 * STAGE, "LDS slice per wave");
+    // every wave's last-stage fragment reads retired before any slice is written
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    mxk::swiglu_bwd_block_lds(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane,
+                              smem + wave * mxk::kSwigluLdsWave);
+  }
   else if constexpr (EPI == 1)
     mxk::store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else
@@ -636,15 +645,21 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
                   reinterpret_cast<uintptr_t>(dgu) % 8 == 0;
   if (!ok) return static_cast<int>(hipErrorInvalidValue);
   const int nwg = (M / XBM) * (F / XBM);
-  // EPI 3: 16-B g/u accesses (MXK_SWIGLU_WIDE=0 keeps the 8-B form, A/B)
-  static const bool wide_ok = [] {
+  // 16-B g/u accesses: EPI 4 (LDS-staged, whole lines) by default, EPI 3
+  // (permlane pairs) with MXK_SWIGLU_WIDE=3, the 8-B form with =0 (A/B)
+  static const int wide_mode = [] {
     const char* e = std::getenv("MXK_SWIGLU_WIDE");
-    return !(e && e[0] == '0');
+    return e ? std::atoi(e) : 4;
   }();
-  const bool wide = wide_ok && reinterpret_cast<uintptr_t>(gu) % 16 == 0 &&
+  const bool wide = wide_mode != 0 && reinterpret_cast<uintptr_t>(gu) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(dgu) % 16 == 0;
-  if (wide)
+  if (wide && wide_mode == 3)
     hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<false, true, 3, 0>), dim3(nwg), dim3(XT), 0, stream,
+                       static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
+                       static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
+                       static_cast<const uint16_t*>(gu));
+  else if (wide)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<false, true, 4, 0>), dim3(nwg), dim3(XT), 0, stream,
                        static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
                        static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
                        static_cast<const uint16_t*>(gu));

@@ -349,6 +349,78 @@ __device__ __forceinline__ void swiglu_bwd_block_wide(const f32x4_t (&acc)[8][8]
   }
 }
 
+// LDS-staged form: the wave's d block goes through its own LDS slice (the
+// stages are free after the K loop; the caller barriers first) in four
+// 32-row passes, and is read back row-major so that every g / u load and
+// dg / du store covers 4 rows x 256 B (16 lanes x 16 B per row) - whole
+// 128-B lines instead of the 16 rows x 64 B of the permlane form.  The g / u
+// loads of pass p + 1 are in flight while pass p is written and computed.
+// lds: 32 x 528 B per wave (512-B fp32 rows + 16-B pad: the 16 rows of a
+// ds_write_b128 group land 4 banks apart).
+constexpr int kSwigluLdsRow = 528;
+constexpr int kSwigluLdsWave = 32 * kSwigluLdsRow;
+__device__ __forceinline__ void swiglu_bwd_block_lds(const f32x4_t (&acc)[8][8],
+                                                     const uint16_t* gu, uint16_t* dgu, long ld,
+                                                     int F, int row0, int col0, int lane,
+                                                     char* lds) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  const int crow = lane & 15, q = lane >> 4;
+  const int rr = lane >> 4, cc = (lane & 15) * 8;   // read phase: row rr of 4, 8 columns
+  uint4 gw[2][8], uw[2][8];
+  auto load = [&](int p, int b) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const long off = static_cast<long>(row0 + p * 32 + it * 4 + rr) * ld + col0 + cc;
+      gw[b][it] = *reinterpret_cast<const uint4*>(gu + off);
+      uw[b][it] = *reinterpret_cast<const uint4*>(gu + off + F);
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int b = p & 1;
+    if (p + 1 < 4) load(p + 1, b ^ 1);
+    // d rows [32p, 32p + 32) = accumulator rows i = 2p, 2p + 1
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        *reinterpret_cast<f32x4_t*>(lds + (ii * 16 + crow) * kSwigluLdsRow + (j * 16 + q * 4) * 4) =
+            acc[2 * p + ii][j];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int r = it * 4 + rr;
+      const char* dp = lds + r * kSwigluLdsRow + cc * 4;
+      const f32x4_t d0 = *reinterpret_cast<const f32x4_t*>(dp);
+      const f32x4_t d1 = *reinterpret_cast<const f32x4_t*>(dp + 16);
+      const float d[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
+      const uint32_t gp[4] = {gw[b][it].x, gw[b][it].y, gw[b][it].z, gw[b][it].w};
+      const uint32_t up[4] = {uw[b][it].x, uw[b][it].y, uw[b][it].z, uw[b][it].w};
+      uint32_t pg[4], pu[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const f2_t g = {__uint_as_float(gp[h] << 16), __uint_as_float(gp[h] & 0xFFFF0000u)};
+        const f2_t u = {__uint_as_float(up[h] << 16), __uint_as_float(up[h] & 0xFFFF0000u)};
+        const f2_t dd = {d[2 * h], d[2 * h + 1]};
+        const f2_t x = g * -1.44269504f;
+        const f2_t sg = {__builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[0])),
+                         __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[1]))};
+        const f2_t t = dd * sg;
+        const f2_t du = t * g;
+        const f2_t dg = t * u * ((g + 1.f) - g * sg);
+        pg[h] = pack2bf(dg[0], dg[1]);
+        pu[h] = pack2bf(du[0], du[1]);
+      }
+      const long off = static_cast<long>(row0 + p * 32 + r) * ld + col0 + cc;
+      *reinterpret_cast<uint4*>(dgu + off) = make_uint4(pg[0], pg[1], pg[2], pg[3]);
+      *reinterpret_cast<uint4*>(dgu + off + F) = make_uint4(pu[0], pu[1], pu[2], pu[3]);
+    }
+    // this pass's LDS reads retire before the next pass overwrites the slice
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __asm__ volatile("" ::: "memory");
+  }
+}
+
 // Per-K-tile instruction positions of the three-barrier GEMM schedules (see
 // gemm_bf16.hip): for MFMA index m (0..127) the fragment read / DMA piece
 // index that follows it (-1: none), and the MFMA after which each wait and
