@@ -110,10 +110,11 @@ class _LinearFn(torch.autograd.Function):
 # y = swiglu(gu) W^T with the SwiGLU backward fused into the input-gradient
 # GEMM's epilogue (mxk_gemm_bf16_dgrad_swiglu): d(act) = dy W never goes to
 # HBM (0.94 GB less traffic per Llama-3-8B layer, no separate element-wise
-# pass, d(act) kept in fp32).  Step time is unchanged (26.19-26.20k vs
-# 26.19k tok/s, profiles/r1_swiglu/): with one workgroup per CU the epilogue's
-# extra g/u reads are not hidden behind MFMA work.  MXK_FUSED_SWIGLU=0 runs
-# the unfused pair.
+# pass, d(act) kept in fp32).  Round 1 measured it step-neutral (the 8-B
+# per-lane g/u accesses made the epilogue slow); with the LDS-staged epilogue
+# (whole-line g/u accesses) the kernel runs 1.52 ms against 1.71 and the step
+# gains 1.1 % (profiles/r2_split_tail/).  MXK_FUSED_SWIGLU=0 runs the
+# unfused pair.
 _USE_FUSED_SWIGLU = os.environ.get("MXK_FUSED_SWIGLU", "1") != "0"
 
 
