@@ -39,8 +39,8 @@
 //   3 w4i   widened plain stores, barrier #3 after m 96
 //   4 w4i   variant 3 with A k1 reads at even m and barrier #1 after m 21
 //   5 w4ip  persistent w4i (one workgroup per CU)
-//   6 w4j   default: w4i with every read/DMA/wait at hipBLASLt's MFMA
-//           positions (+0.5-2 % over 0 on squares and the Llama-3-8B shapes)
+//   6 w4j   w4i with every read/DMA/wait at hipBLASLt's MFMA positions
+//           (+0.5-2 % over 0 on squares and the Llama-3-8B shapes)
 //   7 w4j   two barriers per K-tile (SchedTwoBarrier)
 //   8 w4j   variant 6 with plain (temporal) widened stores
 //   9 x2    the layout kernel of gemm_bf16_layouts.hip (same schedule as 6,
@@ -59,6 +59,10 @@
 //  21-24 w4j schedule 6 with a staggered first round (four CU groups start
 //           1/2/4/8 x ~1024 clocks apart, so C store bursts do not coincide)
 //  25 w4j   variant 23 with plain (temporal) widened stores
+//  26 w4j   default: schedule 6 with the C tile stored through LDS, read
+//           back row-major so every store covers whole lines (4 rows x 256 B
+//           per wave-instruction instead of 16 x 64 B): +1.3 / +3.0 / +0.4 %
+//           over 6 at 8192^3 / 4096^3 / 16384^3 (profiles/r2_gemm_ab/)
 // The earlier schedules (one-barrier w4b, 8-wave, 4-deep ring, w4h, ...)
 // were retired when an ISA audit (tests/test_isa_hazards.py) found their
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
@@ -405,7 +409,13 @@ mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   mxk::mfma_drain(acc);
 
-  if constexpr (EPI == 1) store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+  if constexpr (EPI == 4) {
+    // whole-line stores through LDS; every wave's last fragment reads retired first
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    mxk::store_block_lds<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane,
+                               smem + wave_s * mxk::kStoreLdsWave);
+  } else if constexpr (EPI == 1) store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else if constexpr (EPI == 2) store_block_wide<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else if constexpr (EPI == 3) {
     // DIAGNOSTIC ONLY (ablation variant 10): one lane per wave stores one value,
@@ -749,14 +759,14 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                                      int variant, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 26;
-constexpr int kDefaultVariant = 6;
+constexpr int kNumVariants = 27;
+constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
     "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar",
     "w4j_hb_st", "x2_hb", "diag_nostore", "w4ip_hb_st", "w4ip_hb_nt", "w4j_earlyb",
     "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg", "pp8",
-    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st"};
+    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -814,6 +824,7 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 23: launch_w4i<1, 2, 1, 0, 1, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 24: launch_w4i<1, 2, 1, 0, 1, 0, 8>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 25: launch_w4i<1, 1, 1, 0, 1, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 26: launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 19:
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_pp8<1, 0>), dim3(nwg), dim3(PP_THREADS), 0, stream, a, b,
                          c, M, N, K, lda, ldb, ldc);

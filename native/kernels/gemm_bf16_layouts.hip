@@ -413,7 +413,7 @@ __device__ __forceinline__ void x2_ktile_s(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)
     x2_ktile<AN, BN, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, soa, sob, wave, par);
 }
 
-// EPI 0: 8-B stores, 1: widened 16-B stores, 2: SwiGLU backward, 3: SwiGLU
+// EPI 0: 8-B stores, 1: 16-B stores through LDS (whole lines), 2: SwiGLU backward, 3: SwiGLU
 // backward with 16-B g / u accesses (mxk::swiglu_bwd_block_wide), 4: the same
 // staged through LDS so each access covers whole lines (swiglu_bwd_block_lds)
 // (mxk::swiglu_bwd_block: C = d[g | u], aux = [g | u], both row stride ldc,
@@ -530,8 +530,15 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     mxk::swiglu_bwd_block_lds(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane,
                               smem + wave * mxk::kSwigluLdsWave);
   }
-  else if constexpr (EPI == 1)
-    mxk::store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+  else if constexpr (EPI == 1) {
+    // whole-line stores through LDS (as the TN kernel's default schedule);
+    // every wave's last fragment reads retired before a slice is written
+    static_assert(4 * mxk::kStoreLdsWave <= 2 * STAGE, "LDS slice per wave");
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    mxk::store_block_lds<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane,
+                                smem + wave * mxk::kStoreLdsWave);
+  }
   else
     mxk::store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
 }

@@ -219,6 +219,42 @@ __device__ __forceinline__ void store_block_narrow(const f32x4_t (&acc)[8][8], u
   }
 }
 
+// bf16 store of a wave's 128x128 accumulator block through its own LDS
+// slice (two 64-row passes, 272-B padded rows), read back row-major so each
+// global store covers 4 rows x 256 B (whole lines) instead of the 16 rows x
+// 64 B of store_block_wide.  The caller barriers before the first call (the
+// slices overlap the GEMM's stages).  lds: 64 x 272 B per wave.
+constexpr int kStoreLdsRow = 272;
+constexpr int kStoreLdsWave = 64 * kStoreLdsRow;
+template <bool NT = true>
+__device__ __forceinline__ void store_block_lds(const f32x4_t (&acc)[8][8], uint16_t* C, int ldc,
+                                                int row0, int col0, int lane, char* lds) {
+  const int crow = lane & 15, q = lane >> 4;
+  const int rr = lane >> 4, cc = (lane & 15) * 8;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint2 pk;
+        pk.x = pack2bf(acc[4 * p + ii][j][0], acc[4 * p + ii][j][1]);
+        pk.y = pack2bf(acc[4 * p + ii][j][2], acc[4 * p + ii][j][3]);
+        *reinterpret_cast<uint2*>(lds + (ii * 16 + crow) * kStoreLdsRow + (j * 16 + q * 4) * 2) = pk;
+      }
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int r = it * 4 + rr;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(lds + r * kStoreLdsRow + cc * 2);
+      uint16_t* cp = C + static_cast<size_t>(row0 + p * 64 + r) * ldc + col0 + cc;
+      if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(cp));
+      else *reinterpret_cast<u32x4_t*>(cp) = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __asm__ volatile("" ::: "memory");
+  }
+}
+
 // Fused SwiGLU-backward epilogue of the down-projection's input-gradient GEMM:
 // the block's accumulators are d(act) = dY W2 for act = silu(g) * u, and the
 // lane's 4 consecutive columns of row r are combined with g, u read from
