@@ -603,15 +603,26 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
   const float lt = half_sum(l);
   const float inv = 1.f / lt;
   uint16_t* orow = o + (static_cast<long>(b) * S + myq) * Hq * D + static_cast<long>(hq) * D;
+  // 16-B stores: v_permlane32_swap pairs groups g = 2k, 2k+1 across the lane
+  // halves, so lane half h holds d = 32 db + 16 k + 8 h + 0..7 (half h of
+  // group g holds 4 h + 0..3 of its 8)
 #pragma unroll
   for (int db = 0; db < 4; ++db) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 32 * db + 8 * g + 4 * h;
-      uint2 pk;
-      pk.x = mxk::pack2bf(acc[db][4 * g] * inv, acc[db][4 * g + 1] * inv);
-      pk.y = mxk::pack2bf(acc[db][4 * g + 2] * inv, acc[db][4 * g + 3] * inv);
-      *reinterpret_cast<uint2*>(orow + d) = pk;
+    for (int k = 0; k < 2; ++k) {
+      const int g0 = 2 * k, g1 = 2 * k + 1;
+      const uint32_t x0 = mxk::pack2bf(acc[db][4 * g0] * inv, acc[db][4 * g0 + 1] * inv);
+      const uint32_t x1 = mxk::pack2bf(acc[db][4 * g0 + 2] * inv, acc[db][4 * g0 + 3] * inv);
+      const uint32_t y0 = mxk::pack2bf(acc[db][4 * g1] * inv, acc[db][4 * g1 + 1] * inv);
+      const uint32_t y1 = mxk::pack2bf(acc[db][4 * g1 + 2] * inv, acc[db][4 * g1 + 3] * inv);
+      const auto p0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+      const auto p1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+      uint4 v;
+      v.x = p0[0];
+      v.y = p1[0];
+      v.z = p0[1];
+      v.w = p1[1];
+      *reinterpret_cast<uint4*>(orow + 32 * db + 16 * k + 8 * h) = v;
     }
   }
   if (h == 0) lse[(static_cast<long>(b) * Hq + hq) * S + myq] = m * scale + logf(lt);
