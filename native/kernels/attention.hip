@@ -1141,15 +1141,24 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   }
   }
   uint16_t* row = dq + (static_cast<long>(b) * S + myq) * Hq * D + static_cast<long>(hq) * D;
+  // 16-B stores, lane halves paired by v_permlane32_swap (as the forward's O)
 #pragma unroll
   for (int db = 0; db < 4; ++db) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 32 * db + 8 * g + 4 * h;
-      uint2 pk;
-      pk.x = mxk::pack2bf(acc[db][4 * g] * scale, acc[db][4 * g + 1] * scale);
-      pk.y = mxk::pack2bf(acc[db][4 * g + 2] * scale, acc[db][4 * g + 3] * scale);
-      *reinterpret_cast<uint2*>(row + d) = pk;
+    for (int k = 0; k < 2; ++k) {
+      const int g0 = 2 * k, g1 = 2 * k + 1;
+      const uint32_t x0 = mxk::pack2bf(acc[db][4 * g0] * scale, acc[db][4 * g0 + 1] * scale);
+      const uint32_t x1 = mxk::pack2bf(acc[db][4 * g0 + 2] * scale, acc[db][4 * g0 + 3] * scale);
+      const uint32_t y0 = mxk::pack2bf(acc[db][4 * g1] * scale, acc[db][4 * g1 + 1] * scale);
+      const uint32_t y1 = mxk::pack2bf(acc[db][4 * g1 + 2] * scale, acc[db][4 * g1 + 3] * scale);
+      const auto p0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+      const auto p1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+      uint4 v;
+      v.x = p0[0];
+      v.y = p1[0];
+      v.z = p0[1];
+      v.w = p1[1];
+      *reinterpret_cast<uint4*>(row + 32 * db + 16 * k + 8 * h) = v;
     }
   }
 }
