@@ -24,7 +24,8 @@ LDLIBS_NODE := -ldl -lpthread
 
 KERNEL_SRCS := native/kernels/gemm_bf16.hip native/kernels/vector_add.hip \
                native/kernels/fused_ops.hip native/kernels/optim.hip native/kernels/attention.hip \
-               native/kernels/gemm_bf16_layouts.hip native/kernels/xent.hip
+               native/kernels/gemm_bf16_layouts.hip native/kernels/xent.hip \
+               native/kernels/gemm_bf16_ring.hip
 KERNEL_OBJS := $(patsubst native/kernels/%.hip,$(BUILD)/kernels/%.o,$(KERNEL_SRCS))
 KERNEL_HDRS := $(wildcard native/kernels/*.h)
 
@@ -79,7 +80,7 @@ $(OUT_BIN)/mx-vector-add: $(BUILD)/tools/vector_add_main.o $(BUILD)/kernels/vect
 	@mkdir -p $(OUT_BIN)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^
 
-$(OUT_BIN)/mx-gemm-bench: $(BUILD)/tools/gemm_bench_main.o $(BUILD)/kernels/gemm_bf16.o $(BUILD)/kernels/gemm_bf16_layouts.o
+$(OUT_BIN)/mx-gemm-bench: $(BUILD)/tools/gemm_bench_main.o $(BUILD)/kernels/gemm_bf16.o $(BUILD)/kernels/gemm_bf16_layouts.o $(BUILD)/kernels/gemm_bf16_ring.o
 	@mkdir -p $(OUT_BIN)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrocblas -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
 

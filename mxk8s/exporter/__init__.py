@@ -75,20 +75,43 @@ class MetricWriter:
 
 
 class SmiBackend:
-    """Real backend: libmxnode topology + amd-smi samples, matched by BDF."""
+    """Real backend: libmxnode topology + amd-smi samples, matched by BDF (and
+    partition id: the partitions of a device share its BDF).
+
+    amd-smi enumerates at init, so after a compute-partition change (SPX ->
+    CPX: 8 -> 64 KFD GPUs) or a driver reload the open session still lists
+    the old handles: when the KFD and amd-smi GPU counts disagree the backend
+    re-initialises amd-smi, and it re-maps its indices whenever the session's
+    generation changes (re-initialised by this or another user)."""
 
     def __init__(self, sysfs_root: str = ""):
         self.sysfs_root = sysfs_root
         self.ok, self.err = node.smi_open()
         self.driver = node.smi_driver_version() if self.ok else ""
         self._smi_index: dict[str, int] = {}
+        self._gen = node.smi_generation() if self.ok else 0
+        self.reinits = 0
 
     def gpus(self) -> list[node.GpuInfo]:
         return node.enumerate_gpus(self.sysfs_root)
 
+    def _refresh(self) -> None:
+        n_kfd = len(node.enumerate_gpus(self.sysfs_root))
+        if node.smi_count() != n_kfd:
+            ok, err = node.smi_reinit()
+            self.reinits += 1
+            if not ok:
+                self.err = err
+            self.driver = node.smi_driver_version()
+        gen = node.smi_generation()
+        if gen != self._gen:
+            self._gen = gen
+            self._smi_index.clear()
+
     def samples(self) -> dict[str, node.GpuSample]:
         if not self.ok:
             return {}
+        self._refresh()
         out = {}
         for i in range(max(0, node.smi_count())):
             s = node.smi_sample(i)
@@ -104,6 +127,11 @@ class SmiBackend:
     def processes(self, key: str) -> list:
         i = self._smi_index.get(key)
         return [] if i is None else node.smi_processes(i)
+
+    def close(self) -> None:
+        if self.ok:
+            node.smi_close()
+            self.ok = False
 
     def health(self, index: int) -> int:
         return node.health_check(index, self.sysfs_root, os.environ.get("MXK8S_FAULT_FILE"))

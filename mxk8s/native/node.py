@@ -232,6 +232,10 @@ def lib() -> ctypes.CDLL:
             L.mx_smi_processes.argtypes = [i, ctypes.POINTER(_Proc), i]
             L.mx_smi_processes.restype = i
             L.mx_smi_close.restype = None
+            L.mx_smi_reset.restype = None
+            L.mx_smi_reinit.argtypes = [cp, sz]
+            L.mx_smi_reinit.restype = i
+            L.mx_smi_generation.restype = ctypes.c_uint64
             vp = ctypes.c_void_p
             L.mx_hm_create.argtypes = [ctypes.POINTER(_HealthOpts), cp, sz]
             L.mx_hm_create.restype = vp
@@ -394,7 +398,26 @@ def smi_wait_events(timeout_ms: int, max_events: int = 32) -> list[tuple[int, in
 
 
 def smi_close() -> None:
+    """Release one reference on the process's amd-smi session."""
     lib().mx_smi_close()
+
+
+def smi_reset() -> None:
+    """End the amd-smi session whatever its reference count (tests)."""
+    lib().mx_smi_reset()
+
+
+def smi_reinit() -> tuple[bool, str]:
+    """amdsmi_shut_down + amdsmi_init on the open session: new handles for a
+    changed GPU set (compute-partition change, driver reload)."""
+    err = ctypes.create_string_buffer(512)
+    ok = bool(lib().mx_smi_reinit(err, len(err)))
+    return ok, err.value.decode()
+
+
+def smi_generation() -> int:
+    """Changes on every amd-smi (re)init; cached amd-smi indices are void then."""
+    return int(lib().mx_smi_generation())
 
 
 @dataclasses.dataclass(frozen=True)

@@ -93,8 +93,9 @@ __device__ __forceinline__ void mfma_16x16x32_agpr(f32x4_t& acc, bf16x8_t a, bf1
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
-  static_assert(N == 13 || N == 15 || N == 16, "vm_wait: add the count");
-  if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  static_assert(N == 0 || N == 13 || N == 15 || N == 16, "vm_wait: add the count");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
 }
@@ -297,6 +298,12 @@ __device__ __forceinline__ void ktile_sched(f32x4_t (&acc)[8][8], bf16x8_t (&f0a
   else if constexpr (SCHED == 6)   // SchedHB with raised wave priority
     w4j_ktile<SchedHB, PAR, MODE, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,
                                         off_k1, dma_a, dma_b, kb2, wave_s, par);
+  else if constexpr (SCHED == 7)
+    w4j_ktile<mxk::SchedOneBarrier, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,
+                                               off_k1, dma_a, dma_b, kb2, wave_s, par);
+  else if constexpr (SCHED == 8)
+    w4j_ktile<mxk::SchedOneBarrierSpread, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base,
+                                                     off_k0, off_k1, dma_a, dma_b, kb2, wave_s, par);
   else if constexpr (SCHED == 2)
     w4j_ktile<SchedTwoBarrier, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,
                                           off_k1, dma_a, dma_b, kb2, wave_s, par);
@@ -757,16 +764,18 @@ mxk_gemm_bf16_tn_generic(const uint16_t* __restrict__ A, const uint16_t* __restr
 MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int M, int N, int K,
                                      int lda, int ldb, int ldc, int a_kmajor, int b_kmajor,
                                      int variant, hipStream_t stream);
+int mxk_gemm_bf16_tn_ring_launch(int slots, const void* A, const void* Bt, void* C, int M, int N,
+                                 int K, int lda, int ldb, int ldc, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 27;
+constexpr int kNumVariants = 31;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
     "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar",
     "w4j_hb_st", "x2_hb", "diag_nostore", "w4ip_hb_st", "w4ip_hb_nt", "w4j_earlyb",
     "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg", "pp8",
-    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst"};
+    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -825,6 +834,10 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 24: launch_w4i<1, 2, 1, 0, 1, 0, 8>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 25: launch_w4i<1, 1, 1, 0, 1, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 26: launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 27: launch_w4i<1, 4, 1, 0, 7>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 28: launch_w4i<1, 4, 1, 0, 8>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 29: mxk_gemm_bf16_tn_ring_launch(4, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
+    case 30: mxk_gemm_bf16_tn_ring_launch(5, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 19:
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_pp8<1, 0>), dim3(nwg), dim3(PP_THREADS), 0, stream, a, b,
                          c, M, N, K, lda, ldb, ldc);

@@ -522,6 +522,42 @@ struct SchedTwoBarrier {
   }
 };
 
+// SCHED 7: ONE barrier per K-tile.  The two 64 KiB stages alternate per
+// K-tile (tile t reads buffer t & 1); the barrier sits in the MIDDLE of the
+// tile, after the k-half-1 fragments of stage t were read (m 0..30, retired
+// by the lgkmcnt(0) before it) and after this wave's pieces of stage t+1
+// landed (vmcnt(0): the only DMA in flight is stage t+1's, issued one K-tile
+// earlier).  Past it every wave is done with buffer t & 1 (-> refill with
+// stage t+2, m 64..94 even) and stage t+1 is visible everywhere (-> its
+// k-half-0 fragments, m 65..95 odd).  The DMA gets a whole K-tile to land.
+struct SchedOneBarrier {
+  static constexpr int W1 = 62, B1 = -1, W2 = -1, B2 = -1, W3 = 62, VM3 = 0, B3 = 63;
+  __host__ __device__ static constexpr int a1(int m) { return m < 16 && (m & 1) == 0 ? m >> 1 : -1; }
+  __host__ __device__ static constexpr int b1(int m) {
+    return m >= 16 && m < 32 && (m & 1) == 0 ? (m - 16) >> 1 : -1;
+  }
+  __host__ __device__ static constexpr int adma(int m) {
+    return m >= 64 && m < 80 && (m & 1) == 0 ? (m - 64) >> 1 : -1;
+  }
+  __host__ __device__ static constexpr int bdma(int m) {
+    return m >= 80 && m < 96 && (m & 1) == 0 ? (m - 80) >> 1 : -1;
+  }
+  __host__ __device__ static constexpr int k0(int m) {
+    return m >= 65 && m < 96 && (m & 1) ? (m - 65) >> 1 : -1;
+  }
+};
+
+// SCHED 8: SchedOneBarrier with the 16 pieces spread one per three MFMAs
+// (m 64..109) and the k-half-0 reads one per two (odd m 65..95).
+struct SchedOneBarrierSpread : SchedOneBarrier {
+  __host__ __device__ static constexpr int adma(int m) {
+    return m >= 64 && (m - 64) % 6 == 0 && (m - 64) / 6 < 8 ? (m - 64) / 6 : -1;
+  }
+  __host__ __device__ static constexpr int bdma(int m) {
+    return m >= 67 && (m - 67) % 6 == 0 && (m - 67) / 6 < 8 ? (m - 67) / 6 : -1;
+  }
+};
+
 }  // namespace mxk
 
 // Host-side error plumbing: every launcher returns hipError_t as int so the

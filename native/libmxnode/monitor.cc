@@ -62,6 +62,7 @@ struct mx_health_monitor {
   std::string root, fault_file, state_dir, boot_id;
   int64_t event_q_ms = 60000, ecc_q_ms = 0;
   bool smi = false;
+  uint64_t smi_gen = 0;          // amd-smi session generation the smi_index values belong to
   std::vector<Gpu> gpus;
   std::deque<mx_health_event> log;
   uint64_t seq = 0;
@@ -83,6 +84,24 @@ struct mx_health_monitor {
     std::snprintf(e.message, sizeof(e.message), "%s", msg.c_str());
     log.push_back(e);
     while (log.size() > 1024) log.pop_front();
+  }
+
+  // amd-smi index of every GPU, matched by BDF (+ partition id: partitions of
+  // one device share the BDF).  Returns the number of GPUs left unmatched.
+  int match_smi() {
+    for (auto& g : gpus) g.smi_index = -1;
+    smi_gen = mx_smi_generation();
+    const int ns = mx_smi_count();
+    for (int k = 0; k < ns; ++k) {
+      mx_gpu_sample s;
+      mx_smi_sample(k, &s);
+      for (auto& g : gpus)
+        if (std::strcmp(s.bdf, g.info.pci_bdf) == 0 && s.partition_id == g.info.partition)
+          g.smi_index = k;
+    }
+    int unmatched = 0;
+    for (const auto& g : gpus) unmatched += g.smi_index < 0;
+    return unmatched;
   }
 
   std::string baseline_path() const { return state_dir.empty() ? "" : state_dir + "/ecc-baseline"; }
@@ -148,15 +167,17 @@ extern "C" mx_health_monitor* mx_hm_create(const mx_health_opts* o, char* err, s
     char serr[256] = {0};
     if (mx_smi_open(serr, sizeof(serr))) {
       m->smi = true;
-      // match amd-smi handles to KFD GPUs by BDF; partitions of one device
-      // share the BDF and pair up by partition id
-      const int ns = mx_smi_count();
-      for (int k = 0; k < ns; ++k) {
-        mx_gpu_sample s;
-        mx_smi_sample(k, &s);
-        for (auto& g : m->gpus)
-          if (std::strcmp(s.bdf, g.info.pci_bdf) == 0 && s.partition_id == g.info.partition)
-            g.smi_index = k;
+      // amd-smi enumerates at init: a session opened before a partition change
+      // (SPX -> CPX: 8 -> 64 KFD GPUs) or a driver reload holds the old handle
+      // list.  KFD and amd-smi disagreeing on the count is that case: re-init
+      // and match again (other users of the session re-match on the new
+      // generation).
+      if (m->match_smi() > 0 && mx_smi_count() != static_cast<int>(m->gpus.size())) {
+        if (mx_smi_reinit(serr, sizeof(serr)))
+          m->event(-1, MX_EVT_HEALTH_CHANGE, 0, "amd-smi re-initialised: GPU set changed");
+        else
+          m->event(-1, MX_EVT_HEALTH_CHANGE, 0, std::string("amd-smi re-init failed: ") + serr);
+        m->match_smi();
       }
     } else {
       m->event(-1, MX_EVT_HEALTH_CHANGE, 0, std::string("amd-smi unavailable: ") + serr);
@@ -166,12 +187,20 @@ extern "C" mx_health_monitor* mx_hm_create(const mx_health_opts* o, char* err, s
   return m;
 }
 
-extern "C" void mx_hm_destroy(mx_health_monitor* m) { delete m; }
+extern "C" void mx_hm_destroy(mx_health_monitor* m) {
+  if (m && m->smi) mx_smi_close();
+  delete m;
+}
 
 extern "C" int mx_hm_smi_active(mx_health_monitor* m) { return m && m->smi ? 1 : 0; }
 
 extern "C" int mx_hm_step(mx_health_monitor* m, int wait_ms) {
   if (!m) return -1;
+  // 0. another user re-initialised amd-smi: every cached index is void
+  if (m->smi && mx_smi_generation() != m->smi_gen) {
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->match_smi();
+  }
   // 1. amd-smi events (blocking wait outside the monitor lock)
   int gi[64], ev[64];
   int nev = 0;
@@ -194,6 +223,7 @@ extern "C" int mx_hm_step(mx_health_monitor* m, int wait_ms) {
     sysfs[i] = mx_health_check(m->root.c_str(), static_cast<int>(i), m->fault_file.c_str());
 
   std::lock_guard<std::mutex> lk(m->mu);
+  if (m->smi && mx_smi_generation() != m->smi_gen) m->match_smi();   // re-init during the wait
   const int64_t now = mono_ms();
   for (int k = 0; k < nev; ++k) {
     const int i = m->by_smi(gi[k]);

@@ -199,8 +199,18 @@ typedef struct mx_gpu_sample {
 } mx_gpu_sample;
 
 // 1 if amd-smi could be loaded and initialised, 0 otherwise (msg in err).
+// Reference-counted per process: each successful open needs one close.
 int mx_smi_open(char* err, size_t errlen);
 void mx_smi_close(void);
+// End the session whatever the reference count (tests, process teardown).
+void mx_smi_reset(void);
+// Shut amd-smi down and initialise it again on the open session, so that a
+// changed GPU set (compute-partition change, driver reload) gets new handles.
+// Every amd-smi index from before is void afterwards; 1 on success.
+int mx_smi_reinit(char* err, size_t errlen);
+// Changes whenever amd-smi was (re)initialised; 0 if not open.  Users that
+// cache amd-smi indices re-match them (by BDF + partition) when it changes.
+uint64_t mx_smi_generation(void);
 // Number of GPUs amd-smi sees (after mx_smi_open), -1 if not open.
 int mx_smi_count(void);
 // Sample GPU i (amd-smi enumeration order, matched to BDF by the caller).

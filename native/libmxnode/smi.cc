@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -52,8 +53,15 @@ struct SmiApi {
   std::string driver_version;
 };
 
+// g_mu guards g_api and every amd-smi call except the blocking event wait;
+// g_life orders the session's lifetime against that wait: (re)init and
+// shutdown take it exclusively, mx_smi_wait_events holds it shared across the
+// blocking amdsmi_get_gpu_event_notification.  Lock order: g_life, then g_mu.
 std::mutex g_mu;
+std::shared_mutex g_life;
 SmiApi* g_api = nullptr;
+int g_refs = 0;            // mx_smi_open calls not yet matched by mx_smi_close
+uint64_t g_gen = 0;        // bumped by every amdsmi_init (open or re-init)
 
 template <typename F>
 bool bind(void* h, const char* name, F* slot) {
@@ -70,11 +78,71 @@ void fmt_bdf(uint64_t bdf, char* out, size_t n) {
                 static_cast<unsigned long long>(bdf & 0x7));
 }
 
+// amdsmi_init + enumeration of the GPU processor handles.  amd-smi takes its
+// handle list at init: after a compute-partition change (SPX -> CPX) or a
+// driver reload only a fresh init sees the new partitions.
+bool init_session(SmiApi* api, std::string* why) {
+  api->gpus.clear();
+  api->events_on = false;
+  api->driver_version.clear();
+  amdsmi_status_t st = api->amdsmi_init(AMDSMI_INIT_AMD_GPUS);
+  if (st != AMDSMI_STATUS_SUCCESS) {
+    *why = "amdsmi_init failed: status " + std::to_string(st);
+    return false;
+  }
+  uint32_t nsock = 0;
+  api->amdsmi_get_socket_handles(&nsock, nullptr);
+  std::vector<amdsmi_socket_handle> socks(nsock);
+  if (nsock) api->amdsmi_get_socket_handles(&nsock, socks.data());
+  for (uint32_t s = 0; s < nsock; ++s) {
+    uint32_t np = 0;
+    api->amdsmi_get_processor_handles(socks[s], &np, nullptr);
+    std::vector<amdsmi_processor_handle> ps(np);
+    if (np) api->amdsmi_get_processor_handles(socks[s], &np, ps.data());
+    for (uint32_t p = 0; p < np; ++p) {
+      processor_type_t t;
+      if (api->amdsmi_get_processor_type(ps[p], &t) == AMDSMI_STATUS_SUCCESS &&
+          t == AMDSMI_PROCESSOR_TYPE_AMD_GPU)
+        api->gpus.push_back(ps[p]);
+    }
+  }
+  if (!api->gpus.empty()) {
+    amdsmi_driver_info_t di;
+    std::memset(&di, 0, sizeof(di));
+    if (api->amdsmi_get_gpu_driver_info(api->gpus[0], &di) == AMDSMI_STATUS_SUCCESS)
+      api->driver_version = di.driver_version;
+  }
+  ++g_gen;
+  return true;
+}
+
+void end_session(SmiApi* api) {
+  if (api->events_on && api->amdsmi_stop_gpu_event_notification)
+    for (auto h : api->gpus) api->amdsmi_stop_gpu_event_notification(h);
+  api->events_on = false;
+  api->gpus.clear();
+  api->amdsmi_shut_down();
+}
+
+void destroy_locked() {
+  end_session(g_api);
+  dlclose(g_api->handle);
+  delete g_api;
+  g_api = nullptr;
+  g_refs = 0;
+}
+
 }  // namespace
 
+// Reference-counted: every user (health monitor, exporter, labeller) opens
+// and closes its own reference on the one per-process session.
 extern "C" int mx_smi_open(char* err, size_t errlen) {
+  std::unique_lock<std::shared_mutex> life(g_life);
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_api) return 1;
+  if (g_api) {
+    ++g_refs;
+    return 1;
+  }
   const char* env = std::getenv("MXK8S_AMDSMI_LIB");
   const char* candidates[] = {env, "libamd_smi.so", "/opt/rocm/lib/libamd_smi.so"};
   void* h = nullptr;
@@ -114,48 +182,59 @@ extern "C" int mx_smi_open(char* err, size_t errlen) {
     delete api;
     return 0;
   }
-  amdsmi_status_t st = api->amdsmi_init(AMDSMI_INIT_AMD_GPUS);
-  if (st != AMDSMI_STATUS_SUCCESS) {
-    mx::set_err(err, errlen, "amdsmi_init failed: status " + std::to_string(st));
+  std::string why;
+  if (!init_session(api, &why)) {
+    mx::set_err(err, errlen, why);
     dlclose(h);
     delete api;
     return 0;
   }
-  uint32_t nsock = 0;
-  api->amdsmi_get_socket_handles(&nsock, nullptr);
-  std::vector<amdsmi_socket_handle> socks(nsock);
-  if (nsock) api->amdsmi_get_socket_handles(&nsock, socks.data());
-  for (uint32_t s = 0; s < nsock; ++s) {
-    uint32_t np = 0;
-    api->amdsmi_get_processor_handles(socks[s], &np, nullptr);
-    std::vector<amdsmi_processor_handle> ps(np);
-    if (np) api->amdsmi_get_processor_handles(socks[s], &np, ps.data());
-    for (uint32_t p = 0; p < np; ++p) {
-      processor_type_t t;
-      if (api->amdsmi_get_processor_type(ps[p], &t) == AMDSMI_STATUS_SUCCESS &&
-          t == AMDSMI_PROCESSOR_TYPE_AMD_GPU)
-        api->gpus.push_back(ps[p]);
-    }
-  }
-  if (!api->gpus.empty()) {
-    amdsmi_driver_info_t di;
-    std::memset(&di, 0, sizeof(di));
-    if (api->amdsmi_get_gpu_driver_info(api->gpus[0], &di) == AMDSMI_STATUS_SUCCESS)
-      api->driver_version = di.driver_version;
-  }
   g_api = api;
+  g_refs = 1;
   return 1;
 }
 
+// Releases one reference; the session ends with the last one.
 extern "C" void mx_smi_close(void) {
+  std::unique_lock<std::shared_mutex> life(g_life);
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_api) return;
-  if (g_api->events_on && g_api->amdsmi_stop_gpu_event_notification)
-    for (auto h : g_api->gpus) g_api->amdsmi_stop_gpu_event_notification(h);
-  g_api->amdsmi_shut_down();
-  dlclose(g_api->handle);
-  delete g_api;
-  g_api = nullptr;
+  if (--g_refs > 0) return;
+  destroy_locked();
+}
+
+// Ends the session whatever the reference count (process teardown, tests).
+extern "C" void mx_smi_reset(void) {
+  std::unique_lock<std::shared_mutex> life(g_life);
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_api) destroy_locked();
+}
+
+// amdsmi_shut_down + amdsmi_init on the open session: a new handle list (and
+// generation).  Every index from before is void; users re-match by BDF +
+// partition when mx_smi_generation() changes.  Waits for a blocked
+// mx_smi_wait_events to return.  0 (msg in err) if amd-smi is not open or the
+// init failed (the session then has no GPUs until the next re-init).
+extern "C" int mx_smi_reinit(char* err, size_t errlen) {
+  std::unique_lock<std::shared_mutex> life(g_life);
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_api) {
+    mx::set_err(err, errlen, "amd-smi is not open");
+    return 0;
+  }
+  end_session(g_api);
+  std::string why;
+  if (!init_session(g_api, &why)) {
+    ++g_gen;
+    mx::set_err(err, errlen, why);
+    return 0;
+  }
+  return 1;
+}
+
+extern "C" uint64_t mx_smi_generation(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_api ? g_gen : 0;
 }
 
 extern "C" int mx_smi_count(void) {
@@ -241,6 +320,7 @@ extern "C" int mx_smi_ecc(int i, uint64_t* correctable, uint64_t* uncorrectable)
 }
 
 extern "C" int mx_smi_wait_events(int timeout_ms, int* gpu_out, int* event_out, int max) {
+  std::shared_lock<std::shared_mutex> life(g_life);   // no re-init / shutdown under the wait
   SmiApi* a;
   {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -262,6 +342,7 @@ extern "C" int mx_smi_wait_events(int timeout_ms, int* gpu_out, int* event_out, 
   uint32_t n = static_cast<uint32_t>(ev.size());
   amdsmi_status_t st = a->amdsmi_get_gpu_event_notification(timeout_ms, &n, ev.data());
   if (st != AMDSMI_STATUS_SUCCESS) return st == AMDSMI_STATUS_NO_DATA ? 0 : -1;
+  std::lock_guard<std::mutex> lk(g_mu);
   int count = 0;
   for (uint32_t k = 0; k < n && count < max; ++k) {
     int gi = -1;

@@ -17,8 +17,14 @@
 //   $MXK8S_FAKE_AMDSMI_DIR/fail    if present: amdsmi_init fails
 //
 // Link peers are the other GPUs of the file in order (a full xGMI mesh).
+// partition=<k> puts k in the BDF id's bits 31:28 (compute partitions share
+// the device's BDF).  Like the real library, amdsmi_init takes the handle
+// list: the number of GPUs is fixed until the next init, and a handle from an
+// earlier init is invalid (AMDSMI_STATUS_INVAL) — so a partition change that
+// rewrites the gpus file (8 -> 64 lines) is only seen after a re-init.
 #include <amd_smi/amdsmi.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -35,8 +41,10 @@
 namespace {
 
 std::mutex g_mu;
-bool g_init = false;
+std::atomic<bool> g_init{false};
 size_t g_events_consumed = 0;
+std::atomic<uint32_t> g_gen{0};     // bumped by every amdsmi_init
+std::atomic<uint32_t> g_count{0};   // GPUs enumerated at the last init
 
 std::string dir() {
   const char* d = std::getenv("MXK8S_FAKE_AMDSMI_DIR");
@@ -86,9 +94,17 @@ std::vector<uint64_t> list(const Gpu& g, const char* k) {
   return out;
 }
 
-// handle = (void*)(index + 1)
-int idx(amdsmi_processor_handle h) { return static_cast<int>(reinterpret_cast<uintptr_t>(h)) - 1; }
-amdsmi_processor_handle handle(int i) { return reinterpret_cast<amdsmi_processor_handle>(uintptr_t(i + 1)); }
+// handle = (void*)(generation << 20 | (index + 1)); -1 for a stale or unknown one
+int idx(amdsmi_processor_handle h) {
+  const uintptr_t v = reinterpret_cast<uintptr_t>(h);
+  if (!g_init || (v >> 20) != g_gen) return -1;
+  const int i = static_cast<int>(v & 0xfffff) - 1;
+  return i < static_cast<int>(g_count.load()) ? i : -1;
+}
+amdsmi_processor_handle handle(int i) {
+  return reinterpret_cast<amdsmi_processor_handle>((uintptr_t(g_gen.load()) << 20) |
+                                                   uintptr_t(i + 1));
+}
 
 bool get(amdsmi_processor_handle h, Gpu* out) {
   auto gs = gpus();
@@ -112,6 +128,8 @@ amdsmi_status_t amdsmi_init(uint64_t) {
   std::ifstream fail(dir() + "/fail");
   if (fail.good()) return AMDSMI_STATUS_INIT_ERROR;
   g_init = true;
+  ++g_gen;
+  g_count = static_cast<uint32_t>(gpus().size());
   g_events_consumed = lines_of(dir() + "/events").size();   // only events after init
   return AMDSMI_STATUS_SUCCESS;
 }
@@ -132,7 +150,7 @@ amdsmi_status_t amdsmi_get_socket_handles(uint32_t* count, amdsmi_socket_handle*
 amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle, uint32_t* count,
                                              amdsmi_processor_handle* ps) {
   if (!g_init) return AMDSMI_STATUS_NOT_INIT;
-  const uint32_t n = static_cast<uint32_t>(gpus().size());
+  const uint32_t n = g_count.load();
   if (ps)
     for (uint32_t i = 0; i < n && i < *count; ++i) ps[i] = handle(static_cast<int>(i));
   *count = n;
@@ -149,7 +167,8 @@ amdsmi_status_t amdsmi_get_gpu_bdf_id(amdsmi_processor_handle h, uint64_t* id) {
   if (!get(h, &g)) return AMDSMI_STATUS_INVAL;
   unsigned dom, bus, dev, fn;
   parse_bdf(g["bdf"], &dom, &bus, &dev, &fn);
-  *id = (uint64_t(dom) << 32) | (uint64_t(bus) << 8) | (uint64_t(dev) << 3) | fn;
+  *id = (uint64_t(dom) << 32) | (uint64_t(num(g, "partition") & 0xf) << 28) |
+        (uint64_t(bus) << 8) | (uint64_t(dev) << 3) | fn;
   return AMDSMI_STATUS_SUCCESS;
 }
 

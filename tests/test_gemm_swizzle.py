@@ -112,3 +112,32 @@ def test_w4b_half_dma_source_swizzle_matches_reads():
     for row in range(256):
         for c in range(8):
             assert image[addr_half(row, c)] == (row, c)
+
+
+# ---- ring kernel (gemm_bf16_ring.hip): one 32-deep k-step per slot, 256 rows
+# x 64 B per operand (addr64 layout); DMA piece 4j + w of wave w is 16 rows,
+# lane l -> LDS (4j + w) * 1024 + 16 l from row 16 (4j + w) + (l >> 2),
+# logical chunk (l & 3) ^ G((l >> 2)), G = [0, 2, 3, 1][(r >> 2) & 3].
+def ring_g(r):
+    return (0x1320 >> (4 * ((r >> 2) & 3))) & 3
+
+
+def test_ring_dma_image_matches_reads():
+    assert [ring_g(4 * q) for q in range(4)] == [h(q) for q in range(4)]
+    image = {}
+    for w in range(4):
+        for j in range(4):
+            p = 4 * j + w
+            for l in range(64):
+                r = l >> 2
+                image[p * 1024 + l * 16] = (16 * p + r, (l & 3) ^ ring_g(r))
+    assert len(image) == 256 * 4
+    for row in range(256):
+        for c in range(4):
+            assert image[addr64(row, c)] == (row, c)
+    # the fragment read offset of gemm_bf16_ring.hip: row fr = l & 15 of a
+    # 16-row tile, chunk l >> 4 at ((l >> 4) ^ G(fr)) * 16
+    for base in range(0, 256, 16):
+        for l in range(64):
+            fr = l & 15
+            assert base * 64 + fr * 64 + (((l >> 4) ^ ring_g(fr)) << 4) == addr64(base + fr, l >> 4)

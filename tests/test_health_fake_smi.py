@@ -64,12 +64,12 @@ def fake_smi(monkeypatch):
     if not os.path.exists(FAKE_LIB):
         subprocess.run(["make", "-C", REPO, "fake-amdsmi"], check=True, capture_output=True)
     d = tempfile.mkdtemp(prefix="mxsmi")
-    node.smi_close()
+    node.smi_reset()
     monkeypatch.setenv("MXK8S_AMDSMI_LIB", FAKE_LIB)
     monkeypatch.setenv("MXK8S_FAKE_AMDSMI_DIR", d)
     fs = FakeSmi(d, [g.bdf for g in node.enumerate_gpus(ROOT)])
     yield fs
-    node.smi_close()
+    node.smi_reset()
     shutil.rmtree(d, ignore_errors=True)
 
 
@@ -357,3 +357,108 @@ def test_exporter_energy_counter(fake_smi, tmp_path):
     assert len(en) == 1 and 'gpu="2"' in en[0]
     assert abs(float(en[0].rsplit(" ", 1)[1]) - 1234.568) < 0.05
     assert "# TYPE amd_gpu_energy_joules_total counter" in text
+
+
+def test_refcounted_session_and_reinit_generation(fake_smi):
+    ok, _ = node.smi_open()
+    assert ok and node.smi_count() == 8
+    g0 = node.smi_generation()
+    ok2, _ = node.smi_open()                     # a second user shares the session
+    assert ok2 and node.smi_generation() == g0
+    node.smi_close()
+    assert node.smi_count() == 8                 # still open for the first user
+    # amd-smi enumerates at init: a grown GPU list is only seen after a re-init
+    fake_smi.gpus += [dict(fake_smi.gpus[0], partition=1)]
+    fake_smi.write()
+    assert node.smi_count() == 8
+    assert node.smi_reinit()[0] and node.smi_count() == 9
+    assert node.smi_generation() != g0
+    assert node.smi_sample(8).key == fake_smi.gpus[0]["bdf"] + "#1"
+    node.smi_close()
+    assert node.smi_count() == -1                # last reference gone
+
+
+def test_spx_to_cpx_with_amd_smi_active(fake_smi, tmp_path):
+    """SURVEY R26h / VERDICT r2 #1: a compute-partition change while amd-smi
+    is live.  The plugin's new monitor re-initialises amd-smi (8 -> 64
+    handles) and matches every partition by BDF + partition id, so ECC and
+    VM-fault health cover all 64 partitions; ListAndWatch re-sends 64
+    devices; an exporter backend opened before the change re-maps too."""
+    import test_partition as tp
+    from mxk8s import partition
+    from mxk8s.exporter import Exporter, ExporterConfig, SmiBackend
+
+    root = tp.spx_root(str(tmp_path))
+    state = str(tmp_path / "state")
+    d = tempfile.mkdtemp(prefix="mxdp", dir="/tmp")
+    kube = FakeKubelet(d).start()
+    plugin = AmdGpuDevicePlugin(PluginConfig(plugin_dir=d, sysfs_root=root, health_interval=0.05,
+                                             watch_interval=0.1, use_smi_events=True,
+                                             state_dir=state, reconcile_interval=0.1,
+                                             event_quarantine_s=30)).start()
+    exp_backend = SmiBackend(root)
+    drv = tp.FakeDriver(root)
+    try:
+        stub, watch = _watch(kube)
+        assert len(next(watch).devices) == 8
+        assert all(st.smi_index >= 0 for st in plugin.monitor.status())
+        assert len(exp_backend.samples()) == 8
+        # the node is repartitioned: KFD shows 64 GPUs, amd-smi (after init) 64
+        fake_smi.gpus = [dict(fake_smi.gpus[k], partition=p) for k in range(8) for p in range(8)]
+        fake_smi.write()
+        drv.start()
+        client = tp.FakeNodeClient("n1", {partition.CONFIG_LABEL: "cpx-nps2"})
+        res = partition.PartitionManager(client, "n1", root, settle_timeout=10,
+                                         poll=0.02).reconcile_once()
+        assert res.state == "success", res
+        devs = _wait(lambda: (lambda r: r.devices if len(r.devices) == 64 else None)(next(watch)),
+                     timeout=10)
+        assert devs and len(devs) == 64
+        st = _wait(lambda: (lambda s: s if len(s) == 64 and all(x.smi_index >= 0 for x in s)
+                            else None)(plugin.monitor.status()))
+        assert st, [x.smi_index for x in plugin.monitor.status()]
+        # amd-smi index k is the k-th line: device k // 8, partition k % 8 == KFD order
+        assert [x.smi_index for x in st] == list(range(64))
+        # health of a partition that did not exist before the change
+        fake_smi.event(37, node.EVT_VMFAULT, "partition fault")
+        h = _wait(lambda: (lambda r: r if _health(r).get("37") == api.UNHEALTHY else None)(next(watch)))
+        assert h and sum(v == api.UNHEALTHY for v in _health(h).values()) == 1
+        assert _wait(lambda: all(x.ecc_valid for x in plugin.monitor.status()))
+        fake_smi.set(53, ecc_ue=1)
+        assert _wait(lambda: plugin.state.health["53"] == api.UNHEALTHY)
+        assert plugin.state.reasons["53"] == "uncorrectable ECC errors"
+        # exporter: samples for every partition (re-mapped on the new generation)
+        exp = Exporter(ExporterConfig(sysfs_root=root, pod_resources=False,
+                                      health_state_file=os.path.join(state, "health.json")),
+                       backend=exp_backend)
+        text = exp.sample_once()
+        pw = [l for l in text.splitlines() if l.startswith("amd_gpu_power_watts{")]
+        assert len(pw) == 64 and any('bdf="0000:15:00.0"' in l and 'partition="1"' in l for l in pw)
+        assert len(exp_backend.samples()) == 64
+    finally:
+        drv.stop.set()
+        exp_backend.close()
+        plugin.stop()
+        kube.stop()
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def test_exporter_alone_reinits_after_partition_change(fake_smi, tmp_path):
+    """The exporter runs in its own pod (its own amd-smi session): it notices
+    the KFD / amd-smi count mismatch itself and re-initialises."""
+    import test_partition as tp
+    from mxk8s.exporter import SmiBackend
+
+    root = str(tmp_path / "cpx")
+    tp.make_sysfs.tree_partitioned(root, "CPX", "NPS2")
+    be = SmiBackend(root)                          # session opened with 8 handles
+    try:
+        assert node.smi_count() == 8
+        fake_smi.gpus = [dict(fake_smi.gpus[k], partition=p) for k in range(8) for p in range(8)]
+        fake_smi.write()
+        got = be.samples()
+        assert len(got) == 64 and be.reinits == 1
+        assert got["0000:15:00.0#1"].partition_id == 1
+        assert len(be.samples()) == 64 and be.reinits == 1   # no re-init once they agree
+    finally:
+        be.close()
