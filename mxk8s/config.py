@@ -98,6 +98,9 @@ VALUES: dict = {
     "partitionManager": {"enabled": F("boolean"),
                          "interval": F("integer", "seconds", minimum=5, maximum=86400),
                          "settleTimeout": F("integer", "seconds", minimum=10, maximum=3600),
+                         "drainTimeout": F("integer", "seconds the device plugin gets to "
+                                                      "withdraw every device", minimum=1,
+                                           maximum=3600),
                          "profiles": F("object", "profile name -> {compute, memory}",
                                        items={"type": "object", "additionalProperties": {
                                            "type": "object", "required": ["compute", "memory"],
@@ -105,6 +108,14 @@ VALUES: dict = {
                                                "compute": {"enum": ["SPX", "DPX", "QPX", "CPX"]},
                                                "memory": {"enum": ["NPS1", "NPS2", "NPS4"]}}}}),
                          "resources": RESOURCES},
+    "nodeValidator": {"enabled": F("boolean", "per-node validation chain gating the plugin / exporter"),
+                      "steps": F("array", "validation steps, in order",
+                                 items={"enum": ["driver", "cdi", "vectoradd", "plugin"]}),
+                      "interval": F("integer", "re-validation check period (s)", minimum=5,
+                                    maximum=86400),
+                      "stepTimeout": F("integer", "seconds a step may retry", minimum=10,
+                                       maximum=86400),
+                      "resources": RESOURCES},
     "labeller": {"enabled": F("boolean"), "nfdFeatureFile": F("boolean"),
                  "interval": F("integer", "seconds", minimum=10, maximum=86400),
                  "resources": RESOURCES},

@@ -40,6 +40,9 @@ def main(argv=None) -> int:
                    help="seconds between GPU-set / CDI-spec reconciliations (0 = off)")
     p.add_argument("--partition-naming", choices=["single", "mixed"], default="single",
                    help="compute partitions as <resource> or <resource>-<mode>")
+    p.add_argument("--require-validation", default="",
+                   help="comma list of node-validator steps (e.g. driver) whose markers in "
+                        "<state-dir>/validations must be valid before devices are served")
     p.add_argument("--log-format", choices=["json", "text"], default="json")
     a = p.parse_args(argv)
     setup_logging(a.log_format)
@@ -52,7 +55,8 @@ def main(argv=None) -> int:
                        rename_shared=a.rename_shared, ecc_quarantine_s=a.ecc_quarantine,
                        state_dir=a.state_dir, cdi_spec_path=a.cdi_spec,
                        reconcile_interval=a.reconcile_interval,
-                       partition_naming=a.partition_naming)
+                       partition_naming=a.partition_naming,
+                       require_validation=tuple(x for x in a.require_validation.split(",") if x))
     if a.fault_file:
         cfg.fault_file = a.fault_file
     run_forever(cfg)

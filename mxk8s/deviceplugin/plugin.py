@@ -52,6 +52,8 @@ import grpc
 
 from . import api
 from ..native import node
+from ..partition import DRAIN_ACK_FILE, DRAIN_REASON, boot_id, read_drain
+from ..validate import node as validate_node
 
 log = logging.getLogger("mxk8s.deviceplugin")
 
@@ -87,6 +89,11 @@ class PluginConfig:
     # <resource_name>; "mixed" advertises <resource_name>-<mode> (e.g.
     # amd.com/gpu-cpx), the GPU Operator's MIG "mixed strategy" counterpart
     partition_naming: str = "single"
+    # node-validator markers (<state_dir>/validations/<step>-ready) that must
+    # be valid for the current boot + driver instance before the plugin
+    # serves, and while it advertises devices Healthy (operator-validator
+    # gating: the NVIDIA plugin's init container waits on driver validation)
+    require_validation: tuple = ()
 
     def effective_resource(self, gpus) -> str:
         if self.partition_naming != "mixed" or not gpus:
@@ -97,6 +104,18 @@ class PluginConfig:
         mode = PARTITION_MODES.get(parts.pop(), "xpx")
         base, dot, shared = self.resource_name.partition(".shared")
         return f"{base}-{mode}{dot}{shared}"
+
+    def socket_for(self, resource: str) -> str:
+        """Socket file of the plugin serving ``resource``: the configured name
+        for the base resource, ``<stem>-<mode>.sock`` for a mixed-naming
+        partition resource (a renamed resource never shares the old socket)."""
+        if resource == self.resource_name:
+            return self.socket_name
+        stem, dot, ext = self.socket_name.rpartition(".")
+        tail = resource.rpartition("/")[2]
+        base = self.resource_name.rpartition("/")[2].split(".")[0]
+        suffix = (tail[len(base):] if tail.startswith(base) else "-" + tail).replace(".", "-")
+        return f"{stem}{suffix}.{ext}" if dot else f"{self.socket_name}{suffix}"
 
     def __post_init__(self):
         if self.replicas < 1:
@@ -123,6 +142,7 @@ class DeviceState:
         self.health = {i: api.HEALTHY for i in self.gpus}
         self.reasons = {i: "healthy" for i in self.gpus}
         self.generation = 0
+        self.epoch = 0                # bumped when the advertised resource changes
         self.closed = False
 
     def set_health(self, dev_id: str, healthy: bool, reason: str) -> bool:
@@ -135,6 +155,24 @@ class DeviceState:
             self.generation += 1
             self._cv.notify_all()
             return True
+
+    def set_health_many(self, updates: dict) -> list:
+        """{dev_id: (healthy, reason)} applied atomically: one ListAndWatch
+        re-send carries every change of a health pass.  Returns the IDs whose
+        health changed."""
+        changed = []
+        with self._cv:
+            for dev_id, (healthy, reason) in updates.items():
+                new = api.HEALTHY if healthy else api.UNHEALTHY
+                if self.health.get(dev_id) == new:
+                    continue
+                self.health[dev_id] = new
+                self.reasons[dev_id] = reason
+                changed.append(dev_id)
+            if changed:
+                self.generation += 1
+                self._cv.notify_all()
+        return changed
 
     def devices(self) -> list:
         with self._cv:
@@ -173,6 +211,20 @@ class DeviceState:
             self.closed = True
             self._cv.notify_all()
 
+    def snapshot(self, epoch: int):
+        """(generation, devices) atomically, or None once the state is closed
+        or the advertised resource changed since ``epoch``."""
+        with self._cv:
+            if self.closed or self.epoch != epoch:
+                return None
+            return self.generation, self.devices()
+
+    def bump_epoch(self) -> None:
+        with self._cv:
+            self.epoch += 1
+            self.generation += 1
+            self._cv.notify_all()
+
     def replace_gpus(self, gpus: list[node.GpuInfo]) -> None:
         """New GPU set (reconciliation): known IDs keep their health, new ones
         start healthy, vanished ones are withdrawn; ListAndWatch re-sends."""
@@ -192,14 +244,18 @@ class AmdGpuDevicePlugin:
         self.cfg = config or PluginConfig()
         self.gpus = gpus if gpus is not None else node.enumerate_gpus(self.cfg.sysfs_root)
         self.resource_name = self.cfg.effective_resource(self.gpus)
+        self.socket_name = self.cfg.socket_for(self.resource_name)
         self.state = DeviceState(self.gpus, self.cfg.replicas)
         self._server: Optional[grpc.Server] = None
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self._mon_lock = threading.Lock()
+        self._serve_lock = threading.RLock()   # serve / register / rename / kubelet-restart
         self.monitor = self._new_monitor()
         self.reconciles = {"gpus_changed": 0, "cdi_rewritten": 0}
         self.registrations = 0
+        self._drain_acked: Optional[str] = None
+        self._boot = boot_id()
         self._socket_ino: Optional[int] = None
         self._kubelet_ino: Optional[int] = None
 
@@ -210,14 +266,16 @@ class AmdGpuDevicePlugin:
 
     def ListAndWatch(self, request, context):
         seen = -1
+        epoch = self.state.epoch     # a resource rename ends the streams of the old one
         while not self._stop.is_set() and context.is_active():
-            gen = self.state.generation
+            snap = self.state.snapshot(epoch)
+            if snap is None:
+                return
+            gen, devices = snap
             if gen != seen:
                 seen = gen
-                yield api.ListAndWatchResponse(devices=self.state.devices())
+                yield api.ListAndWatchResponse(devices=devices)
             self.state.wait_change(seen, timeout=1.0)
-            if self.state.closed:
-                return
 
     def GetPreferredAllocation(self, request, context):
         resp = api.PreferredAllocationResponse()
@@ -365,20 +423,43 @@ class AmdGpuDevicePlugin:
 
         status = mon.status()
         bdf_of = {st.index: st.bdf for st in status}
+        # a partition change in progress (mxk8s.partition drain handshake):
+        # every device is withdrawn until the drain file goes away; so is
+        # every device while a required validation is not valid for the
+        # running driver instance (a driver reload voids the markers)
+        drain = read_drain(self.cfg.state_dir, self._boot)
+        pending = self._validation_pending()
         for ev in mon.new_events():
             dev = dev_of(ev.index, bdf_of.get(ev.index, "")) if ev.index >= 0 else None
             level = logging.INFO if ev.kind in (node.EVT_GPU_POST_RESET,
                                                 node.EVT_THERMAL_THROTTLE) else logging.WARNING
             log.log(level, "device %s: %s", dev, ev.message,
                     extra={"device": dev, "event": ev.name, "value": ev.value})
+        updates, bdfs = {}, {}
         for st in status:
             dev = dev_of(st.index, st.bdf)
             if dev is None:
                 continue
-            if self.state.set_health(dev, st.healthy, st.reason):
-                log.warning("device %s -> %s (%s)", dev, "Healthy" if st.healthy else "Unhealthy",
-                            st.reason, extra={"device": dev, "event": "health_change",
-                                              "reason": st.reason, "bdf": st.bdf})
+            updates[dev] = ((False, DRAIN_REASON) if drain else
+                            (False, f"{pending} validation pending") if pending else
+                            (st.healthy, st.reason))
+            bdfs[dev] = st.bdf
+        for dev in self.state.set_health_many(updates):
+            healthy, reason = updates[dev]
+            log.warning("device %s -> %s (%s)", dev, "Healthy" if healthy else "Unhealthy",
+                        reason, extra={"device": dev, "event": "health_change",
+                                       "reason": reason, "bdf": bdfs[dev]})
+        if drain and drain != self._drain_acked:
+            # every device is now Unhealthy in the state ListAndWatch streams
+            ack = os.path.join(self.cfg.state_dir, DRAIN_ACK_FILE)
+            with open(ack + ".tmp", "w") as f:
+                f.write(drain)
+            os.replace(ack + ".tmp", ack)
+            self._drain_acked = drain
+            log.warning("partition drain %s: all devices withdrawn", drain,
+                        extra={"event": "partition_drain"})
+        elif not drain:
+            self._drain_acked = None
         if self.health_state_path:
             os.makedirs(self.cfg.state_dir, exist_ok=True)
             mon.write_state(self.health_state_path)
@@ -396,18 +477,29 @@ class AmdGpuDevicePlugin:
             with self._mon_lock:
                 old, self.monitor = self.monitor, self._new_monitor()
             old.close()
+            name = self.cfg.effective_resource(gpus)
+            renamed = name != self.resource_name
+            if renamed:
+                # held until the new resource is served: the kubelet-restart
+                # watcher must not re-serve the retired socket in between
+                self._serve_lock.acquire()
+                self._retire_endpoint()      # before the new IDs exist in the state
             self.state.replace_gpus(gpus)
             out["gpus_changed"] = True
             self.reconciles["gpus_changed"] += 1
-            name = self.cfg.effective_resource(gpus)
-            if name != self.resource_name:
-                # a partition-mode change under "mixed" naming: a new resource
-                log.warning("resource %s -> %s after the partition change; re-registering",
-                            self.resource_name, name, extra={"event": "resource_renamed",
-                                                             "resource": name})
-                self.resource_name = name
-                if self.cfg.register:
-                    self.register()
+            if renamed:
+                # a partition-mode change under "mixed" naming: a new resource.
+                # The old resource's endpoint must go away, not keep streaming
+                # the new device IDs: stopping its server ends every open
+                # ListAndWatch (kubelet then zeroes the old resource), and the
+                # new resource is served on a socket of its own.
+                log.warning("resource %s -> %s after the partition change; re-serving and "
+                            "re-registering", self.resource_name, name,
+                            extra={"event": "resource_renamed", "resource": name})
+                try:
+                    self._rename(name)
+                finally:
+                    self._serve_lock.release()
                 out["resource_renamed"] = name
         if self.cfg.cdi_spec_path:
             text = node.cdi_spec_text(self.cfg.sysfs_root, self.cfg.cdi_kind)
@@ -431,19 +523,46 @@ class AmdGpuDevicePlugin:
         return out
 
     # ------------------------------------------------------------ lifecycle
+    @property
+    def socket_path(self) -> str:
+        return os.path.join(self.cfg.plugin_dir, self.socket_name)
+
+    def _retire_endpoint(self) -> None:
+        """End every ListAndWatch stream of the resource being retired and stop
+        its server (kubelet then drops the old resource's capacity)."""
+        with self._serve_lock:
+            self.state.bump_epoch()
+            if self._server is not None:
+                self._server.stop(grace=0.5).wait()
+                self._server = None
+            try:
+                os.unlink(self.socket_path)
+            except FileNotFoundError:
+                pass
+
+    def _rename(self, name: str) -> None:
+        with self._serve_lock:
+            if self._server is not None:
+                self._retire_endpoint()
+            self.resource_name = name
+            self.socket_name = self.cfg.socket_for(name)
+            self.serve()
+            if self.cfg.register:
+                self.register()
+
     def serve(self) -> None:
         os.makedirs(self.cfg.plugin_dir, exist_ok=True)
         try:
-            os.unlink(self.cfg.socket_path)
+            os.unlink(self.socket_path)
         except FileNotFoundError:
             pass
         server = grpc.server(concurrent.futures.ThreadPoolExecutor(max_workers=8))
         server.add_generic_rpc_handlers((api.generic_handler("DevicePlugin", self),))
-        server.add_insecure_port("unix:" + self.cfg.socket_path)
+        server.add_insecure_port("unix:" + self.socket_path)
         server.start()
         self._server = server
-        self._socket_ino = _inode(self.cfg.socket_path)
-        log.info("serving %s on %s (%d GPUs)", self.resource_name, self.cfg.socket_path,
+        self._socket_ino = _inode(self.socket_path)
+        log.info("serving %s on %s (%d GPUs)", self.resource_name, self.socket_path,
                  len(self.gpus))
 
     def register(self, timeout: float = 10.0) -> None:
@@ -451,7 +570,7 @@ class AmdGpuDevicePlugin:
             grpc.channel_ready_future(ch).result(timeout=timeout)
             stub = api.Stub(ch, "Registration")
             stub.Register(api.RegisterRequest(
-                version=api.API_VERSION, endpoint=self.cfg.socket_name,
+                version=api.API_VERSION, endpoint=self.socket_name,
                 resource_name=self.resource_name,
                 options=api.DevicePluginOptions(pre_start_required=False,
                                                 get_preferred_allocation_available=True)),
@@ -460,7 +579,23 @@ class AmdGpuDevicePlugin:
         self._kubelet_ino = _inode(self.cfg.kubelet_socket)
         log.info("registered %s with kubelet (%d)", self.resource_name, self.registrations)
 
+    def _validation_pending(self) -> Optional[str]:
+        """First required validation whose marker is not valid, or None."""
+        if not self.cfg.require_validation or not self.cfg.state_dir:
+            return None
+        st = validate_node.status(self.cfg.state_dir, self.cfg.sysfs_root,
+                                  self.cfg.require_validation)
+        return next((k for k, ok in st.items() if not ok), None)
+
     def start(self) -> "AmdGpuDevicePlugin":
+        if self.cfg.require_validation and self.cfg.state_dir:
+            # serve nothing until the node validator vouched for this driver
+            log.info("waiting for validation: %s", ",".join(self.cfg.require_validation))
+            validate_node.wait_for(self.cfg.state_dir, self.cfg.require_validation,
+                                   self.cfg.sysfs_root, poll=min(1.0, self.cfg.watch_interval),
+                                   stop=self._stop.is_set)
+            if self._stop.is_set():
+                return self
         self.serve()
         if self.cfg.register:
             self.register()
@@ -477,7 +612,7 @@ class AmdGpuDevicePlugin:
         for t in self._threads:
             t.join(timeout=5)
         try:
-            os.unlink(self.cfg.socket_path)
+            os.unlink(self.socket_path)
         except FileNotFoundError:
             pass
         with self._mon_lock:
@@ -507,7 +642,7 @@ class AmdGpuDevicePlugin:
 
     def _watch_loop(self) -> None:
         while not self._stop.wait(self.cfg.watch_interval):
-            sock_gone = _inode(self.cfg.socket_path) != self._socket_ino
+            sock_gone = _inode(self.socket_path) != self._socket_ino
             kubelet_new = (self.cfg.register and _inode(self.cfg.kubelet_socket) is not None
                            and _inode(self.cfg.kubelet_socket) != self._kubelet_ino)
             if not (sock_gone or kubelet_new):
@@ -515,11 +650,12 @@ class AmdGpuDevicePlugin:
             log.warning("kubelet restart detected (socket gone=%s, kubelet.sock new=%s); "
                         "re-serving and re-registering", sock_gone, kubelet_new)
             try:
-                if self._server is not None:
-                    self._server.stop(grace=0.2).wait()
-                self.serve()
-                if self.cfg.register:
-                    self.register()
+                with self._serve_lock:
+                    if self._server is not None:
+                        self._server.stop(grace=0.2).wait()
+                    self.serve()
+                    if self.cfg.register:
+                        self.register()
             except Exception:
                 log.exception("re-registration failed; retrying")
                 self._socket_ino = None

@@ -119,6 +119,19 @@ def check_gpu(h: Host) -> list[Check]:
                          "`mxk8s bootstrap --phase runtime` (containerd 2.x has CDI on by default)"))
         out.append(Check("containerd SystemdCgroup", "ok" if sysd else "fail",
                          "true" if sysd else "false", "set SystemdCgroup = true (README.md:123)"))
+    # node-validator markers (operator-validator counterpart): which layer of
+    # the chain last failed, for the running boot + driver instance
+    from ..validate import node as vnode
+    vdir = h.path(vnode.validations_dir("/var/lib/mxk8s"))
+    if not os.path.isdir(vdir):
+        out.append(Check("node validation", "skip", "no /var/lib/mxk8s/validations (validator not deployed)"))
+    else:
+        st = vnode.status(os.path.dirname(vdir), _sysfs_root(h))
+        bad = [k for k, ok in st.items() if not ok]
+        detail = ", ".join(f"{k}={'ready' if ok else 'NOT ready'}" for k, ok in st.items())
+        hint = (f"first failing step: {bad[0]}: `kubectl -n amd-gpu logs -l app=amd-gpu-node-validator "
+                f"-c {bad[0]}-validation`" if bad else "")
+        out.append(Check("node validation", "fail" if bad else "ok", detail, hint))
     sock = h.exists("/var/lib/kubelet/device-plugins/amd-gpu.sock")
     out.append(Check("device plugin socket", "ok" if sock else "fail",
                      "registered socket present" if sock else "amd-gpu.sock missing",

@@ -304,6 +304,8 @@ class ExporterConfig:
     health_state_file: Optional[str] = None   # the device plugin's <state_dir>/health.json
     sysfs_root: str = ""
     pod_resources: bool = True
+    state_dir: Optional[str] = None            # node-validator markers: <state_dir>/validations
+    validation_steps: tuple = ("driver", "cdi", "vectoradd", "plugin")
 
 
 class Exporter:
@@ -317,10 +319,21 @@ class Exporter:
         self._httpd: Optional[http.server.ThreadingHTTPServer] = None
         self.samples_taken = 0
 
+    def validations(self) -> dict:
+        """{step: marker valid for this boot + driver instance} (empty when
+        no state dir is configured)."""
+        if not self.cfg.state_dir:
+            return {}
+        from ..validate import node as vnode
+        return vnode.status(self.cfg.state_dir, self.cfg.sysfs_root, self.cfg.validation_steps)
+
     def components(self) -> dict:
         c = {"amd_smi": bool(getattr(self.backend, "ok", True))}
         c["device_plugin"] = os.path.exists(self.cfg.plugin_socket)
         c["cdi_spec"] = os.path.exists(self.cfg.cdi_spec)
+        v = self.validations()
+        if v:
+            c["validation"] = all(v.values())
         return c
 
     def sample_once(self) -> str:
@@ -343,6 +356,14 @@ class Exporter:
                               plugin_health=load_health_state(self.cfg.health_state_file),
                               xgmi=getattr(self.backend, "xgmi", None),
                               processes=getattr(self.backend, "processes", None))
+        v = self.validations()
+        if v:
+            w = MetricWriter()
+            for step, ok in v.items():
+                w.add("amd_gpu_validation_ready", "gauge",
+                      "1 if the node validator's <step>-ready marker is valid for this boot and "
+                      "driver instance.", 1 if ok else 0, {"step": step})
+            text += w.text()
         with self._lock:
             self._text = text
         self.samples_taken += 1

@@ -20,6 +20,8 @@ def main(argv=None) -> int:
     p.add_argument("--health-state-file", default=None,
                    help="the device plugin's health.json (same verdicts as ListAndWatch)")
     p.add_argument("--sysfs-root", default="")
+    p.add_argument("--state-dir", default=None,
+                   help="node-validator markers (<state-dir>/validations): component 'validation'")
     p.add_argument("--once", action="store_true", help="print one sample and exit")
     p.add_argument("--log-format", choices=["json", "text"], default="json")
     a = p.parse_args(argv)
@@ -27,7 +29,8 @@ def main(argv=None) -> int:
     ex = Exporter(ExporterConfig(port=a.port, interval=a.interval,
                                  pod_resources_socket=a.pod_resources_socket,
                                  resource_name=a.resource_name,
-                                 health_state_file=a.health_state_file, sysfs_root=a.sysfs_root))
+                                 health_state_file=a.health_state_file, sysfs_root=a.sysfs_root,
+                                 state_dir=a.state_dir))
     if a.once:
         sys.stdout.write(ex.sample_once())
         return 0

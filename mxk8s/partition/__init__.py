@@ -23,10 +23,22 @@ Reconcile loop (one node, one DaemonSet pod):
   4. GPUs in use (the kubelet PodResources API shows ``amd.com/gpu*``
      allocations, or amd-smi lists processes): state ``pending`` and retry —
      no workload is ever yanked (the MIG manager evicts GPU clients; a
-     single-node cluster has nowhere to move them);
-  5. write the memory mode, then the compute mode, to every device; wait for
-     the KFD topology to show devices x partitions GPUs; state ``success`` or
-     ``failed`` with the reason in annotation ``amd.com/gpu.partition.config.message``.
+     single-node cluster has nowhere to move them).  The check fails CLOSED:
+     a probe that cannot answer (socket missing, amd-smi not loadable) is
+     ``pending`` too, never "idle";
+  5. drain: write ``<state_dir>/partition-drain`` (hostPath /var/lib/mxk8s,
+     shared with the device plugin), which makes the plugin advertise every
+     device Unhealthy ("partition change in progress") and acknowledge in
+     ``partition-drain.ack``; so no pod can be admitted while sysfs changes.
+     Then the busy check runs AGAIN (a pod admitted between the first check
+     and the drain is caught) — still busy: ``pending``, drain lifted;
+  6. write the memory mode, then the compute mode, to every device; wait for
+     the KFD topology to show devices x partitions GPUs: ``success`` (drain
+     lifted), or — amdgpu took the modes (sysfs reads them back) but did not
+     re-enumerate, as an NPS change needs a driver reload — ``pending-reboot``
+     (drain kept until the node comes back in the requested layout), or
+     ``failed`` when the driver rejected a mode; the reason goes to annotation
+     ``amd.com/gpu.partition.config.message``.
 
 The device plugin's reconciliation (``mxk8s.deviceplugin.plugin``) notices
 the new GPU set and re-advertises (as ``amd.com/gpu`` or, with mixed naming,
@@ -96,19 +108,58 @@ def available_modes(root: str, bdf: str, kind: str) -> set[str]:
     return {t.strip().upper() for t in text.replace(",", " ").split() if t.strip()}
 
 
+DRAIN_FILE = "partition-drain"
+DRAIN_ACK_FILE = "partition-drain.ack"
+DRAIN_REASON = "partition change in progress"
+
+
+def boot_id(path: str = "/proc/sys/kernel/random/boot_id") -> str:
+    return (_read(path) or "unknown").strip()
+
+
+def read_drain(state_dir: Optional[str], boot: Optional[str] = None) -> Optional[str]:
+    """The active drain token in ``state_dir`` (None: no drain).  A drain
+    written in an earlier boot is void: the node came back from the reboot
+    a pending-reboot layout asked for, so the plugin must serve again even if
+    no manager runs to lift it."""
+    if not state_dir:
+        return None
+    text = _read(os.path.join(state_dir, DRAIN_FILE))
+    if not text:
+        return None
+    token, _, drain_boot = text.partition(" ")
+    if drain_boot.strip() and drain_boot.strip() != (boot or boot_id()):
+        return None
+    return token
+
+
+def _write_atomic(path: str, text: str) -> None:
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        f.write(text)
+    os.replace(tmp, path)
+
+
 class PartitionManager:
     def __init__(self, client, node_name: str, sysfs_root: str = "",
                  profiles: Optional[dict] = None,
-                 busy: Optional[Callable[[], list[str]]] = None,
-                 settle_timeout: float = 120.0, poll: float = 1.0):
+                 busy: Optional[Callable[[], Optional[list[str]]]] = None,
+                 settle_timeout: float = 120.0, poll: float = 1.0,
+                 state_dir: Optional[str] = None, drain_timeout: float = 30.0,
+                 plugin_fresh_s: float = 60.0, boot: Optional[str] = None):
         self.client = client
         self.node_name = node_name
         self.root = sysfs_root
         self.profiles = {k: {"compute": v["compute"].upper(), "memory": v["memory"].upper()}
                          for k, v in (profiles or DEFAULT_PROFILES).items()}
+        # busy() -> users, or None when it cannot tell (then: never repartition)
         self.busy = busy or (lambda: [])
         self.settle_timeout = settle_timeout
         self.poll = poll
+        self.state_dir = state_dir
+        self.drain_timeout = drain_timeout
+        self.plugin_fresh_s = plugin_fresh_s
+        self.boot = boot or boot_id()
         self._last_state: Optional[tuple] = None
 
     # ---------------------------------------------------------------- k8s
@@ -157,12 +208,36 @@ class PartitionManager:
         cur = current_modes(self.root, bdfs)
         todo = [b for b in bdfs if cur[b] != prof]
         if not todo:
+            self._set_drain(None)     # e.g. back from the reboot a pending-reboot asked for
             return Result("success", f"{name}: {prof['compute']}/{prof['memory']} on "
                                      f"{len(bdfs)} device(s), {len(gpus)} GPU partitions")
         users = self.busy()
+        if users is None:
+            return Result("pending", "cannot verify that the GPUs are idle (pod-resources or "
+                                     "amd-smi probe unavailable); not repartitioning")
         if users:
             return Result("pending", f"waiting for {len(users)} GPU workload(s) to finish: "
                                      + ", ".join(users[:5]))
+        # withdraw the devices from the scheduler before touching sysfs
+        token = f"{name}@{int(time.time() * 1000)}"
+        keep_drain = False
+        self._set_drain(token)
+        try:
+            if not self._wait_drain_ack(token):
+                return Result("pending", "the device plugin did not acknowledge the drain within "
+                                         f"{self.drain_timeout:.0f} s; not repartitioning")
+            users = self.busy()          # admitted between the first check and the drain?
+            if users is None or users:
+                return Result("pending", "GPU workload(s) started before the drain took effect: "
+                                         + (", ".join(users[:5]) if users else "probe unavailable"))
+            res = self._write_and_settle(name, prof, bdfs, todo, cur)
+            keep_drain = res.state == "pending-reboot"
+            return res
+        finally:
+            if not keep_drain:
+                self._set_drain(None)
+
+    def _write_and_settle(self, name, prof, bdfs, todo, cur) -> Result:
         # memory first (a compute partition is carved out of the memory layout)
         for kind in ("memory", "compute"):
             for b in todo:
@@ -186,21 +261,72 @@ class PartitionManager:
                 return Result("success", f"{name}: {prof['compute']}/{prof['memory']} on "
                                          f"{len(bdfs)} device(s), {n} GPU partitions", applied=True)
             if time.monotonic() >= deadline:
-                return Result("failed", f"{name}: driver shows {n} GPU(s), expected {want} "
+                if all(now[b] == prof for b in bdfs):
+                    # amdgpu took the modes but did not re-enumerate in place (an
+                    # NPS change needs a driver reload): not a failure of the request
+                    return Result("pending-reboot",
+                                  f"{name}: amdgpu reports {prof['compute']}/{prof['memory']} but "
+                                  f"the KFD topology shows {n} GPU(s), expected {want} after "
+                                  f"{self.settle_timeout:.0f} s: reload amdgpu or reboot the node "
+                                  f"(devices stay drained until then)", applied=True)
+                bad = [b for b in bdfs if now[b] != prof]
+                return Result("failed", f"{name}: driver shows {n} GPU(s), expected {want}; "
+                                        f"{len(bad)} device(s) read back other modes "
+                                        f"({bad[0]}: {now[bad[0]]['compute']}/{now[bad[0]]['memory']}) "
                                         f"after {self.settle_timeout:.0f} s", applied=True)
             time.sleep(self.poll)
 
+    # ------------------------------------------------------------- drain
+    def _set_drain(self, token: Optional[str]) -> None:
+        if not self.state_dir:
+            return
+        path = os.path.join(self.state_dir, DRAIN_FILE)
+        if token is None:
+            for p in (path, os.path.join(self.state_dir, DRAIN_ACK_FILE)):
+                try:
+                    os.unlink(p)
+                except FileNotFoundError:
+                    pass
+            return
+        os.makedirs(self.state_dir, exist_ok=True)
+        _write_atomic(path, f"{token} {self.boot}\n")
 
-def pod_resources_users(socket_path: Optional[str], resource: str = "amd.com/gpu") -> list[str]:
-    """Containers holding GPUs (any amd.com/gpu* resource) per the kubelet."""
+    def _plugin_running(self) -> bool:
+        """The device plugin refreshes <state_dir>/health.json every pass."""
+        try:
+            age = time.time() - os.stat(os.path.join(self.state_dir, "health.json")).st_mtime
+        except (OSError, TypeError):
+            return False
+        return age <= self.plugin_fresh_s
+
+    def _wait_drain_ack(self, token: str) -> bool:
+        if not self.state_dir or not self._plugin_running():
+            return True               # no plugin serving: nothing can be admitted
+        deadline = time.monotonic() + self.drain_timeout
+        while time.monotonic() < deadline:
+            if (_read(os.path.join(self.state_dir, DRAIN_ACK_FILE)) or "") == token:
+                return True
+            time.sleep(min(self.poll, 0.1))
+        return False
+
+
+def pod_resources_users(socket_path: Optional[str],
+                        resource: str = "amd.com/gpu") -> Optional[list[str]]:
+    """Containers holding GPUs (any amd.com/gpu* resource) per the kubelet;
+    None when the pod-resources API cannot be asked (fail closed)."""
     if not socket_path or not os.path.exists(socket_path):
-        return []
+        return None
     from ..exporter.podresources import ListPodResourcesRequest, ListPodResourcesResponse, LIST_METHOD
     import grpc
-    with grpc.insecure_channel("unix:" + socket_path) as ch:
-        call = ch.unary_unary(LIST_METHOD, request_serializer=ListPodResourcesRequest.SerializeToString,
-                              response_deserializer=ListPodResourcesResponse.FromString)
-        resp = call(ListPodResourcesRequest(), timeout=5)
+    try:
+        with grpc.insecure_channel("unix:" + socket_path) as ch:
+            call = ch.unary_unary(LIST_METHOD,
+                                  request_serializer=ListPodResourcesRequest.SerializeToString,
+                                  response_deserializer=ListPodResourcesResponse.FromString)
+            resp = call(ListPodResourcesRequest(), timeout=5)
+    except grpc.RpcError as e:
+        log.warning("pod-resources probe failed: %s", e)
+        return None
     out = []
     for pr in resp.pod_resources:
         for c in pr.containers:
@@ -209,11 +335,29 @@ def pod_resources_users(socket_path: Optional[str], resource: str = "amd.com/gpu
     return out
 
 
-def smi_users() -> list[str]:
+def smi_users() -> Optional[list[str]]:
+    """Processes with a context on any GPU per amd-smi; None when amd-smi
+    cannot be opened (fail closed)."""
     ok, _ = node.smi_open()
     if not ok:
-        return []
-    out = []
-    for i in range(max(0, node.smi_count())):
-        out += [f"pid {p.pid} ({p.name})" for p in node.smi_processes(i)]
-    return out
+        return None
+    try:
+        out = []
+        for i in range(max(0, node.smi_count())):
+            out += [f"pid {p.pid} ({p.name})" for p in node.smi_processes(i)]
+        return out
+    finally:
+        node.smi_close()
+
+
+def combined_busy(*probes: Callable[[], Optional[list[str]]]) -> Callable[[], Optional[list[str]]]:
+    """busy() over several probes: None if any probe cannot answer."""
+    def busy():
+        users: list[str] = []
+        for probe in probes:
+            got = probe()
+            if got is None:
+                return None
+            users += got
+        return users
+    return busy

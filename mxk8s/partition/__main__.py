@@ -10,7 +10,7 @@ import time
 
 from ..utils.kube import KubeClient
 from ..utils.logs import setup_logging
-from . import DEFAULT_PROFILES, PartitionManager, pod_resources_users, smi_users
+from . import DEFAULT_PROFILES, PartitionManager, combined_busy, pod_resources_users, smi_users
 
 
 def main(argv=None) -> int:
@@ -22,6 +22,9 @@ def main(argv=None) -> int:
                    help="JSON file {name: {compute: SPX..CPX, memory: NPS1|NPS2}}")
     p.add_argument("--pod-resources-socket", default="/var/lib/kubelet/pod-resources/kubelet.sock")
     p.add_argument("--settle-timeout", type=float, default=120.0)
+    p.add_argument("--state-dir", default="/var/lib/mxk8s",
+                   help="shared with the device plugin: drain handshake files")
+    p.add_argument("--drain-timeout", type=float, default=30.0)
     p.add_argument("--server", default=None, help="API server URL (default: in-cluster)")
     p.add_argument("--token", default=None)
     p.add_argument("--log-format", choices=["json", "text"], default="json")
@@ -36,8 +39,10 @@ def main(argv=None) -> int:
             profiles = json.load(f)
     client = KubeClient(a.server, a.token) if a.server else KubeClient.in_cluster()
     mgr = PartitionManager(client, a.node_name, a.sysfs_root, profiles,
-                           busy=lambda: pod_resources_users(a.pod_resources_socket) + smi_users(),
-                           settle_timeout=a.settle_timeout)
+                           busy=combined_busy(lambda: pod_resources_users(a.pod_resources_socket),
+                                              smi_users),
+                           settle_timeout=a.settle_timeout, state_dir=a.state_dir,
+                           drain_timeout=a.drain_timeout)
     while True:
         try:
             mgr.reconcile_once()

@@ -51,6 +51,19 @@ __device__ __forceinline__ bf16x8_t rd128(const char* p) {
   return *reinterpret_cast<const bf16x8_t*>(p);
 }
 
+// The matrix core is still reading an inline-asm MFMA's A/B registers a few
+// cycles after issue, but hipcc (blind to the asm) treats them as free right
+// after it and may give them to its own VALU temporaries (seen: an address
+// v_add into the B fragment one instruction after its last MFMA; ~1000 wrong
+// outputs per 256x256 tile).  One statement that reads every fragment of the
+// step and then waits keeps them all live to the end of the step and covers
+// the last MFMAs' operand reads (tests/test_isa_hazards.py audits it).
+__device__ __forceinline__ void mfma_sources_done(const bf16x8_t (&a)[8], const bf16x8_t (&b)[8]) {
+  asm volatile("s_nop 4" ::"v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]),
+               "v"(a[6]), "v"(a[7]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]),
+               "v"(b[5]), "v"(b[6]), "v"(b[7]));
+}
+
 // One operand's DMA: 256-row panel, 4 pieces of 16 rows per wave per slot.
 struct RingDma {
   __amdgpu_buffer_rsrc_t rsrc;
@@ -114,6 +127,7 @@ __device__ __forceinline__ void ring_step(f32x4_t (&acc)[8][8], const bf16x8_t (
     if (m == 61) vmwait<VM>();                           // stage s+2 landed (this wave's pieces)
     if (m == 62) __builtin_amdgcn_s_barrier();
   }
+  mfma_sources_done(ca, cb);
 }
 
 template <int R>
@@ -183,8 +197,10 @@ mxk_gemm_bf16_tn_ring(const uint16_t* __restrict__ A, const uint16_t* __restrict
     const int k0 = (s + R < ns ? s + R : ns - 1) * RK * 2;
     ring_step<true, true, VM>(acc, fa0, fb0, fa1, fb1, smem + sl1, a_off, b_off, smem + slot, da,
                               db, wave, k0);
+    // one copy per tile keeps a single tail (set 0); the step ended with
+    // mfma_sources_done, so set 0's last MFMA reads are covered
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {   // one copy per tile keeps a single tail (set 0)
+    for (int i = 0; i < 8; ++i) {
       fa0[i] = fa1[i];
       fb0[i] = fb1[i];
     }

@@ -42,7 +42,7 @@ def test_creates_operands_and_reports_readiness(api):
     ctl = op.Controller(KubeClient(api.url), NS)
     r = ctl.reconcile_once()
     assert _names(api, DS) == ["amd-gpu-stack-device-plugin", "amd-gpu-stack-metrics-exporter",
-                               "amd-gpu-stack-node-labeller"]
+                               "amd-gpu-stack-node-labeller", "amd-gpu-stack-node-validator"]
     assert f"/api/v1/namespaces/{NS}/services/amd-gpu-stack-metrics" in api.objects
     assert f"/apis/batch/v1/namespaces/{NS}/jobs/amd-gpu-stack-validator" in api.objects
     assert "/apis/rbac.authorization.k8s.io/v1/clusterroles/amd-gpu-stack-node-labeller" in api.objects

@@ -149,11 +149,115 @@ def test_manager_rejects_bad_profiles(tmp_path, label, why):
     assert client.node["metadata"]["labels"][partition.STATE_LABEL] == "failed"
 
 
-def test_manager_times_out_when_driver_does_not_reenumerate(tmp_path):
+def test_manager_pending_reboot_when_driver_does_not_reenumerate(tmp_path):
+    """amdgpu takes the modes (sysfs reads them back) but
+    does not re-enumerate in place (an NPS change needs a driver reload):
+    pending-reboot, drain kept; after the "reboot" the next pass sees the
+    layout, reports success and lifts the drain."""
+    root = spx_root(str(tmp_path))
+    state = str(tmp_path / "state")
+    client = FakeNodeClient("n1", {partition.CONFIG_LABEL: "dpx-nps1"})
+    mgr = partition.PartitionManager(client, "n1", root, settle_timeout=0.2, poll=0.02,
+                                     state_dir=state, boot="boot-a")
+    res = mgr.reconcile_once()
+    assert res.state == "pending-reboot" and "expected 16" in res.message and res.applied
+    assert client.node["metadata"]["labels"][partition.STATE_LABEL] == "pending-reboot"
+    assert partition.read_drain(state, "boot-a")          # devices stay withdrawn
+    assert partition.read_drain(state, "boot-b") is None  # void after a reboot
+    make_sysfs.tree_partitioned(root + ".dpx", "DPX", "NPS1")
+    shutil.rmtree(root)
+    os.rename(root + ".dpx", root)
+    res = mgr.reconcile_once()
+    assert res.state == "success" and not res.applied
+    assert partition.read_drain(state, "boot-a") is None
+
+
+def test_manager_fails_when_driver_rejects_mode(tmp_path):
     root = spx_root(str(tmp_path))
     client = FakeNodeClient("n1", {partition.CONFIG_LABEL: "dpx-nps1"})
-    res = partition.PartitionManager(client, "n1", root, settle_timeout=0.2, poll=0.02).reconcile_once()
-    assert res.state == "failed" and "expected 16" in res.message and res.applied
+
+    class Rejecting(threading.Thread):      # amdgpu puts the old mode back
+        def __init__(self):
+            super().__init__(daemon=True)
+            self.stop = threading.Event()
+
+        def run(self):
+            p = os.path.join(root, "sys/bus/pci/devices", make_sysfs.MI355X_BDFS[2],
+                             "current_compute_partition")
+            while not self.stop.wait(0.01):
+                if open(p).read().strip() != "SPX":
+                    open(p, "w").write("SPX\n")
+
+    rej = Rejecting()
+    rej.start()
+    try:
+        res = partition.PartitionManager(client, "n1", root, settle_timeout=0.3,
+                                         poll=0.02).reconcile_once()
+    finally:
+        rej.stop.set()
+    assert res.state == "failed" and make_sysfs.MI355X_BDFS[2] in res.message
+
+
+def test_busy_probes_fail_closed(tmp_path):
+    """an unavailable probe is never read as 'idle'."""
+    root = spx_root(str(tmp_path))
+    client = FakeNodeClient("n1", {partition.CONFIG_LABEL: "cpx-nps1"})
+    busy = partition.combined_busy(lambda: [], lambda: None)
+    res = partition.PartitionManager(client, "n1", root, busy=busy, settle_timeout=1,
+                                     poll=0.02).reconcile_once()
+    assert res.state == "pending" and "cannot verify" in res.message
+    assert partition.current_modes(root, [make_sysfs.MI355X_BDFS[0]])[make_sysfs.MI355X_BDFS[0]] == \
+        {"compute": "SPX", "memory": "NPS1"}
+    assert partition.pod_resources_users(str(tmp_path / "no-such.sock")) is None
+    assert partition.combined_busy(lambda: ["a"], lambda: ["b"])() == ["a", "b"]
+
+
+def test_drain_handshake_with_plugin_and_recheck(tmp_path):
+    """The manager withdraws every device through the plugin (all Unhealthy,
+    acknowledged) BEFORE writing sysfs, and re-checks busy() after the drain:
+    a workload admitted in between keeps the layout unchanged."""
+    root = spx_root(str(tmp_path))
+    state = str(tmp_path / "state")
+    d = tempfile.mkdtemp(prefix="mxdp", dir="/tmp")
+    kube = FakeKubelet(d).start()
+    plugin = AmdGpuDevicePlugin(PluginConfig(plugin_dir=d, sysfs_root=root, health_interval=0.05,
+                                             watch_interval=0.1, use_smi_events=False,
+                                             reconcile_interval=0, state_dir=state)).start()
+    try:
+        reg = kube.wait_registration()
+        watch = iter(kube.plugin_stub(reg.endpoint).ListAndWatch(api.Empty(), timeout=30))
+        assert {x.health for x in next(watch).devices} == {api.HEALTHY}
+        while not os.path.exists(os.path.join(state, "health.json")):
+            time.sleep(0.02)
+        calls = []
+
+        def busy():     # idle at the first check, a pod sneaks in before the second
+            calls.append(1)
+            return [] if len(calls) == 1 else ["ml/late-pod/main"]
+
+        client = FakeNodeClient("n1", {partition.CONFIG_LABEL: "cpx-nps1"})
+        mgr = partition.PartitionManager(client, "n1", root, busy=busy, settle_timeout=1,
+                                         poll=0.02, state_dir=state, drain_timeout=5)
+        res = mgr.reconcile_once()
+        assert res.state == "pending" and "late-pod" in res.message and len(calls) == 2
+        drained = False     # the plugin withdrew every device before the re-check
+        for r in watch:
+            if {x.health for x in r.devices} == {api.UNHEALTHY}:
+                drained = True
+                break
+        assert drained
+        assert plugin.state.reasons["0"] == partition.DRAIN_REASON
+        assert partition.current_modes(root, make_sysfs.MI355X_BDFS[:1])[make_sysfs.MI355X_BDFS[0]] == \
+            {"compute": "SPX", "memory": "NPS1"}
+        assert not os.path.exists(os.path.join(state, partition.DRAIN_FILE))   # lifted
+        end = time.monotonic() + 5
+        while plugin.state.health["0"] != api.HEALTHY and time.monotonic() < end:
+            time.sleep(0.02)
+        assert plugin.state.health["0"] == api.HEALTHY
+    finally:
+        plugin.stop()
+        kube.stop()
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def test_plugin_readvertises_partitions_with_mixed_naming(tmp_path):
@@ -169,12 +273,27 @@ def test_plugin_readvertises_partitions_with_mixed_naming(tmp_path):
     try:
         reg = kube.wait_registration()
         assert reg.resource_name == "amd.com/gpu"
+        old_stub = kube.plugin_stub(reg.endpoint)
+        old_watch = iter(old_stub.ListAndWatch(api.Empty(), timeout=30))
+        assert len(next(old_watch).devices) == 8
         client = FakeNodeClient("n1", {partition.CONFIG_LABEL: "cpx-nps2"})
         res = partition.PartitionManager(client, "n1", root, settle_timeout=10,
                                          poll=0.02).reconcile_once()
         assert res.state == "success"
         reg2 = kube.wait_registration(timeout=15)
         assert reg2.resource_name == "amd.com/gpu-cpx"
+        # the old resource's stream ENDS (it must never advertise the
+        # new partition IDs under the old name) and the new one has its own socket
+        assert reg2.endpoint == "amd-gpu-cpx.sock" and reg.endpoint == "amd-gpu.sock"
+        import grpc
+        seen = []
+        try:
+            for resp in old_watch:
+                seen.append(len(resp.devices))
+        except grpc.RpcError:
+            pass
+        assert all(n == 8 for n in seen), seen
+        assert not os.path.exists(os.path.join(d, "amd-gpu.sock"))
         stub = kube.plugin_stub(reg2.endpoint)
         devs = next(iter(stub.ListAndWatch(api.Empty(), timeout=10))).devices
         assert len(devs) == 64 and all(x.health == api.HEALTHY for x in devs)
