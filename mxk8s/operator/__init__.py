@@ -31,6 +31,10 @@ from __future__ import annotations
 import copy
 import dataclasses
 import logging
+import re
+import threading
+import time
+from fractions import Fraction
 from typing import Optional
 
 from ..chart import render as chart_render
@@ -54,19 +58,61 @@ OPERAND_KINDS = [("apps/v1", "DaemonSet"), ("v1", "Service"), ("v1", "ConfigMap"
                  ("monitoring.coreos.com/v1", "ServiceMonitor")]   # 404 without the CRD: skipped
 
 
+_SUFFIX = {"n": Fraction(1, 10 ** 9), "u": Fraction(1, 10 ** 6), "m": Fraction(1, 1000), "": 1,
+           "k": 10 ** 3, "M": 10 ** 6, "G": 10 ** 9, "T": 10 ** 12, "P": 10 ** 15, "E": 10 ** 18,
+           "Ki": 2 ** 10, "Mi": 2 ** 20, "Gi": 2 ** 30, "Ti": 2 ** 40, "Pi": 2 ** 50, "Ei": 2 ** 60}
+_QTY = re.compile(r"^([+-]?(?:\d+\.?\d*|\.\d+))(?:[eE]([+-]?\d+))?(Ki|Mi|Gi|Ti|Pi|Ei|[numkMGTPE])?$")
+
+
+def parse_quantity(v) -> Optional[Fraction]:
+    """A Kubernetes resource.Quantity (``500m``, ``0.5``, ``1Gi``, ``1e3``) as an
+    exact number; None when ``v`` is not one.  The API server stores
+    quantities in canonical form (``0.5`` -> ``500m``, ``1024Mi`` -> ``1Gi``),
+    so rendered and live values are compared by value, not by spelling."""
+    if isinstance(v, bool):
+        return None
+    if isinstance(v, (int, float)):
+        return Fraction(v)
+    if not isinstance(v, str):
+        return None
+    m = _QTY.match(v.strip())
+    if not m:
+        return None
+    num = Fraction(m.group(1)) * (Fraction(10) ** int(m.group(2)) if m.group(2) else 1)
+    return num * _SUFFIX[m.group(3) or ""]
+
+
+def _named(items) -> bool:
+    return bool(items) and all(isinstance(x, dict) and "name" in x for x in items)
+
+
 def is_subset(want, have) -> bool:
-    """Every field of ``want`` is present with the same value in ``have``
-    (server-side defaults and status on ``have`` are ignored)."""
+    """Every field of ``want`` is present with the same value in ``have``:
+    server-side defaults and status on ``have`` are ignored, quantities
+    compare by value, and lists of named items (containers, env, volumes,
+    volumeMounts, ports) are matched by name, in any order, with extra live
+    items allowed (defaulted or injected ones).  Other lists (args, command,
+    tolerations) keep their order and length."""
     if isinstance(want, dict):
         return isinstance(have, dict) and all(k in have and is_subset(v, have[k])
                                               for k, v in want.items())
     if isinstance(want, list):
-        return isinstance(have, list) and len(want) == len(have) and \
-            all(is_subset(a, b) for a, b in zip(want, have))
-    if isinstance(want, (int, float)) and isinstance(have, str) or \
-            isinstance(have, (int, float)) and isinstance(want, str):
-        return str(want) == str(have)
-    return want == have
+        if not isinstance(have, list):
+            return False
+        if _named(want):
+            by_name = {x.get("name"): x for x in have if isinstance(x, dict)}
+            return all(w["name"] in by_name and is_subset(w, by_name[w["name"]]) for w in want)
+        return len(want) == len(have) and all(is_subset(a, b) for a, b in zip(want, have))
+    if want == have:
+        return True
+    if isinstance(want, bool) or isinstance(have, bool):
+        return False
+    if isinstance(want, (int, float, str)) and isinstance(have, (int, float, str)):
+        if str(want) == str(have):
+            return True
+        qw, qh = parse_quantity(want), parse_quantity(have)
+        return qw is not None and qw == qh
+    return False
 
 
 @dataclasses.dataclass
@@ -77,15 +123,19 @@ class ReconcileResult:
     updated: list = dataclasses.field(default_factory=list)
     deleted: list = dataclasses.field(default_factory=list)
     operands: list = dataclasses.field(default_factory=list)
+    pending: list = dataclasses.field(default_factory=list)   # retried next pass
 
 
 class Controller:
     def __init__(self, client: KubeClient, namespace: str = "amd-gpu",
-                 release: str = "amd-gpu-stack", chart_dir: str = chart_render.CHART_DIR):
+                 release: str = "amd-gpu-stack", chart_dir: str = chart_render.CHART_DIR,
+                 delete_wait_s: float = 5.0):
         self.client = client
         self.namespace = namespace
         self.release = release
         self.chart_dir = chart_dir
+        self.delete_wait_s = delete_wait_s
+        self.wakeups: list[str] = []      # what ended each wait_for_change (tests, logs)
 
     # ---------------------------------------------------------- rendering
     def desired(self, spec: dict) -> list[dict]:
@@ -98,12 +148,22 @@ class Controller:
                                                           self.chart_dir))
         return docs
 
-    def _label(self, obj: dict, policy: str) -> dict:
+    def _label(self, obj: dict, policy: dict) -> dict:
+        """Operand as applied: managed-by + policy labels (garbage collection
+        by this controller) and an ownerReference to the policy, so that the
+        cluster's garbage collector removes every operand when the policy is
+        deleted (ClusterPolicy semantics; the policy is cluster-scoped, so it
+        may own namespaced and cluster-scoped objects alike)."""
         o = copy.deepcopy(obj)
         md = o.setdefault("metadata", {})
         if o["kind"] not in ("ClusterRole", "ClusterRoleBinding", "CustomResourceDefinition"):
             md.setdefault("namespace", self.namespace)
-        md.setdefault("labels", {}).update({MANAGED_BY: MANAGER, POLICY_LABEL: policy})
+        pmd = policy["metadata"]
+        md.setdefault("labels", {}).update({MANAGED_BY: MANAGER, POLICY_LABEL: pmd["name"]})
+        if pmd.get("uid"):
+            md["ownerReferences"] = [{"apiVersion": GROUP_VERSION, "kind": KIND, "name": pmd["name"],
+                                      "uid": pmd["uid"], "controller": True,
+                                      "blockOwnerDeletion": True}]
         return o
 
     # ------------------------------------------------------------- apply
@@ -122,15 +182,46 @@ class Controller:
         if is_subset(obj, live):
             return live
         if obj["kind"] == "Job":    # pod template is immutable: re-create
-            self.client.delete(path)
-            res.updated.append(name)
-            return self.client.create(path.rsplit("/", 1)[0], obj)
+            return self._recreate_job(path, name, obj, live, res)
         new = copy.deepcopy(obj)
         new["metadata"]["resourceVersion"] = live.get("metadata", {}).get("resourceVersion", "")
         res.updated.append(name)
         log.warning("%s drifted from the policy; replacing", name,
                     extra={"event": "operand_drift", "component": name})
         return self.client.replace(path, new)
+
+    def _recreate_job(self, path: str, name: str, obj: dict, live: dict,
+                      res: ReconcileResult) -> dict:
+        """Delete with Background propagation (the server's default for Jobs
+        is Orphan: the old validator pod, holding GPUs, would keep running and
+        the Job would linger behind the orphan finalizer), wait briefly for it
+        to be gone, then create.  Still there, or a 409 on the create: the
+        re-creation is pending and retried on the next pass, never raised."""
+        if "deletionTimestamp" not in live.get("metadata", {}):
+            self.client.delete(path, propagation="Background")
+            log.warning("%s drifted from the policy; re-creating", name,
+                        extra={"event": "operand_drift", "component": name})
+        end = time.monotonic() + self.delete_wait_s
+        while True:
+            try:
+                cur = self.client.get(path)
+            except KubeError as e:
+                if e.status != 404:
+                    raise
+                break
+            if time.monotonic() >= end:
+                res.pending.append(name)
+                return cur
+            time.sleep(0.05)
+        try:
+            new = self.client.create(path.rsplit("/", 1)[0], obj)
+        except KubeError as e:
+            if e.status != 409:
+                raise
+            res.pending.append(name)
+            return live
+        res.updated.append(name)
+        return new
 
     def garbage_collect(self, policy: str, keep: set, res: ReconcileResult) -> None:
         sel = f"{MANAGED_BY}={MANAGER},{POLICY_LABEL}={policy}"
@@ -183,29 +274,110 @@ class Controller:
             return res
         keep = set()
         not_ready = []
+        prev = {(o.get("kind"), o.get("name")): o
+                for o in (pol.get("status") or {}).get("operands", []) or []}
+        now = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
         for d in docs:
-            obj = self._label(d, name)
+            obj = self._label(d, pol)
             live = self.apply(obj, res)
             keep.add(object_path(obj, self.namespace))
             r = self.readiness(live)
             if r is not None:
-                res.operands.append({"kind": obj["kind"], "name": obj["metadata"]["name"],
-                                     "ready": r})
+                key = (obj["kind"], obj["metadata"]["name"])
+                old = prev.get(key)
+                ltt = old.get("lastTransitionTime") if old and old.get("ready") == r else now
+                res.operands.append({"kind": key[0], "name": key[1], "ready": r,
+                                     "lastTransitionTime": ltt or now})
                 if not r:
                     not_ready.append(obj["metadata"]["name"])
         self.garbage_collect(name, keep, res)
-        if not_ready:
+        if not_ready or res.pending:
             res.state = "notReady"
-            res.message = "waiting for " + ", ".join(not_ready)
+            res.message = "waiting for " + ", ".join(not_ready + [f"{p} (re-creating)"
+                                                                  for p in res.pending])
         else:
             res.message = f"{len(keep)} operand objects in sync"
         self._status(pol, res)
         return res
 
     def _status(self, pol: dict, res: ReconcileResult) -> None:
-        self.client.patch_status(f"{POLICIES}/{pol['metadata']['name']}", {
-            "state": res.state, "message": res.message, "operands": res.operands,
-            "observedGeneration": pol["metadata"].get("generation", 1)})
+        st = {"state": res.state, "message": res.message, "operands": res.operands,
+              "observedGeneration": pol["metadata"].get("generation", 1)}
+        old = pol.get("status") or {}
+        if all(old.get(k) == v for k, v in st.items()):
+            return                         # no status write (and no watch event) when in sync
+        self.client.patch_status(f"{POLICIES}/{pol['metadata']['name']}", st)
+
+    # ----------------------------------------------------------- watching
+    def _watched(self) -> list[tuple[str, Optional[str]]]:
+        sel = f"{MANAGED_BY}={MANAGER}"
+        return [(POLICIES, None),
+                (collection_path("apps/v1", "DaemonSet", self.namespace), sel),
+                (collection_path("batch/v1", "Job", self.namespace), sel)]
+
+    def wait_for_change(self, timeout: float, stop=None) -> str:
+        """Block until a policy or a managed DaemonSet / Job changes (a watch
+        per collection, resumed at the collection's resourceVersion), or
+        ``timeout`` (the resync: drift on kinds not watched).  Returns what
+        woke it ("watch:<collection>" / "resync" / "stop")."""
+        woke = threading.Event()
+        why: list[str] = []
+
+        def watch_one(path, sel, rv):
+            try:
+                for ev in self.client.watch(path, rv, timeout, sel):
+                    if ev.get("type") in ("ADDED", "MODIFIED", "DELETED"):
+                        why.append("watch:" + path.rsplit("/", 1)[1])
+                        woke.set()
+                        return
+                    if ev.get("type") == "ERROR":   # e.g. 410 Gone: resync now
+                        why.append("watch-error")
+                        woke.set()
+                        return
+            except Exception as e:                  # API server blip: fall back to the resync
+                log.debug("watch %s failed: %s", path, e)
+
+        threads = []
+        for path, sel in self._watched():
+            try:
+                _, rv = self.client.list_with_version(path, sel)
+            except KubeError as e:
+                if e.status == 404:
+                    continue
+                raise
+            t = threading.Thread(target=watch_one, args=(path, sel, rv), daemon=True)
+            t.start()
+            threads.append(t)
+        end = time.monotonic() + timeout
+        while not woke.is_set():
+            if stop is not None and stop():
+                self.wakeups.append("stop")
+                return "stop"
+            left = end - time.monotonic()
+            if left <= 0:
+                self.wakeups.append("resync")
+                return "resync"
+            woke.wait(min(left, 0.2))
+        self.wakeups.append(why[0] if why else "watch")
+        return self.wakeups[-1]
+
+    def run(self, interval: float = 300.0, stop=None) -> None:
+        """Level-triggered loop: reconcile, then sleep until something this
+        controller owns (or its policy) changes, at most ``interval`` s."""
+        while stop is None or not stop():
+            try:
+                r = self.reconcile_once()
+                if r.created or r.updated or r.deleted or r.pending:
+                    log.info("reconciled: %s (created %d, updated %d, deleted %d, pending %d)",
+                             r.state, len(r.created), len(r.updated), len(r.deleted),
+                             len(r.pending))
+            except Exception as e:   # API server blip: retry after the next wake-up
+                log.error("reconcile failed: %s", e)
+            try:
+                self.wait_for_change(interval, stop)
+            except Exception as e:
+                log.error("watch setup failed: %s", e)
+                time.sleep(min(interval, 5.0))
 
 
 def crd() -> dict:

@@ -15,7 +15,9 @@ def main(argv=None) -> int:
     p = argparse.ArgumentParser(description=__doc__)
     p.add_argument("--namespace", default="amd-gpu")
     p.add_argument("--release", default="amd-gpu-stack")
-    p.add_argument("--interval", type=float, default=30.0, help="0 = reconcile once")
+    p.add_argument("--interval", type=float, default=300.0,
+                   help="resync period (s): between resyncs the controller sleeps on watches "
+                        "of its policy and its DaemonSets / Jobs; 0 = reconcile once")
     p.add_argument("--server", default=None, help="API server URL (default: in-cluster)")
     p.add_argument("--token", default=None)
     p.add_argument("--log-format", choices=["json", "text"], default="json")
@@ -24,18 +26,15 @@ def main(argv=None) -> int:
     log = logging.getLogger("mxk8s.operator")
     client = KubeClient(a.server, a.token) if a.server else KubeClient.in_cluster()
     ctl = Controller(client, a.namespace, a.release)
-    while True:
+    if a.interval <= 0:
         try:
-            r = ctl.reconcile_once()
-            if r.created or r.updated or r.deleted:
-                log.info("reconciled: %s (created %d, updated %d, deleted %d)", r.state,
-                         len(r.created), len(r.updated), len(r.deleted))
-        except Exception as e:   # API server blip: retry next interval
+            ctl.reconcile_once()
+        except Exception as e:
             log.error("reconcile failed: %s", e)
-        if a.interval <= 0:
-            return 0
-        time.sleep(a.interval)
-
+            return 1
+        return 0
+    ctl.run(a.interval)
+    return 0
 
 if __name__ == "__main__":
     sys.exit(main())

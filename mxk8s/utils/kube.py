@@ -77,8 +77,36 @@ class KubeClient:
         return self.merge_patch(f"/api/v1/nodes/{name}", {"metadata": {"labels": labels}})
 
     def list(self, path: str, label_selector: Optional[str] = None) -> list:
+        return self.list_with_version(path, label_selector)[0]
+
+    def list_with_version(self, path: str, label_selector: Optional[str] = None) -> tuple[list, str]:
+        """(items, the collection's resourceVersion): where a watch resumes."""
         q = "?labelSelector=" + urllib.parse.quote(label_selector) if label_selector else ""
-        return self._req("GET", path + q).get("items", [])
+        doc = self._req("GET", path + q)
+        return doc.get("items", []), str(doc.get("metadata", {}).get("resourceVersion", ""))
+
+    def watch(self, path: str, resource_version: str = "", timeout_s: float = 30.0,
+              label_selector: Optional[str] = None):
+        """Yield the watch events ({"type": ADDED|MODIFIED|DELETED|ERROR,
+        "object": ...}) of a collection after ``resource_version``, until the
+        server ends the watch (``timeoutSeconds``)."""
+        q = {"watch": "1", "timeoutSeconds": str(max(1, int(timeout_s)))}
+        if resource_version:
+            q["resourceVersion"] = resource_version
+        if label_selector:
+            q["labelSelector"] = label_selector
+        req = urllib.request.Request(self.server + path + "?" + urllib.parse.urlencode(q))
+        req.add_header("Accept", "application/json")
+        if self.token:
+            req.add_header("Authorization", f"Bearer {self.token}")
+        try:
+            with urllib.request.urlopen(req, timeout=timeout_s + 10, context=self._ctx) as r:
+                for line in r:
+                    line = line.strip()
+                    if line:
+                        yield json.loads(line)
+        except urllib.error.HTTPError as e:
+            raise KubeError(e.code, e.read().decode(errors="replace")[:500]) from None
 
     def create(self, collection: str, obj: dict) -> dict:
         return self._req("POST", collection, obj)
@@ -86,8 +114,13 @@ class KubeClient:
     def replace(self, path: str, obj: dict) -> dict:
         return self._req("PUT", path, obj)
 
-    def delete(self, path: str) -> dict:
-        return self._req("DELETE", path)
+    def delete(self, path: str, propagation: Optional[str] = None) -> dict:
+        """``propagation``: Background | Foreground | Orphan (DeleteOptions).
+        The API server's default for batch/v1 Jobs is Orphan: the Job's pods
+        keep running and the Job lingers behind the orphan finalizer."""
+        body = None if propagation is None else {"kind": "DeleteOptions", "apiVersion": "v1",
+                                                 "propagationPolicy": propagation}
+        return self._req("DELETE", path, body)
 
     def patch_status(self, path: str, status: dict) -> dict:
         return self.merge_patch(path + "/status", {"status": status})

@@ -3,6 +3,8 @@ in-process fake API server: create from the policy, readiness in status,
 drift repair, garbage collection on spec change, invalid specs rejected
 without touching the operands."""
 import copy
+import threading
+import time
 
 import pytest
 import yaml
@@ -164,3 +166,123 @@ def test_service_monitor_operand_created_and_collected(api):
     api.objects[POL]["metadata"]["generation"] = 2
     r = ctl.reconcile_once()
     assert "ServiceMonitor/amd-gpu-stack-metrics" in r.deleted and sm not in api.objects
+
+
+def test_is_subset_quantities_and_named_lists():
+    """server-side canonical quantities and defaulted /
+    injected named list items are not drift; a real change still is."""
+    assert op.is_subset({"cpu": "0.5", "memory": "1024Mi"}, {"cpu": "500m", "memory": "1Gi"})
+    assert not op.is_subset({"cpu": "0.5"}, {"cpu": "50m"})
+    want = {"env": [{"name": "A", "value": "1"}], "volumes": [{"name": "x"}, {"name": "y"}]}
+    have = {"env": [{"name": "INJ", "value": "2"}, {"name": "A", "value": "1"}],
+            "volumes": [{"name": "y", "hostPath": {"path": "/y"}}, {"name": "x"}]}
+    assert op.is_subset(want, have)
+    assert not op.is_subset({"env": [{"name": "A", "value": "1"}]}, {"env": [{"name": "A", "value": "2"}]})
+    assert not op.is_subset({"args": ["--a", "--b"]}, {"args": ["--b", "--a"]})   # order kept
+    assert not op.is_subset({"enabled": True}, {"enabled": "True"})
+    assert op.parse_quantity("1e3") == 1000 and op.parse_quantity("30s") is None
+
+
+def test_normalising_server_zero_writes_after_first_reconcile():
+    srv = FakeApiServer(normalize=True).start()
+    try:
+        _policy(srv, {"devicePlugin": {"resources": {"requests": {"cpu": "0.05", "memory": "65536Ki"},
+                                                     "limits": {"memory": "0.25Gi"}}}})
+        ctl = op.Controller(KubeClient(srv.url), NS)
+        r = ctl.reconcile_once()
+        assert r.created
+        live = srv.objects[f"{DS}/amd-gpu-stack-device-plugin"]["spec"]["template"]["spec"]
+        c = live["containers"][0]
+        assert c["resources"]["requests"] == {"cpu": "50m", "memory": "64Mi"}   # canonicalised
+        assert live["volumes"][0]["name"] == "kube-api-access"                  # injected
+        writes = {m: srv.count(m) for m in ("POST", "PUT", "DELETE")}
+        for _ in range(3):
+            r = ctl.reconcile_once()
+            assert not (r.created or r.updated or r.deleted or r.pending), r
+        assert {m: srv.count(m) for m in ("POST", "PUT", "DELETE")} == writes
+    finally:
+        srv.stop()
+
+
+def test_owner_references_and_transition_times(api):
+    _policy(api)
+    uid = api.objects[POL]["metadata"]["uid"]
+    ctl = op.Controller(KubeClient(api.url), NS)
+    ctl.reconcile_once()
+    for p, o in api.objects.items():
+        if p == POL:
+            continue
+        refs = o["metadata"].get("ownerReferences")
+        assert refs == [{"apiVersion": op.GROUP_VERSION, "kind": op.KIND, "name": "default",
+                         "uid": uid, "controller": True, "blockOwnerDeletion": True}], p
+    st = {o["name"]: o for o in api.objects[POL]["status"]["operands"]}
+    t0 = st["amd-gpu-stack-device-plugin"]["lastTransitionTime"]
+    assert st["amd-gpu-stack-device-plugin"]["ready"] is False and t0.endswith("Z")
+    api.objects[POL]["status"]["operands"][0]["lastTransitionTime"] = "2020-01-01T00:00:00Z"
+    ctl.reconcile_once()          # no transition: the time is kept
+    kept = {o["name"]: o for o in api.objects[POL]["status"]["operands"]}
+    first = api.objects[POL]["status"]["operands"][0]["name"]
+    assert kept[first]["lastTransitionTime"] == "2020-01-01T00:00:00Z"
+    _ready(api, "amd-gpu-stack-device-plugin")
+    ctl.reconcile_once()
+    now = {o["name"]: o for o in api.objects[POL]["status"]["operands"]}
+    assert now["amd-gpu-stack-device-plugin"]["ready"] is True
+    assert now["amd-gpu-stack-device-plugin"]["lastTransitionTime"] != "2020-01-01T00:00:00Z"
+
+
+def test_job_recreate_uses_background_propagation_and_tolerates_lingering():
+    """a plain DELETE of a Job orphans its pod and the Job lingers
+    behind the orphan finalizer, so an immediate POST gets 409."""
+    srv = FakeApiServer(job_orphan_linger=0.6).start()
+    job = f"/apis/batch/v1/namespaces/{NS}/jobs/amd-gpu-stack-validator"
+    try:
+        _policy(srv)
+        ctl = op.Controller(KubeClient(srv.url), NS, delete_wait_s=2.0)
+        ctl.reconcile_once()
+        uid0 = srv.objects[job]["metadata"]["uid"]
+        srv.objects[job]["spec"]["template"]["spec"]["containers"][0]["args"].append("--x")
+        r = ctl.reconcile_once()          # Background: gone at once, re-created this pass
+        assert "Job/amd-gpu-stack-validator" in r.updated and not r.pending
+        assert srv.objects[job]["metadata"]["uid"] != uid0
+        # a Job stuck behind a finalizer (someone else's orphan delete): pending, no raise
+        srv.handle("DELETE", job, None)
+        assert "deletionTimestamp" in srv.objects[job]["metadata"]
+        ctl.delete_wait_s = 0.1
+        srv.objects[job]["spec"]["template"]["spec"]["containers"][0]["args"].append("--y")
+        r = ctl.reconcile_once()
+        assert r.pending == ["Job/amd-gpu-stack-validator"] and r.state == "notReady"
+        time.sleep(0.8)                   # the garbage collector releases it
+        r = ctl.reconcile_once()
+        assert "Job/amd-gpu-stack-validator" in r.created and not r.pending
+    finally:
+        srv.stop()
+
+
+def test_controller_wakes_on_watch_events_not_the_resync(api):
+    ctl = op.Controller(KubeClient(api.url), NS)
+    stop = threading.Event()
+    t = threading.Thread(target=ctl.run, args=(60.0, stop.is_set), daemon=True)
+    t.start()
+    try:
+        time.sleep(0.3)
+        _policy(api)                       # a new policy: applied well before the 60 s resync
+        end = time.monotonic() + 5
+        while f"{DS}/amd-gpu-stack-device-plugin" not in api.objects and time.monotonic() < end:
+            time.sleep(0.05)
+        assert f"{DS}/amd-gpu-stack-device-plugin" in api.objects
+        assert "watch:gpustackpolicies" in ctl.wakeups
+        # drift on a managed DaemonSet (a PUT, so the server emits an event)
+        path = f"{DS}/amd-gpu-stack-node-labeller"
+        time.sleep(0.5)
+        o = copy.deepcopy(api.objects[path])
+        o["spec"]["template"]["spec"]["containers"][0]["args"].append("--bogus")
+        api.handle("PUT", path, o)
+        end = time.monotonic() + 5
+        while "--bogus" in api.objects[path]["spec"]["template"]["spec"]["containers"][0]["args"] \
+                and time.monotonic() < end:
+            time.sleep(0.05)
+        assert "--bogus" not in api.objects[path]["spec"]["template"]["spec"]["containers"][0]["args"]
+        assert "watch:daemonsets" in ctl.wakeups and "resync" not in ctl.wakeups
+    finally:
+        stop.set()
+        t.join(timeout=5)
