@@ -445,6 +445,8 @@ def main(argv=None) -> int:
     p.add_argument("--bucket-mb", type=float, default=512.0, help="ddp mode: all-reduce bucket size")
     p.add_argument("--no-zero", action="store_true", help="ddp mode: replicated optimizer (no ZeRO-1)")
     p.add_argument("--no-tuned-gemms", action="store_true", help="ddp mode: default hipBLASLt picks")
+    p.add_argument("--grad-reduce", choices=["bf16", "fp32"], default="bf16",
+                   help="ddp mode: gradient wire format (fp32: one bf16 rounding instead of n-1)")
     args = p.parse_args(argv)
 
     world, rank, _ = _dist_env()

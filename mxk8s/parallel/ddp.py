@@ -17,6 +17,10 @@ Design (MI355X-first rather than a copy of torch DDP's call pattern):
   16 GB of Llama-3-8B bf16 gradients = ~32 buckets;
 * the 1/world average and gradient clipping are folded into the fused
   optimizer kernel (``mxk8s.parallel.optim``), not applied as separate passes;
+* ``reduce_dtype="fp32"``: a bucket is cast to fp32 when it completes and
+  reduced in fp32 (2x the bytes on the wire), then rounded to bf16 ONCE; the
+  bf16 default rounds the running sum at every ring hop (world - 1 bf16
+  roundings per element at world 8, tests/test_ddp_cpu.py measures both);
 * ``shard_optimizer=True`` (ZeRO-1): buckets are padded to world*64 elements,
   each bucket is REDUCE-SCATTERED instead of all-reduced (rank r keeps chunk
   r), the fp32 master/moments exist only for the rank's shard (12 B/param /
@@ -151,7 +155,9 @@ class FlatDDP:
 
     def __init__(self, module: nn.Module, bucket_mb: float = 512.0,
                  process_group=None, broadcast_from: Optional[int] = 0,
-                 shard_optimizer: bool = False):
+                 shard_optimizer: bool = False, reduce_dtype: str = "bf16"):
+        if reduce_dtype not in ("bf16", "fp32"):
+            raise ValueError(f"reduce_dtype must be bf16 or fp32, got {reduce_dtype!r}")
         self.module = module
         self.group = process_group
         self.world = dist.get_world_size(process_group) if mxdist.active() else 1
@@ -178,6 +184,16 @@ class FlatDDP:
         self.grad_shard = (torch.zeros(shard_off, dtype=self.space.dtype,
                                        device=self.space.grad_buf.device)
                            if self.sharded else None)
+        # fp32 wire format: per-bucket fp32 staging (the whole gradient space,
+        # since every bucket may be in flight at once) and, sharded, an fp32
+        # copy of the rank's shard; only when the gradients are not fp32 already
+        self.reduce_fp32 = (reduce_dtype == "fp32" and self.world > 1 and
+                            self.space.dtype != torch.float32)
+        dev = self.space.grad_buf.device
+        self._f32 = (torch.empty(self.space.numel, dtype=torch.float32, device=dev)
+                     if self.reduce_fp32 else None)
+        self._f32_shard = (torch.empty(shard_off, dtype=torch.float32, device=dev)
+                           if self.reduce_fp32 and self.sharded else None)
         self._sync_enabled = True
         self._hooks = []
         if self.world > 1:
@@ -208,13 +224,31 @@ class FlatDDP:
             return
         b.launched = True
         g = self.space.grad_buf[b.start:b.end]
+        if self.reduce_fp32:
+            wire = self._f32[b.start:b.end]
+            wire.copy_(g)
+        else:
+            wire = g
         if self.sharded:
             c = b.chunk(self.world)
-            b.handle = dist.reduce_scatter_tensor(self.grad_shard[b.shard_off:b.shard_off + c], g,
-                                                  op=dist.ReduceOp.SUM, group=self.group,
+            out = (self._f32_shard if self.reduce_fp32 else self.grad_shard)[b.shard_off:b.shard_off + c]
+            b.handle = dist.reduce_scatter_tensor(out, wire, op=dist.ReduceOp.SUM, group=self.group,
                                                   async_op=True)
         else:
-            b.handle = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            b.handle = dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def _finish_bucket(self, b: Bucket) -> None:
+        """Wait for bucket b's reduction (a stream wait under RCCL) and, with
+        the fp32 wire format, round its result to bf16 once."""
+        b.handle.wait()
+        if not self.reduce_fp32:
+            return
+        if self.sharded:
+            c = b.chunk(self.world)
+            self.grad_shard[b.shard_off:b.shard_off + c].copy_(
+                self._f32_shard[b.shard_off:b.shard_off + c])
+        else:
+            self.space.grad_buf[b.start:b.end].copy_(self._f32[b.start:b.end])
 
     def _on_grad(self, p) -> None:
         if not self._sync_enabled:
@@ -242,7 +276,7 @@ class FlatDDP:
                     self._launch(b)
             for b in self.buckets:
                 if b.handle is not None:
-                    b.handle.wait()
+                    self._finish_bucket(b)
         self._reset_buckets()
 
     def zero_grad(self) -> None:

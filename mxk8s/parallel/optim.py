@@ -203,7 +203,12 @@ class ShardedFlatAdamW:
          in place into the rank's chunk of ``param_buf``, then an async
          in-place all-gather of that bucket — the all-gather of bucket b runs
          on the RCCL stream while AdamW of bucket b+1 runs;
-      3. the compute stream waits on every all-gather (no host sync).
+      3. the compute stream waits on every all-gather (no host sync) — or,
+         with :meth:`enable_overlap`, each module's forward pre-hook waits for
+         the all-gathers of just the buckets holding its parameters, and the
+         buckets are updated + gathered in the order the forward needs them:
+         the 16 GB (Llama-3-8B) parameter all-gather then runs under the
+         next forward instead of in front of it.
     """
 
     def __init__(self, ddp, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
@@ -238,10 +243,55 @@ class ShardedFlatAdamW:
         if dev.type == "cuda":
             n_part = _lib.lib().mxk_sumsq_partials(ddp.shard_numel)
             self._partials = torch.zeros(n_part, dtype=torch.float32, device=dev)
+        self._order = list(range(len(ddp.buckets)))     # bucket update / gather order
+        self._pending: dict[int, object] = {}           # bucket index -> all-gather handle
+        self._module_buckets: list = []                 # per hooked module: bucket indices
+        self.waits: list[int] = []                      # bucket indices as waited (tests)
 
     @property
     def last_grad_norm(self) -> torch.Tensor:
         return self._scale[1]
+
+    def enable_overlap(self, stages) -> bool:
+        """``stages``: [(params, module)] in the order the forward needs the
+        parameters (``mxk8s.train.ddp_llama.overlap_stages``: the embedding
+        with every 1-D weight first — the fused norms read the next layer's
+        weight a layer early — then each block, then the LM head); every
+        trainable parameter in exactly one stage.  Buckets are then updated
+        and all-gathered in first-need order, and the module's forward
+        pre-hook waits for the buckets holding its stage's parameters only."""
+        ddp = self.ddp
+        bucket_of = {}
+        for i, b in enumerate(ddp.buckets):
+            for p in b.params:
+                bucket_of[id(p)] = i
+        need, first, seen = [], {}, 0
+        for k, (params, _) in enumerate(stages):
+            idx = sorted({bucket_of[id(p)] for p in params})
+            seen += len(params)
+            need.append(idx)
+            for i in idx:
+                first.setdefault(i, k)
+        if seen != len(ddp.space.params) or len(first) != len(ddp.buckets):
+            raise ValueError(f"overlap stages cover {seen} of {len(ddp.space.params)} parameters")
+        self._order = sorted(range(len(ddp.buckets)), key=lambda i: (first[i], i))
+        self._module_buckets = need
+        for k, (_, module) in enumerate(stages):
+            module.register_forward_pre_hook(
+                lambda mod, args, k=k: self._wait_buckets(self._module_buckets[k]))
+        return True
+
+    def _wait_buckets(self, idx) -> None:
+        for i in idx:
+            h = self._pending.pop(i, None)
+            if h is not None:
+                h.wait()
+                self.waits.append(i)
+
+    def synchronize(self) -> None:
+        """Wait for every pending parameter all-gather (before reading the
+        parameters outside a hooked forward: checkpoints, evaluation)."""
+        self._wait_buckets(list(self._pending))
 
     def _clip(self) -> None:
         ddp = self.ddp
@@ -293,19 +343,20 @@ class ShardedFlatAdamW:
 
     @torch.no_grad()
     def step(self) -> None:
+        self.synchronize()      # a bucket no forward consumed (its chunk is rewritten below)
         self.step_count += 1
         ddp, sp = self.ddp, self.ddp.space
         self._clip()
-        handles = []
-        seg_i = 0
-        for b in ddp.buckets:
-            while seg_i < len(self.segments) and self.segments[seg_i][0] is b:
-                _, so, lo, n, wd = self.segments[seg_i]
+        segs: dict[int, list] = {}
+        index = {id(b): i for i, b in enumerate(ddp.buckets)}
+        for seg in self.segments:
+            segs.setdefault(index[id(seg[0])], []).append(seg)
+        for i in self._order:
+            b = ddp.buckets[i]
+            for _, so, lo, n, wd in segs.get(i, []):
                 self._adamw_segment(so, lo, n, wd)
-                seg_i += 1
             lo, hi = ddp.shard_range(b)
-            handles.append(self._dist.all_gather_into_tensor(
-                sp.param_buf[b.start:b.end], sp.param_buf[lo:hi], group=ddp.group,
-                async_op=True))
-        for h in handles:
-            h.wait()
+            self._pending[i] = self._dist.all_gather_into_tensor(
+                sp.param_buf[b.start:b.end], sp.param_buf[lo:hi], group=ddp.group, async_op=True)
+        if not self._module_buckets:
+            self.synchronize()  # no overlap: every parameter is whole when step() returns

@@ -48,7 +48,8 @@ def use_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
 
 
 def build(cfg: LlamaConfig, device: torch.device, bucket_mb: float, lr: float = 3e-4,
-          zero: bool = True, overlap: bool | None = None):
+          zero: bool = True, overlap: bool | None = None, reduce_dtype: str = "bf16",
+          gather_overlap: bool = True):
     """Model + DDP + optimizer.  ``zero`` shards the AdamW state and step over
     the ranks (ZeRO-1, reduce-scatter + all-gather); it only applies with
     more than one rank.  ``overlap`` (``MXK_OPT_OVERLAP=1``) runs the
@@ -56,15 +57,21 @@ def build(cfg: LlamaConfig, device: torch.device, bucket_mb: float, lr: float = 
     (``FlatAdamW.enable_overlap``); bit-identical, but measured neutral on
     one MI355X (617-618 ms per step either way, profiles/r2_ddp/
     opt_overlap_ab.log: the forward GEMMs leave no CU slots for the update
-    kernels), so off by default."""
+    kernels), so off by default.  ``gather_overlap`` (ZeRO-1): each bucket's
+    parameter all-gather is waited for by the forward pre-hook of the first
+    module that reads it, so the all-gather of the whole model runs under the
+    next forward instead of in front of it.  ``reduce_dtype`` "fp32" reduces
+    gradients in fp32 on the wire (one bf16 rounding instead of world - 1)."""
     if overlap is None:
         overlap = os.environ.get("MXK_OPT_OVERLAP", "0") == "1"
     with torch.device(device):
         model = Llama(cfg)
     model = model.to(torch.bfloat16)
-    ddp = FlatDDP(model, bucket_mb=bucket_mb, shard_optimizer=zero)
+    ddp = FlatDDP(model, bucket_mb=bucket_mb, shard_optimizer=zero, reduce_dtype=reduce_dtype)
     if ddp.sharded:
         opt = ShardedFlatAdamW(ddp, lr=lr)
+        if gather_overlap:
+            opt.enable_overlap(overlap_stages(model))
     else:
         opt = FlatAdamW(ddp.space, lr=lr, grad_scale=ddp.grad_scale)
         if overlap and device.type == "cuda":
@@ -119,7 +126,8 @@ def run_ddp_bench(args) -> dict:
     bucket_mb = getattr(args, "bucket_mb", 512.0)
     tuned = False if getattr(args, "no_tuned_gemms", False) else use_tuned_gemms()
     zero = not getattr(args, "no_zero", False)
-    model, ddp, opt = build(cfg, dev, bucket_mb, zero=zero)
+    reduce_dtype = getattr(args, "grad_reduce", "bf16")
+    model, ddp, opt = build(cfg, dev, bucket_mb, zero=zero, reduce_dtype=reduce_dtype)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     nbatches = 4
@@ -179,6 +187,9 @@ def run_ddp_bench(args) -> dict:
         "peak_mem_gib": round(peak_mem / 2 ** 30, 2),
         "mean_loss": final_loss,
         "bucket_mb": bucket_mb,
+        "grad_reduce_dtype": reduce_dtype,
+        "param_gather": ("overlapped with the next forward" if getattr(opt, "_module_buckets", None)
+                         else "in step()") if ddp.sharded else None,
         "tuned_gemms": tuned,
         "grad_norm_last": float(opt.last_grad_norm.item()),
         "losses": [round(float(x), 6) for x in torch.stack(losses).float().tolist()] if losses else [],
@@ -201,6 +212,8 @@ def main(argv=None) -> int:
                    help="do not load the TunableOp GEMM table")
     p.add_argument("--no-zero", action="store_true",
                    help="replicate the optimizer (all-reduce) instead of ZeRO-1 sharding")
+    p.add_argument("--grad-reduce", choices=["bf16", "fp32"], default="bf16",
+                   help="gradient wire format of the reduce-scatter / all-reduce")
     a = p.parse_args(argv)
     out = run_ddp_bench(a)
     if mxdist.world_info()[1] == 0:

@@ -317,3 +317,94 @@ def test_overlap_stages_cover_every_parameter_once():
     assert opt.enable_overlap(stages) is False and opt._stages is None
     merged = opt._merge_ranges([(0, 10), (64, 100), (space.n_decay, space.n_decay + 4)])
     assert all((a < space.n_decay) == (b <= space.n_decay) for a, b in merged)
+
+
+def _zero8_worker(rank, world, port, outdir):
+    """8 gloo ranks, bf16 tiny Llama: ZeRO-1 with the bf16 and the fp32 wire
+    format, and fp32 + the all-gather overlapped with the next forward."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from mxk8s.parallel.optim import ShardedFlatAdamW
+    from mxk8s.train.ddp_llama import overlap_stages
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = LlamaConfig.tiny()
+    out = {}
+    for run, (rdt, overlap) in {"bf16": ("bf16", False), "fp32": ("fp32", False),
+                                "fp32_overlap": ("fp32", True)}.items():
+        torch.manual_seed(0)
+        model = Llama(cfg).to(torch.bfloat16)
+        ddp = FlatDDP(model, bucket_mb=0.05, shard_optimizer=True, reduce_dtype=rdt)
+        opt = ShardedFlatAdamW(ddp, lr=1e-3)
+        seen = {}
+        if overlap:
+            stages = overlap_stages(model)
+            opt.enable_overlap(stages)
+            # runs AFTER the optimizer's wait hook: what the module reads
+            for k, (params, module) in enumerate(stages):
+                module.register_forward_pre_hook(
+                    lambda m, a, k=k, params=params: seen.__setitem__(
+                        k, [p.detach().clone() for p in params]))
+        checks = []
+        for step in range(3):
+            loss = model.loss(_batch(rank * 10 + step, cfg))
+            if overlap and step > 0:
+                opt.synchronize()       # compare the forward's view with the final gather
+                checks.append(all(torch.equal(a, p.detach()) for k, (params, _) in enumerate(stages)
+                                  for a, p in zip(seen[k], params)))
+            loss.backward()
+            ddp.finish_grad_sync()
+            if step == 0:
+                out[run + "_local"] = ddp.space.grad_buf.clone()
+                out[run + "_shard"] = ddp.grad_shard.clone()
+                out[run + "_ranges"] = [ddp.shard_range(b) for b in ddp.buckets]
+            opt.step()
+            ddp.zero_grad()
+        opt.synchronize()
+        out[run + "_params"] = ddp.space.param_buf.clone()
+        out[run + "_checks"] = checks
+        out[run + "_waits"] = list(opt.waits)
+        out[run + "_order"] = list(opt._order)
+    torch.save(out, os.path.join(outdir, f"z8_{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_zero1_eight_ranks_fp32_wire_and_gather_overlap():
+    """at world 8 the bucketed reduce-scatter with the fp32 wire
+    format equals the exact sum of the 8 local bf16 gradients to one bf16
+    rounding (the bf16 wire format rounds at every hop); the all-gather
+    overlapped with the next forward never lets a module read a bucket before
+    its gather finished and changes no bit of the result."""
+    world = 8
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_zero8_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        z = [torch.load(os.path.join(d, f"z8_{i}.pt"), weights_only=True) for i in range(world)]
+    # same initial params -> same local gradients in every run
+    for r in range(world):
+        assert torch.equal(z[r]["bf16_local"], z[r]["fp32_local"])
+    exact = sum(z[r]["fp32_local"].double() for r in range(world))
+    errs = {}
+    for run in ("bf16", "fp32"):
+        worst = 0.0
+        for r in range(world):
+            shard = z[r][run + "_shard"].double()
+            so = 0
+            for lo, hi in z[r][run + "_ranges"]:
+                ref = exact[lo:hi]
+                got = shard[so:so + hi - lo]
+                so += hi - lo
+                big = ref.abs() > 1e-3 * exact.abs().max()
+                if big.any():
+                    worst = max(worst, ((got - ref).abs()[big] / ref.abs()[big]).max().item())
+        errs[run] = worst
+    assert errs["fp32"] <= 2.0 ** -8, errs                 # one bf16 rounding
+    assert errs["bf16"] > errs["fp32"], errs               # 7 roundings at world 8
+    for r in range(world):
+        assert torch.equal(z[r]["fp32_overlap_params"], z[r]["fp32_params"])   # bit-identical
+        assert z[r]["fp32_overlap_checks"] and all(z[r]["fp32_overlap_checks"])
+        order = z[r]["fp32_overlap_order"]
+        assert sorted(order) == list(range(len(order))) and order != sorted(order)
+        assert set(z[r]["fp32_overlap_waits"]) == set(order)
+    for r in range(1, world):
+        assert torch.equal(z[r]["fp32_params"], z[0]["fp32_params"])
