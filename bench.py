@@ -163,54 +163,85 @@ def _full_check(A, Bt, C):
     return err, tol
 
 
+def allreduce_sizes(args, world) -> list[int]:
+    """Message sizes (bytes) of the sweep: an explicit ``--allreduce-sizes``
+    MiB list, else the protocol's 8 B - 8 GiB in x2 steps (BASELINE.md
+    "Measurement protocol"; nccl-tests ``-b 8 -e 8G -f 2``) at n > 1, and three
+    sizes at n = 1 (a 1-rank all-reduce moves no data: only the code path)."""
+    if args.allreduce_sizes:
+        return [int(s) << 20 for s in args.allreduce_sizes.split(",") if s]
+    if world == 1:
+        return [1 << 20, 64 << 20, 1 << 30]
+    out, b = [], args.allreduce_min_bytes
+    while b <= args.allreduce_max_bytes:
+        out.append(b)
+        b *= 2
+    return out
+
+
 def run_allreduce(args, dev, world, rank) -> dict:
-    """Real collective (RCCL at every N on GPUs): correctness, then a size sweep."""
+    """Real collective (RCCL at every N on GPUs): an exact-sum check per dtype,
+    then the size sweep, each size timed with an event pair around its
+    iterations (hipEvents on a GPU), slowest rank's time."""
     import torch
     import torch.distributed as dist
 
-    # correctness: every rank contributes rank+1; sum is exact in bf16 for n <= 8
-    probe = torch.full(((1 << 20) // 2,), float(rank + 1), device=dev, dtype=torch.bfloat16)
-    dist.all_reduce(probe)
-    _sync(dev)
-    want = world * (world + 1) / 2
-    bad = int((probe != want).sum().item())
-    if bad:
-        raise SystemExit(f"all-reduce check failed on rank {rank}: {bad} elements != {want}")
-
-    sizes_mib = [int(s) for s in args.allreduce_sizes.split(",") if s]
+    dtypes = {"bf16": torch.bfloat16, "fp32": torch.float32}
+    names = [d for d in args.allreduce_dtypes.split(",") if d]
+    sizes = allreduce_sizes(args, world)
+    timer = _Timer(dev)
     sweep = []
-    for mib in sizes_mib:
-        nbytes = mib << 20
-        buf = torch.ones(nbytes // 2, device=dev, dtype=torch.bfloat16)
-        iters = max(3, min(20, (2048 // max(mib, 1))))
-        for _ in range(2):
-            dist.all_reduce(buf)
+    for name in names:
+        dt_ = dtypes[name]
+        esz = torch.tensor([], dtype=dt_).element_size()
+        # correctness: every rank contributes rank+1; the sum is exact in bf16 for n <= 8
+        probe = torch.full(((1 << 20) // esz,), float(rank + 1), device=dev, dtype=dt_)
+        dist.all_reduce(probe)
         _sync(dev)
-        _barrier(dev)
-        _sync(dev)
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            dist.all_reduce(buf)
-        _sync(dev)
-        dt = (time.perf_counter() - t0) / iters
-        dt = _max_over_ranks(dt, dev)
-        algbw = nbytes / dt / 1e9
-        busbw = algbw * 2 * (world - 1) / world
-        sweep.append({"bytes": nbytes, "ms": round(dt * 1e3, 4), "iters": iters,
-                      "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2)})
+        want = world * (world + 1) / 2
+        bad = int((probe != want).sum().item())
+        if bad:
+            raise SystemExit(f"{name} all-reduce check failed on rank {rank}: {bad} elements != {want}")
+        del probe
+        buf = torch.ones(max(sizes) // esz, device=dev, dtype=dt_)
+        for nbytes in sizes:
+            n = max(1, nbytes // esz)
+            x = buf[:n]
+            iters = max(3, min(50, (4 << 30) // max(nbytes, 1)))
+            for _ in range(2):
+                dist.all_reduce(x)
+            _sync(dev)
+            _barrier(dev)
+            _sync(dev)
+            mk = timer.marks(2)
+            timer.record(mk, 0)
+            for _ in range(iters):
+                dist.all_reduce(x)
+            timer.record(mk, 1)
+            dt = timer.elapsed_ms(mk)[0] / iters / 1e3
+            dt = _max_over_ranks(dt, dev)
+            algbw = n * esz / dt / 1e9
+            sweep.append({"bytes": n * esz, "dtype": name, "ms": round(dt * 1e3, 5), "iters": iters,
+                          # a 1-rank all-reduce moves nothing: no bandwidth to report
+                          "algbw_GBps": round(algbw, 2) if world > 1 else None,
+                          "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2)})
         del buf
-    head = next((s for s in sweep if s["bytes"] == args.allreduce_mib << 20), sweep[-1] if sweep else None)
+    head = next((s for s in sweep if s["bytes"] == args.allreduce_mib << 20 and s["dtype"] == names[0]),
+                sweep[-1] if sweep else None)
+    peak = {d: max((s["busbw_GBps"] for s in sweep if s["dtype"] == d), default=None) for d in names}
     return {
         "backend": dist.get_backend(),
         "rccl_ranks": dist.get_world_size(),
-        "dtype": "bf16", "op": "sum", "check": "exact (sum of rank+1)",
+        "dtypes": names, "op": "sum", "check": "exact (sum of rank+1) per dtype",
+        "timing": "event pair around the iterations of each size (hipEvents on GPUs), slowest rank",
         "bytes": head["bytes"] if head else None,
         "ms": head["ms"] if head else None,
         "algbw_GBps": head["algbw_GBps"] if head else None,
         "busbw_GBps": head["busbw_GBps"] if head else None,
+        "busbw_peak_GBps": peak if world > 1 else None,
         "sweep": sweep,
         "note": ("1-rank communicator: RCCL completes an in-place all-reduce without moving "
-                 "data, so algbw here is not a bandwidth; busbw is 0 by definition")
+                 "data, so there is no algbw (null) and busbw is 0 by definition")
         if world == 1 else None,
     }
 
@@ -432,8 +463,12 @@ def main(argv=None) -> int:
     p.add_argument("--mode", choices=["validator", "ddp"], default="validator")
     p.add_argument("--size", type=int, default=8192, help="GEMM M=N=K (validator mode)")
     p.add_argument("--allreduce-mib", type=int, default=256, help="headline all-reduce size")
-    p.add_argument("--allreduce-sizes", default="1,4,16,64,256,1024",
-                   help="all-reduce sweep sizes in MiB (comma list)")
+    p.add_argument("--allreduce-sizes", default="",
+                   help="all-reduce sweep sizes in MiB (comma list); default: the protocol's "
+                        "8 B - 8 GiB x2 sweep at n > 1")
+    p.add_argument("--allreduce-min-bytes", type=int, default=8)
+    p.add_argument("--allreduce-max-bytes", type=int, default=8 << 30)
+    p.add_argument("--allreduce-dtypes", default="bf16,fp32")
     p.add_argument("--ab-rounds", type=int, default=12, help="A/B-interleaved hipBLASLt rounds")
     p.add_argument("--ab-sizes", default="4096,16384",
                    help="other square sizes A/B'd against hipBLASLt for context (not the metric)")

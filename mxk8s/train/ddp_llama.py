@@ -149,9 +149,12 @@ def run_ddp_bench(args) -> dict:
     sync()
     t0 = time.perf_counter()
     losses = []
-    for i in range(args.steps):
-        losses.append(train_step(model, ddp, opt, batches[i % nbatches]))
-    sync()
+    # "bench.timed" bounds the steady-state steps on a rocprofv3 marker trace:
+    # scripts/kernel_breakdown.py --trace keeps only the kernels inside it
+    with roctx.range("bench.timed"):
+        for i in range(args.steps):
+            losses.append(train_step(model, ddp, opt, batches[i % nbatches]))
+        sync()
     mxdist.barrier()
     sync()
     dt = time.perf_counter() - t0

@@ -41,10 +41,15 @@ def _check_contract(out, n):
     assert gc["elements"] == 256 * 256
     assert gc["max_abs_err_first"] <= gc["tolerance"] and gc["max_abs_err_after_timed"] <= gc["tolerance"]
     ar = out["allreduce"]
-    assert ar["rccl_ranks"] == n and ar["op"] == "sum"
-    assert [s["bytes"] for s in ar["sweep"]] == [1 << 20, 2 << 20]
+    assert ar["rccl_ranks"] == n and ar["op"] == "sum" and ar["dtypes"] == ["bf16", "fp32"]
+    assert [(s["bytes"], s["dtype"]) for s in ar["sweep"]] == \
+        [(1 << 20, "bf16"), (2 << 20, "bf16"), (1 << 20, "fp32"), (2 << 20, "fp32")]
     for s in ar["sweep"]:
-        assert s["busbw_GBps"] == pytest.approx(s["algbw_GBps"] * 2 * (n - 1) / n, rel=0.02, abs=0.011)
+        if n == 1:      # no meaningless "bandwidth" at n = 1
+            assert s["algbw_GBps"] is None and s["busbw_GBps"] == 0.0
+        else:
+            assert s["busbw_GBps"] == pytest.approx(s["algbw_GBps"] * 2 * (n - 1) / n, rel=0.02,
+                                                    abs=0.011)
     assert out["hipblaslt_ab"]["launches_each"] == 2 * 20
     assert [x["M"] for x in out["ab_other_sizes"]] == [128] and out["ab_other_sizes"][0]["check_ok"]
 
@@ -52,7 +57,21 @@ def _check_contract(out, n):
 def test_bench_single_rank_contract():
     out = _run_bench()
     _check_contract(out, 1)
-    assert out["allreduce"]["busbw_GBps"] == 0.0
+    assert out["allreduce"]["busbw_GBps"] == 0.0 and out["allreduce"]["algbw_GBps"] is None
+    assert out["allreduce"]["busbw_peak_GBps"] is None
+
+
+def test_protocol_allreduce_sizes():
+    """Default sweep at n > 1: 8 B - 8 GiB in x2 steps (BASELINE.md protocol)."""
+    sys.path.insert(0, REPO)
+    import argparse
+
+    import bench
+    a = argparse.Namespace(allreduce_sizes="", allreduce_min_bytes=8, allreduce_max_bytes=8 << 30)
+    sizes = bench.allreduce_sizes(a, 8)
+    assert sizes[0] == 8 and sizes[-1] == 8 << 30 and len(sizes) == 31
+    assert all(b == 2 * a_ for a_, b in zip(sizes, sizes[1:]))
+    assert len(bench.allreduce_sizes(a, 1)) == 3
 
 
 def test_bench_self_relaunch_four_ranks():
