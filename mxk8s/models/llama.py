@@ -25,7 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.attention import flash_attention, supported as flash_supported
-from ..ops.linear import Linear, SwiGLULinear
+from ..ops.linear import Linear, SwiGLULinear, swiglu_mlp
 from ..ops.xent import cross_entropy
 from ..ops.fused import add_rmsnorm, qkv_rope, rmsnorm, rope_tables
 
@@ -113,6 +113,10 @@ class MLP(nn.Module):
         self.w2 = SwiGLULinear(cfg.ffn_dim, cfg.dim)
 
     def forward(self, x):
+        if x.is_cuda and x.dtype == torch.bfloat16:
+            # one node: up-projection with SwiGLU in its epilogue, down
+            # projection, fused dgrad-SwiGLU backward (mxk8s.ops.linear)
+            return swiglu_mlp(x, self.w13.weight, self.w2.weight)
         return self.w2(self.w13(x))
 
 

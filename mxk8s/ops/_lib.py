@@ -38,6 +38,7 @@ _SIGNATURES = {
                                  ctypes.POINTER(ctypes.c_int), _vp]),
     "mxk_gemm_bf16_split_workspace": (_l, []),
     "mxk_gemm_bf16_dgrad_swiglu": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "mxk_gemm_bf16_w13_swiglu": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_tn_variant": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_tn_num_variants": (_i, []),
     "mxk_gemm_bf16_tn_is_ablation": (_i, [_i]),

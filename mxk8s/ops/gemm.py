@@ -17,8 +17,9 @@ from . import _lib
 
 # Split tail (mxk_gemm_bf16_ex_ws): an output whose 256^2 tiles leave the
 # last round of the CUs at most half full (the Llama-3-8B wqkv / w2 weight
-# gradients: 384 / 896 tiles on 256 CUs) runs its tail tiles as two K halves
-# each; MXK_SPLIT_TAIL=0 turns it off (A/B).
+# gradients: 384 / 896 tiles on 256 CUs; the wo forward at micro-batch 1:
+# 128 tiles) runs its tail tiles as two K halves each, for every operand
+# layout including the forward's TN; MXK_SPLIT_TAIL=0 turns it off (A/B).
 _USE_SPLIT_TAIL = os.environ.get("MXK_SPLIT_TAIL", "1") != "0"
 _split_ws: dict = {}
 
@@ -99,7 +100,7 @@ def gemm_bf16_ex(a: torch.Tensor, b: torch.Tensor, a_kmajor: bool, b_kmajor: boo
     N, K2 = (b.shape if b_kmajor else (b.shape[1], b.shape[0]))
     if K != K2 or tuple(out.shape) != (M, N) or not is_fast_shape(M, N, K):
         return False
-    if variant == 1 and _USE_SPLIT_TAIL and not (a_kmajor and b_kmajor):
+    if variant == 1 and _USE_SPLIT_TAIL:
         ws = _split_workspace(a.device)
         split = ctypes.c_int(0)
         st = _lib.lib().mxk_gemm_bf16_ex_ws(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K,

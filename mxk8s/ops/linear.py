@@ -30,28 +30,23 @@ _USE_MXK_WGRAD = os.environ.get("MXK_WGRAD", "1") != "0"
 _USE_MXK_DGRAD = os.environ.get("MXK_DGRAD", "1") != "0"
 
 
-# y = x W^T (both operands K-major) on the hand-written TN kernel instead of
-# hipBLASLt; off by default: hipBLASLt's tuned picks are 1-2 % faster on the
-# Llama-3-8B forward shapes in isolation (profiles/r1_gemm_w4h/gemm_fwd_shapes.log)
-# and the whole step runs 25.5k vs 26.0k tok/s with MXK_FWD=1
-# (profiles/r1_swiglu/fwd_*.log).
-_USE_MXK_FWD = os.environ.get("MXK_FWD", "0") != "0"
-
-
+# y = x W^T (both operands K-major) runs on the hand-written TN kernel (the
+# validator's GEMM, gemm_bf16.hip) with the split tail when the last round of
+# tiles is at most half full; no library GEMM in the training step.  Shapes
+# that do not tile (M, N % 256, K % 64; tests, toy models) take the kernel's
+# bounds-checked MFMA path; CPU tensors the PyTorch reference.
 def _fwd(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    if _USE_MXK_FWD and x.is_cuda and x.is_contiguous() and weight.is_contiguous():
-        x2 = x.reshape(-1, x.shape[-1])
-        out = torch.empty((x2.shape[0], weight.shape[0]), device=x.device, dtype=x.dtype)
-        if not _tail_heavy(*out.shape) and gemm_bf16_ex(x2, weight, True, True, out):
-            return out.view(*x.shape[:-1], weight.shape[0])
-    return torch.matmul(x, weight.t())
-
-
-def _tail_heavy(M: int, N: int, cus: int = 256) -> bool:
-    """Few 256x256 tiles with a half-empty last round (e.g. 384 tiles on 256
-    CUs): hipBLASLt's stream-K kernels balance that tail, ours do not."""
-    tiles = (M // 256) * (N // 256)
-    return tiles < 2 * cus and 0 < tiles % cus <= cus // 2
+    if not x.is_cuda or x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
+        return torch.matmul(x, weight.t())
+    x2 = x.reshape(-1, x.shape[-1])
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    out = torch.empty((x2.shape[0], weight.shape[0]), device=x.device, dtype=x.dtype)
+    w = weight if weight.is_contiguous() else weight.contiguous()
+    if not gemm_bf16_ex(x2, w, True, True, out):
+        from .gemm import gemm_bf16_tn
+        gemm_bf16_tn(x2, w, out)          # bounds-checked MFMA kernel (any shape)
+    return out.view(*x.shape[:-1], weight.shape[0])
 
 
 def _wgrad_into(sink: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
@@ -148,6 +143,73 @@ class _SwiGLULinearFn(torch.autograd.Function):
         dgu = _dgrad_swiglu(dy, weight, gu) if ctx.needs_input_grad[0] else None
         dw = _weight_grad(weight, dy, h) if ctx.needs_input_grad[1] else None
         return dgu, dw
+
+
+# gu = x W13^T and h = silu(g) * u in ONE launch (mxk_gemm_bf16_w13_swiglu:
+# the activation runs in the GEMM's epilogue from the fp32 accumulators, the
+# separate element-wise pass over gu disappears).  MXK_FUSED_W13=0 runs the
+# GEMM and mxk_swiglu_fwd separately.
+_USE_FUSED_W13 = os.environ.get("MXK_FUSED_W13", "1") != "0"
+
+
+def w13_swiglu(x2: torch.Tensor, w13: torch.Tensor):
+    """(gu, h) of the MLP up-projection, or None when the fused kernel does not
+    take the shape (M % 256, F % 128, K % 64, aligned, bf16 GPU tensors)."""
+    from . import _lib
+    if not (_USE_FUSED_W13 and x2.is_cuda and x2.dtype == torch.bfloat16 and
+            w13.dtype == torch.bfloat16 and x2.is_contiguous() and w13.is_contiguous()):
+        return None
+    M, K = x2.shape
+    F = w13.shape[0] // 2
+    gu = torch.empty((M, 2 * F), device=x2.device, dtype=x2.dtype)
+    h = torch.empty((M, F), device=x2.device, dtype=x2.dtype)
+    st = _lib.lib().mxk_gemm_bf16_w13_swiglu(x2.data_ptr(), w13.data_ptr(), gu.data_ptr(),
+                                             h.data_ptr(), M, F, K, x2.stride(0), w13.stride(0),
+                                             gu.stride(0), h.stride(0), _lib.stream_ptr(x2.device))
+    if st == 1:      # hipErrorInvalidValue: shape / alignment not taken
+        return None
+    _lib.check(st, "mxk_gemm_bf16_w13_swiglu")
+    return gu, h
+
+
+class _SwiGLUMLPFn(torch.autograd.Function):
+    """y = swiglu(x W13^T) W2^T as one autograd node: fused up-projection +
+    activation forward, fused dgrad-SwiGLU backward; both weight gradients go
+    straight into the flat gradient buffer (W2's first, as autograd would
+    order the two nodes)."""
+
+    @staticmethod
+    def forward(ctx, x, w13, w2):
+        from .fused import swiglu_fwd
+        x2 = x.reshape(-1, x.shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        r = w13_swiglu(x2, w13)
+        if r is None:
+            gu = _fwd(x2, w13)
+            h = swiglu_fwd(gu)
+        else:
+            gu, h = r
+        ctx.save_for_backward(x2, gu, h, w13, w2)
+        ctx.xshape = x.shape
+        return _fwd(h, w2).view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gu, h, w13, w2 = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        need_x, need_w13, need_w2 = ctx.needs_input_grad
+        dgu = _dgrad_swiglu(dy2, w2, gu) if (need_x or need_w13) else None
+        dw2 = _weight_grad(w2, dy2, h) if need_w2 else None
+        dx = _dgrad(dgu, w13).view(ctx.xshape) if need_x else None
+        dw13 = _weight_grad(w13, dgu, x2) if need_w13 else None
+        return dx, dw13, dw2
+
+
+def swiglu_mlp(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
+    return _SwiGLUMLPFn.apply(x, w13, w2)
 
 
 class Linear(nn.Linear):

@@ -225,13 +225,17 @@ using mxk::SchedTwoBarrier;
 
 // Table-driven K-tile: S gives, per MFMA index m, the fragment reads, DMA
 // pieces, waits and barriers that follow MFMA m (see w4i_ktile for MODE).
-template <class S, int PAR, int MODE, int ORDER = 0, int PRIO = 0>
+// SPLITA: A fragments 0-3 at a_base, 4-7 at a_hi (the w13 SwiGLU kernel
+// rotates one wave's row blocks by 4); otherwise a_hi is unused.
+template <class S, int PAR, int MODE, int ORDER = 0, int PRIO = 0, bool SPLITA = false>
 __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                           bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                           bf16x8_t (&f1b)[8], char* smem, int a_base, int b_base,
                                           int off_k0, int off_k1, const DmaK& dma_a,
-                                          const DmaK& dma_b, int kb2, int wave_s, int par = 0) {
+                                          const DmaK& dma_b, int kb2, int wave_s, int par = 0,
+                                          int a_hi = 0) {
   constexpr int SUB = 2048;
+  auto aoff = [&](int r) { return SPLITA && r >= 4 ? a_hi + (r - 4) * SUB : a_base + r * SUB; };
   const int px = PAR == 2 ? par : PAR;
   char* X = smem + px * W4B_STAGE_BYTES;
   char* Y = smem + (px ^ 1) * W4B_STAGE_BYTES;
@@ -247,7 +251,7 @@ __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
         const int i = ORDER ? q : o, j = ORDER ? o : q;
         if (h == 0) mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
         else mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
-        if (S::a1(m) >= 0) f1a[S::a1(m)] = lds_read_b128(X + a_base + S::a1(m) * SUB + off_k1);
+        if (S::a1(m) >= 0) f1a[S::a1(m)] = lds_read_b128(X + aoff(S::a1(m)) + off_k1);
         if (MODE == 1 && m == S::W1) __builtin_amdgcn_s_waitcnt(0xC07F);
         if (MODE == 1 && m == S::B1) __builtin_amdgcn_s_barrier();
         if (MODE == 1 && S::adma(m) >= 0) dma_a.issue(X, S::adma(m), kb2, wave_s);
@@ -264,7 +268,7 @@ __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
         if (MODE != 3 && S::k0(m) >= 0) {
           const int r = S::k0(m);
           if (r < 8) f0b[r] = lds_read_b128(Y + b_base + r * SUB + off_k0);
-          else f0a[r - 8] = lds_read_b128(Y + a_base + (r - 8) * SUB + off_k0);
+          else f0a[r - 8] = lds_read_b128(Y + aoff(r - 8) + off_k0);
         }
       }
     }
@@ -693,6 +697,155 @@ mxk_gemm_bf16_tn_pp8(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// MLP up-projection with the SwiGLU activation in its epilogue:
+//   gu[M][2F] = x[M][K] . W13[2F][K]^T   (W13 = [gate | up] rows, as stored)
+//   h[M][F]   = silu(gu[:, :F]) * gu[:, F:]   (from the fp32 accumulators)
+// The separate element-wise pass (read gu, write h: 1.4 GB per Llama-3-8B
+// layer at micro-batch 8) disappears; gu is still written (the backward's
+// fused dgrad-SwiGLU epilogue reads it).  A 256-column tile is 128 gate
+// columns [g0, g0+128) and the MATCHING 128 up columns [F+g0, F+g0+128): the
+// B panel's pieces 4..7 (tile rows 128-255) read W13 rows F-128 further down,
+// so waves wn = 0 hold g and waves wn = 1 hold u of the same (row, column)
+// in the same lane/register positions.  Epilogue: both store their half of
+// gu (LDS-staged, whole lines); then each pair exchanges half its rows
+// through LDS (the gate wave keeps rows 0-63 and takes u of them, the up wave
+// takes g of rows 64-127) and each computes and stores h of 64 rows.
+// Same K loop as the default schedule (hipBLASLt's instruction positions).
+template <int PAR, int MODE>
+__device__ __forceinline__ void w13_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
+                                          bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
+                                          bf16x8_t (&f1b)[8], char* smem, int a_lo, int a_hi,
+                                          int b_base, int off_k0, int off_k1, const DmaK& dma_a,
+                                          const DmaK& dma_b, int kb2, int wave_s, int par = 0) {
+  w4j_ktile<SchedHB, PAR, MODE, 0, 0, true>(acc, f0a, f0b, f1a, f1b, smem, a_lo, b_base, off_k0,
+                                            off_k1, dma_a, dma_b, kb2, wave_s, par, a_hi);
+}
+
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_w13_swiglu(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W13,
+                         uint16_t* __restrict__ GU, uint16_t* __restrict__ H, int M, int F, int K,
+                         int ldx, int ldw, int ldgu, int ldh) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;               // 0: gate columns, 1: up columns
+  int m0, n0v;
+  w4b_tile<1>(blockIdx.x, gridDim.x, M / BM, F / 128, &m0, &n0v);
+  const int g0 = n0v >> 1;                 // first gate column of the tile
+  const DmaK dma_a = make_dmak(X, ldx, m0, lane, wave_s);
+  DmaK dma_b = make_dmak(W13, ldw, g0, lane, wave_s);
+  // tile rows 128..255 of the B panel are the up rows F + g0 ..: pieces 4..7
+  dma_b.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(W13 + static_cast<size_t>(g0) * ldw),
+                                                 0, (F + 128) * ldw * 2, 0x00020000);
+#pragma unroll
+  for (int p = 4; p < 8; ++p) dma_b.voff[p] += static_cast<uint32_t>((F - 128) * ldw * 2);
+
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  // the up waves accumulate their row blocks rotated by 4 (acc[i] = rows
+  // 16 ((i + 4) & 7)): then every wave hands acc[4..7] to its partner and
+  // keeps acc[0..3], one code path for both roles
+  const int a_lo = (wm * 8 + (wn ? 4 : 0)) * SUB;
+  const int a_hi = (wm * 8 + (wn ? 0 : 4)) * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / BK;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_OP_BYTES, p, 0, wave_s);
+  if (ns > 1) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_a.issue(smem + W4B_STAGE_BYTES, p, BK * 2, wave_s);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_STAGE_BYTES + W4B_OP_BYTES, p, BK * 2, wave_s);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    f0a[i] = lds_read_b128(smem + (i < 4 ? a_lo + i * SUB : a_hi + (i - 4) * SUB) + off_k0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+
+  int s = 0;
+  int kb = 2 * BK * 2;
+  for (; s + 2 <= ns - 2; s += 2) {
+    w13_ktile<0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
+                    kb, wave_s);
+    w13_ktile<1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
+                    kb + BK * 2, wave_s);
+    kb += 2 * BK * 2;
+  }
+  if (s < ns - 2) {
+    w13_ktile<0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
+                    kb, wave_s);
+    ++s;
+  }
+  if (ns >= 2) {
+    w13_ktile<2, 2>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
+                    0, wave_s, s & 1);
+    ++s;
+  }
+  w13_ktile<2, 3>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b, 0,
+                  wave_s, s & 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  mxk::mfma_drain(acc);
+
+  // 1. gu: each wave its half (gate -> columns g0.., up -> F + g0..), its two
+  //    64-row passes swapped back for the rotated up waves
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  mxk::store_block_lds<false>(acc, GU, ldgu, m0 + wm * 128, (wn ? F : 0) + g0, lane,
+                              smem + wave_s * mxk::kStoreLdsWave, wn);
+  __builtin_amdgcn_s_barrier();            // every staging slice is free again
+  // 2. hand acc[4..7] to the partner (gate: g of rows 64-127, up: u of rows
+  //    0-63) through region (wm, wn); take the partner's from (wm, wn ^ 1)
+  char* mine_out = smem + (wm * 2 + wn) * 32768 + lane * 16;
+  const char* theirs = smem + (wm * 2 + (wn ^ 1)) * 32768 + lane * 16;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      *reinterpret_cast<f32x4_t*>(mine_out + (i * 8 + j) * 1024) = acc[4 + i][j];
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  const bool up = wn != 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4_t o = *reinterpret_cast<const f32x4_t*>(theirs + (i * 8 + j) * 1024);
+      f32x4_t hv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g = up ? o[e] : acc[i][j][e], u = up ? acc[i][j][e] : o[e];
+        hv[e] = g * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(g * -1.44269504f)) * u;
+      }
+      acc[i][j] = hv;
+    }
+  // 3. h of the kept 64 rows (gate wave: rows 0-63 of its block, up: 64-127)
+  mxk::store_block_wide<false, 4, 8>(reinterpret_cast<const f32x4_t(&)[4][8]>(acc[0]), H, ldh,
+                                     m0 + wm * 128 + (wn ? 64 : 0), g0, lane);
+}
+
+// ---------------------------------------------------------------------------
 // Generic bounds-checked MFMA GEMM (any M, N, K; K-contiguous operands).
 // 64x64 tile, 256 threads (2x2 waves of 32x32), register-staged through LDS.
 // Used for shapes the 256x256 kernel does not tile exactly.
@@ -900,6 +1053,24 @@ MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int 
                        static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
                        static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
   }
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// gu = x . W13^T and h = silu(gu[:, :F]) * gu[:, F:] in one launch (see the
+// kernel).  M % 256, F % 128, K % 64, 16-B aligned operands, ld* % 8.
+MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, void* h, int M,
+                                     int F, int K, int ldx, int ldw, int ldgu, int ldh,
+                                     hipStream_t stream) {
+  auto al = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  if (M <= 0 || F <= 0 || K <= 0 || M % BM || F % 128 || K % BK || ldx % 8 || ldw % 8 ||
+      ldgu % 8 || ldh % 8 || !al(x) || !al(w13) || !al(gu) || !al(h) ||
+      static_cast<long>(F + 128) * ldw * 2 >= (1L << 31))
+    return static_cast<int>(hipErrorInvalidValue);
+  const int nwg = (M / BM) * (F / 128);
+  hipLaunchKernelGGL(mxk_gemm_bf16_w13_swiglu, dim3(nwg), dim3(W4_THREADS), 0, stream,
+                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
+                     static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu,
+                     ldh);
   MXK_RETURN_LAUNCH_STATUS();
 }
 

@@ -730,7 +730,7 @@ MXK_API int mxk_gemm_bf16_ex_ws(const void* A, const void* B, void* C, int M, in
   const int cus = device_cus();
   const long nwg = M > 0 && N > 0 ? static_cast<long>(M / XBM) * (N / XBM) : 0;
   const int tail = nwg > 0 ? static_cast<int>(nwg % cus) : 0;
-  const bool want = !(a_kmajor && b_kmajor) && tail > 0 && 2 * tail <= cus && K % (2 * XBK) == 0 &&
+  const bool want = tail > 0 && 2 * tail <= cus && K % (2 * XBK) == 0 &&
                     K >= 16 * XBK && ws != nullptr &&
                     ws_bytes >= static_cast<long>(2 * tail) * XBM * XBM * 4 &&
                     reinterpret_cast<uintptr_t>(ws) % 16 == 0;
@@ -752,7 +752,9 @@ MXK_API int mxk_gemm_bf16_ex_ws(const void* A, const void* B, void* C, int M, in
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);
   auto w = static_cast<float*>(ws);
-  if (a_kmajor)
+  if (a_kmajor && b_kmajor)   // forward y = x W^T: the TN tail
+    launch_split<false, false>(sched, wide, nwg, q_full, stream, a, b, c, M, N, K, lda, ldb, ldc, w);
+  else if (a_kmajor)
     launch_split<false, true>(sched, wide, nwg, q_full, stream, a, b, c, M, N, K, lda, ldb, ldc, w);
   else if (b_kmajor)
     launch_split<true, false>(sched, wide, nwg, q_full, stream, a, b, c, M, N, K, lda, ldb, ldc, w);

@@ -226,9 +226,12 @@ __device__ __forceinline__ void store_block_narrow(const f32x4_t (&acc)[8][8], u
 // slices overlap the GEMM's stages).  lds: 64 x 272 B per wave.
 constexpr int kStoreLdsRow = 272;
 constexpr int kStoreLdsWave = 64 * kStoreLdsRow;
+// rot 1: acc[4p..4p+3] hold rows 64 (p ^ 1) .. (the w13 SwiGLU kernel's
+// rotated up waves); the two passes then write each other's rows.
 template <bool NT = true>
 __device__ __forceinline__ void store_block_lds(const f32x4_t (&acc)[8][8], uint16_t* C, int ldc,
-                                                int row0, int col0, int lane, char* lds) {
+                                                int row0, int col0, int lane, char* lds,
+                                                int rot = 0) {
   const int crow = lane & 15, q = lane >> 4;
   const int rr = lane >> 4, cc = (lane & 15) * 8;
 #pragma unroll
@@ -246,7 +249,7 @@ __device__ __forceinline__ void store_block_lds(const f32x4_t (&acc)[8][8], uint
     for (int it = 0; it < 16; ++it) {
       const int r = it * 4 + rr;
       const u32x4_t v = *reinterpret_cast<const u32x4_t*>(lds + r * kStoreLdsRow + cc * 2);
-      uint16_t* cp = C + static_cast<size_t>(row0 + p * 64 + r) * ldc + col0 + cc;
+      uint16_t* cp = C + static_cast<size_t>(row0 + (p ^ rot) * 64 + r) * ldc + col0 + cc;
       if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(cp));
       else *reinterpret_cast<u32x4_t*>(cp) = v;
     }
