@@ -2,6 +2,9 @@
 #
 #   make            build every native artefact in-tree
 #   make kernels    HIP kernel library  mxk8s/_lib/libmxkernels.so
+#   make gemm-exp   the same library with every A/B GEMM schedule
+#                   (-DMXK_GEMM_EXPERIMENTS) -> mxk8s/_lib/libmxkernels_exp.so,
+#                   selected with MXK_KERNELS_LIB (python -m mxk8s.validate.gemm)
 #   make node       C++ node library    mxk8s/_lib/libmxnode.so (+ CLIs in bin/)
 #   make tools      validator binaries  bin/mx-vector-add bin/mx-gemm-bench bin/mx-allreduce-perf
 #   make test-native  host unit tests of libmxnode (ASan+UBSan build)
@@ -24,16 +27,17 @@ LDLIBS_NODE := -ldl -lpthread
 
 KERNEL_SRCS := native/kernels/gemm_bf16.hip native/kernels/vector_add.hip \
                native/kernels/fused_ops.hip native/kernels/optim.hip native/kernels/attention.hip \
-               native/kernels/gemm_bf16_layouts.hip native/kernels/xent.hip \
-               native/kernels/gemm_bf16_ring.hip
+               native/kernels/gemm_bf16_layouts.hip native/kernels/xent.hip
 KERNEL_OBJS := $(patsubst native/kernels/%.hip,$(BUILD)/kernels/%.o,$(KERNEL_SRCS))
+EXP_SRCS    := $(KERNEL_SRCS) native/kernels/gemm_bf16_ring.hip
+EXP_OBJS    := $(patsubst native/kernels/%.hip,$(BUILD)/exp/%.o,$(EXP_SRCS))
 KERNEL_HDRS := $(wildcard native/kernels/*.h)
 
 NODE_SRCS := $(wildcard native/libmxnode/*.cc)
 NODE_OBJS := $(patsubst native/libmxnode/%.cc,$(BUILD)/node/%.o,$(NODE_SRCS))
 NODE_HDRS := $(wildcard native/libmxnode/*.h)
 
-.PHONY: all kernels node tools clean test-native test-native-tsan fake-amdsmi
+.PHONY: all kernels gemm-exp node tools clean test-native test-native-tsan fake-amdsmi
 all: kernels node tools fake-amdsmi
 
 kernels: $(OUT_LIB)/libmxkernels.so
@@ -43,6 +47,16 @@ $(BUILD)/kernels/%.o: native/kernels/%.hip $(KERNEL_HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OUT_LIB)/libmxkernels.so: $(KERNEL_OBJS)
+	@mkdir -p $(OUT_LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+gemm-exp: $(OUT_LIB)/libmxkernels_exp.so
+
+$(BUILD)/exp/%.o: native/kernels/%.hip $(KERNEL_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DMXK_GEMM_EXPERIMENTS -c $< -o $@
+
+$(OUT_LIB)/libmxkernels_exp.so: $(EXP_OBJS)
 	@mkdir -p $(OUT_LIB)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
@@ -80,7 +94,7 @@ $(OUT_BIN)/mx-vector-add: $(BUILD)/tools/vector_add_main.o $(BUILD)/kernels/vect
 	@mkdir -p $(OUT_BIN)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^
 
-$(OUT_BIN)/mx-gemm-bench: $(BUILD)/tools/gemm_bench_main.o $(BUILD)/kernels/gemm_bf16.o $(BUILD)/kernels/gemm_bf16_layouts.o $(BUILD)/kernels/gemm_bf16_ring.o
+$(OUT_BIN)/mx-gemm-bench: $(BUILD)/tools/gemm_bench_main.o $(BUILD)/kernels/gemm_bf16.o $(BUILD)/kernels/gemm_bf16_layouts.o
 	@mkdir -p $(OUT_BIN)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrocblas -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
 

@@ -11,6 +11,11 @@ interleaved (cdna_hip_programming.md §5.4 rule 24) when --variants is given.
 
     python -m mxk8s.validate.gemm --sizes 4096,8192,16384 [--variants all]
 
+The production library carries the shipped schedules only; the A/B records
+(schedules measured neutral or negative, the no-store ablation) are in
+``make gemm-exp``'s libmxkernels_exp.so, selected with
+``MXK_KERNELS_LIB=mxk8s/_lib/libmxkernels_exp.so``.
+
 Prints one ``RESULT {json}`` line per (size, kernel).
 """
 from __future__ import annotations
@@ -124,13 +129,19 @@ def main(argv=None) -> int:
     a = p.parse_args(argv)
     if a.device is not None:
         torch.cuda.set_device(a.device)
-    nv = _lib.lib().mxk_gemm_bf16_tn_num_variants()
+    L = _lib.lib()
+    nv = L.mxk_gemm_bf16_tn_num_variants()
     if a.variants == "all":
-        variants = list(range(nv))
+        variants = [v for v in range(nv) if L.mxk_gemm_bf16_tn_variant_built(v)]
     elif a.variants:
         variants = [int(x) for x in a.variants.split(",")]
     else:
         variants = []
+    missing = [v for v in variants if not L.mxk_gemm_bf16_tn_variant_built(v)]
+    if missing:
+        raise SystemExit(f"schedules {missing} are A/B records, not in {_lib.KERNEL_LIB_PATH}: "
+                         "`make gemm-exp` and run with "
+                         "MXK_KERNELS_LIB=mxk8s/_lib/libmxkernels_exp.so")
     sizes = [int(x) for x in a.sizes.split(",")] if a.sizes else []
     sizes += [tuple(int(v) for v in x.split("x")) for x in a.shapes.split(",") if x]
     run(sizes, variants, a.iters, a.warmup_s, a.rounds,

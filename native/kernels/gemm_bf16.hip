@@ -32,7 +32,9 @@
 //    panels chip-wide (Infinity Cache reuse).
 //
 // Schedules (mxk_gemm_bf16_tn_variant, A/B-timed by python -m
-// mxk8s.validate.gemm --variants all):
+// mxk8s.validate.gemm --variants all).  The production library builds 0, 1,
+// 6, 9 and 26; the others are A/B records, compiled only into `make
+// gemm-exp`'s libmxkernels_exp.so (-DMXK_GEMM_EXPERIMENTS):
 //   0 w4i   super-block map, non-temporal widened stores, late barrier #3
 //   1 w4i   8-byte stores (C not 16-B aligned or ldc % 8 != 0)
 //   2 w4i   widened plain stores, barrier #3 after m 91
@@ -63,6 +65,13 @@
 //           back row-major so every store covers whole lines (4 rows x 256 B
 //           per wave-instruction instead of 16 x 64 B): +1.3 / +3.0 / +0.4 %
 //           over 6 at 8192^3 / 4096^3 / 16384^3 (profiles/r2_gemm_ab/)
+//  27 w4j   26 with ONE barrier per K-tile (SchedOneBarrier), 28 the same
+//           with the DMA spread: -5 / -1 % at 8192^3, -6 / -10 % at 16384^3
+//           (profiles/r3_gemm/)
+//  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
+//           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
+//           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
+//           line is fetched twice; profiles/r3_gemm/)
 // The earlier schedules (one-barrier w4b, 8-wave, 4-deep ring, w4h, ...)
 // were retired when an ISA audit (tests/test_isa_hazards.py) found their
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
@@ -958,6 +967,13 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
   switch (v) {
     case 0: launch_w4i<1, 2, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 1: launch_w4i<1, 0, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 6: launch_w4i<1, 2, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 9:
+      // the layout kernel (gemm_bf16_layouts.hip) on K-major operands
+      mxk_gemm_bf16_ex_variant(A, Bt, C, M, N, K, lda, ldb, ldc, 1, 1, 2, stream);
+      break;
+    case 26: launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+#ifdef MXK_GEMM_EXPERIMENTS
     case 2: launch_w4i<1, 1, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 3: launch_w4i<1, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 4: launch_w4i<1, 1, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
@@ -967,13 +983,8 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
                          b, c, M, N, K, lda, ldb, ldc);
       break;
     }
-    case 6: launch_w4i<1, 2, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 7: launch_w4i<1, 2, 1, 0, 2>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 8: launch_w4i<1, 1, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 9:
-      // the layout kernel (gemm_bf16_layouts.hip) on K-major operands
-      mxk_gemm_bf16_ex_variant(A, Bt, C, M, N, K, lda, ldb, ldc, 1, 1, 2, stream);
-      break;
     case 10: launch_w4i<1, 3, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 13: launch_w4i<1, 2, 1, 0, 3>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 14: launch_w4i<1, 2, 1, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
@@ -986,7 +997,6 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 23: launch_w4i<1, 2, 1, 0, 1, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 24: launch_w4i<1, 2, 1, 0, 1, 0, 8>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 25: launch_w4i<1, 1, 1, 0, 1, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 26: launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 27: launch_w4i<1, 4, 1, 0, 7>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 28: launch_w4i<1, 4, 1, 0, 8>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 29: mxk_gemm_bf16_tn_ring_launch(4, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
@@ -1010,7 +1020,20 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
                            a, b, c, M, N, K, lda, ldb, ldc);
       break;
     }
+#endif
   }
+}
+
+// Production builds carry the default (26), its base schedule (6), the
+// first structure (0), the 8-byte-store fallback (1) and the layout kernel
+// (9); every other schedule is an A/B record, built only with
+// -DMXK_GEMM_EXPERIMENTS (`make gemm-exp` -> libmxkernels_exp.so).
+bool variant_built(int v) {
+#ifdef MXK_GEMM_EXPERIMENTS
+  return v >= 0 && v < kNumVariants;
+#else
+  return v == 0 || v == 1 || v == 6 || v == 9 || v == 26;
+#endif
 }
 
 // every schedule but 1 stores 16 B per lane: C 16-B aligned, ldc % 8 == 0
@@ -1025,6 +1048,7 @@ MXK_API int mxk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int
   if (M % BM || N % BN || K % BK || variant < 0 || variant >= kNumVariants ||
       (variant != kNarrowCVariant && !wide_c_ok(C, ldc)))
     return static_cast<int>(hipErrorInvalidValue);
+  if (!variant_built(variant)) return static_cast<int>(hipErrorNotSupported);
   launch_256(variant, (M / BM) * (N / BN), stream, A, Bt, C, M, N, K, lda, ldb, ldc);
   MXK_RETURN_LAUNCH_STATUS();
 }
@@ -1033,6 +1057,7 @@ MXK_API int mxk_gemm_bf16_tn_num_variants(void) { return kNumVariants; }
 MXK_API const char* mxk_gemm_bf16_tn_variant_name(int variant) {
   return variant >= 0 && variant < kNumVariants ? kVariantNames[variant] : nullptr;
 }
+MXK_API int mxk_gemm_bf16_tn_variant_built(int variant) { return variant_built(variant); }
 // Variant 10 is a timing ablation (no C store): never correctness-checked or used.
 MXK_API int mxk_gemm_bf16_tn_is_ablation(int variant) { return variant == 10; }
 

@@ -130,7 +130,12 @@ __device__ __forceinline__ void ring_step(f32x4_t (&acc)[8][8], const bf16x8_t (
   mfma_sources_done(ca, cb);
 }
 
-template <int R>
+// EXTRA = (K / 32 - 1) odd, chosen by the launcher: each instance has one
+// tail with fixed fragment registers.  (A runtime branch needs either two
+// tails, which spill, or a register copy of one set into the other right in
+// front of asm MFMAs, whose operand reads the hazard recognizer does not see:
+// acc[0][0] of every wave came out wrong, scripts/gpu/ring_diag.py.)
+template <int R, bool EXTRA>
 __global__ void __launch_bounds__(RTHREADS, 1)
 mxk_gemm_bf16_tn_ring(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                       uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -192,20 +197,15 @@ mxk_gemm_bf16_tn_ring(const uint16_t* __restrict__ A, const uint16_t* __restrict
                               db, wave, k1);
     slot = sl2;
   }
-  if (s < ns - 1) {   // one more step with a successor: its fragments land in set 1
+  if constexpr (EXTRA) {   // ns - 1 odd: one more step with a successor (into set 1)
     const int sl1 = next_slot(slot);
     const int k0 = (s + R < ns ? s + R : ns - 1) * RK * 2;
     ring_step<true, true, VM>(acc, fa0, fb0, fa1, fb1, smem + sl1, a_off, b_off, smem + slot, da,
                               db, wave, k0);
-    // one copy per tile keeps a single tail (set 0); the step ended with
-    // mfma_sources_done, so set 0's last MFMA reads are covered
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      fa0[i] = fa1[i];
-      fb0[i] = fb1[i];
-    }
+    ring_step<false, false, VM>(acc, fa1, fb1, fa0, fb0, smem, a_off, b_off, smem, da, db, wave, 0);
+  } else {
+    ring_step<false, false, VM>(acc, fa0, fb0, fa1, fb1, smem, a_off, b_off, smem, da, db, wave, 0);
   }
-  ring_step<false, false, VM>(acc, fa0, fb0, fa1, fb1, smem, a_off, b_off, smem, da, db, wave, 0);
   // every clamped refill has landed and every wave is past its last read
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -224,17 +224,20 @@ int mxk_gemm_bf16_tn_ring_launch(int slots, const void* A, const void* Bt, void*
   auto* a = static_cast<const uint16_t*>(A);
   auto* b = static_cast<const uint16_t*>(Bt);
   auto* c = static_cast<uint16_t*>(C);
-  switch (slots) {
-    case 4:
-      hipLaunchKernelGGL(mxk_gemm_bf16_tn_ring<4>, grid, dim3(RTHREADS), 0, stream, a, b, c, M, N,
-                         K, lda, ldb, ldc);
-      break;
-    case 5:
-      hipLaunchKernelGGL(mxk_gemm_bf16_tn_ring<5>, grid, dim3(RTHREADS), 0, stream, a, b, c, M, N,
-                         K, lda, ldb, ldc);
-      break;
-    default:
-      return static_cast<int>(hipErrorInvalidValue);
-  }
+  const bool extra = ((K / RK - 1) & 1) != 0;
+  if (slots == 4 && extra)
+    hipLaunchKernelGGL((mxk_gemm_bf16_tn_ring<4, true>), grid, dim3(RTHREADS), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc);
+  else if (slots == 4)
+    hipLaunchKernelGGL((mxk_gemm_bf16_tn_ring<4, false>), grid, dim3(RTHREADS), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc);
+  else if (slots == 5 && extra)
+    hipLaunchKernelGGL((mxk_gemm_bf16_tn_ring<5, true>), grid, dim3(RTHREADS), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc);
+  else if (slots == 5)
+    hipLaunchKernelGGL((mxk_gemm_bf16_tn_ring<5, false>), grid, dim3(RTHREADS), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc);
+  else
+    return static_cast<int>(hipErrorInvalidValue);
   return static_cast<int>(hipGetLastError());
 }

@@ -7,7 +7,8 @@ set -o pipefail
 OUT=${1:-gpurun_out/r3d}
 mkdir -p "$OUT"
 export PYTHONPATH=.
-timeout -k 10 150 python -u scripts/gpu/ring_check.py 26,29,30 > "$OUT/ring_check.log" 2>&1 && \
+EXP=mxk8s/_lib/libmxkernels_exp.so
+MXK_KERNELS_LIB=$EXP timeout -k 10 150 python -u scripts/gpu/ring_check.py 26,29,30 > "$OUT/ring_check.log" 2>&1 && \
 timeout -k 10 300 python -u -m pytest tests/test_gpu_mlp_fused.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_mlp.log" 2>&1 && \
-timeout -k 10 300 python -u -m mxk8s.validate.gemm --sizes 8192,4096,16384 --variants 26,29,30 --iters 96 --rounds 12 > "$OUT/gemm_ab.log" 2>&1 && \
+MXK_KERNELS_LIB=$EXP timeout -k 10 300 python -u -m mxk8s.validate.gemm --sizes 8192,4096,16384 --variants 26,29,30 --iters 96 --rounds 12 > "$OUT/gemm_ab.log" 2>&1 && \
 timeout -k 10 420 python -u bench.py --mode ddp --steps 6 --warmup 2 > "$OUT/bench_ddp.log" 2>&1

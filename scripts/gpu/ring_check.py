@@ -36,3 +36,4 @@ for M, N, K in shapes:
         print(f"v{v} {M}x{N}x{K}: status {st} max_err {e:.4g} tol {tol:.3g} bad {bad}{where}",
               flush=True)
 print("ALL OK" if ok_all else "FAILURES", flush=True)
+sys.exit(0 if ok_all else 1)

@@ -71,9 +71,10 @@ def test_gemm_every_schedule_vs_fp32(cuda_device, M, N, K):
     bt = _rand((N, K), cuda_device, 24).bfloat16()
     ref = a.float() @ bt.float().t()
     tol = ref.abs().max().item() * 2 ** -7 + 1e-3
-    for v in range(L.mxk_gemm_bf16_tn_num_variants()):
-        if L.mxk_gemm_bf16_tn_is_ablation(v):
-            continue
+    built = [v for v in range(L.mxk_gemm_bf16_tn_num_variants())
+             if L.mxk_gemm_bf16_tn_variant_built(v) and not L.mxk_gemm_bf16_tn_is_ablation(v)]
+    assert 26 in built and 1 in built            # the default and the narrow-C fallback
+    for v in built:
         c = torch.full((M, N), float("nan"), device=cuda_device, dtype=torch.bfloat16)
         st = L.mxk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
                                         v, _lib.stream_ptr(cuda_device))
@@ -82,8 +83,8 @@ def test_gemm_every_schedule_vs_fp32(cuda_device, M, N, K):
         assert err <= tol, (v, err)
 
 
-@pytest.mark.parametrize("M,N,K,variants", [(8192, 8192, 8192, (6, 19)), (16384, 16384, 512, (6,)),
-                                            (16384, 6144, 4096, (6, 19))])
+@pytest.mark.parametrize("M,N,K,variants", [(8192, 8192, 8192, (26, 6)), (16384, 16384, 512, (26,)),
+                                            (16384, 6144, 4096, (26, 6))])
 def test_gemm_headline_shapes_full_output_vs_fp32(cuda_device, M, N, K, variants):
     """The long-K headline shape and the XCD super-block map at 64x64 tiles,
     the WHOLE output against an fp32 GEMM (tolerance 2^-7 max|ref|)."""
