@@ -5,23 +5,29 @@ the manual reboot gate, /root/reference/README.md:70-84).
 Everything the trainer owns lives in a handful of flat buffers
 (:class:`~mxk8s.parallel.ddp.FlatParamSpace`, the AdamW master / moment
 buffers), so a checkpoint is a few large contiguous tensors — no per-parameter
-state dicts, no pickles:
+state dicts, no pickles.  Format ``mxk8s-flat-v2``:
 
-  <dir>/params.safetensors        bf16 parameters (rank 0; identical on all ranks)
-  <dir>/optim-rank<r>.safetensors fp32 master / exp_avg / exp_avg_sq of rank r
-                                  (its ZeRO-1 shard, or the full buffers when
-                                  the optimizer is replicated — then rank 0 only)
-  <dir>/meta.json                 step, world size, layout fingerprint, sharding
+  <dir>/step-<N>/params.safetensors        bf16 parameters (rank 0; identical on all ranks)
+  <dir>/step-<N>/optim-rank<r>.safetensors fp32 master / exp_avg / exp_avg_sq of rank r
+                                           (its ZeRO-1 shard, or the full buffers when
+                                           the optimizer is replicated — then rank 0 only)
+  <dir>/meta.json                          commit record: step, world size, layout
+                                           fingerprint, sharding, and which step-<N>
+
+Every save writes a NEW step directory; ``meta.json`` — written by rank 0
+after a barrier that every rank reaches once its shard is on disk, then
+renamed into place — is what makes it current.  An interrupted save leaves
+the previous step directory and the previous ``meta.json`` untouched, so the
+job resumes from the last complete checkpoint; the ``keep`` newest complete
+step directories are retained, older ones are removed after the commit.
+Every shard also carries its own ``step_count`` / ``layout`` / ``save_step``,
+which ``load`` checks against ``meta.json``.
 
 Loading checks the layout fingerprint (parameter shapes, offsets, bucket
 padding) and, for sharded state, the world size, and refuses mismatches.
-Files are written to a temporary name and renamed, so a crash mid-save never
-leaves a truncated file in place; ``meta.json`` — the commit record — is
-written by rank 0 only after a barrier that every rank reaches once its shard
-is on disk, and every shard carries its own ``step_count`` / ``layout`` /
-``save_step``, which ``load`` checks against ``meta.json``: a rank that died
-mid-save leaves the previous meta.json next to a newer shard, and that mix is
-refused instead of silently resumed.
+Format ``mxk8s-flat-v1`` directories (shards directly in ``<dir>``) still
+load; their shards may predate the ``save_step`` tag, which is then not
+checked.
 """
 from __future__ import annotations
 
@@ -51,43 +57,71 @@ def _atomic_save(tensors: dict, path: str, meta: Optional[dict] = None) -> None:
     os.replace(tmp, path)
 
 
-def _check_shard(path: str, meta: dict, want: dict) -> None:
-    """A shard's own safetensors metadata must match the commit record."""
+def _check_shard(path: str, meta: dict, want: dict, legacy: bool = False) -> None:
+    """A shard's own safetensors metadata must match the commit record (v1
+    shards written before the save_step tag existed skip that key)."""
     from safetensors import safe_open
     with safe_open(path, framework="pt") as f:
         have = f.metadata() or {}
-    bad = {k: (have.get(k), v) for k, v in want.items() if have.get(k) != v}
+    bad = {k: (have.get(k), v) for k, v in want.items()
+           if have.get(k) != v and not (legacy and k == "save_step" and k not in have)}
     if bad:
         raise ValueError(f"{path}: shard does not match meta.json (step {meta['step']}): "
                          + ", ".join(f"{k}={h!r} expected {w!r}" for k, (h, w) in bad.items())
-                         + " — a save was interrupted; resume from an older checkpoint")
+                         + " — the shard was overwritten after meta.json was committed")
 
 
-def save(ckpt_dir: str, ddp, opt, step: int) -> None:
-    """Collective: every rank calls it (rank 0 writes params + meta)."""
+FORMAT = "mxk8s-flat-v2"
+LEGACY_FORMAT = "mxk8s-flat-v1"
+
+
+def step_dirname(step: int) -> str:
+    return f"step-{step:09d}"
+
+
+def _write_meta(ckpt_dir: str, meta: dict) -> None:
+    tmp = os.path.join(ckpt_dir, "meta.json.tmp")
+    with open(tmp, "w") as f:
+        json.dump(meta, f, indent=1)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, os.path.join(ckpt_dir, "meta.json"))
+
+
+def _prune(ckpt_dir: str, current: str, keep: int) -> None:
+    """Remove step directories beyond the ``keep`` newest (never ``current``)."""
+    import shutil
+    steps = sorted(d for d in os.listdir(ckpt_dir)
+                   if d.startswith("step-") and os.path.isdir(os.path.join(ckpt_dir, d)))
+    for d in steps[:max(0, len(steps) - max(1, keep))]:
+        if d != current:
+            shutil.rmtree(os.path.join(ckpt_dir, d), ignore_errors=True)
+
+
+def save(ckpt_dir: str, ddp, opt, step: int, keep: int = 2) -> None:
+    """Collective: every rank calls it (rank 0 writes params + the commit record)."""
     world, rank, _ = mxdist.world_info()
     sharded = bool(getattr(ddp, "sharded", False))
-    os.makedirs(ckpt_dir, exist_ok=True)
+    sub = step_dirname(step)
+    sdir = os.path.join(ckpt_dir, sub)
+    os.makedirs(sdir, exist_ok=True)
     fp = layout_fingerprint(ddp.space)
     if hasattr(opt, "synchronize"):
         opt.synchronize()      # pending side-stream updates (FlatAdamW overlap)
     if sharded or rank == 0:
         _atomic_save({"master": opt.master, "exp_avg": opt.exp_avg, "exp_avg_sq": opt.exp_avg_sq},
-                      os.path.join(ckpt_dir, f"optim-rank{rank if sharded else 0}.safetensors"),
+                      os.path.join(sdir, f"optim-rank{rank if sharded else 0}.safetensors"),
                       {"step_count": opt.step_count, "layout": fp, "save_step": step})
     if rank == 0:
-        _atomic_save({"params": ddp.space.param_buf}, os.path.join(ckpt_dir, "params.safetensors"),
+        _atomic_save({"params": ddp.space.param_buf}, os.path.join(sdir, "params.safetensors"),
                      {"layout": fp, "save_step": step})
     # every shard is on disk before the commit record names this step
     mxdist.barrier()
     if rank == 0:
-        meta = {"step": step, "optimizer_step": opt.step_count, "world_size": world,
-                "sharded": sharded, "layout": fp, "numel": ddp.space.numel,
-                "format": "mxk8s-flat-v1"}
-        tmp = os.path.join(ckpt_dir, "meta.json.tmp")
-        with open(tmp, "w") as f:
-            json.dump(meta, f, indent=1)
-        os.replace(tmp, os.path.join(ckpt_dir, "meta.json"))
+        _write_meta(ckpt_dir, {"step": step, "optimizer_step": opt.step_count, "world_size": world,
+                               "sharded": sharded, "layout": fp, "numel": ddp.space.numel,
+                               "format": FORMAT, "path": sub})
+        _prune(ckpt_dir, sub, keep)
     mxdist.barrier()
 
 
@@ -98,8 +132,13 @@ def load(ckpt_dir: str, ddp, opt) -> int:
         opt.synchronize()      # no side-stream update may land after the restore
     with open(os.path.join(ckpt_dir, "meta.json")) as f:
         meta = json.load(f)
-    if meta.get("format") != "mxk8s-flat-v1":
-        raise ValueError(f"{ckpt_dir}: not an mxk8s flat checkpoint")
+    fmt = meta.get("format")
+    if fmt == FORMAT:
+        sdir = os.path.join(ckpt_dir, meta["path"])
+    elif fmt == LEGACY_FORMAT:
+        sdir = ckpt_dir
+    else:
+        raise ValueError(f"{ckpt_dir}: not an mxk8s flat checkpoint (format {fmt!r})")
     fp = layout_fingerprint(ddp.space)
     if meta["layout"] != fp:
         raise ValueError(f"{ckpt_dir}: parameter layout {meta['layout']} != model layout {fp}")
@@ -108,11 +147,12 @@ def load(ckpt_dir: str, ddp, opt) -> int:
         raise ValueError(f"{ckpt_dir}: saved with world_size={meta['world_size']} "
                          f"sharded={meta['sharded']}, running world_size={world} sharded={sharded}")
     dev = ddp.space.param_buf.device
-    ppath = os.path.join(ckpt_dir, "params.safetensors")
-    opath = os.path.join(ckpt_dir, f"optim-rank{rank if sharded else 0}.safetensors")
-    _check_shard(ppath, meta, {"layout": meta["layout"], "save_step": str(meta["step"])})
+    ppath = os.path.join(sdir, "params.safetensors")
+    opath = os.path.join(sdir, f"optim-rank{rank if sharded else 0}.safetensors")
+    legacy = fmt == LEGACY_FORMAT
+    _check_shard(ppath, meta, {"layout": meta["layout"], "save_step": str(meta["step"])}, legacy)
     _check_shard(opath, meta, {"layout": meta["layout"], "save_step": str(meta["step"]),
-                               "step_count": str(meta["optimizer_step"])})
+                               "step_count": str(meta["optimizer_step"])}, legacy)
     params = load_file(ppath)["params"]
     with torch.no_grad():
         ddp.space.param_buf.copy_(params.to(dev))

@@ -208,9 +208,11 @@ def test_ddp_trainer_torchrun_two_ranks_cpu(tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2+zero1"
     assert d["value"] > 0 and d["steps"] == 2
-    assert sorted(os.listdir(ck)) == ["meta.json", "optim-rank0.safetensors",
-                                      "optim-rank1.safetensors", "params.safetensors"]
-    assert json.load(open(os.path.join(ck, "meta.json")))["step"] == 3
+    assert sorted(os.listdir(ck)) == ["meta.json", "step-000000003"]
+    assert sorted(os.listdir(os.path.join(ck, "step-000000003"))) == [
+        "optim-rank0.safetensors", "optim-rank1.safetensors", "params.safetensors"]
+    meta = json.load(open(os.path.join(ck, "meta.json")))
+    assert meta["step"] == 3 and meta["format"] == "mxk8s-flat-v2"
 
 
 def _ckpt_worker(rank, world, port, outdir, sharded):
@@ -257,8 +259,10 @@ def test_checkpoint_resume_matches_uninterrupted(sharded):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_ckpt_worker, args=(world, _free_port(), d, sharded), nprocs=world, join=True)
         files = sorted(os.listdir(os.path.join(d, "ck")))
-        assert "meta.json" in files and "params.safetensors" in files
-        assert ("optim-rank1.safetensors" in files) == sharded
+        assert "meta.json" in files
+        sfiles = os.listdir(os.path.join(d, "ck", "step-000000002"))
+        assert "params.safetensors" in sfiles
+        assert ("optim-rank1.safetensors" in sfiles) == sharded
         for r in range(world):
             c = torch.load(os.path.join(d, f"c{r}.pt"), weights_only=True)
             assert torch.equal(c["a"], c["b"])
@@ -280,9 +284,11 @@ def test_checkpoint_rejects_layout_mismatch(tmp_path):
         checkpoint.load(str(tmp_path / "ck"), d2, FlatAdamW(d2.space))
 
 
-def test_checkpoint_rejects_interrupted_overwrite(tmp_path):
-    """A rank that died mid-save leaves a newer shard beside the previous
-    meta.json: load refuses the mix instead of resuming it."""
+def test_checkpoint_interrupted_save_keeps_previous(tmp_path):
+    """A save that dies before its commit record leaves the previous step
+    directory and meta.json in charge: the job resumes from the last complete
+    checkpoint; a shard overwritten under a committed step is refused."""
+    import json
     from mxk8s.train import checkpoint
     torch.manual_seed(0)
     model = Llama(LlamaConfig.tiny())
@@ -290,15 +296,58 @@ def test_checkpoint_rejects_interrupted_overwrite(tmp_path):
     opt = FlatAdamW(ddp.space)
     ck = str(tmp_path / "ck")
     checkpoint.save(ck, ddp, opt, step=5)
-    assert checkpoint.load(ck, ddp, opt) == 5
-    # the optimizer shard of a later save landed, its meta.json never did
+    saved = opt.master.clone()
+    # a later save wrote its shards into step-8, then the job died (no meta.json)
     opt.step_count += 3
+    with torch.no_grad():
+        opt.master.add_(1.0)
+    s8 = os.path.join(ck, checkpoint.step_dirname(8))
+    os.makedirs(s8)
     checkpoint._atomic_save({"master": opt.master, "exp_avg": opt.exp_avg, "exp_avg_sq": opt.exp_avg_sq},
-                            os.path.join(ck, "optim-rank0.safetensors"),
+                            os.path.join(s8, "optim-rank0.safetensors"),
+                            {"step_count": opt.step_count, "layout": checkpoint.layout_fingerprint(ddp.space),
+                             "save_step": 8})
+    assert checkpoint.load(ck, ddp, opt) == 5
+    assert torch.equal(opt.master, saved) and opt.step_count == json.load(open(os.path.join(ck, "meta.json")))["optimizer_step"]
+    # overwriting the committed step's shard in place is detected
+    s5 = os.path.join(ck, checkpoint.step_dirname(5))
+    checkpoint._atomic_save({"master": opt.master, "exp_avg": opt.exp_avg, "exp_avg_sq": opt.exp_avg_sq},
+                            os.path.join(s5, "optim-rank0.safetensors"),
                             {"step_count": opt.step_count, "layout": checkpoint.layout_fingerprint(ddp.space),
                              "save_step": 8})
     with pytest.raises(ValueError, match="shard does not match meta.json"):
         checkpoint.load(ck, ddp, opt)
+
+
+def test_checkpoint_retention_and_legacy_v1(tmp_path):
+    """Only the `keep` newest step directories survive a save; a v1 directory
+    (shards beside meta.json, shards without the save_step tag) still loads."""
+    import json
+    from safetensors.torch import save_file
+    from mxk8s.train import checkpoint
+    torch.manual_seed(0)
+    model = Llama(LlamaConfig.tiny())
+    ddp = FlatDDP(model)
+    opt = FlatAdamW(ddp.space)
+    ck = str(tmp_path / "ck")
+    for st in (1, 2, 3, 4):
+        checkpoint.save(ck, ddp, opt, step=st, keep=2)
+    assert sorted(d for d in os.listdir(ck) if d.startswith("step-")) == \
+        [checkpoint.step_dirname(3), checkpoint.step_dirname(4)]
+    assert checkpoint.load(ck, ddp, opt) == 4
+    # legacy v1: written by an earlier version of save()
+    v1 = str(tmp_path / "v1")
+    os.makedirs(v1)
+    fp = checkpoint.layout_fingerprint(ddp.space)
+    save_file({"params": ddp.space.param_buf.detach().clone()}, os.path.join(v1, "params.safetensors"),
+              metadata={"layout": fp})
+    save_file({"master": opt.master.clone(), "exp_avg": opt.exp_avg.clone(),
+               "exp_avg_sq": opt.exp_avg_sq.clone()}, os.path.join(v1, "optim-rank0.safetensors"),
+              metadata={"layout": fp, "step_count": str(opt.step_count)})
+    json.dump({"step": 7, "optimizer_step": opt.step_count, "world_size": 1, "sharded": False,
+               "layout": fp, "numel": ddp.space.numel, "format": "mxk8s-flat-v1"},
+              open(os.path.join(v1, "meta.json"), "w"))
+    assert checkpoint.load(v1, ddp, opt) == 7
 
 
 def test_overlap_stages_cover_every_parameter_once():
