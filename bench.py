@@ -482,6 +482,9 @@ def main(argv=None) -> int:
     p.add_argument("--no-tuned-gemms", action="store_true", help="ddp mode: default hipBLASLt picks")
     p.add_argument("--grad-reduce", choices=["bf16", "fp32"], default="bf16",
                    help="ddp mode: gradient wire format (fp32: one bf16 rounding instead of n-1)")
+    p.add_argument("--rccl-profile", choices=["none", "xgmi-node"], default="xgmi-node",
+                   help="RCCL environment preset for N > 1 (mxk8s/parallel/rccl_env.py); "
+                        "variables already set win")
     args = p.parse_args(argv)
 
     world, rank, _ = _dist_env()
@@ -502,6 +505,12 @@ def main(argv=None) -> int:
             return subprocess.call(cmd)
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
 
+    rccl_vars = None
+    if world > 1:
+        # before anything initialises HIP / RCCL in this process
+        from mxk8s.parallel import rccl_env
+        rccl_vars = rccl_env.apply(args.rccl_profile)
+
     if args.mode == "validator":
         if args.steps is None:
             args.steps = 50
@@ -516,6 +525,8 @@ def main(argv=None) -> int:
         from mxk8s.train.ddp_llama import run_ddp_bench
         out = run_ddp_bench(args)
 
+    if rccl_vars is not None:
+        out["rccl_env"] = {"profile": args.rccl_profile, "vars": rccl_vars}
     if rank == 0:
         print(json.dumps(out), flush=True)
     try:

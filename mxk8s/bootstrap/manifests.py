@@ -74,6 +74,11 @@ def gemm_validator() -> dict:
                      "volumes": [_dshm("8Gi")]}}
 
 
+def _rccl_env() -> list:
+    from ..parallel import rccl_env
+    return [{"name": k, "value": v} for k, v in sorted(rccl_env.resolve("xgmi-node").items())]
+
+
 def rccl_allreduce_8gpu() -> dict:
     return {"apiVersion": "v1", "kind": "Pod",
             "metadata": {"name": "rccl-allreduce", "labels": {"app": "mxk8s-validator"}},
@@ -82,7 +87,8 @@ def rccl_allreduce_8gpu() -> dict:
                      "containers": [_gpu_container(
                          "rccl", ["python3", "-m", "mxk8s.validate", "--tests=rccl", "--gpus=8",
                                   "--rccl-min-bytes=8", "--rccl-max-bytes=8589934592",
-                                  "--rccl-scaling=1,2,4,8"], 8, cpu="16", mem="128Gi")],
+                                  "--rccl-scaling=1,2,4,8"], 8, extra_env=_rccl_env(),
+                         cpu="16", mem="128Gi")],
                      "volumes": [_dshm("64Gi")]}}
 
 
@@ -97,7 +103,7 @@ def llama3_ddp_8gpu() -> dict:
                              ["python3", "-m", "torch.distributed.run", "--standalone",
                               "--nproc-per-node=8", "/opt/mxk8s/bench.py", "--mode=ddp",
                               "--gpus=8", "--steps=10", "--warmup=3", "--seq-len=2048"],
-                             8, cpu="64", mem="512Gi")],
+                             8, extra_env=_rccl_env(), cpu="64", mem="512Gi")],
                          "volumes": [_dshm("64Gi")]}}}}
 
 

@@ -132,6 +132,11 @@ VALUES: dict = {
                                            items={"type": "object",
                                                   "additionalProperties": {"type": "string"}})},
                  "resources": RESOURCES},
+    "rccl": {"profile": F("string", "RCCL environment preset (mxk8s/parallel/rccl_env.py)",
+                          enum=["none", "xgmi-node"]),
+             "env": F("object", "extra NCCL_* / RCCL_* / TORCH_NCCL_* variables",
+                      items={"type": "object", "additionalProperties": {"type": "string"},
+                             "propertyNames": {"pattern": "^(NCCL_|RCCL_|TORCH_NCCL_|HSA_NO_SCRATCH_RECLAIM|HSA_FORCE_FINE_GRAIN)"}})},
     "validator": {"enabled": F("boolean"),
                   "gpus": F("integer", "amd.com/gpu requested by the validator pod", minimum=1,
                             maximum=8),
@@ -221,8 +226,11 @@ def _check(schema: dict, v: Any, path: str, errs: list) -> None:
     if t == "object":
         props = schema.get("properties", {})
         extra = schema.get("additionalProperties", True)
+        names = schema.get("propertyNames", {}).get("pattern")
         for k, x in v.items():
             p = f"{path}.{k}" if path else k
+            if names and not re.search(names, k):
+                errs.append(f"{p}: key does not match {names}")
             if k in props:
                 _check(props[k], x, p, errs)
             elif extra is False:

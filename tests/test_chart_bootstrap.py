@@ -102,6 +102,38 @@ def test_chart_values_overrides():
         render.render(render.load_values(sets=["validator.gpus=9"]))
 
 
+def test_chart_rccl_env_matches_profiles():
+    """rccl.profile / rccl.env render into the validator Job exactly as
+    mxk8s/parallel/rccl_env.py resolves them (explicit env wins over the
+    profile); unknown variables are rejected by the values schema."""
+    from mxk8s.parallel import rccl_env
+
+    def job_env(sets):
+        docs = _docs(render.load_values(sets=sets))
+        job = next(d for d in docs if d["kind"] == "Job")
+        env = job["spec"]["template"]["spec"]["containers"][0]["env"]
+        names = [e["name"] for e in env]
+        assert len(names) == len(set(names))
+        return {e["name"]: e["value"] for e in env if e["name"] != "HSA_ENABLE_IPC_MODE_LEGACY"}
+
+    assert job_env([]) == rccl_env.resolve("xgmi-node")
+    assert job_env(["rccl.profile=none"]) == {}
+    got = job_env(["rccl.env.NCCL_MIN_NCHANNELS=32", "rccl.env.NCCL_IB_DISABLE=0"])
+    assert got == rccl_env.resolve("xgmi-node", {"NCCL_MIN_NCHANNELS": "32", "NCCL_IB_DISABLE": "0"})
+    assert got["NCCL_IB_DISABLE"] == "0"
+    from mxk8s.config import validate_values
+    assert validate_values(render.load_values(sets=["rccl.env.NCCL_PROTO=Simple"])) == []
+    assert any("LD_PRELOAD" in e for e in
+               validate_values(render.load_values(sets=["rccl.env.LD_PRELOAD=x"])))
+    with pytest.raises(ValueError):
+        rccl_env.resolve("xgmi-node", {"LD_PRELOAD": "x"})
+    env = {"NCCL_IB_DISABLE": "0"}
+    assert rccl_env.apply("xgmi-node", environ=env)["NCCL_IB_DISABLE"] == "0"   # set wins
+    assert env["TORCH_NCCL_HIGH_PRIORITY"] == "1"
+    ex = manifests.rccl_allreduce_8gpu()["spec"]["containers"][0]["env"]
+    assert {e["name"] for e in ex} >= set(rccl_env.resolve("xgmi-node"))
+
+
 def test_chart_service_monitor():
     """exporter.serviceMonitor (dcgm-exporter serviceMonitor counterpart):
     off by default; on, a ServiceMonitor selects the metrics Service's port."""
