@@ -102,8 +102,11 @@ __device__ __forceinline__ void mfma_16x16x32_agpr(f32x4_t& acc, bf16x8_t a, bf1
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
-  static_assert(N == 0 || N == 13 || N == 15 || N == 16, "vm_wait: add the count");
+  static_assert(N == 0 || N == 13 || N == 14 || N == 15 || N == 16 || N == 30,
+                "vm_wait: add the count");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else if constexpr (N == 30) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
   else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
@@ -236,13 +239,20 @@ using mxk::SchedTwoBarrier;
 // pieces, waits and barriers that follow MFMA m (see w4i_ktile for MODE).
 // SPLITA: A fragments 0-3 at a_base, 4-7 at a_hi (the w13 SwiGLU kernel
 // rotates one wave's row blocks by 4); otherwise a_hi is unused.
-template <class S, int PAR, int MODE, int ORDER = 0, int PRIO = 0, bool SPLITA = false>
+// HOOK(m) runs after MFMA m (the trickle-store kernel's one C store per
+// K-tile); m is a constant once the loops are unrolled.
+struct NoHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+template <class S, int PAR, int MODE, int ORDER = 0, int PRIO = 0, bool SPLITA = false,
+          class HOOK = NoHook>
 __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                           bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                           bf16x8_t (&f1b)[8], char* smem, int a_base, int b_base,
                                           int off_k0, int off_k1, const DmaK& dma_a,
                                           const DmaK& dma_b, int kb2, int wave_s, int par = 0,
-                                          int a_hi = 0) {
+                                          int a_hi = 0, const HOOK& hook = HOOK{}) {
   constexpr int SUB = 2048;
   auto aoff = [&](int r) { return SPLITA && r >= 4 ? a_hi + (r - 4) * SUB : a_base + r * SUB; };
   const int px = PAR == 2 ? par : PAR;
@@ -260,6 +270,7 @@ __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
         const int i = ORDER ? q : o, j = ORDER ? o : q;
         if (h == 0) mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
         else mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
+        hook(m);
         if (S::a1(m) >= 0) f1a[S::a1(m)] = lds_read_b128(X + aoff(S::a1(m)) + off_k1);
         if (MODE == 1 && m == S::W1) __builtin_amdgcn_s_waitcnt(0xC07F);
         if (MODE == 1 && m == S::B1) __builtin_amdgcn_s_barrier();
@@ -560,6 +571,209 @@ mxk_gemm_bf16_tn_w4ip(const uint16_t* __restrict__ A, const uint16_t* __restrict
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+
+// ---------------------------------------------------------------------------
+// w4t (schedule 31): persistent schedule 26 whose C store tail is trickled
+// into the next tile's main loop instead of burst at the end of each tile.
+//
+// The store tail costs ~3.4 % at 8192^3 (no-store ablation, variant 10):
+// every CU finishes its tile at the same moment and 256 x 128 KiB = 32 MiB
+// go to HBM at once, while the next tiles' first DMA waits sit behind those
+// stores (vmcnt counts loads and stores together, in issue order).  Here a
+// tile's C leaves in two halves through the same LDS staging as schedule 26
+// (whole-line stores): rows 64..127 of each wave block as a 16 MiB burst
+// issued AFTER the next tile's two prologue stages (so the first stage wait
+// does not include them), rows 0..63 kept in 64 VGPRs (16 x 16 B per lane)
+// and stored one whole-line instruction per K-tile during the next tile's
+// first 16 K-tiles (MFMA 3, ahead of that K-tile's DMA pieces).  Waits: the
+// first K-tile's stage wait lets the 16 burst stores and its trickle store
+// stay in flight (vmcnt 30), the other trickle K-tiles their one store (14).
+// Needs K >= 18 * 64 (16 trickle K-tiles + the two DMA-less tails); the
+// launcher runs schedule 26 below that.
+struct SchedHBTrk0 : mxk::SchedHB { static constexpr int VM3 = 30; };
+struct SchedHBTrk : mxk::SchedHB { static constexpr int VM3 = 14; };
+
+struct TrickleStore {
+  u32x4_t v;
+  uint16_t* p;
+  __device__ __forceinline__ void operator()(int m) const {
+    if (m == 3) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
+  }
+};
+
+// rows 64 p .. 64 p + 63 of the wave's 128 x 128 block through the LDS slice
+// (schedule 26's layout, mx_common.h store_block_lds) into 16 whole-line
+// vectors per lane: vector it is row 4 it + (lane >> 4), 8 columns at
+// 8 (lane & 15).
+__device__ __forceinline__ void stage_half(const f32x4_t (&acc)[8][8], int p, int lane, char* lds,
+                                           u32x4_t (&out)[16]) {
+  const int crow = lane & 15, q = lane >> 4;
+  const int rr = lane >> 4, cc = (lane & 15) * 8;
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint2 pk;
+      pk.x = mxk::pack2bf(acc[4 * p + ii][j][0], acc[4 * p + ii][j][1]);
+      pk.y = mxk::pack2bf(acc[4 * p + ii][j][2], acc[4 * p + ii][j][3]);
+      *reinterpret_cast<uint2*>(lds + (ii * 16 + crow) * mxk::kStoreLdsRow + (j * 16 + q * 4) * 2) = pk;
+    }
+#pragma unroll
+  for (int it = 0; it < 16; ++it)
+    out[it] = *reinterpret_cast<const u32x4_t*>(lds + (it * 4 + rr) * mxk::kStoreLdsRow + cc * 2);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __asm__ volatile("" ::: "memory");
+}
+
+template <int Q>
+__device__ __forceinline__ void trickle_ktiles(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
+                                               bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
+                                               bf16x8_t (&f1b)[8], char* smem, int a_base,
+                                               int b_base, int off_k0, int off_k1,
+                                               const DmaK& dma_a, const DmaK& dma_b, int& kb,
+                                               int wave_s, const u32x4_t (&buf)[16], uint16_t* tp,
+                                               size_t tstride) {
+  const TrickleStore h0{buf[Q], tp + Q * tstride};
+  const TrickleStore h1{buf[Q + 1], tp + (Q + 1) * tstride};
+  if constexpr (Q == 0)
+    w4j_ktile<SchedHBTrk0, 0, 1, 0, 0, false, TrickleStore>(acc, f0a, f0b, f1a, f1b, smem, a_base,
+                                                            b_base, off_k0, off_k1, dma_a, dma_b,
+                                                            kb, wave_s, 0, 0, h0);
+  else
+    w4j_ktile<SchedHBTrk, 0, 1, 0, 0, false, TrickleStore>(acc, f0a, f0b, f1a, f1b, smem, a_base,
+                                                           b_base, off_k0, off_k1, dma_a, dma_b,
+                                                           kb, wave_s, 0, 0, h0);
+  w4j_ktile<SchedHBTrk, 1, 1, 0, 0, false, TrickleStore>(acc, f0a, f0b, f1a, f1b, smem, a_base,
+                                                         b_base, off_k0, off_k1, dma_a, dma_b,
+                                                         kb + BK * 2, wave_s, 0, 0, h1);
+  kb += 2 * BK * 2;
+  if constexpr (Q + 2 < 16)
+    trickle_ktiles<Q + 2>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                          dma_b, kb, wave_s, buf, tp, tstride);
+}
+
+template <int MAP>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4t(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int ns = K / BK;                       // >= 18 (launcher)
+
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
+  const int rr = lane >> 4, cc = (lane & 15) * 8;
+  const size_t tstride = static_cast<size_t>(4) * ldc;   // trickle vector it -> it + 1
+
+  int t = blockIdx.x;
+  int m0, n0;
+  w4b_tile<MAP>(t, ntiles, tiles_m, tiles_n, &m0, &n0);
+  DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
+  DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
+  auto prologue = [&]() {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_OP_BYTES, p, 0, wave_s);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_a.issue(smem + W4B_STAGE_BYTES, p, BK * 2, wave_s);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_STAGE_BYTES + W4B_OP_BYTES, p, BK * 2, wave_s);
+  };
+  prologue();
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // stage 0
+  __builtin_amdgcn_s_barrier();
+
+  u32x4_t buf[16];                                    // previous tile's rows 0..63
+  uint16_t* tp = C;
+  bool trickle = false;
+  while (true) {
+    f32x4_t acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+
+    int s = 0;
+    int kb = 2 * BK * 2;
+    if (trickle) {
+      trickle_ktiles<0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                        dma_b, kb, wave_s, buf, tp, tstride);
+      s = 16;
+    }
+    for (; s + 2 <= ns - 2; s += 2) {
+      ktile_sched<1, 0, 1, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                 dma_a, dma_b, kb, wave_s);
+      ktile_sched<1, 1, 1, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                 dma_a, dma_b, kb + BK * 2, wave_s);
+      kb += 2 * BK * 2;
+    }
+    if (s < ns - 2) {
+      ktile_sched<1, 0, 1, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                 dma_a, dma_b, kb, wave_s);
+      ++s;
+    }
+    ktile_sched<1, 2, 2, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                               dma_a, dma_b, 0, wave_s, s & 1);
+    ++s;
+    ktile_sched<1, 2, 3, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                               dma_a, dma_b, 0, wave_s, s & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mxk::mfma_drain(acc);
+    // every wave's last fragment reads retired: the stages are free for staging
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+
+    char* lds = smem + wave_s * mxk::kStoreLdsWave;
+    uint16_t* row0 = C + static_cast<size_t>(m0 + wm * 128 + rr) * ldc + n0 + wn * 128 + cc;
+    const int tn = t + static_cast<int>(gridDim.x);
+    if (tn >= ntiles) {
+      u32x4_t hi[16];
+      stage_half(acc, 0, lane, lds, buf);
+      stage_half(acc, 1, lane, lds, hi);
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        __builtin_nontemporal_store(buf[it], reinterpret_cast<u32x4_t*>(row0 + it * tstride));
+        __builtin_nontemporal_store(hi[it], reinterpret_cast<u32x4_t*>(row0 + (16 + it) * tstride));
+      }
+      break;
+    }
+    u32x4_t hi[16];
+    stage_half(acc, 0, lane, lds, buf);
+    stage_half(acc, 1, lane, lds, hi);
+    tp = row0;
+    __builtin_amdgcn_s_barrier();                     // every wave read its slice back
+    t = tn;
+    w4b_tile<MAP>(t, ntiles, tiles_m, tiles_n, &m0, &n0);
+    dma_a = make_dmak(A, lda, m0, lane, wave_s);
+    dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
+    prologue();
+#pragma unroll
+    for (int it = 0; it < 16; ++it)
+      __builtin_nontemporal_store(hi[it], reinterpret_cast<u32x4_t*>(tp + (16 + it) * tstride));
+    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // stage 0 (stage 1 + the 16 stores in flight)
+    __builtin_amdgcn_s_barrier();
+    trickle = true;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // ---------------------------------------------------------------------------
 // pp8 (schedule 19): 8 waves, two per SIMD, in a compute / load ping-pong.
@@ -930,14 +1144,14 @@ int mxk_gemm_bf16_tn_ring_launch(int slots, const void* A, const void* Bt, void*
                                  int K, int lda, int ldb, int ldc, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 31;
+constexpr int kNumVariants = 32;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
     "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar",
     "w4j_hb_st", "x2_hb", "diag_nostore", "w4ip_hb_st", "w4ip_hb_nt", "w4j_earlyb",
     "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg", "pp8",
-    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst"};
+    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst", "w4t_trickle"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -1001,6 +1215,16 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 28: launch_w4i<1, 4, 1, 0, 8>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 29: mxk_gemm_bf16_tn_ring_launch(4, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 30: mxk_gemm_bf16_tn_ring_launch(5, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
+    case 31: {
+      if (K < 18 * BK) {   // fewer K-tiles than the trickle phase needs
+        launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
+        break;
+      }
+      const int grid = nwg < num_cus() ? nwg : num_cus();
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4t<1>), dim3(grid), dim3(W4_THREADS), 0, stream, a, b,
+                         c, M, N, K, lda, ldb, ldc);
+      break;
+    }
     case 19:
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_pp8<1, 0>), dim3(nwg), dim3(PP_THREADS), 0, stream, a, b,
                          c, M, N, K, lda, ldb, ldc);

@@ -10,7 +10,7 @@ L = _lib.lib()
 dev = torch.device("cuda", 0)
 variants = [int(v) for v in sys.argv[1].split(",")]
 shapes = [(256, 256, k) for k in (64, 128, 192, 256, 320, 384, 448, 512)] + \
-         [(4096, 4096, 4096), (8192, 8192, 8192)]
+         [(4096, 4096, 4096), (4608, 4608, 2048), (16384, 6144, 4096), (8192, 8192, 8192)]
 ok_all = True
 for M, N, K in shapes:
     g = torch.Generator(device=dev)
