@@ -77,6 +77,8 @@
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
 // stay in profiles/r1_gemm_*/ (numbered by the old ids: old 34 = 0,
 // 31 = 1, 29 = 2, 30 = 3, 32 = 4, 35 = 5, 36 = 6).
+#include <type_traits>
+
 #include "mx_common.h"
 
 namespace {
@@ -102,10 +104,11 @@ __device__ __forceinline__ void mfma_16x16x32_agpr(f32x4_t& acc, bf16x8_t a, bf1
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
-  static_assert(N == 0 || N == 13 || N == 14 || N == 15 || N == 16 || N == 30,
+  static_assert(N == 0 || N == 13 || N == 14 || N == 15 || N == 16 || N == 22 || N == 30,
                 "vm_wait: add the count");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else if constexpr (N == 22) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
   else if constexpr (N == 30) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
   else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
@@ -591,6 +594,7 @@ mxk_gemm_bf16_tn_w4ip(const uint16_t* __restrict__ A, const uint16_t* __restrict
 // Needs K >= 18 * 64 (16 trickle K-tiles + the two DMA-less tails); the
 // launcher runs schedule 26 below that.
 struct SchedHBTrk0 : mxk::SchedHB { static constexpr int VM3 = 30; };
+struct SchedHBTrk0L : mxk::SchedHB { static constexpr int VM3 = 22; };
 struct SchedHBTrk : mxk::SchedHB { static constexpr int VM3 = 14; };
 
 struct TrickleStore {
@@ -598,6 +602,17 @@ struct TrickleStore {
   uint16_t* p;
   __device__ __forceinline__ void operator()(int m) const {
     if (m == 3) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
+  }
+};
+
+// LDS-held part (schedule 32): read after MFMA 1, stored after MFMA 9
+struct TrickleLds {
+  const char* src;
+  uint16_t* p;
+  u32x4_t& v;
+  __device__ __forceinline__ void operator()(int m) const {
+    if (m == 1) v = *reinterpret_cast<const u32x4_t*>(src);
+    if (m == 9) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
   }
 };
 
@@ -625,38 +640,51 @@ __device__ __forceinline__ void stage_half(const f32x4_t (&acc)[8][8], int p, in
   __asm__ volatile("" ::: "memory");
 }
 
-template <int Q>
+// Trickle K-tiles Q, Q + 1 (of NQ): Q < 16 stores VGPR vector buf[Q] (C row
+// 4 Q + lane/16 of the previous tile's wave block), 16 <= Q < 24 the LDS
+// vector Q - 16 of rows 64..95 (lane-linear, 1 KiB per vector per wave).
+template <int Q, int NQ, class S0>
 __device__ __forceinline__ void trickle_ktiles(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                                bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                                bf16x8_t (&f1b)[8], char* smem, int a_base,
                                                int b_base, int off_k0, int off_k1,
                                                const DmaK& dma_a, const DmaK& dma_b, int& kb,
                                                int wave_s, const u32x4_t (&buf)[16], uint16_t* tp,
-                                               size_t tstride) {
-  const TrickleStore h0{buf[Q], tp + Q * tstride};
-  const TrickleStore h1{buf[Q + 1], tp + (Q + 1) * tstride};
-  if constexpr (Q == 0)
-    w4j_ktile<SchedHBTrk0, 0, 1, 0, 0, false, TrickleStore>(acc, f0a, f0b, f1a, f1b, smem, a_base,
-                                                            b_base, off_k0, off_k1, dma_a, dma_b,
-                                                            kb, wave_s, 0, 0, h0);
-  else
-    w4j_ktile<SchedHBTrk, 0, 1, 0, 0, false, TrickleStore>(acc, f0a, f0b, f1a, f1b, smem, a_base,
-                                                           b_base, off_k0, off_k1, dma_a, dma_b,
-                                                           kb, wave_s, 0, 0, h0);
-  w4j_ktile<SchedHBTrk, 1, 1, 0, 0, false, TrickleStore>(acc, f0a, f0b, f1a, f1b, smem, a_base,
-                                                         b_base, off_k0, off_k1, dma_a, dma_b,
-                                                         kb + BK * 2, wave_s, 0, 0, h1);
+                                               size_t tstride, const char* lsrc) {
+  auto one = [&](auto qc, auto parc, int kbx) {
+    constexpr int q = decltype(qc)::value;
+    constexpr int par = decltype(parc)::value;
+    using SS = std::conditional_t<q == 0, S0, SchedHBTrk>;
+    if constexpr (q < 16) {
+      const TrickleStore h{buf[q], tp + q * tstride};
+      w4j_ktile<SS, par, 1, 0, 0, false, TrickleStore>(acc, f0a, f0b, f1a, f1b, smem, a_base,
+                                                       b_base, off_k0, off_k1, dma_a, dma_b, kbx,
+                                                       wave_s, 0, 0, h);
+    } else {
+      u32x4_t v;
+      const TrickleLds h{lsrc + (q - 16) * 1024, tp + q * tstride, v};
+      w4j_ktile<SS, par, 1, 0, 0, false, TrickleLds>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base,
+                                                     off_k0, off_k1, dma_a, dma_b, kbx, wave_s, 0,
+                                                     0, h);
+    }
+  };
+  one(std::integral_constant<int, Q>{}, std::integral_constant<int, 0>{}, kb);
+  one(std::integral_constant<int, Q + 1>{}, std::integral_constant<int, 1>{}, kb + BK * 2);
   kb += 2 * BK * 2;
-  if constexpr (Q + 2 < 16)
-    trickle_ktiles<Q + 2>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                          dma_b, kb, wave_s, buf, tp, tstride);
+  if constexpr (Q + 2 < NQ)
+    trickle_ktiles<Q + 2, NQ, S0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
+                                  dma_a, dma_b, kb, wave_s, buf, tp, tstride, lsrc);
 }
 
-template <int MAP>
+// LQ (schedule 32): the LDS grows to the full 160 KiB and its last 32 KiB
+// hold rows 64..95 of each wave block (8 KiB per wave), trickled in K-tiles
+// 16..23, so only rows 96..127 (8 MiB chip-wide) leave as a burst.
+template <int MAP, bool LQ>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4t(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  constexpr int XTRA = LQ ? 32768 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES + XTRA];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -713,10 +741,17 @@ mxk_gemm_bf16_tn_w4t(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 
     int s = 0;
     int kb = 2 * BK * 2;
+    char* xq = smem + 2 * W4B_STAGE_BYTES + wave_s * 8192 + lane * 16;   // LQ vectors
     if (trickle) {
-      trickle_ktiles<0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                        dma_b, kb, wave_s, buf, tp, tstride);
-      s = 16;
+      if constexpr (LQ) {
+        trickle_ktiles<0, 24, SchedHBTrk0L>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,
+                                            off_k1, dma_a, dma_b, kb, wave_s, buf, tp, tstride, xq);
+        s = 24;
+      } else {
+        trickle_ktiles<0, 16, SchedHBTrk0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,
+                                           off_k1, dma_a, dma_b, kb, wave_s, buf, tp, tstride, xq);
+        s = 16;
+      }
     }
     for (; s + 2 <= ns - 2; s += 2) {
       ktile_sched<1, 0, 1, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1,
@@ -758,6 +793,10 @@ mxk_gemm_bf16_tn_w4t(const uint16_t* __restrict__ A, const uint16_t* __restrict_
     u32x4_t hi[16];
     stage_half(acc, 0, lane, lds, buf);
     stage_half(acc, 1, lane, lds, hi);
+    if constexpr (LQ) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) *reinterpret_cast<u32x4_t*>(xq + it * 1024) = hi[it];
+    }
     tp = row0;
     __builtin_amdgcn_s_barrier();                     // every wave read its slice back
     t = tn;
@@ -766,9 +805,11 @@ mxk_gemm_bf16_tn_w4t(const uint16_t* __restrict__ A, const uint16_t* __restrict_
     dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
     prologue();
 #pragma unroll
-    for (int it = 0; it < 16; ++it)
+    for (int it = LQ ? 8 : 0; it < 16; ++it)
       __builtin_nontemporal_store(hi[it], reinterpret_cast<u32x4_t*>(tp + (16 + it) * tstride));
-    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // stage 0 (stage 1 + the 16 stores in flight)
+    // stage 0 landed (stage 1 and the 16 / 8 burst stores still in flight)
+    if constexpr (LQ) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     trickle = true;
   }
@@ -1144,14 +1185,14 @@ int mxk_gemm_bf16_tn_ring_launch(int slots, const void* A, const void* Bt, void*
                                  int K, int lda, int ldb, int ldc, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 32;
+constexpr int kNumVariants = 33;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
     "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar",
     "w4j_hb_st", "x2_hb", "diag_nostore", "w4ip_hb_st", "w4ip_hb_nt", "w4j_earlyb",
     "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg", "pp8",
-    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst", "w4t_trickle"};
+    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst", "w4t_trickle", "w4t_trickle_lds"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -1215,14 +1256,19 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 28: launch_w4i<1, 4, 1, 0, 8>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 29: mxk_gemm_bf16_tn_ring_launch(4, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 30: mxk_gemm_bf16_tn_ring_launch(5, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
-    case 31: {
-      if (K < 18 * BK) {   // fewer K-tiles than the trickle phase needs
+    case 31:
+    case 32: {
+      if (K < (v == 31 ? 18 : 26) * BK) {   // fewer K-tiles than the trickle phase needs
         launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
         break;
       }
       const int grid = nwg < num_cus() ? nwg : num_cus();
-      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4t<1>), dim3(grid), dim3(W4_THREADS), 0, stream, a, b,
-                         c, M, N, K, lda, ldb, ldc);
+      if (v == 31)
+        hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4t<1, false>), dim3(grid), dim3(W4_THREADS), 0, stream,
+                           a, b, c, M, N, K, lda, ldb, ldc);
+      else
+        hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4t<1, true>), dim3(grid), dim3(W4_THREADS), 0, stream,
+                           a, b, c, M, N, K, lda, ldb, ldc);
       break;
     }
     case 19:
