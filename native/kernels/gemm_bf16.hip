@@ -244,9 +244,7 @@ using mxk::SchedTwoBarrier;
 // rotates one wave's row blocks by 4); otherwise a_hi is unused.
 // HOOK(m) runs after MFMA m (the trickle-store kernel's one C store per
 // K-tile); m is a constant once the loops are unrolled.
-struct NoHook {
-  __device__ __forceinline__ void operator()(int) const {}
-};
+using mxk::NoHook;
 
 template <class S, int PAR, int MODE, int ORDER = 0, int PRIO = 0, bool SPLITA = false,
           class HOOK = NoHook>
@@ -597,49 +595,6 @@ struct SchedHBTrk0 : mxk::SchedHB { static constexpr int VM3 = 30; };
 struct SchedHBTrk0L : mxk::SchedHB { static constexpr int VM3 = 22; };
 struct SchedHBTrk : mxk::SchedHB { static constexpr int VM3 = 14; };
 
-struct TrickleStore {
-  u32x4_t v;
-  uint16_t* p;
-  __device__ __forceinline__ void operator()(int m) const {
-    if (m == 3) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
-  }
-};
-
-// LDS-held part (schedule 32): read after MFMA 1, stored after MFMA 9
-struct TrickleLds {
-  const char* src;
-  uint16_t* p;
-  u32x4_t& v;
-  __device__ __forceinline__ void operator()(int m) const {
-    if (m == 1) v = *reinterpret_cast<const u32x4_t*>(src);
-    if (m == 9) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
-  }
-};
-
-// rows 64 p .. 64 p + 63 of the wave's 128 x 128 block through the LDS slice
-// (schedule 26's layout, mx_common.h store_block_lds) into 16 whole-line
-// vectors per lane: vector it is row 4 it + (lane >> 4), 8 columns at
-// 8 (lane & 15).
-__device__ __forceinline__ void stage_half(const f32x4_t (&acc)[8][8], int p, int lane, char* lds,
-                                           u32x4_t (&out)[16]) {
-  const int crow = lane & 15, q = lane >> 4;
-  const int rr = lane >> 4, cc = (lane & 15) * 8;
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      uint2 pk;
-      pk.x = mxk::pack2bf(acc[4 * p + ii][j][0], acc[4 * p + ii][j][1]);
-      pk.y = mxk::pack2bf(acc[4 * p + ii][j][2], acc[4 * p + ii][j][3]);
-      *reinterpret_cast<uint2*>(lds + (ii * 16 + crow) * mxk::kStoreLdsRow + (j * 16 + q * 4) * 2) = pk;
-    }
-#pragma unroll
-  for (int it = 0; it < 16; ++it)
-    out[it] = *reinterpret_cast<const u32x4_t*>(lds + (it * 4 + rr) * mxk::kStoreLdsRow + cc * 2);
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __asm__ volatile("" ::: "memory");
-}
-
 // Trickle K-tiles Q, Q + 1 (of NQ): Q < 16 stores VGPR vector buf[Q] (C row
 // 4 Q + lane/16 of the previous tile's wave block), 16 <= Q < 24 the LDS
 // vector Q - 16 of rows 64..95 (lane-linear, 1 KiB per vector per wave).
@@ -656,14 +611,14 @@ __device__ __forceinline__ void trickle_ktiles(f32x4_t (&acc)[8][8], bf16x8_t (&
     constexpr int par = decltype(parc)::value;
     using SS = std::conditional_t<q == 0, S0, SchedHBTrk>;
     if constexpr (q < 16) {
-      const TrickleStore h{buf[q], tp + q * tstride};
-      w4j_ktile<SS, par, 1, 0, 0, false, TrickleStore>(acc, f0a, f0b, f1a, f1b, smem, a_base,
+      const mxk::TrickleStore h{buf[q], tp + q * tstride};
+      w4j_ktile<SS, par, 1, 0, 0, false, mxk::TrickleStore>(acc, f0a, f0b, f1a, f1b, smem, a_base,
                                                        b_base, off_k0, off_k1, dma_a, dma_b, kbx,
                                                        wave_s, 0, 0, h);
     } else {
       u32x4_t v;
-      const TrickleLds h{lsrc + (q - 16) * 1024, tp + q * tstride, v};
-      w4j_ktile<SS, par, 1, 0, 0, false, TrickleLds>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base,
+      const mxk::TrickleLds h{lsrc + (q - 16) * 1024, tp + q * tstride, v};
+      w4j_ktile<SS, par, 1, 0, 0, false, mxk::TrickleLds>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base,
                                                      off_k0, off_k1, dma_a, dma_b, kbx, wave_s, 0,
                                                      0, h);
     }
@@ -781,8 +736,8 @@ mxk_gemm_bf16_tn_w4t(const uint16_t* __restrict__ A, const uint16_t* __restrict_
     const int tn = t + static_cast<int>(gridDim.x);
     if (tn >= ntiles) {
       u32x4_t hi[16];
-      stage_half(acc, 0, lane, lds, buf);
-      stage_half(acc, 1, lane, lds, hi);
+      mxk::stage_half(acc, 0, lane, lds, buf);
+      mxk::stage_half(acc, 1, lane, lds, hi);
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
         __builtin_nontemporal_store(buf[it], reinterpret_cast<u32x4_t*>(row0 + it * tstride));
@@ -791,8 +746,8 @@ mxk_gemm_bf16_tn_w4t(const uint16_t* __restrict__ A, const uint16_t* __restrict_
       break;
     }
     u32x4_t hi[16];
-    stage_half(acc, 0, lane, lds, buf);
-    stage_half(acc, 1, lane, lds, hi);
+    mxk::stage_half(acc, 0, lane, lds, buf);
+    mxk::stage_half(acc, 1, lane, lds, hi);
     if constexpr (LQ) {
 #pragma unroll
       for (int it = 0; it < 8; ++it) *reinterpret_cast<u32x4_t*>(xq + it * 1024) = hi[it];

@@ -300,12 +300,15 @@ mxk_gemm_bf16_x_kernel(const uint16_t* __restrict__ A, const uint16_t* __restric
 //   m 97..127 odd next k-half-0 fragments from Y (B, then A)
 // MODE 1: with DMA; 2: no DMA, vmcnt(0) at barrier #3; 3: last K-tile.
 // ---------------------------------------------------------------------------
-template <bool AN, bool BN, int PAR, int MODE>
+// VMX >= 0 replaces the stage wait's vmcnt (the trickle kernel's C stores
+// sit among the DMA pieces); HOOK(m) runs after MFMA m.
+template <bool AN, bool BN, int PAR, int MODE, int VMX = -1, class HOOK = mxk::NoHook>
 __device__ __forceinline__ void x2_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                          bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                          bf16x8_t (&f1b)[8], char* smem, const XOp<AN>& oa,
                                          const XOp<BN>& ob, int wm, int wn, uint32_t soa,
-                                         uint32_t sob, int wave, int par = 0) {
+                                         uint32_t sob, int wave, int par = 0,
+                                         const HOOK& hook = HOOK{}) {
   constexpr int A_BYTES = XOp<AN>::BYTES;
   constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
   const int px = PAR == 2 ? par : PAR;
@@ -321,6 +324,7 @@ __device__ __forceinline__ void x2_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8
         const int m = h * 64 + i * 8 + j;
         if (h == 0) xmfma(acc[i][j], f0b[j], f0a[i]);
         else xmfma(acc[i][j], f1b[j], f1a[i]);
+        hook(m);
         if (m < 16 && (m & 1)) f1a[m >> 1] = oa.frag(X, wm * 8 + (m >> 1), 1);
         if (MODE == 1 && m == 19) {
           __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -336,7 +340,7 @@ __device__ __forceinline__ void x2_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8
         if (MODE == 1 && m >= 57 && (m - 57) % 6 == 0 && (m - 57) / 6 < 8)
           ob.issue_s(X + A_BYTES, (m - 57) / 6, sob, wave);
         if (MODE != 3 && m == 96) {
-          if constexpr (MODE == 1) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+          if constexpr (MODE == 1) mxk::vm_wait_n<(VMX >= 0 ? VMX : 15)>();
           else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
         }
@@ -353,12 +357,13 @@ __device__ __forceinline__ void x2_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8
 
 // SCHED 1: the same K-tile at hipBLASLt's instruction positions
 // (mxk::SchedHB; a "read" is one operand fragment as above).
-template <class S, bool AN, bool BN, int PAR, int MODE>
+template <class S, bool AN, bool BN, int PAR, int MODE, int VMX = -1, class HOOK = mxk::NoHook>
 __device__ __forceinline__ void x2_ktile_tab(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                              bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                              bf16x8_t (&f1b)[8], char* smem, const XOp<AN>& oa,
                                              const XOp<BN>& ob, int wm, int wn, uint32_t soa,
-                                             uint32_t sob, int wave, int par = 0) {
+                                             uint32_t sob, int wave, int par = 0,
+                                             const HOOK& hook = HOOK{}) {
   constexpr int A_BYTES = XOp<AN>::BYTES;
   constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
   const int px = PAR == 2 ? par : PAR;
@@ -373,6 +378,7 @@ __device__ __forceinline__ void x2_ktile_tab(f32x4_t (&acc)[8][8], bf16x8_t (&f0
         const int m = h * 64 + i * 8 + j;
         if (h == 0) xmfma(acc[i][j], f0b[j], f0a[i]);
         else xmfma(acc[i][j], f1b[j], f1a[i]);
+        hook(m);
         if (S::a1(m) >= 0) f1a[S::a1(m)] = oa.frag(X, wm * 8 + S::a1(m), 1);
         if (MODE == 1 && m == S::W1) __builtin_amdgcn_s_waitcnt(0xC07F);
         if (MODE == 1 && m == S::B1) __builtin_amdgcn_s_barrier();
@@ -383,8 +389,7 @@ __device__ __forceinline__ void x2_ktile_tab(f32x4_t (&acc)[8][8], bf16x8_t (&f0
         if (MODE == 1 && S::bdma(m) >= 0) ob.issue_s(X + A_BYTES, S::bdma(m), sob, wave);
         if (MODE != 3 && m == S::W3) {
           if constexpr (MODE == 1) {
-            static_assert(S::VM3 == 13, "x2 tables: add the vmcnt");
-            asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+            mxk::vm_wait_n<(VMX >= 0 ? VMX : S::VM3)>();
           } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           }
@@ -400,17 +405,21 @@ __device__ __forceinline__ void x2_ktile_tab(f32x4_t (&acc)[8][8], bf16x8_t (&f0
   }
 }
 
-template <int SCHED, bool AN, bool BN, int PAR, int MODE>
+// VMD: how many vector-memory ops beyond the schedule's own pieces are
+// younger than the stage being waited for (trickle stores), added to its count.
+template <int SCHED, bool AN, bool BN, int PAR, int MODE, int VMD = 0, class HOOK = mxk::NoHook>
 __device__ __forceinline__ void x2_ktile_s(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                            bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                            bf16x8_t (&f1b)[8], char* smem, const XOp<AN>& oa,
                                            const XOp<BN>& ob, int wm, int wn, uint32_t soa,
-                                           uint32_t sob, int wave, int par = 0) {
+                                           uint32_t sob, int wave, int par = 0,
+                                           const HOOK& hook = HOOK{}) {
   if constexpr (SCHED == 1)
-    x2_ktile_tab<mxk::SchedHB, AN, BN, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn,
-                                                  soa, sob, wave, par);
+    x2_ktile_tab<mxk::SchedHB, AN, BN, PAR, MODE, (VMD ? mxk::SchedHB::VM3 + VMD : -1), HOOK>(
+        acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, soa, sob, wave, par, hook);
   else
-    x2_ktile<AN, BN, PAR, MODE>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, soa, sob, wave, par);
+    x2_ktile<AN, BN, PAR, MODE, (VMD ? 15 + VMD : -1), HOOK>(acc, f0a, f0b, f1a, f1b, smem, oa, ob,
+                                                           wm, wn, soa, sob, wave, par, hook);
 }
 
 // EPI 0: 8-B stores, 1: 16-B stores through LDS (whole lines), 2: SwiGLU backward, 3: SwiGLU
@@ -543,6 +552,151 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     mxk::store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
+// x2t: persistent x2 with the C store tail trickled into the next tile's
+// main loop (gemm_bf16.hip schedule 31, same mechanism): rows 64..127 of
+// each wave block leave as a burst after the next tile's prologue DMA, rows
+// 0..63 stay in 64 VGPRs and go out one whole-line store per K-tile in the
+// next tile's first 16 K-tiles.  Needs K >= 18 * 64 (the launcher falls
+// back to x2 below that).
+template <int Q, int SCHED, bool AN, bool BN>
+__device__ __forceinline__ void x2_trickle(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
+                                           bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
+                                           bf16x8_t (&f1b)[8], char* smem, const XOp<AN>& oa,
+                                           const XOp<BN>& ob, int wm, int wn, uint32_t& sa,
+                                           uint32_t& sb, uint32_t ka, uint32_t kb, int wave,
+                                           const u32x4_t (&buf)[16], uint16_t* tp, size_t tstride) {
+  using H = mxk::TrickleStoreT<false>;
+  const H h0{buf[Q], tp + Q * tstride};
+  const H h1{buf[Q + 1], tp + (Q + 1) * tstride};
+  // K-tile 0: the 16 burst stores and its own trickle store are younger than stage 1
+  x2_ktile_s<SCHED, AN, BN, 0, 1, (Q == 0 ? 17 : 1), H>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm,
+                                                        wn, sa, sb, wave, 0, h0);
+  x2_ktile_s<SCHED, AN, BN, 1, 1, 1, H>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa + ka,
+                                        sb + kb, wave, 0, h1);
+  sa += 2 * ka;
+  sb += 2 * kb;
+  if constexpr (Q + 2 < 16)
+    x2_trickle<Q + 2, SCHED, AN, BN>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, ka, kb,
+                                     wave, buf, tp, tstride);
+}
+
+template <bool AN, bool BN, int SCHED>
+__global__ void __launch_bounds__(XT, 1)
+mxk_gemm_bf16_x2t_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                         uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  constexpr int A_BYTES = XOp<AN>::BYTES;
+  constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
+  static_assert(4 * mxk::kStoreLdsWave <= 2 * STAGE, "LDS slice per wave");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1;
+  const int wn = wave & 1;
+  const int tiles_m = M / XBM, tiles_n = N / XBM;
+  const int ntiles = tiles_m * tiles_n;
+  const int ns = K / XBK;                       // >= 18 (launcher)
+  const int rr = lane >> 4, cc = (lane & 15) * 8;
+  const size_t tstride = static_cast<size_t>(4) * ldc;
+
+  int t = blockIdx.x;
+  int m0, n0;
+  mxk::w4b_tile<1>(t, ntiles, tiles_m, tiles_n, &m0, &n0);
+  XOp<AN> oa;
+  XOp<BN> ob;
+  auto setup = [&]() {
+    oa.init(A, lda, m0, K, lane, wave);
+    ob.init(B, ldb, n0, K, lane, wave);
+    oa.set_lds(smem, mxk::lds_addr32(smem));
+    ob.set_lds(smem, mxk::lds_addr32(smem));
+  };
+  setup();
+  const uint32_t ka = oa.kstep(), kb = ob.kstep();
+  auto prologue = [&]() {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) oa.issue_s(smem, p, 0, wave);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) ob.issue_s(smem + A_BYTES, p, 0, wave);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) oa.issue_s(smem + STAGE, p, ka, wave);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) ob.issue_s(smem + STAGE + A_BYTES, p, kb, wave);
+  };
+  prologue();
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  u32x4_t buf[16];
+  uint16_t* tp = C;
+  bool trickle = false;
+  while (true) {
+    f32x4_t acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f0b[j] = ob.frag(smem + A_BYTES, wn * 8 + j, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f0a[i] = oa.frag(smem, wm * 8 + i, 0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+
+    int s = 0;
+    uint32_t sa = 2 * ka, sb = 2 * kb;
+    if (trickle) {
+      x2_trickle<0, SCHED, AN, BN>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, ka, kb,
+                                   wave, buf, tp, tstride);
+      s = 16;
+    }
+    for (; s + 2 <= ns - 2; s += 2) {
+      x2_ktile_s<SCHED, AN, BN, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, wave);
+      x2_ktile_s<SCHED, AN, BN, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa + ka,
+                                      sb + kb, wave);
+      sa += 2 * ka;
+      sb += 2 * kb;
+    }
+    if (s < ns - 2) {
+      x2_ktile_s<SCHED, AN, BN, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, wave);
+      ++s;
+    }
+    x2_ktile_s<SCHED, AN, BN, 2, 2>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
+    ++s;
+    x2_ktile_s<SCHED, AN, BN, 2, 3>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mxk::mfma_drain(acc);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+
+    char* lds = smem + wave * mxk::kStoreLdsWave;
+    uint16_t* row0 = C + static_cast<size_t>(m0 + wm * 128 + rr) * ldc + n0 + wn * 128 + cc;
+    const int tn = t + static_cast<int>(gridDim.x);
+    u32x4_t hi[16];
+    mxk::stage_half(acc, 0, lane, lds, buf);
+    mxk::stage_half(acc, 1, lane, lds, hi);
+    if (tn >= ntiles) {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        *reinterpret_cast<u32x4_t*>(row0 + it * tstride) = buf[it];
+        *reinterpret_cast<u32x4_t*>(row0 + (16 + it) * tstride) = hi[it];
+      }
+      break;
+    }
+    tp = row0;
+    __builtin_amdgcn_s_barrier();                     // every wave read its slice back
+    t = tn;
+    mxk::w4b_tile<1>(t, ntiles, tiles_m, tiles_n, &m0, &n0);
+    setup();
+    prologue();
+#pragma unroll
+    for (int it = 0; it < 16; ++it) *reinterpret_cast<u32x4_t*>(tp + (16 + it) * tstride) = hi[it];
+    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // stage 0 (stage 1 + 16 stores in flight)
+    __builtin_amdgcn_s_barrier();
+    trickle = true;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // C tile of split pair t = ws[2t] + ws[2t + 1]; grid (32, tail tiles), each
 // thread 8 consecutive columns of one row (two 8-B stores: ldc % 4 == 0).
 __global__ void __launch_bounds__(256)
@@ -594,6 +748,24 @@ static void launch_x(int sched, bool wide, int nwg, hipStream_t stream, const ui
 MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,
                              int lda, int ldb, int ldc, hipStream_t stream);
 
+namespace {
+int device_cus();
+}
+
+// x2t: persistent trickle-store layout kernel, one workgroup per CU at most
+template <bool AN, bool BN>
+static void launch_xt(int sched, int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b,
+                      uint16_t* c, int M, int N, int K, int lda, int ldb, int ldc) {
+  const int cus = device_cus();
+  const int grid = nwg < cus ? nwg : cus;
+  if (sched == 1)
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2t_kernel<AN, BN, 1>), dim3(grid), dim3(XT), 0, stream, a, b,
+                       c, M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((mxk_gemm_bf16_x2t_kernel<AN, BN, 0>), dim3(grid), dim3(XT), 0, stream, a, b,
+                       c, M, N, K, lda, ldb, ldc);
+}
+
 // a_kmajor: A stored [M][K] (1) or [K][M] (0); b_kmajor: B stored [N][K] (1)
 // or [K][N] (0).  Row strides lda/ldb/ldc in elements.  Tiles exactly:
 // M % 256, N % 256, K % 64; returns hipErrorInvalidValue otherwise (callers
@@ -603,6 +775,8 @@ MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int 
 //     (+2-10 % on the Llama-3-8B wgrad shapes); mixed (dgrad) -> x2
 //   2 x2 at hipBLASLt's positions, 3 x2, 0 the one-barrier x kernel
 //   (2, 3 and 0 run every layout on the layout kernel, for A/B)
+//   4 x2t (persistent, trickled C stores; variant 1's schedule per layout,
+//     hipBLASLt positions for TN; x2 when K < 18 * 64)
 MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int M, int N, int K,
                                      int lda, int ldb, int ldc, int a_kmajor, int b_kmajor,
                                      int variant, hipStream_t stream) {
@@ -614,8 +788,27 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                   (b_kmajor || bytes(K, ldb) < (1L << 32)) &&
                   reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(C) % 8 == 0 && variant >= 0 && variant <= 3;
+                  reinterpret_cast<uintptr_t>(C) % 8 == 0 && variant >= 0 && variant <= 4;
   if (!ok) return static_cast<int>(hipErrorInvalidValue);
+  if (variant == 1 && a_kmajor && b_kmajor)
+    return mxk_gemm_bf16_tn(A, B, C, M, N, K, lda, ldb, ldc, stream);
+  if (variant == 4 && K >= 18 * XBK && (ldc % 8 == 0) && reinterpret_cast<uintptr_t>(C) % 16 == 0) {
+    const int xs = (a_kmajor == b_kmajor) ? 1 : 0;
+    const int xn = (M / XBM) * (N / XBM);
+    auto a = static_cast<const uint16_t*>(A);
+    auto b = static_cast<const uint16_t*>(B);
+    auto c = static_cast<uint16_t*>(C);
+    if (a_kmajor && b_kmajor)
+      launch_xt<false, false>(xs, xn, stream, a, b, c, M, N, K, lda, ldb, ldc);
+    else if (a_kmajor)
+      launch_xt<false, true>(xs, xn, stream, a, b, c, M, N, K, lda, ldb, ldc);
+    else if (b_kmajor)
+      launch_xt<true, false>(xs, xn, stream, a, b, c, M, N, K, lda, ldb, ldc);
+    else
+      launch_xt<true, true>(xs, xn, stream, a, b, c, M, N, K, lda, ldb, ldc);
+    MXK_RETURN_LAUNCH_STATUS();
+  }
+  if (variant == 4) variant = 1;
   if (variant == 1 && a_kmajor && b_kmajor)
     return mxk_gemm_bf16_tn(A, B, C, M, N, K, lda, ldb, ldc, stream);
   const int sched = variant == 0 ? -1 : variant == 2 ? 1 : variant == 3 ? 0

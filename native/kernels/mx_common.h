@@ -258,6 +258,70 @@ __device__ __forceinline__ void store_block_lds(const f32x4_t (&acc)[8][8], uint
   }
 }
 
+// s_waitcnt vmcnt(N) with a compile-time N (the "memory" clobber keeps the
+// compiler from moving LDS / global accesses across it)
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// K-tile hook that does nothing (the K-tile bodies call hook(m) after MFMA m)
+struct NoHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+// ---- trickled C stores (persistent GEMMs, gemm_bf16.hip schedule 31/32 and
+// the layout kernel's x2t): a finished tile's C leaves partly as one
+// whole-line store per K-tile of the next tile.
+template <bool NT = true>
+struct TrickleStoreT {
+  u32x4_t v;
+  uint16_t* p;
+  __device__ __forceinline__ void operator()(int m) const {
+    if (m == 3) {
+      if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
+      else *reinterpret_cast<u32x4_t*>(p) = v;
+    }
+  }
+};
+using TrickleStore = TrickleStoreT<true>;
+
+// LDS-held part (schedule 32): read after MFMA 1, stored after MFMA 9
+struct TrickleLds {
+  const char* src;
+  uint16_t* p;
+  u32x4_t& v;
+  __device__ __forceinline__ void operator()(int m) const {
+    if (m == 1) v = *reinterpret_cast<const u32x4_t*>(src);
+    if (m == 9) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
+  }
+};
+
+// rows 64 p .. 64 p + 63 of the wave's 128 x 128 block through the LDS slice
+// (schedule 26's layout, mx_common.h store_block_lds) into 16 whole-line
+// vectors per lane: vector it is row 4 it + (lane >> 4), 8 columns at
+// 8 (lane & 15).
+__device__ __forceinline__ void stage_half(const f32x4_t (&acc)[8][8], int p, int lane, char* lds,
+                                           u32x4_t (&out)[16]) {
+  const int crow = lane & 15, q = lane >> 4;
+  const int rr = lane >> 4, cc = (lane & 15) * 8;
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint2 pk;
+      pk.x = pack2bf(acc[4 * p + ii][j][0], acc[4 * p + ii][j][1]);
+      pk.y = pack2bf(acc[4 * p + ii][j][2], acc[4 * p + ii][j][3]);
+      *reinterpret_cast<uint2*>(lds + (ii * 16 + crow) * kStoreLdsRow + (j * 16 + q * 4) * 2) = pk;
+    }
+#pragma unroll
+  for (int it = 0; it < 16; ++it)
+    out[it] = *reinterpret_cast<const u32x4_t*>(lds + (it * 4 + rr) * kStoreLdsRow + cc * 2);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __asm__ volatile("" ::: "memory");
+}
+
 // Fused SwiGLU-backward epilogue of the down-projection's input-gradient GEMM:
 // the block's accumulators are d(act) = dY W2 for act = silu(g) * u, and the
 // lane's 4 consecutive columns of row r are combined with g, u read from
