@@ -1183,6 +1183,21 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
       mxk_gemm_bf16_ex_variant(A, Bt, C, M, N, K, lda, ldb, ldc, 1, 1, 2, stream);
       break;
     case 26: launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 31:
+    case 32: {
+      if (K < (v == 31 ? 18 : 26) * BK) {   // fewer K-tiles than the trickle phase needs
+        launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
+        break;
+      }
+      const int grid = nwg < num_cus() ? nwg : num_cus();
+      if (v == 31)
+        hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4t<1, false>), dim3(grid), dim3(W4_THREADS), 0, stream,
+                           a, b, c, M, N, K, lda, ldb, ldc);
+      else
+        hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4t<1, true>), dim3(grid), dim3(W4_THREADS), 0, stream,
+                           a, b, c, M, N, K, lda, ldb, ldc);
+      break;
+    }
 #ifdef MXK_GEMM_EXPERIMENTS
     case 2: launch_w4i<1, 1, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 3: launch_w4i<1, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
@@ -1211,21 +1226,6 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 28: launch_w4i<1, 4, 1, 0, 8>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 29: mxk_gemm_bf16_tn_ring_launch(4, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 30: mxk_gemm_bf16_tn_ring_launch(5, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
-    case 31:
-    case 32: {
-      if (K < (v == 31 ? 18 : 26) * BK) {   // fewer K-tiles than the trickle phase needs
-        launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc);
-        break;
-      }
-      const int grid = nwg < num_cus() ? nwg : num_cus();
-      if (v == 31)
-        hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4t<1, false>), dim3(grid), dim3(W4_THREADS), 0, stream,
-                           a, b, c, M, N, K, lda, ldb, ldc);
-      else
-        hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4t<1, true>), dim3(grid), dim3(W4_THREADS), 0, stream,
-                           a, b, c, M, N, K, lda, ldb, ldc);
-      break;
-    }
     case 19:
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_pp8<1, 0>), dim3(nwg), dim3(PP_THREADS), 0, stream, a, b,
                          c, M, N, K, lda, ldb, ldc);
@@ -1250,14 +1250,14 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
 }
 
 // Production builds carry the default (26), its base schedule (6), the
-// first structure (0), the 8-byte-store fallback (1) and the layout kernel
-// (9); every other schedule is an A/B record, built only with
+// first structure (0), the 8-byte-store fallback (1), the layout kernel (9)
+// and the trickle-store schedule (31); every other schedule is an A/B record, built only with
 // -DMXK_GEMM_EXPERIMENTS (`make gemm-exp` -> libmxkernels_exp.so).
 bool variant_built(int v) {
 #ifdef MXK_GEMM_EXPERIMENTS
   return v >= 0 && v < kNumVariants;
 #else
-  return v == 0 || v == 1 || v == 6 || v == 9 || v == 26;
+  return v == 0 || v == 1 || v == 6 || v == 9 || v == 26 || v == 31;
 #endif
 }
 

@@ -558,7 +558,7 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
 // 0..63 stay in 64 VGPRs and go out one whole-line store per K-tile in the
 // next tile's first 16 K-tiles.  Needs K >= 18 * 64 (the launcher falls
 // back to x2 below that).
-template <int Q, int SCHED, bool AN, bool BN>
+template <int Q, int NB, int SCHED, bool AN, bool BN>
 __device__ __forceinline__ void x2_trickle(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                            bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                            bf16x8_t (&f1b)[8], char* smem, const XOp<AN>& oa,
@@ -575,12 +575,12 @@ __device__ __forceinline__ void x2_trickle(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)
                                         sb + kb, wave, 0, h1);
   sa += 2 * ka;
   sb += 2 * kb;
-  if constexpr (Q + 2 < 16)
-    x2_trickle<Q + 2, SCHED, AN, BN>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, ka, kb,
+  if constexpr (Q + 2 < NB)
+    x2_trickle<Q + 2, NB, SCHED, AN, BN>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, ka, kb,
                                      wave, buf, tp, tstride);
 }
 
-template <bool AN, bool BN, int SCHED>
+template <bool AN, bool BN, int SCHED, int NB = (AN && BN ? 8 : AN ? 12 : 16)>
 __global__ void __launch_bounds__(XT, 1)
 mxk_gemm_bf16_x2t_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                          uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -626,7 +626,8 @@ mxk_gemm_bf16_x2t_kernel(const uint16_t* __restrict__ A, const uint16_t* __restr
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  u32x4_t buf[16];
+  static_assert(NB % 2 == 0 && NB <= 16, "trickle vectors");
+  u32x4_t buf[16];                                    // 0..NB-1 trickled
   uint16_t* tp = C;
   bool trickle = false;
   while (true) {
@@ -645,9 +646,9 @@ mxk_gemm_bf16_x2t_kernel(const uint16_t* __restrict__ A, const uint16_t* __restr
     int s = 0;
     uint32_t sa = 2 * ka, sb = 2 * kb;
     if (trickle) {
-      x2_trickle<0, SCHED, AN, BN>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, ka, kb,
-                                   wave, buf, tp, tstride);
-      s = 16;
+      x2_trickle<0, NB, SCHED, AN, BN>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, ka,
+                                       kb, wave, buf, tp, tstride);
+      s = NB;
     }
     for (; s + 2 <= ns - 2; s += 2) {
       x2_ktile_s<SCHED, AN, BN, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, sa, sb, wave);
@@ -682,6 +683,10 @@ mxk_gemm_bf16_x2t_kernel(const uint16_t* __restrict__ A, const uint16_t* __restr
       }
       break;
     }
+    // vectors beyond NB go out now, ahead of the next prologue (the stage-0
+    // wait then covers them, so no count below changes)
+#pragma unroll
+    for (int it = NB; it < 16; ++it) *reinterpret_cast<u32x4_t*>(row0 + it * tstride) = buf[it];
     tp = row0;
     __builtin_amdgcn_s_barrier();                     // every wave read its slice back
     t = tn;

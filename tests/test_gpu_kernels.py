@@ -277,6 +277,35 @@ def test_gemm_layouts_vs_fp32(cuda_device, layout, variant, M, N, K):
     assert not gemm_bf16_ex(a[:, :-64] if ak else a[:-64], b, ak, bk, out, variant=variant)
 
 
+@pytest.mark.parametrize("layout", ["tn", "nn", "nt_wgrad", "tt"])
+@pytest.mark.parametrize("M,N,K", [(4608, 4608, 1152), (8192, 8192, 2048), (1024, 768, 1216)])
+def test_gemm_trickle_store_layouts_vs_fp32(cuda_device, layout, M, N, K):
+    """Persistent trickle-store layout kernel (ex variant 4): 324 tiles on the
+    CUs (some workgroups one tile, some two: the trickle phase runs for some,
+    not others), 1024 tiles (four per CU, three trickle phases each) and a
+    grid smaller than the chip; K at and above the 18-K-tile minimum.  The
+    WHOLE output against fp32."""
+    from mxk8s.ops.gemm import gemm_bf16_ex
+    g = torch.Generator(device=cuda_device).manual_seed(13)
+    r = lambda *s: (torch.rand(*s, device=cuda_device, generator=g) * 2 - 1).bfloat16()  # noqa: E731
+    if layout == "tn":
+        a, b, ak, bk = r(M, K), r(N, K), True, True
+        ref = a.float() @ b.float().t()
+    elif layout == "nn":
+        a, b, ak, bk = r(M, K), r(K, N), True, False
+        ref = a.float() @ b.float()
+    elif layout == "tt":
+        a, b, ak, bk = r(K, M), r(N, K), False, True
+        ref = a.float().t() @ b.float().t()
+    else:
+        a, b, ak, bk = r(K, M), r(K, N), False, False
+        ref = a.float().t() @ b.float()
+    out = torch.full((M, N), float("nan"), device=cuda_device, dtype=torch.bfloat16)
+    assert gemm_bf16_ex(a, b, ak, bk, out, variant=4)
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 2 ** -7 * ref.abs().max().item() + 1e-3, err
+
+
 @pytest.mark.parametrize("layout", ["nn", "nt_wgrad", "tt"])
 @pytest.mark.parametrize("M,N,K", [(2048, 2048, 1024), (6144, 4096, 1024), (4096, 14336, 2048)])
 def test_gemm_split_tail_vs_fp32(cuda_device, layout, M, N, K):

@@ -90,3 +90,22 @@ def test_detector_flags_a_close_accumulator_spill():
            "\ts_mov_b32 s0, 1\n\tscratch_store_dwordx4 off, a[252:255], off offset:4\n"
            ".Lfunc_end0:\n")
     assert close_accumulator_reads(asm) == {"_Zbar": 1}
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src", ["gemm_bf16.hip", "gemm_bf16_layouts.hip"])
+def test_counted_wait_gemms_do_not_spill(src, tmp_path):
+    """The GEMM loops wait for their LDS-DMA stages with COUNTED vmcnt waits
+    (all but the N youngest vector-memory ops).  A register spill or reload
+    is a vector-memory op the count does not expect: a reload inside the loop
+    lets the wait pass one DMA piece early (seen: the trickle-store layout
+    kernel's wgrad instance at 10 spills gave wrong tiles, the 9 without
+    spills were exact).  Every shipped counted-wait GEMM kernel: no spills."""
+    asm = _asm(src, str(tmp_path / (src + ".s")))
+    names = re.findall(r"^\s+\.name:\s+(_Z\S+)", asm, re.M)
+    counts = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s+(\d+)", asm)]
+    assert len(names) == len(counts) and names
+    pat = re.compile(r"mxk_gemm_bf16_(tn_w4t|x2t_kernel|tn_w4i|x2_kernel)")
+    checked = {n: c for n, c in zip(names, counts) if pat.search(n)}
+    assert checked, "no counted-wait GEMM kernel found"
+    assert {n: c for n, c in checked.items() if c} == {}
