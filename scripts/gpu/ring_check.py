@@ -31,8 +31,13 @@ for M, N, K in shapes:
         ok_all &= ok
         where = ""
         if not ok and bad:
-            idx = (err > tol).nonzero()[:4].tolist()
-            where = f" first bad (row,col) {idx}"
+            nz = (err > tol).nonzero()
+            idx = nz[:4].tolist()
+            r, c = nz[:, 0], nz[:, 1]
+            where = (f" first bad (row,col) {idx} rows [{int(r.min())}, {int(r.max())}]"
+                     f" cols [{int(c.min())}, {int(c.max())}] distinct tiles "
+                     f"{sorted(set((int(a) // 256, int(b) // 256) for a, b in nz[::97].tolist()))[:8]}"
+                     f" rows%128 {sorted(set((r % 128).tolist()))[:40]}")
         print(f"v{v} {M}x{N}x{K}: status {st} max_err {e:.4g} tol {tol:.3g} bad {bad}{where}",
               flush=True)
 print("ALL OK" if ok_all else "FAILURES", flush=True)
