@@ -1,12 +1,13 @@
 #!/usr/bin/env bash
 # End-of-round GPU pass: the full GPU test tier, the driver's smoke(), the
-# headline bench at the driver's arguments, the DDP step and its kernel
-# profile.  Every step has its own time limit; the first failure ends the call.
+# headline bench at the driver's arguments, the DDP step, and the DDP step's
+# steady-state kernel breakdown (kernel trace bounded by the bench.timed roctx
+# range).  Every step has its own time limit; the first failure ends the call.
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 R=$PWD
-mkdir -p gpurun_out/final
-O=gpurun_out/final
+O=${1:-gpurun_out/final}
+mkdir -p "$O"
 export PYTHONPATH=$R${PYTHONPATH:+:$PYTHONPATH}
 step() {   # name, seconds, command...
   local name=$1 secs=$2
@@ -17,12 +18,7 @@ step() {   # name, seconds, command...
   tail -2 "$O/$name.out"
   [ $rc -eq 0 ] || exit $rc
 }
-step pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+step pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
 step bench_driver_args 300 python3 bench.py --steps 20 --warmup 5
 step bench_ddp 400 python3 bench.py --mode ddp --steps 10 --warmup 3
-cd /tmp
-export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_ddp -o run -- \
-  python3 $R/bench.py --mode ddp --steps 4 --warmup 2 > $R/$O/prof_ddp.out 2> $R/$O/prof_ddp.err
-rc=$?; echo "prof_ddp rc=$rc"; exit $rc
