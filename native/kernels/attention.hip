@@ -629,6 +629,299 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
 }
 
 // ---------------------------------------------------------------------------
+// Forward, 8-wave ping-pong (variant 5).  The kernels above run each wave's
+// QK^T MFMAs, its softmax (VALU, ~700 issue cycles per 64-key tile: 32 v_exp
+// at 8 cycles each, scale/shift, row max and sum, bf16 packs) and its PV
+// MFMAs back to back, and all four waves of a workgroup pass the same
+// barriers, so a SIMD's matrix pipe idles whenever its waves are in the
+// softmax (PMC: MFMA busy 40 %, VALU/MFMA co-execution 13 %).
+// Here one 512-thread workgroup = 8 waves x 32 query rows (256 rows of one
+// (batch, q-head)); SIMD s holds wave s (group A, rows 32 s ..) and wave s + 4
+// (group B, rows 128 + 32 s ..).  Both groups run the same per-tile sequence
+//     M_j: S_j = K_j . Q^T (16 MFMAs) and O += V_{j-1}^T . P_{j-1} (16 MFMAs)
+//     S_j: mask, row max, lazy rescale of O, exp2, row sum, P_j to bf16
+// one phase apart, with one workgroup barrier per phase: while group A is in
+// M_j, group B is in S_{j-1}, and the other way round, so every SIMD pairs
+// one wave's matrix work with its partner's softmax (the FA3 ping-pong, here
+// between the two waves of a SIMD).  K and V tiles arrive by LDS-DMA into
+// 3-slot rings (K_j is read in phases 2j / 2j+1, V_j in 2j+2 / 2j+3): at
+// every even phase 2i each wave issues its 4 pieces of K_{i+2} and V_{i+1},
+// and waits for them (counted vmcnt, 4 pieces left in flight) at the end of
+// phase 2i+3.  Math, LDS image, swizzle and operand mapping are variant 4's.
+// Causal: tile j is skipped by a wave whose 32 rows all precede key 64 j
+// (the workgroup still walks every phase: one barrier schedule).
+namespace {
+constexpr int PP_BQ = 256;     // query rows per workgroup (8 waves x 32)
+constexpr int PP_NT = 512;
+constexpr int PP_SLOTS = 3;    // K ring and V ring depth
+}  // namespace
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(PP_NT, 1)
+mxk_attn_fwd_pp_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                       const uint16_t* __restrict__ v, uint16_t* __restrict__ o,
+                       float* __restrict__ lse, int S, int Hq, int Hkv, long q_tok, long k_tok,
+                       long v_tok, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * PP_SLOTS * TILE_BYTES];   // K ring | V ring
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2;
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  const int nqb = S / PP_BQ;
+  int bh, qb;
+  map_block_xcd(blockIdx.x, gridDim.x, nqb, Hq / Hkv, CAUSAL, &bh, &qb);
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hkv = hq / (Hq / Hkv);
+  const int q0 = qb * PP_BQ;
+  const int qw0 = q0 + wave * 32;
+  const int myq = qw0 + r32;
+
+  const uint16_t* qb_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
+  const uint16_t* kb_ptr = k + static_cast<long>(b) * S * k_tok + static_cast<long>(hkv) * D;
+  const uint16_t* vb_ptr = v + static_cast<long>(b) * S * v_tok + static_cast<long>(hkv) * D;
+
+  bf16x8_t qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    qf[s] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + static_cast<long>(myq) * q_tok + 16 * s + 8 * h);
+
+  const int n = (CAUSAL ? min(S, q0 + PP_BQ) : S) / BKV;
+
+  // DMA: wave w moves the 1-KiB pieces g = 2w, 2w + 1 (rows 4g .. 4g + 3) of
+  // each tile; lane i lands at row 4g + (i >> 4), slot i & 15, so it fetches
+  // chunk (i & 15) ^ ((i >> 4) << 2 | (g & 3)) (the swz() image).
+  const mxk::u32x4 rk = mxk::make_rsrc(kb_ptr, static_cast<unsigned>(S * k_tok * 2));
+  const mxk::u32x4 rv = mxk::make_rsrc(vb_ptr, static_cast<unsigned>(S * v_tok * 2));
+  const int prow = lane >> 4, pslot = lane & 15;
+  uint32_t kvo[2], vvo[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int g = 2 * wave + p;
+    const int row = 4 * g + prow;
+    const int ch = pslot ^ ((prow << 2) | (g & 3));
+    kvo[p] = static_cast<uint32_t>(row * k_tok * 2 + ch * 16);
+    vvo[p] = static_cast<uint32_t>(row * v_tok * 2 + ch * 16);
+  }
+  const uint32_t k_step = static_cast<uint32_t>(BKV * k_tok * 2);
+  const uint32_t v_step = static_cast<uint32_t>(BKV * v_tok * 2);
+  const uint32_t sm32 = mxk::lds_addr32(&smem[0]);
+  auto issue_k = [&](int j) {
+    const uint32_t d = sm32 + (j % PP_SLOTS) * TILE_BYTES + (2 * wave) * 1024;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) mxk::dma16m(rk, d + p * 1024, kvo[p], j * k_step);
+  };
+  auto issue_v = [&](int j) {
+    const uint32_t d = sm32 + (PP_SLOTS + j % PP_SLOTS) * TILE_BYTES + (2 * wave) * 1024;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) mxk::dma16m(rv, d + p * 1024, vvo[p], j * v_step);
+  };
+  issue_k(0);
+  issue_v(0);
+  if (n > 1) issue_k(1);
+
+  int koff[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) koff[s] = swz(r32, 2 * s + h);
+  const int G = lane >> 4, i16 = lane & 15;
+  const int tr_key = 4 * h + (i16 >> 2);
+  const int tr_ch = 2 * (G & 1) + ((i16 & 3) >> 1);
+  const int tr_byte = 8 * (i16 & 1);
+  int voff[4][2];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    voff[db][0] = swz(tr_key, 4 * db + tr_ch) + tr_byte;
+    voff[db][1] = swz(tr_key + 8, 4 * db + tr_ch) + tr_byte;
+  }
+
+  const float c = scale * 1.4426950408889634f;   // scores -> log2 domain
+  const f32x2_t cc = {c, c};
+  float m = -INFINITY, l = 0.f;
+  f32x16_t acc[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[db][r] = 0.f;
+  f32x16_t s0, s1;
+  bf16x8_t pf[4];
+
+#pragma unroll
+  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]));
+  vm_wait0();   // Q, K_0, V_0, K_1
+  __syncthreads();
+
+  // tile j is active for this wave unless all its rows precede key 64 j;
+  // the active tiles are a prefix 0 .. na - 1
+  const int na = CAUSAL ? min(n, (qw0 + 31) / BKV + 1) : n;
+
+  // end of global phase ph: counted wait for the DMA this wave issued at
+  // phase ph - 3 (odd ph), the workgroup barrier, then the next even phase's
+  // DMA (K_{i+2}, V_{i+1} at phase 2i)
+  auto issue_for = [&](int ph) {
+    const int i = ph >> 1;
+    if (i + 2 < n) issue_k(i + 2);
+    if (i + 1 < n) issue_v(i + 1);
+  };
+  auto end_phase = [&](int ph) {
+    if ((ph & 1) && ph >= 3) {
+      if (((ph - 3) >> 1) + 3 < n) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS reads retired
+    __builtin_amdgcn_s_barrier();
+    if (ph & 1) issue_for(ph + 1);
+  };
+
+  // operands are read one group ahead of their MFMAs (two-slot rings:
+  // K 4 x b128 per k-step pair, V^T 4 x (2 transposed b64) per db); the
+  // sched_barrier fences keep the compiler from hoisting every read of the
+  // phase (64 + 64 VGPRs) ahead of the first MFMA
+  auto qk = [&](int j) {
+    const char* kt = smem + (j % PP_SLOTS) * TILE_BYTES;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
+    bf16x8_t ka[2][4];
+    auto read_k = [&](int pr, int slot) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        ka[slot][2 * e] = lds_b128(kt + koff[2 * pr + e]);
+        ka[slot][2 * e + 1] = lds_b128(kt + koff[2 * pr + e] + 32 * 256);
+      }
+    };
+    read_k(0, 0);
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) {
+      if (pr < 3) read_k(pr + 1, (pr + 1) & 1);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        s0 = mfma32(ka[pr & 1][2 * e], qf[2 * pr + e], s0);
+        s1 = mfma32(ka[pr & 1][2 * e + 1], qf[2 * pr + e], s1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto pv = [&](int j) {
+    const char* vt = smem + (PP_SLOTS + j % PP_SLOTS) * TILE_BYTES;
+    bf16x8_t va[2][4];
+    auto read_v = [&](int db, int slot) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        va[slot][ks] = cat8(lds_tr_b64(vt + voff[db][0] + ks * 4096),
+                            lds_tr_b64(vt + voff[db][1] + ks * 4096));
+    };
+    read_v(0, 0);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      if (db < 3) read_v(db + 1, (db + 1) & 1);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) acc[db] = mfma32(va[db & 1][ks], pf[ks], acc[db]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  auto softmax = [&](int j) {
+    const int kv0 = j * BKV;
+    if (CAUSAL && kv0 + BKV - 1 > qw0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kv0 + crow(r, h);
+        if (key > myq) s0[r] = -INFINITY;
+        if (key + 32 > myq) s1[r] = -INFINITY;
+      }
+    }
+    float mx = s0[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s0[r]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s1[r]);
+    mx = half_max(mx);
+    float m_new = fmaxf(m, mx);
+    // lazy rescale (variant 4): keep the stale max unless the new one
+    // exceeds it by more than 2^8 in the exp2 domain
+    const bool grow = (m_new - m) * c > 8.f;
+    if (!grow) m_new = m;
+    const float alpha = grow ? fexp2((m - m_new) * c) : 1.f;
+    m = m_new;
+    if (__builtin_amdgcn_ballot_w64(grow)) {
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[db][r] *= alpha;
+    }
+    const f32x2_t nmc = {-m_new * c, -m_new * c};
+    f32x2_t ls2 = {0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      f32x2_t x0 = {s0[r], s0[r + 1]};
+      f32x2_t x1 = {s1[r], s1[r + 1]};
+      x0 = __builtin_elementwise_fma(x0, cc, nmc);
+      x1 = __builtin_elementwise_fma(x1, cc, nmc);
+      x0[0] = fexp2(x0[0]);
+      x0[1] = fexp2(x0[1]);
+      x1[0] = fexp2(x1[0]);
+      x1[1] = fexp2(x1[1]);
+      ls2 += x0 + x1;
+      s0[r] = x0[0];
+      s0[r + 1] = x0[1];
+      s1[r] = x1[0];
+      s1[r + 1] = x1[1];
+    }
+    l = l * alpha + (ls2[0] + ls2[1]);
+    pf[0] = pack8(s0, 0);
+    pf[1] = pack8(s0, 8);
+    pf[2] = pack8(s1, 0);
+    pf[3] = pack8(s1, 8);
+  };
+
+  // global phase ph: group A runs its local phase ph, group B ph - 1; local
+  // phase 2j is M_j = {QK_j, PV_{j-1}}, 2j + 1 is S_j; M_na is PV_{na-1}
+  // alone.  Barriers follow global phases 0 .. 2n (phase 2n + 1 is B's M_n).
+  issue_for(0);
+  int ph = 0;
+  if (grp) end_phase(ph++);
+  qk(0);
+  end_phase(ph++);
+  softmax(0);
+  end_phase(ph++);
+  for (int j = 1; j < na; ++j) {
+    qk(j);
+    pv(j - 1);
+    end_phase(ph++);
+    softmax(j);
+    end_phase(ph++);
+  }
+  pv(na - 1);
+  for (; ph <= 2 * n; ++ph) end_phase(ph);
+
+  const float lt = half_sum(l);
+  const float inv = 1.f / lt;
+  uint16_t* orow = o + (static_cast<long>(b) * S + myq) * Hq * D + static_cast<long>(hq) * D;
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int g0 = 2 * kk, g1 = 2 * kk + 1;
+      const uint32_t x0 = mxk::pack2bf(acc[db][4 * g0] * inv, acc[db][4 * g0 + 1] * inv);
+      const uint32_t x1 = mxk::pack2bf(acc[db][4 * g0 + 2] * inv, acc[db][4 * g0 + 3] * inv);
+      const uint32_t y0 = mxk::pack2bf(acc[db][4 * g1] * inv, acc[db][4 * g1 + 1] * inv);
+      const uint32_t y1 = mxk::pack2bf(acc[db][4 * g1 + 2] * inv, acc[db][4 * g1 + 3] * inv);
+      const auto p0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+      const auto p1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+      uint4 vv;
+      vv.x = p0[0];
+      vv.y = p1[0];
+      vv.z = p0[1];
+      vv.w = p1[1];
+      *reinterpret_cast<uint4*>(orow + 32 * db + 16 * kk + 8 * h) = vv;
+    }
+  }
+  if (h == 0) lse[(static_cast<long>(b) * Hq + hq) * S + myq] = m * scale + logf(lt);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA outlives the workgroup
+}
+
+// ---------------------------------------------------------------------------
 // variant: 0 = register-staged K/V, 1 = LDS-DMA with the loop unrolled by 2
 // (static LDS buffer), 2 = LDS-DMA, 3 = 2 with the PIPE body (operands read a
 // group ahead, exp of P chunk ks+1 under the PV MFMAs of chunk ks, lazy
@@ -642,7 +935,7 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
                                  long k_tok, long v_tok, float scale, int causal, int variant,
                                  hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv ||
-      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 4 ||
+      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 5 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) % 16)
     return static_cast<int>(hipErrorInvalidValue);
@@ -653,7 +946,16 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
   const auto* kp = static_cast<const uint16_t*>(k);
   const auto* vp = static_cast<const uint16_t*>(v);
   auto* op = static_cast<uint16_t*>(o);
-  if (variant == 4) {
+  if (variant == 5 && S % PP_BQ) variant = 4;
+  if (variant == 5) {
+    const int nwg5 = B * Hq * (S / PP_BQ);
+    if (causal)
+      hipLaunchKernelGGL(mxk_attn_fwd_pp_kernel<true>, dim3(nwg5), dim3(PP_NT), 0, stream, qp, kp,
+                         vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    else
+      hipLaunchKernelGGL(mxk_attn_fwd_pp_kernel<false>, dim3(nwg5), dim3(PP_NT), 0, stream, qp, kp,
+                         vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  } else if (variant == 4) {
     if (causal)
       hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<true, true, true>), dim3(nwg), dim3(NT), 0, stream,
                          qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
