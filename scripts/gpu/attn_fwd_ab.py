@@ -20,24 +20,25 @@ def main():
     qkv = torch.randn(B, S, (Hq + 2 * Hkv) * D, device=dev, generator=g).bfloat16()
     q, k, v = qkv.split([Hq * D, Hkv * D, Hkv * D], dim=-1)
     q, k, v = q.view(B, S, Hq, D), k.view(B, S, Hkv, D), v.view(B, S, Hkv, D)
-    outs = {vv: A.attn_fwd(q, k, v, causal=True, variant=vv) for vv in variants}
+    causal = os.environ.get("CAUSAL", "1") == "1"
+    outs = {vv: A.attn_fwd(q, k, v, causal=causal, variant=vv) for vv in variants}
     for vv in variants[1:]:
         same = all(torch.equal(x, y) for x, y in zip(outs[variants[0]], outs[vv]))
         print(f"RESULT variant={vv} bit-identical to variant={variants[0]}: {same}", flush=True)
-    fl = 4 * B * Hq * S * S * D / 2
+    fl = 4 * B * Hq * S * S * D / (2 if causal else 1)
     ts = {vv: [] for vv in variants}
     for _ in range(10):
         for vv in variants:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(5):
-                A.attn_fwd(q, k, v, causal=True, variant=vv)
+                A.attn_fwd(q, k, v, causal=causal, variant=vv)
             e.record()
             e.synchronize()
             ts[vv].append(s.elapsed_time(e) / 5)
     for vv, t in ts.items():
         m = statistics.median(t[2:])
-        print(f"RESULT fwd variant={vv} B={B} ms={m:.4f} tflops={fl / m / 1e9:.1f}", flush=True)
+        print(f"RESULT fwd causal={int(causal)} variant={vv} B={B} ms={m:.4f} tflops={fl / m / 1e9:.1f}", flush=True)
 
 
 if __name__ == "__main__":
