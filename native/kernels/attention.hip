@@ -656,7 +656,7 @@ constexpr int PP_NT = 512;
 constexpr int PP_SLOTS = 3;    // K ring and V ring depth
 }  // namespace
 
-template <bool CAUSAL>
+template <bool CAUSAL, bool PRIO = false, int DIAG = 0>
 __global__ void __launch_bounds__(PP_NT, 1)
 mxk_attn_fwd_pp_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                        const uint16_t* __restrict__ v, uint16_t* __restrict__ o,
@@ -779,6 +779,11 @@ mxk_attn_fwd_pp_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   // sched_barrier fences keep the compiler from hoisting every read of the
   // phase (64 + 64 VGPRs) ahead of the first MFMA
   auto qk = [&](int j) {
+    if constexpr (DIAG == 2) {   // timing ablation: no MFMAs
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s0[r] = qf[r >> 1][r & 7] * 1e-3f; s1[r] = s0[r] + j; }
+      return;
+    }
     const char* kt = smem + (j % PP_SLOTS) * TILE_BYTES;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
@@ -803,6 +808,11 @@ mxk_attn_fwd_pp_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     }
   };
   auto pv = [&](int j) {
+    if constexpr (DIAG == 2) {
+#pragma unroll
+      for (int db = 0; db < 4; ++db) acc[db][0] += static_cast<float>(pf[db][0]);
+      return;
+    }
     const char* vt = smem + (PP_SLOTS + j % PP_SLOTS) * TILE_BYTES;
     bf16x8_t va[2][4];
     auto read_v = [&](int db, int slot) {
@@ -822,6 +832,14 @@ mxk_attn_fwd_pp_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   };
 
   auto softmax = [&](int j) {
+    if constexpr (DIAG == 1) {   // timing ablation: P = packed raw scores
+      pf[0] = pack8(s0, 0);
+      pf[1] = pack8(s0, 8);
+      pf[2] = pack8(s1, 0);
+      pf[3] = pack8(s1, 8);
+      l += s0[0];
+      return;
+    }
     const int kv0 = j * BKV;
     if (CAUSAL && kv0 + BKV - 1 > qw0) {
 #pragma unroll
@@ -878,21 +896,34 @@ mxk_attn_fwd_pp_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   // global phase ph: group A runs its local phase ph, group B ph - 1; local
   // phase 2j is M_j = {QK_j, PV_{j-1}}, 2j + 1 is S_j; M_na is PV_{na-1}
   // alone.  Barriers follow global phases 0 .. 2n (phase 2n + 1 is B's M_n).
+  // PRIO (variant 6): a wave raises its priority for its MFMA phase.  The
+  // SIMD's vector-issue arbiter prefers the older wave at equal priority, so
+  // without it group A's softmax VALU (waves 0-3, older) takes the issue
+  // slots group B's MFMAs need and the two phases serialise (PMC of variant
+  // 5: MFMA busy 29 %, co-execution 4 % of SIMD cycles).
+  auto prio_hi = [&]() { if constexpr (PRIO) __builtin_amdgcn_s_setprio(1); };
+  auto prio_lo = [&]() { if constexpr (PRIO) __builtin_amdgcn_s_setprio(0); };
   issue_for(0);
   int ph = 0;
   if (grp) end_phase(ph++);
+  prio_hi();
   qk(0);
+  prio_lo();
   end_phase(ph++);
   softmax(0);
   end_phase(ph++);
   for (int j = 1; j < na; ++j) {
+    prio_hi();
     qk(j);
     pv(j - 1);
+    prio_lo();
     end_phase(ph++);
     softmax(j);
     end_phase(ph++);
   }
+  prio_hi();
   pv(na - 1);
+  prio_lo();
   for (; ph <= 2 * n; ++ph) end_phase(ph);
 
   const float lt = half_sum(l);
@@ -935,7 +966,7 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
                                  long k_tok, long v_tok, float scale, int causal, int variant,
                                  hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv ||
-      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 5 ||
+      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 8 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) % 16)
     return static_cast<int>(hipErrorInvalidValue);
@@ -946,15 +977,30 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
   const auto* kp = static_cast<const uint16_t*>(k);
   const auto* vp = static_cast<const uint16_t*>(v);
   auto* op = static_cast<uint16_t*>(o);
-  if (variant == 5 && S % PP_BQ) variant = 4;
-  if (variant == 5) {
+  if (variant >= 5 && S % PP_BQ) variant = 4;
+  if (variant >= 5) {
     const int nwg5 = B * Hq * (S / PP_BQ);
-    if (causal)
+    if (variant == 7 || variant == 8) {   // timing ablations (wrong outputs)
+      if (variant == 7)
+        hipLaunchKernelGGL((mxk_attn_fwd_pp_kernel<true, false, 1>), dim3(nwg5), dim3(PP_NT), 0,
+                           stream, qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+      else
+        hipLaunchKernelGGL((mxk_attn_fwd_pp_kernel<true, false, 2>), dim3(nwg5), dim3(PP_NT), 0,
+                           stream, qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    } else if (variant == 6) {
+      if (causal)
+        hipLaunchKernelGGL((mxk_attn_fwd_pp_kernel<true, true>), dim3(nwg5), dim3(PP_NT), 0, stream,
+                           qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+      else
+        hipLaunchKernelGGL((mxk_attn_fwd_pp_kernel<false, true>), dim3(nwg5), dim3(PP_NT), 0, stream,
+                           qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    } else if (causal) {
       hipLaunchKernelGGL(mxk_attn_fwd_pp_kernel<true>, dim3(nwg5), dim3(PP_NT), 0, stream, qp, kp,
                          vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
-    else
+    } else {
       hipLaunchKernelGGL(mxk_attn_fwd_pp_kernel<false>, dim3(nwg5), dim3(PP_NT), 0, stream, qp, kp,
                          vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+    }
   } else if (variant == 4) {
     if (causal)
       hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<true, true, true>), dim3(nwg), dim3(NT), 0, stream,
