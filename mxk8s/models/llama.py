@@ -5,7 +5,9 @@ step on amd.com/gpu=8".  The reference has no model code at all (SURVEY.md
 §2.5); this is a from-scratch MI355X-first implementation:
 
 * fused projections: one [q|k|v] GEMM per attention block and one [gate|up]
-  GEMM per MLP (fewer, larger hipBLASLt GEMMs);
+  GEMM per MLP (fewer, larger GEMMs), every product of the step on the
+  hand-written MFMA kernels (``mxk8s.ops.linear``; SwiGLU fused into the
+  [gate|up] epilogue);
 * hand-written HIP kernels for the memory-bound glue: RMSNorm fwd/bwd,
   SwiGLU fwd/bwd, rotary embedding fwd/bwd (``mxk8s.ops.fused``);
 * causal GQA attention through the hand-written gfx950 flash-attention

@@ -4,7 +4,7 @@ flat gradient buffer of :class:`~mxk8s.parallel.ddp.FlatParamSpace`.
 With stock ``nn.Linear`` autograd produces dW in a fresh tensor and
 ``AccumulateGrad`` adds it into the (pre-zeroed) flat ``.grad`` view: for
 Llama-3-8B that is a 16 GB memset plus a 48 GB read-read-write add pass per
-step (~10 ms on MI355X).  Here the dW GEMM (hipBLASLt) writes its output
+step (~10 ms on MI355X).  Here the dW GEMM (the hand-written layout kernel) writes its output
 directly into ``weight.main_grad`` — overwrite on the first backward after
 ``zero_grad`` (so no memset), ``addmm_`` accumulation on later micro-batches —
 and then tells the DDP bucketer that the gradient is ready (the role the

@@ -35,6 +35,9 @@ def use_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
     """Load the PyTorch TunableOp table of the Llama-3-8B step's hipBLASLt /
     rocBLAS GEMMs (fastest solution per shape, found once with
     scripts/gpu/tune_gemms.sh on MI355X) read-only: no tuning at run time.
+    Since round 3 every GEMM of the step runs on the hand-written kernels, so
+    the table only matters for the A/B switches (MXK_WGRAD=0 / MXK_DGRAD=0)
+    and shapes outside the kernels' tiling.
     TunableOp ignores the table if the torch / hipBLASLt / rocBLAS versions
     or the GPU arch recorded in it differ."""
     if not (torch.cuda.is_available() and os.path.exists(path)):
