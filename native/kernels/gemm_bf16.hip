@@ -68,6 +68,9 @@
 //  27 w4j   26 with ONE barrier per K-tile (SchedOneBarrier), 28 the same
 //           with the DMA spread: -5 / -1 % at 8192^3, -6 / -10 % at 16384^3
 //           (profiles/r3_gemm/)
+//  33-36    26 with its K loop moved against the 64-B instruction-fetch
+//           blocks by s_nop padding in front of it: loop head at 16 / 0 /
+//           28 / 4 mod 64 B (26 itself: 48)
 //  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
 //           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
 //           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
@@ -337,7 +340,8 @@ __device__ __forceinline__ void ktile_sched(f32x4_t (&acc)[8][8], bf16x8_t (&f0a
                                    dma_a, dma_b, kb2, wave_s, par);
 }
 
-template <int MAP, int EPI, int LATE = 0, int R1 = 0, int SCHED = 0, int ROT = 0, int STAG = 0>
+template <int MAP, int EPI, int LATE = 0, int R1 = 0, int SCHED = 0, int ROT = 0, int STAG = 0,
+          int ALN = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -418,6 +422,15 @@ mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   // K-tiles 0 .. ns-3 carry the DMA of stage s+2 (k offset kb = (s+2)*128 B)
   int s = 0;
   int kb = 2 * BK * 2;
+  // ALN (A/B of code placement): pad with s_nop to a 64-B boundary here,
+  // then ALN - 1 more 4-B s_nops, so the K loop's first instruction moves
+  // against the instruction-fetch blocks (MI355X_MICROARCH 'code-placement
+  // sensitivity')
+  if constexpr (ALN >= 1) {
+    asm volatile(".p2alignl 6, 0xbf800000" ::: "memory");
+#pragma unroll
+    for (int i = 1; i < ALN; ++i) asm volatile("s_nop 0" ::: "memory");
+  }
   for (; s + 2 <= ns - 2; s += 2) {
     ktile_sched<SCHED, 0, 1, LATE, R1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
                           dma_b, wrap(kb), wave_s);
@@ -1140,14 +1153,15 @@ int mxk_gemm_bf16_tn_ring_launch(int slots, const void* A, const void* Bt, void*
                                  int K, int lda, int ldb, int ldc, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 33;
+constexpr int kNumVariants = 37;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
     "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar",
     "w4j_hb_st", "x2_hb", "diag_nostore", "w4ip_hb_st", "w4ip_hb_nt", "w4j_earlyb",
     "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg", "pp8",
-    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst", "w4t_trickle", "w4t_trickle_lds"};
+    "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst", "w4t_trickle", "w4t_trickle_lds", "w4j_ldsst_aln64", "w4j_ldsst_aln64p4",
+    "w4j_ldsst_aln64p8", "w4j_ldsst_aln64p12"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -1162,10 +1176,10 @@ int num_cus() {
   return cus;
 }
 
-template <int MAP, int EPI, int LATE, int R1 = 0, int SCHED = 0, int ROT = 0, int STAG = 0>
+template <int MAP, int EPI, int LATE, int R1 = 0, int SCHED = 0, int ROT = 0, int STAG = 0, int ALN = 0>
 void launch_w4i(int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b, uint16_t* c,
                 int M, int N, int K, int lda, int ldb, int ldc) {
-  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4i<MAP, EPI, LATE, R1, SCHED, ROT, STAG>), dim3(nwg), dim3(W4_THREADS),
+  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4i<MAP, EPI, LATE, R1, SCHED, ROT, STAG, ALN>), dim3(nwg), dim3(W4_THREADS),
                      0, stream, a, b, c, M, N, K, lda, ldb, ldc);
 }
 
@@ -1224,6 +1238,10 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 25: launch_w4i<1, 1, 1, 0, 1, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 27: launch_w4i<1, 4, 1, 0, 7>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 28: launch_w4i<1, 4, 1, 0, 8>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 33: launch_w4i<1, 4, 1, 0, 1, 0, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 34: launch_w4i<1, 4, 1, 0, 1, 0, 0, 23>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 35: launch_w4i<1, 4, 1, 0, 1, 0, 0, 14>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 36: launch_w4i<1, 4, 1, 0, 1, 0, 0, 24>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 29: mxk_gemm_bf16_tn_ring_launch(4, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 30: mxk_gemm_bf16_tn_ring_launch(5, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 19:
