@@ -35,8 +35,14 @@ _USE_MXK_DGRAD = os.environ.get("MXK_DGRAD", "1") != "0"
 # tiles is at most half full; no library GEMM in the training step.  Shapes
 # that do not tile (M, N % 256, K % 64; tests, toy models) take the kernel's
 # bounds-checked MFMA path; CPU tensors the PyTorch reference.
+# MXK_FWD_LIB=1 (A/B measurements only, with MXK_FUSED_W13=0): the forward
+# products on torch.matmul / hipBLASLt, the round-2 routing, so a same-box
+# step A/B can price the hand-written forward path.
+_FWD_LIB = os.environ.get("MXK_FWD_LIB", "0") == "1"
+
+
 def _fwd(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    if not x.is_cuda or x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
+    if _FWD_LIB or not x.is_cuda or x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
         return torch.matmul(x, weight.t())
     x2 = x.reshape(-1, x.shape[-1])
     if not x2.is_contiguous():
