@@ -953,6 +953,327 @@ mxk_attn_fwd_pp_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
 }
 
 // ---------------------------------------------------------------------------
+// Forward, one wave per SIMD with two interleaved row groups (variant 9).
+// One 256-thread workgroup = 4 waves x 64 query rows; a wave owns two 32-row
+// groups, g0 = rows 32 w .. and g1 = rows 32 (7 - w) .. of the block
+// (mirrored, so every wave has the same causal work), and the whole 512
+// registers of its SIMD.  Per 64-key tile j the wave issues four blocks of
+// 16 v_mfma_f32_32x32x16_bf16
+//     B1 QK(g0, K_j)  B2 PV(g1, V_{j-1})  B3 QK(g1, K_j)  B4 PV(g0, V_j)
+// and places the softmax of the OTHER group's scores between them, one
+// short VALU chunk behind each MFMA (<= ~6 issues: the MFMA holds the SIMD's
+// vector issue for 8 of its 32 cycles, the rest is free): softmax(g0, j) in
+// B2 + B3, softmax(g1, j) in B4 + B1 of the next tile.  Each group's rare
+// lazy rescale (variant 4's 2^8 threshold) is a branch between blocks, so
+// the interleaved blocks stay branch-free.  K ring 2 slots, V ring 3 slots
+// (V_j is read in B4 of tile j and B2 of tile j + 1), LDS-DMA issued after
+// the tile's barrier and waited one tile later.  Diagonal tiles mask S with
+// selects before the softmax (groups whose rows all precede the tile still
+// run it: P = 0).
+namespace {
+constexpr int W1_BQ = 256;
+
+typedef unsigned u32x4v_t __attribute__((ext_vector_type(4)));
+
+struct W1Grp {
+  f32x16_t s0, s1;      // S^T of the two 32-key halves (query on the lane)
+  f32x16_t o[4];        // O^T accumulators
+  u32x4v_t p[4];        // P^T operands of the PV MFMAs (bf16 pairs)
+  float m, l;           // running row max (stale by <= 2^8) and row sum
+  float mq[4], mx, alpha, nmc;
+  float la[4];
+  bool grow;
+};
+
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float r;
+  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// softmax chunk k (0..31) of a group whose scores s0 / s1 are final; chunks
+// 0-15 run beside one MFMA block, 16-31 beside the next
+__device__ __forceinline__ void w1_sm(W1Grp& g, int k, float cs) {
+  if (k < 4) {                       // row max, four chains (v_max3)
+    const int r = 4 * k;
+    if (k == 0) {
+      g.mq[0] = fmaxf(g.s0[0], g.s0[1]);
+      g.mq[1] = fmaxf(g.s0[2], g.s0[3]);
+      g.mq[2] = fmaxf(g.s1[0], g.s1[1]);
+      g.mq[3] = fmaxf(g.s1[2], g.s1[3]);
+    } else {
+      g.mq[0] = max3(g.mq[0], g.s0[r], g.s0[r + 1]);
+      g.mq[1] = max3(g.mq[1], g.s0[r + 2], g.s0[r + 3]);
+      g.mq[2] = max3(g.mq[2], g.s1[r], g.s1[r + 1]);
+      g.mq[3] = max3(g.mq[3], g.s1[r + 2], g.s1[r + 3]);
+    }
+  } else if (k == 4) {
+    g.mx = half_max(max3(g.mq[0], g.mq[1], fmaxf(g.mq[2], g.mq[3])));
+  } else if (k == 5) {
+    float m_new = fmaxf(g.m, g.mx);
+    g.grow = (m_new - g.m) * cs > 8.f;
+    if (!g.grow) m_new = g.m;
+    g.alpha = g.grow ? fexp2((g.m - m_new) * cs) : 1.f;
+    g.m = m_new;
+    g.nmc = -m_new * cs;
+    g.la[0] = g.la[1] = g.la[2] = g.la[3] = 0.f;
+  } else if (k < 22) {               // exp2 of two scores per chunk, packed to bf16
+    const int e = k - 6;             // 0..15: pair (r, r + 1) of s0 (e < 8) or s1
+    const f32x16_t& x = e < 8 ? g.s0 : g.s1;
+    const int r = 2 * (e & 7);
+    const float e0 = fexp2(fmaf(x[r], cs, g.nmc));
+    const float e1 = fexp2(fmaf(x[r + 1], cs, g.nmc));
+    g.la[e & 3] += e0 + e1;
+    // pack8(s, base) order: P operand t = 2 (e >> 3) + ((e & 7) >> 2), word e & 3
+    g.p[2 * (e >> 3) + ((e & 7) >> 2)][e & 3] = mxk::pack2bf(e0, e1);
+  } else if (k == 26) {
+    g.l = g.l * g.alpha + ((g.la[0] + g.la[1]) + (g.la[2] + g.la[3]));
+  }
+}
+}  // namespace
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(NT, 1)
+mxk_attn_fwd_w1_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                       const uint16_t* __restrict__ v, uint16_t* __restrict__ o,
+                       float* __restrict__ lse, int S, int Hq, int Hkv, long q_tok, long k_tok,
+                       long v_tok, float scale) {
+  constexpr int VS = 3, KS = 3;
+  // LDS: K ring [0, 48 KiB), V ring [48, 96 KiB); the V ring's base is folded
+  // into the per-lane V read offsets, so every LDS read is base VGPR +
+  // immediate < 64 KiB (a larger constant costs an extra address register per
+  // read stream: the build spills)
+  constexpr int VB = KS * TILE_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[(VS + KS) * TILE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  const int nqb = S / W1_BQ;
+  int bh, qb;
+  map_block_xcd(blockIdx.x, gridDim.x, nqb, Hq / Hkv, CAUSAL, &bh, &qb);
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hkv = hq / (Hq / Hkv);
+  const int q0 = qb * W1_BQ;
+  const int qw0 = q0 + 32 * wave, qw1 = q0 + 32 * (7 - wave);
+  const int myq0 = qw0 + r32, myq1 = qw1 + r32;
+
+  const uint16_t* qb_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
+  const uint16_t* kb_ptr = k + static_cast<long>(b) * S * k_tok + static_cast<long>(hkv) * D;
+  const uint16_t* vb_ptr = v + static_cast<long>(b) * S * v_tok + static_cast<long>(hkv) * D;
+
+  bf16x8_t qf0[8], qf1[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    qf0[s] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + static_cast<long>(myq0) * q_tok + 16 * s + 8 * h);
+    qf1[s] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + static_cast<long>(myq1) * q_tok + 16 * s + 8 * h);
+  }
+  const int n = (CAUSAL ? min(S, q0 + W1_BQ) : S) / BKV;
+
+  // DMA: wave w moves pieces 4w + p of each tile (variant 4's map)
+  const mxk::u32x4 rk = mxk::make_rsrc(kb_ptr, static_cast<unsigned>(S * k_tok * 2));
+  const mxk::u32x4 rv = mxk::make_rsrc(vb_ptr, static_cast<unsigned>(S * v_tok * 2));
+  const int prow = lane >> 4, pslot = lane & 15;
+  const uint32_t k_row = static_cast<uint32_t>(k_tok) * 2u, v_row = static_cast<uint32_t>(v_tok) * 2u;
+  uint32_t kvo[4], vvo[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const uint32_t row = static_cast<uint32_t>(4 * (4 * wave + p) + prow);
+    const uint32_t ch = static_cast<uint32_t>(pslot ^ ((prow << 2) | p));
+    kvo[p] = row * k_row + ch * 16u;
+    vvo[p] = row * v_row + ch * 16u;
+  }
+  const uint32_t k_step = static_cast<uint32_t>(BKV) * k_row;
+  const uint32_t v_step = static_cast<uint32_t>(BKV) * v_row;
+  const uint32_t sm32 = mxk::lds_addr32(&smem[0]);
+  auto issue = [&](int j) __attribute__((always_inline)) {
+    const uint32_t dk = sm32 + (j % KS) * TILE_BYTES + (4 * wave) * 1024;
+    const uint32_t dv = sm32 + VB + (j % VS) * TILE_BYTES + (4 * wave) * 1024;
+    const uint32_t ks = __builtin_amdgcn_readfirstlane(j * k_step);
+    const uint32_t vs = __builtin_amdgcn_readfirstlane(j * v_step);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      mxk::dma16m(rk, __builtin_amdgcn_readfirstlane(dk + p * 1024), kvo[p], ks);
+      mxk::dma16m(rv, __builtin_amdgcn_readfirstlane(dv + p * 1024), vvo[p], vs);
+    }
+  };
+  issue(0);
+  if (n > 1) issue(1);
+
+  int koff[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) koff[s] = swz(r32, 2 * s + h);
+  const int G = lane >> 4, i16 = lane & 15;
+  const int tr_key = 4 * h + (i16 >> 2);
+  const int tr_ch = 2 * (G & 1) + ((i16 & 3) >> 1);
+  const int tr_byte = 8 * (i16 & 1);
+  int voff[4][2];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    voff[db][0] = VB + swz(tr_key, 4 * db + tr_ch) + tr_byte;
+    voff[db][1] = VB + swz(tr_key + 8, 4 * db + tr_ch) + tr_byte;
+  }
+
+  const float cs = scale * 1.4426950408889634f;   // scores -> log2 domain
+  W1Grp g0, g1;
+  g0.m = g1.m = -INFINITY;
+  g0.l = g1.l = 0.f;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { g0.o[db][r] = 0.f; g1.o[db][r] = 0.f; }
+
+#pragma unroll
+  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf0[s]), "v"(qf1[s]));
+  if (n > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // tile 0 (tile 1 flies on)
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // MFMA blocks, operands read one group of 4 MFMAs ahead; SM(c) runs the
+  // softmax chunk that follows MFMA c of the block (c = 0..15)
+  auto qk_block = [&](W1Grp& g, const bf16x8_t (&qf)[8], int kslot, auto&& SM) __attribute__((always_inline)) {
+    const char* kt = smem + kslot * TILE_BYTES;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { g.s0[r] = 0.f; g.s1[r] = 0.f; }
+    bf16x8_t ka[2][4];
+    auto rd = [&](int pr, int slot) __attribute__((always_inline)) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        ka[slot][2 * e] = lds_b128(kt + koff[2 * pr + e]);
+        ka[slot][2 * e + 1] = lds_b128(kt + koff[2 * pr + e] + 32 * 256);
+      }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) {
+      if (pr < 3) rd(pr + 1, (pr + 1) & 1);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        g.s0 = mfma32(ka[pr & 1][2 * e], qf[2 * pr + e], g.s0);
+        SM(4 * pr + 2 * e);
+        __builtin_amdgcn_sched_barrier(0);
+        g.s1 = mfma32(ka[pr & 1][2 * e + 1], qf[2 * pr + e], g.s1);
+        SM(4 * pr + 2 * e + 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  auto pv_block = [&](W1Grp& g, int vslot, auto&& SM) __attribute__((always_inline)) {
+    const char* vt = smem + vslot * TILE_BYTES;   // VB is inside voff
+    bf16x8_t va[2][4];
+    auto rd = [&](int db, int slot) __attribute__((always_inline)) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        va[slot][ks] = cat8(lds_tr_b64(vt + voff[db][0] + ks * 4096),
+                            lds_tr_b64(vt + voff[db][1] + ks * 4096));
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      if (db < 3) rd(db + 1, (db + 1) & 1);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        g.o[db] = mfma32(va[db & 1][ks], __builtin_bit_cast(bf16x8_t, g.p[ks]), g.o[db]);
+        SM(4 * db + ks);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  auto rescale = [&](W1Grp& g) __attribute__((always_inline)) {
+    if (__builtin_amdgcn_ballot_w64(g.grow)) {
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) g.o[db][r] *= g.alpha;
+    }
+  };
+  auto mask = [&](W1Grp& g, int kv0, int myq) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kv0 + crow(r, h);
+      g.s0[r] = key > myq ? -INFINITY : g.s0[r];
+      g.s1[r] = key + 32 > myq ? -INFINITY : g.s1[r];
+    }
+  };
+  auto none = [&](int) __attribute__((always_inline)) {};
+  auto sm0a = [&](int c) __attribute__((always_inline)) { w1_sm(g0, c, cs); };
+  auto sm0b = [&](int c) __attribute__((always_inline)) { w1_sm(g0, 16 + c, cs); };
+  auto sm1a = [&](int c) __attribute__((always_inline)) { w1_sm(g1, c, cs); };
+  auto sm1b = [&](int c) __attribute__((always_inline)) { w1_sm(g1, 16 + c, cs); };
+
+  const int jd = CAUSAL ? q0 / BKV : n;   // tiles j >= jd are diagonal (masked)
+  // one tile: K_j and V_j in ring slot j % 3
+  auto tile = [&](int sl, int j, auto firstc) __attribute__((always_inline)) {
+    constexpr bool first = decltype(firstc)::value;
+    const int sp = sl == 0 ? 2 : sl - 1;
+    const bool diag = CAUSAL && j >= jd;
+    // B1: QK(g0, K_j) beside the second half of softmax(g1, j - 1)
+    if constexpr (first) qk_block(g0, qf0, sl, none);
+    else qk_block(g0, qf0, sl, sm1b);
+    if (diag) mask(g0, j * BKV, myq0);
+    if constexpr (!first) {
+      rescale(g1);
+      // B2: PV(g1, V_{j-1}) beside the first half of softmax(g0, j)
+      pv_block(g1, sp, sm0a);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) sm0a(c);
+    }
+    // B3: QK(g1, K_j) beside the second half of softmax(g0, j)
+    qk_block(g1, qf1, sl, sm0b);
+    if (diag) mask(g1, j * BKV, myq1);
+    rescale(g0);
+    // B4: PV(g0, V_j) beside the first half of softmax(g1, j)
+    pv_block(g0, sl, sm1a);
+    // K_{j+1}, V_{j+1} landed (issued one tile ago); the barrier also
+    // certifies that K_j's and V_{j-1}'s slots are no longer read
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    if (j + 2 < n) issue(j + 2);
+  };
+  // one loop body with a runtime ring slot (a v_add per LDS read stream and
+  // tile; unrolled by the ring depth the register allocator spills)
+  tile(0, 0, std::true_type{});
+  for (int j = 1, sl = 1; j < n; ++j, sl = sl == 2 ? 0 : sl + 1) tile(sl, j, std::false_type{});
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sm1b(c);
+  rescale(g1);
+  pv_block(g1, (n - 1) % 3, none);
+
+  auto store = [&](W1Grp& g, int myq) __attribute__((always_inline)) {
+    const float lt = half_sum(g.l);
+    const float inv = 1.f / lt;
+    uint16_t* orow = o + (static_cast<long>(b) * S + myq) * Hq * D + static_cast<long>(hq) * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int a0 = 2 * kk, a1 = 2 * kk + 1;
+        const uint32_t x0 = mxk::pack2bf(g.o[db][4 * a0] * inv, g.o[db][4 * a0 + 1] * inv);
+        const uint32_t x1 = mxk::pack2bf(g.o[db][4 * a0 + 2] * inv, g.o[db][4 * a0 + 3] * inv);
+        const uint32_t y0 = mxk::pack2bf(g.o[db][4 * a1] * inv, g.o[db][4 * a1 + 1] * inv);
+        const uint32_t y1 = mxk::pack2bf(g.o[db][4 * a1 + 2] * inv, g.o[db][4 * a1 + 3] * inv);
+        const auto p0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+        const auto p1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+        uint4 vv;
+        vv.x = p0[0];
+        vv.y = p1[0];
+        vv.z = p0[1];
+        vv.w = p1[1];
+        *reinterpret_cast<uint4*>(orow + 32 * db + 16 * kk + 8 * h) = vv;
+      }
+    }
+    if (h == 0) lse[(static_cast<long>(b) * Hq + hq) * S + myq] = g.m * scale + logf(lt);
+  };
+  store(g0, myq0);
+  store(g1, myq1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
 // variant: 0 = register-staged K/V, 1 = LDS-DMA with the loop unrolled by 2
 // (static LDS buffer), 2 = LDS-DMA, 3 = 2 with the PIPE body (operands read a
 // group ahead, exp of P chunk ks+1 under the PV MFMAs of chunk ks, lazy
@@ -966,7 +1287,7 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
                                  long k_tok, long v_tok, float scale, int causal, int variant,
                                  hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv ||
-      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 8 ||
+      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 9 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) % 16)
     return static_cast<int>(hipErrorInvalidValue);
@@ -977,6 +1298,20 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
   const auto* kp = static_cast<const uint16_t*>(k);
   const auto* vp = static_cast<const uint16_t*>(v);
   auto* op = static_cast<uint16_t*>(o);
+  if (variant == 9) {
+    if (S % W1_BQ) {
+      variant = 4;
+    } else {
+      const int nwg9 = B * Hq * (S / W1_BQ);
+      if (causal)
+        hipLaunchKernelGGL(mxk_attn_fwd_w1_kernel<true>, dim3(nwg9), dim3(NT), 0, stream, qp, kp, vp,
+                           op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+      else
+        hipLaunchKernelGGL(mxk_attn_fwd_w1_kernel<false>, dim3(nwg9), dim3(NT), 0, stream, qp, kp,
+                           vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+      MXK_RETURN_LAUNCH_STATUS();
+    }
+  }
   if (variant >= 5 && S % PP_BQ) variant = 4;
   if (variant >= 5) {
     const int nwg5 = B * Hq * (S / PP_BQ);

@@ -1,0 +1,16 @@
+#!/usr/bin/env bash
+# Attention forward variant 9 (4 waves, one per SIMD, two interleaved row
+# groups per wave): GPU numerics of every forward variant, then the
+# Llama-3-8B-shape A/B against variant 4 (causal and full).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+OUT=${1:-gpurun_out/r3a9}
+mkdir -p "$OUT"
+export PYTHONPATH=.
+timeout -k 10 300 python -u -m pytest tests/test_gpu_attention.py -k fwd -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_fwd.log" 2>&1
+rc=$?; tail -2 "$OUT/pytest_fwd.log"; [ $rc -eq 0 ] || exit $rc
+VARIANTS=4,9 timeout -k 10 200 python -u scripts/gpu/attn_fwd_ab.py > "$OUT/fwd_ab.log" 2>&1 && \
+CAUSAL=0 VARIANTS=4,9 timeout -k 10 200 python -u scripts/gpu/attn_fwd_ab.py > "$OUT/fwd_ab_full.log" 2>&1
+rc=$?
+grep RESULT "$OUT"/fwd_ab*.log
+exit $rc
