@@ -71,6 +71,10 @@
 //  33-36    26 with its K loop moved against the 64-B instruction-fetch
 //           blocks by s_nop padding in front of it: loop head at 16 / 0 /
 //           28 / 4 mod 64 B (26 itself: 48)
+//  37-38    26 without the operand XOR swizzle (37: linear LDS image, the
+//           DMA reads each row's 128 B in lane order; 38: only the 64-B
+//           halves swapped) - prices the permuted DMA source against the
+//           LDS bank conflicts it removes; 39 / 40: XOR masks 6 / 5
 //  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
 //           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
 //           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
@@ -156,13 +160,15 @@ struct DmaK {
 };
 
 __device__ __forceinline__ DmaK make_dmak(const uint16_t* src, int ld, int row0, int lane,
-                                          int wave) {
+                                          int wave, int swm = 7) {
   DmaK d;
   const uint16_t* base = src + static_cast<size_t>(row0) * ld;
   d.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, 256 * ld * 2,
                                              0x00020000);
   const int r = lane >> 3;
-  const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & 7);
+  // swm 7: the full XOR swizzle; 4: only the 64-B halves swap (each 4-lane
+  // group keeps an ascending 64-B source run); 0: linear (A/B variants 37/38)
+  const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & swm);
   const uint32_t lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
 #pragma unroll
   for (int p = 0; p < 8; ++p)
@@ -341,7 +347,7 @@ __device__ __forceinline__ void ktile_sched(f32x4_t (&acc)[8][8], bf16x8_t (&f0a
 }
 
 template <int MAP, int EPI, int LATE = 0, int R1 = 0, int SCHED = 0, int ROT = 0, int STAG = 0,
-          int ALN = 0>
+          int ALN = 0, int SWM = 7>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -364,11 +370,11 @@ mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   const int wn = wave_s & 1;
   int m0, n0;
   w4b_tile<MAP>(blockIdx.x, gridDim.x, M / BM, N / BN, &m0, &n0);
-  const DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
-  const DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
+  const DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s, SWM);
+  const DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s, SWM);
 
   const int frow = lane & 15;
-  const int fch = (lane >> 4) ^ (frow >> 1);
+  const int fch = (lane >> 4) ^ ((frow >> 1) & SWM);
   const int off_k0 = frow * 128 + fch * 16;
   const int off_k1 = frow * 128 + (fch ^ 4) * 16;
   constexpr int SUB = 2048;
@@ -1153,7 +1159,7 @@ int mxk_gemm_bf16_tn_ring_launch(int slots, const void* A, const void* Bt, void*
                                  int K, int lda, int ldb, int ldc, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 37;
+constexpr int kNumVariants = 41;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -1161,7 +1167,8 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "w4j_hb_st", "x2_hb", "diag_nostore", "w4ip_hb_st", "w4ip_hb_nt", "w4j_earlyb",
     "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg", "pp8",
     "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst", "w4t_trickle", "w4t_trickle_lds", "w4j_ldsst_aln64", "w4j_ldsst_aln64p4",
-    "w4j_ldsst_aln64p8", "w4j_ldsst_aln64p12"};
+    "w4j_ldsst_aln64p8", "w4j_ldsst_aln64p12", "w4j_ldsst_linear", "w4j_ldsst_swz_half",
+    "w4j_ldsst_swz6", "w4j_ldsst_swz5"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -1176,10 +1183,11 @@ int num_cus() {
   return cus;
 }
 
-template <int MAP, int EPI, int LATE, int R1 = 0, int SCHED = 0, int ROT = 0, int STAG = 0, int ALN = 0>
+template <int MAP, int EPI, int LATE, int R1 = 0, int SCHED = 0, int ROT = 0, int STAG = 0, int ALN = 0,
+          int SWM = 7>
 void launch_w4i(int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b, uint16_t* c,
                 int M, int N, int K, int lda, int ldb, int ldc) {
-  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4i<MAP, EPI, LATE, R1, SCHED, ROT, STAG, ALN>), dim3(nwg), dim3(W4_THREADS),
+  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4i<MAP, EPI, LATE, R1, SCHED, ROT, STAG, ALN, SWM>), dim3(nwg), dim3(W4_THREADS),
                      0, stream, a, b, c, M, N, K, lda, ldb, ldc);
 }
 
@@ -1242,6 +1250,10 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 34: launch_w4i<1, 4, 1, 0, 1, 0, 0, 23>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 35: launch_w4i<1, 4, 1, 0, 1, 0, 0, 14>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 36: launch_w4i<1, 4, 1, 0, 1, 0, 0, 24>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 37: launch_w4i<1, 4, 1, 0, 1, 0, 0, 0, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 38: launch_w4i<1, 4, 1, 0, 1, 0, 0, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 39: launch_w4i<1, 4, 1, 0, 1, 0, 0, 0, 6>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 40: launch_w4i<1, 4, 1, 0, 1, 0, 0, 0, 5>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 29: mxk_gemm_bf16_tn_ring_launch(4, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 30: mxk_gemm_bf16_tn_ring_launch(5, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 19:
