@@ -2,7 +2,8 @@
 #
 #   make            build every native artefact in-tree
 #   make kernels    HIP kernel library  mxk8s/_lib/libmxkernels.so
-#   make gemm-exp   the same library with every A/B GEMM schedule
+#   make gemm-exp   the same library with every A/B GEMM schedule and the
+#                   attention forward A/B variants 5-9
 #                   (-DMXK_GEMM_EXPERIMENTS) -> mxk8s/_lib/libmxkernels_exp.so,
 #                   selected with MXK_KERNELS_LIB (python -m mxk8s.validate.gemm)
 #   make node       C++ node library    mxk8s/_lib/libmxnode.so (+ CLIs in bin/)

@@ -628,6 +628,10 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
   if (h == 0) lse[(static_cast<long>(b) * Hq + hq) * S + myq] = m * scale + logf(lt);
 }
 
+// The forward A/B records below (variants 5-9) are built only into the
+// experiments library (`make gemm-exp` -> libmxkernels_exp.so, selected with
+// MXK_KERNELS_LIB); the production library carries variants 0-4.
+#ifdef MXK_GEMM_EXPERIMENTS
 // ---------------------------------------------------------------------------
 // Forward, 8-wave ping-pong (variant 5).  The kernels above run each wave's
 // QK^T MFMAs, its softmax (VALU, ~700 issue cycles per 64-key tile: 32 v_exp
@@ -1273,6 +1277,8 @@ mxk_attn_fwd_w1_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+#endif  // MXK_GEMM_EXPERIMENTS
+
 // ---------------------------------------------------------------------------
 // variant: 0 = register-staged K/V, 1 = LDS-DMA with the loop unrolled by 2
 // (static LDS buffer), 2 = LDS-DMA, 3 = 2 with the PIPE body (operands read a
@@ -1298,6 +1304,9 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
   const auto* kp = static_cast<const uint16_t*>(k);
   const auto* vp = static_cast<const uint16_t*>(v);
   auto* op = static_cast<uint16_t*>(o);
+#ifndef MXK_GEMM_EXPERIMENTS
+  if (variant >= 5) return static_cast<int>(hipErrorNotSupported);
+#else
   if (variant == 9) {
     if (S % W1_BQ) {
       variant = 4;
@@ -1336,7 +1345,10 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
       hipLaunchKernelGGL(mxk_attn_fwd_pp_kernel<false>, dim3(nwg5), dim3(PP_NT), 0, stream, qp, kp,
                          vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
     }
-  } else if (variant == 4) {
+    MXK_RETURN_LAUNCH_STATUS();
+  }
+#endif
+  if (variant == 4) {
     if (causal)
       hipLaunchKernelGGL((mxk_attn_fwd_dma_kernel<true, true, true>), dim3(nwg), dim3(NT), 0, stream,
                          qp, kp, vp, op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
@@ -1373,6 +1385,15 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
                          op, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
   }
   MXK_RETURN_LAUNCH_STATUS();
+}
+
+// 1 if forward variant v is in this build (5-9 only in the experiments library)
+MXK_API int mxk_attn_fwd_variant_built(int v) {
+#ifdef MXK_GEMM_EXPERIMENTS
+  return v >= 0 && v <= 9;
+#else
+  return v >= 0 && v <= 4;
+#endif
 }
 
 MXK_API int mxk_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B,

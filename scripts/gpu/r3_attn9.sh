@@ -7,6 +7,8 @@ cd "${GRAFT_REPO_ROOT:-.}"
 OUT=${1:-gpurun_out/r3a9}
 mkdir -p "$OUT"
 export PYTHONPATH=.
+# forward variants 5-9 are A/B records: experiments library (make gemm-exp)
+export MXK_KERNELS_LIB=${MXK_KERNELS_LIB:-$PWD/mxk8s/_lib/libmxkernels_exp.so}
 timeout -k 10 300 python -u -m pytest tests/test_gpu_attention.py -k fwd -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_fwd.log" 2>&1
 rc=$?; tail -2 "$OUT/pytest_fwd.log"; [ $rc -eq 0 ] || exit $rc
 VARIANTS=4,9 timeout -k 10 200 python -u scripts/gpu/attn_fwd_ab.py > "$OUT/fwd_ab.log" 2>&1 && \

@@ -10,6 +10,8 @@ R=$PWD
 OUT=$R/${1:-gpurun_out/r3diag}
 mkdir -p "$OUT"
 export PYTHONPATH=$R TMPDIR=/tmp
+# forward variants 5-9 are A/B records: experiments library (make gemm-exp)
+export MXK_KERNELS_LIB=${MXK_KERNELS_LIB:-$PWD/mxk8s/_lib/libmxkernels_exp.so}
 VARIANTS=4,5,7,8 timeout -k 10 200 python3 -u scripts/gpu/attn_fwd_ab.py > $OUT/attn_diag.log 2>&1 || exit $?
 grep RESULT $OUT/attn_diag.log
 cd /tmp

@@ -9,6 +9,8 @@ R=$PWD
 OUT=$R/${1:-gpurun_out/r3pmc}
 mkdir -p "$OUT"
 export PYTHONPATH=$R TMPDIR=/tmp
+# forward variants 5-9 are A/B records: experiments library (make gemm-exp)
+export MXK_KERNELS_LIB=${MXK_KERNELS_LIB:-$PWD/mxk8s/_lib/libmxkernels_exp.so}
 step() {
   local name=$1 secs=$2
   shift 2
