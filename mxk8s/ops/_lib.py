@@ -44,6 +44,7 @@ _SIGNATURES = {
     "mxk_gemm_bf16_tn_is_ablation": (_i, [_i]),
     "mxk_gemm_bf16_tn_variant_built": (_i, [_i]),
     "mxk_attn_fwd_variant_built": (_i, [_i]),
+    "mxk_gemm_bf16_ex_variant_built": (_i, [_i]),
     "mxk_gemm_bf16_tn_variant_name": (ctypes.c_char_p, [_i]),
     "mxk_vector_add_f32": (_i, [_vp, _vp, _vp, _l, _vp]),
     "mxk_vector_add_bf16": (_i, [_vp, _vp, _vp, _l, _vp]),

@@ -1205,6 +1205,7 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
       mxk_gemm_bf16_ex_variant(A, Bt, C, M, N, K, lda, ldb, ldc, 1, 1, 2, stream);
       break;
     case 26: launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+#ifdef MXK_GEMM_EXPERIMENTS
     case 31:
     case 32: {
       if (K < (v == 31 ? 18 : 26) * BK) {   // fewer K-tiles than the trickle phase needs
@@ -1220,7 +1221,6 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
                            a, b, c, M, N, K, lda, ldb, ldc);
       break;
     }
-#ifdef MXK_GEMM_EXPERIMENTS
     case 2: launch_w4i<1, 1, 0>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 3: launch_w4i<1, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 4: launch_w4i<1, 1, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
@@ -1280,14 +1280,15 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
 }
 
 // Production builds carry the default (26), its base schedule (6), the
-// first structure (0), the 8-byte-store fallback (1), the layout kernel (9)
-// and the trickle-store schedule (31); every other schedule is an A/B record, built only with
+// first structure (0), the 8-byte-store fallback (1) and the layout kernel
+// (9); every other schedule (incl. the trickle stores 31/32, measured
+// neutral to -4 %) is an A/B record, built only with
 // -DMXK_GEMM_EXPERIMENTS (`make gemm-exp` -> libmxkernels_exp.so).
 bool variant_built(int v) {
 #ifdef MXK_GEMM_EXPERIMENTS
   return v >= 0 && v < kNumVariants;
 #else
-  return v == 0 || v == 1 || v == 6 || v == 9 || v == 26 || v == 31;
+  return v == 0 || v == 1 || v == 6 || v == 9 || v == 26;
 #endif
 }
 

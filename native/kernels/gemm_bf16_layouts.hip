@@ -750,6 +750,15 @@ static void launch_x(int sched, bool wide, int nwg, hipStream_t stream, const ui
                        c, M, N, K, lda, ldb, ldc);
 }
 
+// 1 if layout-kernel variant v is in this build (4, x2t: experiments only)
+MXK_API int mxk_gemm_bf16_ex_variant_built(int v) {
+#ifdef MXK_GEMM_EXPERIMENTS
+  return v >= 0 && v <= 4;
+#else
+  return v >= 0 && v <= 3;
+#endif
+}
+
 MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,
                              int lda, int ldb, int ldc, hipStream_t stream);
 
@@ -797,6 +806,9 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
   if (!ok) return static_cast<int>(hipErrorInvalidValue);
   if (variant == 1 && a_kmajor && b_kmajor)
     return mxk_gemm_bf16_tn(A, B, C, M, N, K, lda, ldb, ldc, stream);
+#ifdef MXK_GEMM_EXPERIMENTS
+  // x2t, the persistent trickle-store kernel: an A/B record (mixed against
+  // x2 on the Llama-3-8B step shapes, profiles/r3_pass1/layouts_ab.log)
   if (variant == 4 && K >= 18 * XBK && (ldc % 8 == 0) && reinterpret_cast<uintptr_t>(C) % 16 == 0) {
     const int xs = (a_kmajor == b_kmajor) ? 1 : 0;
     const int xn = (M / XBM) * (N / XBM);
@@ -813,6 +825,7 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
       launch_xt<true, true>(xs, xn, stream, a, b, c, M, N, K, lda, ldb, ldc);
     MXK_RETURN_LAUNCH_STATUS();
   }
+#endif
   if (variant == 4) variant = 1;
   if (variant == 1 && a_kmajor && b_kmajor)
     return mxk_gemm_bf16_tn(A, B, C, M, N, K, lda, ldb, ldc, stream);

@@ -9,6 +9,7 @@ OUT=${1:-gpurun_out/r3g}
 mkdir -p "$OUT"
 export PYTHONPATH=.
 EXP=mxk8s/_lib/libmxkernels_exp.so
+export MXK_KERNELS_LIB=$EXP   # the trickle-store kernels are experiments-only
 timeout -k 10 200 python -u scripts/gpu/ring_check.py 26,31 > "$OUT/check.log" 2>&1 && \
 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -k "trickle or every_schedule or headline" -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_trickle.log" 2>&1 && \
 timeout -k 10 400 python -u -m mxk8s.validate.gemm --sizes 8192,4096,16384 --variants 26,31 --iters 96 --rounds 12 > "$OUT/gemm_ab.log" 2>&1 && \

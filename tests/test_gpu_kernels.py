@@ -285,7 +285,10 @@ def test_gemm_trickle_store_layouts_vs_fp32(cuda_device, layout, M, N, K):
     not others), 1024 tiles (four per CU, three trickle phases each) and a
     grid smaller than the chip; K at and above the 18-K-tile minimum.  The
     WHOLE output against fp32."""
+    from mxk8s.ops import _lib
     from mxk8s.ops.gemm import gemm_bf16_ex
+    if not _lib.lib().mxk_gemm_bf16_ex_variant_built(4):
+        pytest.skip("x2t is an A/B record (experiments library only)")
     g = torch.Generator(device=cuda_device).manual_seed(13)
     r = lambda *s: (torch.rand(*s, device=cuda_device, generator=g) * 2 - 1).bfloat16()  # noqa: E731
     if layout == "tn":
