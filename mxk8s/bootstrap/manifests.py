@@ -58,8 +58,10 @@ def hip_vector_add() -> dict:
             "spec": {"restartPolicy": "OnFailure", "tolerations": TOLERATIONS,
                      "containers": [_gpu_container(
                          "hip-vector-add",
-                         ["sh", "-c", "rocminfo | grep -E '^\\s+Name:\\s+gfx' ; "
-                                      "exec /opt/mxk8s/bin/mx-vector-add --n 50000 --check"],
+                         ["sh", "-c", "rocminfo | grep -E '^\\s+Name:\\s+gfx' ; ls -l /dev/dri ; "
+                                      "env | grep '^AMD_GPU_' ; "
+                                      "exec /opt/mxk8s/bin/mx-vector-add --n 50000 --check "
+                                      "--expect-gpus 1 --expect-arch gfx950"],
                          1, cpu="1", mem="2Gi")],
                      "volumes": [_dshm("1Gi")]}}
 

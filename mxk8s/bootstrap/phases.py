@@ -33,6 +33,7 @@ import time
 from typing import Callable, Optional, Sequence
 
 from . import hostfiles as hf
+from ..validate import isolation
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -339,9 +340,13 @@ def phase_validate(ctx: Context) -> None:
                  "--timeout=600s")
         r = _kubectl(ctx, "logs", f"pod/{name}", capture=True, check=False)
         if not ctx.dry_run and name == "hip-vector-add":
-            lines = [l for l in (r.stdout or "").splitlines() if l.startswith("RESULT ")]
-            if not lines or not json.loads(lines[-1][7:]).get("pass"):
-                raise PhaseError(f"{name}: no passing RESULT line in logs")
+            # BASELINE.md:37: every RESULT line passes, the pod sees exactly
+            # its one allocated gfx950 GPU (and only its render node)
+            results = isolation.parse_results((r.stdout or "").splitlines())
+            problems = isolation.check_results(results, gpus=1, arch="gfx950")
+            if problems:
+                raise PhaseError(f"{name}: " + "; ".join(problems))
+            ctx.out(f"{name}: isolation ok ({len(results)} RESULT line(s))")
 
 
 PHASES: list[tuple[str, Callable[[Context], None]]] = [

@@ -382,6 +382,9 @@ class AmdGpuDevicePlugin:
         c.envs["AMD_GPU_DEVICE_IDS"] = ",".join(str(g.index) for g in gpus)
         c.envs["AMD_GPU_BDFS"] = ",".join(g.bdf for g in gpus)
         c.envs["AMD_GPU_ARCH"] = gpus[0].arch if gpus else ""
+        # the render nodes this container must see, and no others: the pod's
+        # payload (mx-vector-add) checks /dev/dri against it (BASELINE.md:37)
+        c.envs["AMD_GPU_RENDER_NODES"] = ",".join(dict.fromkeys(g.render_path for g in gpus))
         c.annotations["amd.com/gpu.devices"] = ",".join(g.uuid for g in gpus)
         if self.cfg.use_cdi:
             for g in gpus:

@@ -6,14 +6,28 @@
 // and prints one machine-readable line:
 //   RESULT {"test":"vectoradd","pass":true,...}
 // Exit status 0 iff the check passed.
+//
+// Device isolation (BASELINE.md:37, "pod sees exactly 1 gfx950 agent"): the
+// pod must see exactly the GPUs its amd.com/gpu limit allocated and nothing
+// else.  The expected set comes from the flags or, by default, from the
+// environment the device plugin's Allocate sets (AMD_GPU_DEVICE_IDS,
+// AMD_GPU_ARCH, AMD_GPU_BDFS, AMD_GPU_RENDER_NODES).  A CDI spec that injects
+// every render node, or a plugin that hands out the wrong minor, fails here.
 //   mx-vector-add [--n 50000] [--check] [--device 0] [--bw-mib 1024]
+//                 [--expect-gpus N] [--expect-arch gfx950]
+#include <dirent.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <set>
+#include <sstream>
+#include <string>
 #include <vector>
 
 extern "C" int mxk_vector_add_f32(const void* a, const void* b, void* c, long n, hipStream_t s);
@@ -28,16 +42,64 @@ extern "C" int mxk_vector_add_f32(const void* a, const void* b, void* c, long n,
     }                                                                               \
   } while (0)
 
+namespace {
+
+std::vector<std::string> split_csv(const char* s) {
+  std::vector<std::string> out;
+  if (!s) return out;
+  std::stringstream ss(s);
+  std::string item;
+  while (std::getline(ss, item, ','))
+    if (!item.empty()) out.push_back(item);
+  return out;
+}
+
+// "0000:05:00.0#3" (a compute partition of that device) -> "0000:05:00.0"
+std::string norm_bdf(std::string b) {
+  b = b.substr(0, b.find('#'));
+  for (auto& c : b) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  return b;
+}
+
+std::string json_list(const std::set<std::string>& v) {
+  std::string o = "[";
+  for (const auto& x : v) o += (o.size() > 1 ? ",\"" : "\"") + x + "\"";
+  return o + "]";
+}
+
+// /dev/dri/renderD* visible in this mount namespace
+std::set<std::string> render_nodes() {
+  std::set<std::string> out;
+  if (DIR* d = opendir("/dev/dri")) {
+    while (dirent* e = readdir(d))
+      if (!std::strncmp(e->d_name, "renderD", 7)) out.insert(std::string("/dev/dri/") + e->d_name);
+    closedir(d);
+  }
+  return out;
+}
+
+}  // namespace
+
 int main(int argc, char** argv) {
   long n = 50000;   // the CUDA-samples vectorAdd default the operator validator uses
   int dev = 0;
   long bw_mib = 1024;
+  // expected allocation: flags override the Allocate environment
+  const auto env_ids = split_csv(std::getenv("AMD_GPU_DEVICE_IDS"));
+  int expect_gpus = env_ids.empty() ? -1 : static_cast<int>(std::set<std::string>(env_ids.begin(), env_ids.end()).size());
+  std::string expect_arch = std::getenv("AMD_GPU_ARCH") ? std::getenv("AMD_GPU_ARCH") : "";
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--n") && i + 1 < argc) n = std::atol(argv[++i]);
     else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) dev = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--bw-mib") && i + 1 < argc) bw_mib = std::atol(argv[++i]);
+    else if (!std::strcmp(argv[i], "--expect-gpus") && i + 1 < argc) expect_gpus = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--expect-arch") && i + 1 < argc) expect_arch = argv[++i];
     else if (!std::strcmp(argv[i], "--check")) {}
-    else { std::fprintf(stderr, "usage: %s [--n N] [--device D] [--bw-mib M]\n", argv[0]); return 2; }
+    else {
+      std::fprintf(stderr, "usage: %s [--n N] [--device D] [--bw-mib M] [--expect-gpus N] "
+                   "[--expect-arch gfx950]\n", argv[0]);
+      return 2;
+    }
   }
   int count = 0;
   HIP_OK(hipGetDeviceCount(&count));
@@ -95,11 +157,39 @@ int main(int argc, char** argv) {
   HIP_OK(hipFree(da));
   HIP_OK(hipFree(db));
   HIP_OK(hipFree(dc));
-  const bool pass = mismatches == 0;
+  // ---- isolation: exactly the allocated GPUs, of the expected arch ----
+  std::string arch = prop.gcnArchName;
+  arch = arch.substr(0, arch.find(':'));   // "gfx950:sramecc+:xnack-" -> "gfx950"
+  std::set<std::string> bdfs;
+  for (int d = 0; d < count; ++d) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), d) == hipSuccess) bdfs.insert(norm_bdf(bus));
+  }
+  std::set<std::string> want_bdfs;
+  for (const auto& b : split_csv(std::getenv("AMD_GPU_BDFS"))) want_bdfs.insert(norm_bdf(b));
+  const auto nodes = render_nodes();
+  std::set<std::string> want_nodes;
+  for (const auto& r : split_csv(std::getenv("AMD_GPU_RENDER_NODES"))) want_nodes.insert(r);
+  const bool gpus_ok = expect_gpus < 0 || count == expect_gpus;
+  const bool arch_ok = expect_arch.empty() || arch == expect_arch;
+  // BDFs: partitions of one device share a BDF, so compare the sets
+  const bool bdf_ok = want_bdfs.empty() || bdfs == want_bdfs;
+  // render nodes: checked when /dev/dri is mounted the way CDI / DeviceSpecs
+  // inject it (one node per allocated GPU or partition)
+  const bool render_ok = want_nodes.empty() || nodes == want_nodes;
+  const bool isolated = gpus_ok && arch_ok && bdf_ok && render_ok;
+
+  const bool pass = mismatches == 0 && isolated;
   std::printf("RESULT {\"test\":\"vectoradd\",\"pass\":%s,\"n\":%ld,\"mismatches\":%ld,"
-              "\"device\":%d,\"visible_gpus\":%d,\"arch\":\"%s\",\"cus\":%d,"
-              "\"hbm_bytes\":%zu,\"stream_GBps\":%.1f}\n",
-              pass ? "true" : "false", n, mismatches, dev, count, prop.gcnArchName,
+              "\"device\":%d,\"visible_gpus\":%d,\"expected_gpus\":%d,\"arch\":\"%s\","
+              "\"expected_arch\":\"%s\",\"bdfs\":%s,\"expected_bdfs\":%s,"
+              "\"render_nodes\":%s,\"expected_render_nodes\":%s,"
+              "\"isolation\":{\"gpus\":%s,\"arch\":%s,\"bdf\":%s,\"render\":%s},"
+              "\"cus\":%d,\"hbm_bytes\":%zu,\"stream_GBps\":%.1f}\n",
+              pass ? "true" : "false", n, mismatches, dev, count, expect_gpus, arch.c_str(),
+              expect_arch.c_str(), json_list(bdfs).c_str(), json_list(want_bdfs).c_str(),
+              json_list(nodes).c_str(), json_list(want_nodes).c_str(), gpus_ok ? "true" : "false",
+              arch_ok ? "true" : "false", bdf_ok ? "true" : "false", render_ok ? "true" : "false",
               prop.multiProcessorCount, prop.totalGlobalMem, gbps);
   return pass ? 0 : 1;
 }

@@ -72,8 +72,10 @@ if [ $PLAN -eq 0 ]; then
 fi
 run kubectl apply -f "$REPO/deploy/examples/hip-vector-add.yaml"
 wait_pod hip-vector-add 300s
-results_of hip-vector-add | check_all_pass
-record 2 '{"test":"hip-vector-add","pass":true}'
+# every RESULT line passes AND the pod sees exactly its 1 allocated gfx950
+# GPU / render node (BASELINE.md:37)
+results_of hip-vector-add | run env PYTHONPATH="$REPO" python3 -m mxk8s.validate.isolation --gpus 1 --arch gfx950
+record 2 '{"test":"hip-vector-add","pass":true,"isolation":true}'
 
 step "config 3: validator pod amd.com/gpu=1, bf16 MFMA GEMM"
 run kubectl apply -f "$REPO/deploy/examples/gemm-validator.yaml"

@@ -68,6 +68,8 @@ def test_allocate_cdi_and_devicespecs(plugin_dir):
         assert ("/dev/dri/card3", "/dev/dri/card3", "rw") in paths
         assert c.envs["AMD_GPU_DEVICE_IDS"] == "0,2"
         assert c.envs["AMD_GPU_ARCH"] == "gfx950"
+        # the pod's payload compares /dev/dri with exactly these (BASELINE.md:37)
+        assert c.envs["AMD_GPU_RENDER_NODES"] == "/dev/dri/renderD128,/dev/dri/renderD130"
         bad = api.AllocateRequest()
         bad.container_requests.add(devices_ids=["9"])
         with pytest.raises(grpc.RpcError) as e:

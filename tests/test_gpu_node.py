@@ -90,6 +90,36 @@ def test_vector_add_binary_passes():
     assert res and res[-1]["test"] == "vectoradd" and res[-1]["pass"], res
 
 
+def test_vector_add_binary_checks_isolation():
+    """Config 2's isolation criterion on the real device (BASELINE.md:37):
+    the one-GPU box passes --expect-gpus 1 --expect-arch gfx950 with the
+    Allocate environment of its own render node, and fails (exit 1,
+    pass=false) when told to expect 8 GPUs, another arch or another node."""
+    from mxk8s.validate import isolation
+    exe = os.path.join(BIN, "mx-vector-add")
+    ok = _results(_run([exe, "--n", "50000", "--bw-mib", "0", "--expect-gpus", "1",
+                        "--expect-arch", "gfx950"]))
+    r = ok[-1]
+    assert r["pass"] and r["visible_gpus"] == 1 and r["arch"] == "gfx950", r
+    assert all(r["isolation"].values()), r
+    assert isolation.check_results(ok, gpus=1, arch="gfx950") == [], r
+    env_ok = dict(os.environ, AMD_GPU_RENDER_NODES=",".join(r["render_nodes"]),
+                  AMD_GPU_BDFS=",".join(r["bdfs"]), AMD_GPU_DEVICE_IDS="0", AMD_GPU_ARCH="gfx950")
+    p = subprocess.run([exe, "--n", "50000", "--bw-mib", "0"], capture_output=True, text=True,
+                       timeout=120, env=env_ok)
+    assert p.returncode == 0, p.stdout[-2000:]
+    for args, env in (
+            (["--expect-gpus", "8"], None),
+            (["--expect-arch", "gfx942"], None),
+            ([], dict(env_ok, AMD_GPU_RENDER_NODES="/dev/dri/renderD250")),
+            ([], dict(env_ok, AMD_GPU_BDFS="0000:ff:00.0"))):
+        p = subprocess.run([exe, "--n", "50000", "--bw-mib", "0", *args], capture_output=True,
+                           text=True, timeout=120, env=env or os.environ)
+        bad = _results(p.stdout)
+        assert p.returncode == 1 and bad and bad[-1]["pass"] is False, (args, p.stdout[-2000:])
+        assert isolation.check_results(bad, gpus=1, arch="gfx950"), (args, bad)
+
+
 def test_gemm_bench_binary_self_checks():
     out = _run([os.path.join(BIN, "mx-gemm-bench"), "--sizes", "4096", "--iters", "10",
                 "--warmup-ms", "200"])
