@@ -225,15 +225,27 @@ class DeviceState:
             self.generation += 1
             self._cv.notify_all()
 
-    def replace_gpus(self, gpus: list[node.GpuInfo]) -> None:
+    def replace_gpus(self, gpus: list[node.GpuInfo], gate: Optional[str] = None) -> None:
         """New GPU set (reconciliation): known IDs keep their health, new ones
-        start healthy, vanished ones are withdrawn; ListAndWatch re-sends."""
+        start healthy, vanished ones are withdrawn; ListAndWatch re-sends.
+        ``gate`` (a partition drain or a pending validation): EVERY ID, new
+        ones included, starts Unhealthy with that reason — a repartition
+        during a drain must not advertise its new partitions before the next
+        health pass."""
         with self._cv:
             self.gpus = {str(g.index): g for g in gpus}
-            self.health = {i: self.health.get(i, api.HEALTHY) for i in self.gpus}
-            self.reasons = {i: self.reasons.get(i, "healthy") for i in self.gpus}
+            if gate:
+                self.health = {i: api.UNHEALTHY for i in self.gpus}
+                self.reasons = {i: gate for i in self.gpus}
+            else:
+                self.health = {i: self.health.get(i, api.HEALTHY) for i in self.gpus}
+                self.reasons = {i: self.reasons.get(i, "healthy") for i in self.gpus}
             self.generation += 1
             self._cv.notify_all()
+
+    def all_unhealthy(self) -> bool:
+        with self._cv:
+            return all(h == api.UNHEALTHY for h in self.health.values())
 
 
 class AmdGpuDevicePlugin:
@@ -430,8 +442,8 @@ class AmdGpuDevicePlugin:
         # every device is withdrawn until the drain file goes away; so is
         # every device while a required validation is not valid for the
         # running driver instance (a driver reload voids the markers)
+        gate = self._gate()
         drain = read_drain(self.cfg.state_dir, self._boot)
-        pending = self._validation_pending()
         for ev in mon.new_events():
             dev = dev_of(ev.index, bdf_of.get(ev.index, "")) if ev.index >= 0 else None
             level = logging.INFO if ev.kind in (node.EVT_GPU_POST_RESET,
@@ -443,17 +455,24 @@ class AmdGpuDevicePlugin:
             dev = dev_of(st.index, st.bdf)
             if dev is None:
                 continue
-            updates[dev] = ((False, DRAIN_REASON) if drain else
-                            (False, f"{pending} validation pending") if pending else
-                            (st.healthy, st.reason))
+            updates[dev] = (False, gate) if gate else (st.healthy, st.reason)
             bdfs[dev] = st.bdf
+        if gate:
+            # devices the monitor did not match (index / BDF mismatch, a
+            # partition the monitor does not enumerate) are withdrawn too
+            for dev in list(gpus):
+                if dev not in updates:
+                    updates[dev] = (False, gate)
+                    bdfs[dev] = gpus[dev].bdf
         for dev in self.state.set_health_many(updates):
             healthy, reason = updates[dev]
             log.warning("device %s -> %s (%s)", dev, "Healthy" if healthy else "Unhealthy",
                         reason, extra={"device": dev, "event": "health_change",
                                        "reason": reason, "bdf": bdfs[dev]})
-        if drain and drain != self._drain_acked:
-            # every device is now Unhealthy in the state ListAndWatch streams
+        if drain and drain != self._drain_acked and self.state.all_unhealthy():
+            # every advertised device is now Unhealthy in the state
+            # ListAndWatch streams (checked, not assumed: only then may the
+            # partition manager write the new modes)
             ack = os.path.join(self.cfg.state_dir, DRAIN_ACK_FILE)
             with open(ack + ".tmp", "w") as f:
                 f.write(drain)
@@ -487,7 +506,7 @@ class AmdGpuDevicePlugin:
                 # watcher must not re-serve the retired socket in between
                 self._serve_lock.acquire()
                 self._retire_endpoint()      # before the new IDs exist in the state
-            self.state.replace_gpus(gpus)
+            self.state.replace_gpus(gpus, gate=self._gate())
             out["gpus_changed"] = True
             self.reconciles["gpus_changed"] += 1
             if renamed:
@@ -581,6 +600,16 @@ class AmdGpuDevicePlugin:
         self.registrations += 1
         self._kubelet_ino = _inode(self.cfg.kubelet_socket)
         log.info("registered %s with kubelet (%d)", self.resource_name, self.registrations)
+
+    def _gate(self) -> Optional[str]:
+        """Why every device must be withdrawn right now (None: nothing): a
+        partition change in progress (mxk8s.partition drain handshake), or a
+        required validation that is not valid for the running driver
+        instance (a driver reload / repartition voids the markers)."""
+        if read_drain(self.cfg.state_dir, self._boot):
+            return DRAIN_REASON
+        pending = self._validation_pending()
+        return f"{pending} validation pending" if pending else None
 
     def _validation_pending(self) -> Optional[str]:
         """First required validation whose marker is not valid, or None."""

@@ -35,7 +35,7 @@ import re
 import threading
 import time
 from fractions import Fraction
-from typing import Optional
+from typing import Optional, Sequence
 
 from ..chart import render as chart_render
 from ..chart.gotpl import FailError
@@ -86,23 +86,49 @@ def _named(items) -> bool:
     return bool(items) and all(isinstance(x, dict) and "name" in x for x in items)
 
 
-def is_subset(want, have) -> bool:
-    """Every field of ``want`` is present with the same value in ``have``:
-    server-side defaults and status on ``have`` are ignored, quantities
-    compare by value, and lists of named items (containers, env, volumes,
-    volumeMounts, ports) are matched by name, in any order, with extra live
-    items allowed (defaulted or injected ones).  Other lists (args, command,
-    tolerations) keep their order and length."""
+# Named list items the API server or an admission webhook may add to a live
+# object without the chart asking for them; every other extra item is drift.
+# A cluster with its own mutating webhooks lists their names with
+# Controller(injected=...) / the operator's --injected-name flag.
+INJECTED_NAME_PREFIXES = ("kube-api-access",)
+# lists whose order is semantic: init containers run in order (the node
+# validator's driver -> cdi -> vectoradd -> plugin chain depends on it)
+ORDERED_NAMED_LISTS = ("initContainers", "containers")
+
+
+def is_subset(want, have, key: str = "", injected: tuple = INJECTED_NAME_PREFIXES) -> bool:
+    """``have`` (live) is in sync with ``want`` (rendered): every field of
+    ``want`` is present with the same value, server-side defaults and status
+    on ``have`` are ignored, and quantities compare by value.  Lists of named
+    items (containers, env, volumes, volumeMounts, ports) are matched by
+    name, so that server-defaulted fields inside an item are tolerated; but
+    the set of names must be the same — an item the chart dropped, or one it
+    added, is drift — except names an admission controller injects
+    (``INJECTED_NAME_PREFIXES``).  ``initContainers`` / ``containers`` must
+    also keep their order.  Other lists (args, command, tolerations) keep
+    their order and length."""
     if isinstance(want, dict):
-        return isinstance(have, dict) and all(k in have and is_subset(v, have[k])
+        return isinstance(have, dict) and all(k in have and is_subset(v, have[k], k, injected)
                                               for k, v in want.items())
     if isinstance(want, list):
         if not isinstance(have, list):
             return False
         if _named(want):
-            by_name = {x.get("name"): x for x in have if isinstance(x, dict)}
-            return all(w["name"] in by_name and is_subset(w, by_name[w["name"]]) for w in want)
-        return len(want) == len(have) and all(is_subset(a, b) for a, b in zip(want, have))
+            live = [x for x in have if not (isinstance(x, dict) and isinstance(x.get("name"), str)
+                                            and x["name"].startswith(injected))]
+            if not _named(live) and live:
+                return False
+            want_names = [w["name"] for w in want]
+            live_names = [x["name"] for x in live]
+            if key in ORDERED_NAMED_LISTS:
+                if want_names != live_names:
+                    return False
+            elif sorted(want_names) != sorted(live_names):
+                return False
+            by_name = {x["name"]: x for x in live}
+            return all(is_subset(w, by_name[w["name"]], "", injected) for w in want)
+        return len(want) == len(have) and all(is_subset(a, b, "", injected)
+                                              for a, b in zip(want, have))
     if want == have:
         return True
     if isinstance(want, bool) or isinstance(have, bool):
@@ -129,8 +155,9 @@ class ReconcileResult:
 class Controller:
     def __init__(self, client: KubeClient, namespace: str = "amd-gpu",
                  release: str = "amd-gpu-stack", chart_dir: str = chart_render.CHART_DIR,
-                 delete_wait_s: float = 5.0):
+                 delete_wait_s: float = 5.0, injected: Sequence[str] = ()):
         self.client = client
+        self.injected = tuple(INJECTED_NAME_PREFIXES) + tuple(injected)
         self.namespace = namespace
         self.release = release
         self.chart_dir = chart_dir
@@ -179,7 +206,7 @@ class Controller:
             res.created.append(name)
             log.info("creating %s", name, extra={"event": "operand_created", "component": name})
             return self.client.create(coll, obj)
-        if is_subset(obj, live):
+        if is_subset(obj, live, injected=self.injected):
             return live
         if obj["kind"] == "Job":    # pod template is immutable: re-create
             return self._recreate_job(path, name, obj, live, res)
@@ -322,10 +349,20 @@ class Controller:
         woke it ("watch:<collection>" / "resync" / "stop")."""
         woke = threading.Event()
         why: list[str] = []
+        cancels: list = []
+        lock = threading.Lock()
+        done = threading.Event()        # set when this call returns: late opens cancel themselves
+
+        def opened(cancel):
+            with lock:
+                cancels.append(cancel)
+                late = done.is_set()
+            if late:
+                cancel()
 
         def watch_one(path, sel, rv):
             try:
-                for ev in self.client.watch(path, rv, timeout, sel):
+                for ev in self.client.watch(path, rv, timeout, sel, on_open=opened):
                     if ev.get("type") in ("ADDED", "MODIFIED", "DELETED"):
                         why.append("watch:" + path.rsplit("/", 1)[1])
                         woke.set()
@@ -335,7 +372,8 @@ class Controller:
                         woke.set()
                         return
             except Exception as e:                  # API server blip: fall back to the resync
-                log.debug("watch %s failed: %s", path, e)
+                if not done.is_set():
+                    log.debug("watch %s failed: %s", path, e)
 
         threads = []
         for path, sel in self._watched():
@@ -345,21 +383,32 @@ class Controller:
                 if e.status == 404:
                     continue
                 raise
-            t = threading.Thread(target=watch_one, args=(path, sel, rv), daemon=True)
+            t = threading.Thread(target=watch_one, args=(path, sel, rv), daemon=True,
+                                 name="mxk8s-watch")
             t.start()
             threads.append(t)
         end = time.monotonic() + timeout
-        while not woke.is_set():
-            if stop is not None and stop():
-                self.wakeups.append("stop")
-                return "stop"
-            left = end - time.monotonic()
-            if left <= 0:
-                self.wakeups.append("resync")
-                return "resync"
-            woke.wait(min(left, 0.2))
-        self.wakeups.append(why[0] if why else "watch")
-        return self.wakeups[-1]
+        result = None
+        while result is None:
+            if woke.is_set():
+                result = why[0] if why else "watch"
+            elif stop is not None and stop():
+                result = "stop"
+            elif end - time.monotonic() <= 0:
+                result = "resync"
+            else:
+                woke.wait(min(end - time.monotonic(), 0.2))
+        # end the other collections' long polls now instead of leaving their
+        # threads (and API-server watch connections) open for up to `timeout`
+        with lock:
+            done.set()
+            pending = list(cancels)
+        for cancel in pending:
+            cancel()
+        for t in threads:
+            t.join(timeout=2.0)
+        self.wakeups.append(result)
+        return result
 
     def run(self, interval: float = 300.0, stop=None) -> None:
         """Level-triggered loop: reconcile, then sleep until something this

@@ -21,11 +21,14 @@ def main(argv=None) -> int:
     p.add_argument("--server", default=None, help="API server URL (default: in-cluster)")
     p.add_argument("--token", default=None)
     p.add_argument("--log-format", choices=["json", "text"], default="json")
+    p.add_argument("--injected-name", action="append", default=[],
+                   help="name prefix of list items a mutating webhook adds to the operands "
+                        "(not drift); repeatable")
     a = p.parse_args(argv)
     setup_logging(a.log_format)
     log = logging.getLogger("mxk8s.operator")
     client = KubeClient(a.server, a.token) if a.server else KubeClient.in_cluster()
-    ctl = Controller(client, a.namespace, a.release)
+    ctl = Controller(client, a.namespace, a.release, injected=a.injected_name)
     if a.interval <= 0:
         try:
             ctl.reconcile_once()

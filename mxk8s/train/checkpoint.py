@@ -12,14 +12,18 @@ state dicts, no pickles.  Format ``mxk8s-flat-v2``:
                                            (its ZeRO-1 shard, or the full buffers when
                                            the optimizer is replicated — then rank 0 only)
   <dir>/meta.json                          commit record: step, world size, layout
-                                           fingerprint, sharding, and which step-<N>
+                                           fingerprint, sharding, which step-<N>, and
+                                           the committed step-<N> history
 
 Every save writes a NEW step directory; ``meta.json`` — written by rank 0
 after a barrier that every rank reaches once its shard is on disk, then
 renamed into place — is what makes it current.  An interrupted save leaves
 the previous step directory and the previous ``meta.json`` untouched, so the
-job resumes from the last complete checkpoint; the ``keep`` newest complete
-step directories are retained, older ones are removed after the commit.
+job resumes from the last complete checkpoint.  ``meta.json`` also lists the
+committed step directories (``history``); after each commit the ``keep``
+newest of those are retained and every other step directory is removed —
+older commits and the uncommitted leftovers of interrupted saves alike, so a
+stale higher-numbered directory never evicts a usable checkpoint.
 Every shard also carries its own ``step_count`` / ``layout`` / ``save_step``,
 which ``load`` checks against ``meta.json``.
 
@@ -88,13 +92,33 @@ def _write_meta(ckpt_dir: str, meta: dict) -> None:
     os.replace(tmp, os.path.join(ckpt_dir, "meta.json"))
 
 
-def _prune(ckpt_dir: str, current: str, keep: int) -> None:
-    """Remove step directories beyond the ``keep`` newest (never ``current``)."""
+def _read_meta(ckpt_dir: str) -> Optional[dict]:
+    try:
+        with open(os.path.join(ckpt_dir, "meta.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def _history(prev: Optional[dict], current: str, keep: int) -> list[str]:
+    """Committed step directories, oldest first, ending with ``current``:
+    the previous commit record's history (or its single ``path`` for records
+    written before the history existed), truncated to the ``keep`` newest."""
+    hist = []
+    if prev and prev.get("format") == FORMAT:
+        hist = list(prev.get("history") or ([prev["path"]] if prev.get("path") else []))
+    hist = [h for h in hist if h != current] + [current]
+    return hist[-max(1, keep):]
+
+
+def _prune(ckpt_dir: str, history: list[str]) -> None:
+    """Remove every step directory that is not one of the retained COMMITTED
+    ones: older commits beyond ``keep`` and uncommitted directories left by
+    an interrupted save (never counted toward ``keep``, whatever their step
+    number)."""
     import shutil
-    steps = sorted(d for d in os.listdir(ckpt_dir)
-                   if d.startswith("step-") and os.path.isdir(os.path.join(ckpt_dir, d)))
-    for d in steps[:max(0, len(steps) - max(1, keep))]:
-        if d != current:
+    for d in os.listdir(ckpt_dir):
+        if d.startswith("step-") and d not in history and os.path.isdir(os.path.join(ckpt_dir, d)):
             shutil.rmtree(os.path.join(ckpt_dir, d), ignore_errors=True)
 
 
@@ -118,10 +142,11 @@ def save(ckpt_dir: str, ddp, opt, step: int, keep: int = 2) -> None:
     # every shard is on disk before the commit record names this step
     mxdist.barrier()
     if rank == 0:
+        history = _history(_read_meta(ckpt_dir), sub, keep)
         _write_meta(ckpt_dir, {"step": step, "optimizer_step": opt.step_count, "world_size": world,
                                "sharded": sharded, "layout": fp, "numel": ddp.space.numel,
-                               "format": FORMAT, "path": sub})
-        _prune(ckpt_dir, sub, keep)
+                               "format": FORMAT, "path": sub, "history": history})
+        _prune(ckpt_dir, history)
     mxdist.barrier()
 
 

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import json
 import os
+import socket
 import ssl
 import urllib.error
 import urllib.parse
@@ -62,6 +63,10 @@ class KubeClient:
                 return json.loads(r.read() or b"{}")
         except urllib.error.HTTPError as e:
             raise KubeError(e.code, e.read().decode(errors="replace")[:500]) from None
+        except (OSError, ValueError, AttributeError):
+            if not cancelled:
+                raise
+            return      # cancelled by the caller (connection shut down under the read)
 
     def get(self, path: str) -> dict:
         return self._req("GET", path)
@@ -86,10 +91,12 @@ class KubeClient:
         return doc.get("items", []), str(doc.get("metadata", {}).get("resourceVersion", ""))
 
     def watch(self, path: str, resource_version: str = "", timeout_s: float = 30.0,
-              label_selector: Optional[str] = None):
+              label_selector: Optional[str] = None, on_open=None):
         """Yield the watch events ({"type": ADDED|MODIFIED|DELETED|ERROR,
         "object": ...}) of a collection after ``resource_version``, until the
-        server ends the watch (``timeoutSeconds``)."""
+        server ends the watch (``timeoutSeconds``).  ``on_open(cancel)`` gets a
+        callable that ends this watch from another thread (it shuts the
+        long-poll connection down, so the blocked read returns at once)."""
         q = {"watch": "1", "timeoutSeconds": str(max(1, int(timeout_s)))}
         if resource_version:
             q["resourceVersion"] = resource_version
@@ -99,8 +106,16 @@ class KubeClient:
         req.add_header("Accept", "application/json")
         if self.token:
             req.add_header("Authorization", f"Bearer {self.token}")
+        cancelled = []
+
+        def cancel(r):
+            cancelled.append(True)
+            _shutdown(r)
+
         try:
             with urllib.request.urlopen(req, timeout=timeout_s + 10, context=self._ctx) as r:
+                if on_open is not None:
+                    on_open(lambda: cancel(r))
                 for line in r:
                     line = line.strip()
                     if line:
@@ -148,3 +163,16 @@ def object_path(obj: dict, default_namespace: Optional[str] = None) -> str:
     md = obj.get("metadata", {})
     ns = None if obj["kind"] in CLUSTER_SCOPED else (md.get("namespace") or default_namespace)
     return collection_path(obj["apiVersion"], obj["kind"], ns) + "/" + md["name"]
+
+
+def _shutdown(resp) -> None:
+    """Unblock a thread reading a streaming HTTP response and close it."""
+    try:
+        sock = resp.fp.raw._sock            # http.client.HTTPResponse over a socket
+        sock.shutdown(socket.SHUT_RDWR)
+    except (AttributeError, OSError):
+        pass
+    try:
+        resp.close()
+    except Exception:                       # already closed / mid-read in the other thread
+        pass

@@ -236,9 +236,11 @@ class NodeValidator:
     def __init__(self, state_dir: str, root: str = "", steps=STEPS,
                  cdi_spec: str = "/etc/cdi/amd.com-gpu.json", cdi_kind: str = "amd.com/gpu",
                  plugin_dir: str = "/var/lib/kubelet/device-plugins",
-                 plugin_socket: str = "amd-gpu.sock", step_timeout: float = 300.0,
+                 plugin_socket: Optional[str] = None, step_timeout: float = 300.0,
                  poll: float = 1.0,
-                 vectoradd: Callable[[int], tuple[bool, str]] = _run_vectoradd):
+                 vectoradd: Callable[[int], tuple[bool, str]] = _run_vectoradd,
+                 resource_name: str = "amd.com/gpu", partition_naming: str = "single",
+                 rename_shared: bool = False, replicas: int = 1):
         unknown = [s for s in steps if s not in STEPS]
         if unknown:
             raise ValueError(f"unknown validation step(s): {unknown}")
@@ -248,6 +250,21 @@ class NodeValidator:
         self.step_timeout, self.poll = step_timeout, poll
         self.vectoradd = vectoradd
         self.runs = 0
+        self.resource_name, self.partition_naming = resource_name, partition_naming
+        self.rename_shared, self.replicas = rename_shared, replicas
+
+    def plugin_socket_for(self, gpus) -> str:
+        """The socket the device plugin serves for the current GPU set: the
+        explicit --plugin-socket, else resolved exactly as the plugin does
+        (PluginConfig.effective_resource / socket_for), so a CPX/DPX node
+        under partitionNaming=mixed is probed on amd-gpu-<mode>.sock."""
+        if self.plugin_socket:
+            return self.plugin_socket
+        from ..deviceplugin.plugin import PluginConfig
+        cfg = PluginConfig(resource_name=self.resource_name, plugin_dir=self.plugin_dir,
+                           partition_naming=self.partition_naming, replicas=self.replicas,
+                           rename_shared=self.rename_shared, register=False)
+        return cfg.socket_for(cfg.effective_resource(gpus))
 
     def check(self, step: str) -> tuple[bool, dict]:
         if step == "driver":
@@ -257,10 +274,10 @@ class NodeValidator:
         if step == "vectoradd":
             return check_vectoradd(self.root, self.vectoradd)
         try:
-            n = len(node.enumerate_gpus(self.root))
+            gpus = node.enumerate_gpus(self.root)
         except RuntimeError:
-            n = 1
-        return check_plugin(self.plugin_dir, self.plugin_socket, n)
+            gpus = []
+        return check_plugin(self.plugin_dir, self.plugin_socket_for(gpus), max(1, len(gpus)))
 
     def run_chain(self, stop: Optional[Callable[[], bool]] = None) -> bool:
         """Run the steps in order; each is retried until it passes or its
@@ -311,7 +328,12 @@ def main(argv=None) -> int:
     p.add_argument("--cdi-spec", default="/etc/cdi/amd.com-gpu.json")
     p.add_argument("--cdi-kind", default="amd.com/gpu")
     p.add_argument("--plugin-dir", default="/var/lib/kubelet/device-plugins")
-    p.add_argument("--plugin-socket", default="amd-gpu.sock")
+    p.add_argument("--plugin-socket", default=None,
+                   help="default: the socket the plugin serves for the current GPU set")
+    p.add_argument("--resource-name", default="amd.com/gpu")
+    p.add_argument("--partition-naming", choices=["single", "mixed"], default="single")
+    p.add_argument("--replicas", type=int, default=1)
+    p.add_argument("--rename-shared", default="false")
     p.add_argument("--log-format", choices=["json", "text"], default="json")
     a = p.parse_args(argv)
     setup_logging(a.log_format)
@@ -320,7 +342,10 @@ def main(argv=None) -> int:
         return 0 if wait_for(a.state_dir, steps, a.sysfs_root, a.timeout) else 1
     v = NodeValidator(a.state_dir, a.sysfs_root, [s for s in a.steps.split(",") if s],
                       a.cdi_spec, a.cdi_kind, a.plugin_dir, a.plugin_socket,
-                      step_timeout=a.timeout if a.timeout > 0 else 300.0)
+                      step_timeout=a.timeout if a.timeout > 0 else 300.0,
+                      resource_name=a.resource_name, partition_naming=a.partition_naming,
+                      replicas=a.replicas,
+                      rename_shared=str(a.rename_shared).lower() in ("1", "true", "yes"))
     if a.watch <= 0:
         return 0 if v.run_chain() else 1
     fp = None

@@ -335,6 +335,20 @@ def test_checkpoint_retention_and_legacy_v1(tmp_path):
     assert sorted(d for d in os.listdir(ck) if d.startswith("step-")) == \
         [checkpoint.step_dirname(3), checkpoint.step_dirname(4)]
     assert checkpoint.load(ck, ddp, opt) == 4
+    assert json.load(open(os.path.join(ck, "meta.json")))["history"] == \
+        [checkpoint.step_dirname(3), checkpoint.step_dirname(4)]
+    # uncommitted directories never count toward `keep`.  A stale,
+    # HIGHER-numbered step-900 (a run that died after writing its shards) and
+    # an incomplete step-200 between the commits: resuming and saving 300
+    # keeps the two newest COMMITTED steps (4, 300) and drops the leftovers.
+    for stale in (900, 200):
+        d = os.path.join(ck, checkpoint.step_dirname(stale))
+        os.makedirs(d)
+        open(os.path.join(d, "optim-rank0.safetensors"), "w").close()
+    checkpoint.save(ck, ddp, opt, step=300, keep=2)
+    assert sorted(d for d in os.listdir(ck) if d.startswith("step-")) == \
+        [checkpoint.step_dirname(4), checkpoint.step_dirname(300)]
+    assert checkpoint.load(ck, ddp, opt) == 300
     # legacy v1: written by an earlier version of save()
     v1 = str(tmp_path / "v1")
     os.makedirs(v1)

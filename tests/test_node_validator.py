@@ -207,3 +207,52 @@ def test_exporter_and_doctor_report_validations(tmp_path):
     checks = doctor.check_gpu(doctor.Host(root, kubectl=lambda *a: (127, "no kubectl")))
     c = next(c for c in checks if c.name == "node validation")
     assert c.status == "fail" and "driver=ready" in c.detail and "cdi-validation" in c.hint
+
+
+def test_plugin_step_finds_the_mixed_naming_partition_socket(tmp_path):
+    """with partitionNaming=mixed on a CPX node the plugin serves
+    amd.com/gpu-cpx on amd-gpu-cpx.sock; the plugin validation must probe that
+    socket (resolved as the plugin resolves it), not amd-gpu.sock — else the
+    node-validator crash-loops on every partitioned node."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests", "fixtures"))
+    import make_sysfs
+    root = str(tmp_path / "root")
+    make_sysfs.tree_partitioned(root, "CPX", "NPS2")
+    state = str(tmp_path / "state")
+    d = tempfile.mkdtemp(prefix="mxdp", dir="/tmp")
+    kube = FakeKubelet(d).start()
+    plugin = AmdGpuDevicePlugin(PluginConfig(plugin_dir=d, sysfs_root=root, health_interval=0.05,
+                                             watch_interval=0.1, use_smi_events=False,
+                                             reconcile_interval=0,
+                                             partition_naming="mixed")).start()
+    try:
+        reg = kube.wait_registration()
+        assert reg.resource_name == "amd.com/gpu-cpx" and reg.endpoint == "amd-gpu-cpx.sock"
+        v = vnode.NodeValidator(state, root, ["plugin"], plugin_dir=d, step_timeout=5, poll=0.05,
+                                partition_naming="mixed")
+        assert v.plugin_socket_for(node.enumerate_gpus(root)) == "amd-gpu-cpx.sock"
+        assert v.run_chain()
+        pm = vnode.read_marker(state, "plugin")["detail"]
+        assert pm["socket"].endswith("amd-gpu-cpx.sock") and pm["devices"] == 64
+        # single naming on the same node: the base socket (what the plugin serves then)
+        assert vnode.NodeValidator(state, root, ["plugin"], plugin_dir=d).plugin_socket_for(
+            node.enumerate_gpus(root)) == "amd-gpu.sock"
+    finally:
+        plugin.stop()
+        kube.stop()
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def test_chart_passes_the_plugin_naming_to_the_validator():
+    from mxk8s.chart import render
+    values = render.deep_merge(render.load_values(render.CHART_DIR),
+                               {"devicePlugin": {"partitionNaming": "mixed"}})
+    docs = render.manifests(render.render(values))
+    ds = next(x for x in docs if x["kind"] == "DaemonSet"
+              and x["metadata"]["name"].endswith("node-validator"))
+    pod = ds["spec"]["template"]["spec"]
+    for c in pod["initContainers"] + pod["containers"]:
+        cmd = " ".join(c["command"])
+        if "plugin" in cmd.split("--steps=", 1)[-1].split()[0]:
+            assert "--partition-naming=mixed" in cmd and "--resource-name=amd.com/gpu" in cmd, cmd

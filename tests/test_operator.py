@@ -174,8 +174,9 @@ def test_is_subset_quantities_and_named_lists():
     assert op.is_subset({"cpu": "0.5", "memory": "1024Mi"}, {"cpu": "500m", "memory": "1Gi"})
     assert not op.is_subset({"cpu": "0.5"}, {"cpu": "50m"})
     want = {"env": [{"name": "A", "value": "1"}], "volumes": [{"name": "x"}, {"name": "y"}]}
-    have = {"env": [{"name": "INJ", "value": "2"}, {"name": "A", "value": "1"}],
-            "volumes": [{"name": "y", "hostPath": {"path": "/y"}}, {"name": "x"}]}
+    have = {"env": [{"name": "A", "value": "1"}],
+            "volumes": [{"name": "y", "hostPath": {"path": "/y"}}, {"name": "x"},
+                        {"name": "kube-api-access-7xk2p", "projected": {}}]}   # injected
     assert op.is_subset(want, have)
     assert not op.is_subset({"env": [{"name": "A", "value": "1"}]}, {"env": [{"name": "A", "value": "2"}]})
     assert not op.is_subset({"args": ["--a", "--b"]}, {"args": ["--b", "--a"]})   # order kept
@@ -183,12 +184,34 @@ def test_is_subset_quantities_and_named_lists():
     assert op.parse_quantity("1e3") == 1000 and op.parse_quantity("30s") is None
 
 
+def test_is_subset_named_list_membership_and_order_are_drift():
+    """an env var / volume / container the chart DROPPED is still
+    on the live object -> drift (else the change is never applied); one the
+    chart added is missing live -> drift; init containers run in order, so a
+    re-ordering is drift; env order alone is not."""
+    live = {"env": [{"name": "A", "value": "1"}, {"name": "OLD", "value": "x"}]}
+    assert not op.is_subset({"env": [{"name": "A", "value": "1"}]}, live)
+    assert not op.is_subset({"env": [{"name": "A", "value": "1"}, {"name": "NEW", "value": "y"},
+                                     {"name": "OLD", "value": "x"}]}, live)
+    assert op.is_subset({"env": [{"name": "OLD", "value": "x"}, {"name": "A", "value": "1"}]}, live)
+    chain = [{"name": n, "image": "i"} for n in ("driver", "cdi", "vectoradd", "plugin")]
+    spec = {"template": {"spec": {"initContainers": chain, "containers": [{"name": "main"}]}}}
+    swapped = {"template": {"spec": {"initContainers": [chain[1], chain[0], *chain[2:]],
+                                     "containers": [{"name": "main"}]}}}
+    assert op.is_subset(spec, spec)
+    assert not op.is_subset(spec, swapped)
+    two = {"containers": [{"name": "a"}, {"name": "b"}]}
+    assert not op.is_subset(two, {"containers": [{"name": "b"}, {"name": "a"}]})
+    assert not op.is_subset({"containers": [{"name": "a"}]}, two)      # a container removed
+
+
 def test_normalising_server_zero_writes_after_first_reconcile():
     srv = FakeApiServer(normalize=True).start()
     try:
         _policy(srv, {"devicePlugin": {"resources": {"requests": {"cpu": "0.05", "memory": "65536Ki"},
                                                      "limits": {"memory": "0.25Gi"}}}})
-        ctl = op.Controller(KubeClient(srv.url), NS)
+        # the fake server's "mutating webhook" injects INJECTED_BY_WEBHOOK
+        ctl = op.Controller(KubeClient(srv.url), NS, injected=["INJECTED_BY_WEBHOOK"])
         r = ctl.reconcile_once()
         assert r.created
         live = srv.objects[f"{DS}/amd-gpu-stack-device-plugin"]["spec"]["template"]["spec"]
@@ -286,3 +309,27 @@ def test_controller_wakes_on_watch_events_not_the_resync(api):
     finally:
         stop.set()
         t.join(timeout=5)
+
+
+def test_wait_for_change_leaves_no_watch_threads_behind(api):
+    """each wakeup ends the OTHER collections' long polls too, so
+    repeated wakeups (DaemonSet status churn) do not pile up threads and
+    API-server watch connections for up to the resync interval."""
+    ctl = op.Controller(KubeClient(api.url), NS)
+    _policy(api)
+    ctl.reconcile_once()
+    path = f"{DS}/amd-gpu-stack-node-labeller"
+
+    def live():
+        return [t for t in threading.enumerate() if t.name == "mxk8s-watch" and t.is_alive()]
+
+    for i in range(6):
+        def poke():
+            time.sleep(0.3)
+            o = copy.deepcopy(api.objects[path])
+            o.setdefault("status", {})["observedGeneration"] = i + 1
+            api.handle("PUT", path, o)
+        threading.Thread(target=poke, daemon=True).start()
+        assert ctl.wait_for_change(60.0).startswith("watch:")
+        assert live() == [], live()
+    assert ctl.wait_for_change(0.5) == "resync" and live() == []

@@ -308,3 +308,49 @@ def test_plugin_readvertises_partitions_with_mixed_naming(tmp_path):
         plugin.stop()
         kube.stop()
         shutil.rmtree(d, ignore_errors=True)
+
+
+def test_repartition_during_drain_keeps_new_partitions_withdrawn(tmp_path):
+    """a repartition while the drain file is present must advertise
+    the NEW partition IDs Unhealthy from the start (reconcile_once, before any
+    health pass), and the drain ack is written only once every advertised ID
+    is Unhealthy in the state ListAndWatch streams."""
+    root = spx_root(str(tmp_path))
+    state = str(tmp_path / "state")
+    plugin = AmdGpuDevicePlugin(PluginConfig(plugin_dir=str(tmp_path / "dp"), sysfs_root=root,
+                                             use_smi_events=False, reconcile_interval=0,
+                                             state_dir=state, register=False))
+    assert set(plugin.state.health.values()) == {api.HEALTHY}
+    mgr = partition.PartitionManager(FakeNodeClient("n1", {}), "n1", root, state_dir=state)
+    mgr._set_drain("t1")
+    ack = os.path.join(state, partition.DRAIN_ACK_FILE)
+    # the driver re-enumerates as CPX x NPS2 while the drain is active
+    tmp = root + ".new"
+    make_sysfs.tree_partitioned(tmp, "CPX", "NPS2")
+    shutil.rmtree(root)
+    os.rename(tmp, root)
+    out = plugin.reconcile_once()
+    assert out["gpus_changed"] and len(plugin.state.gpus) == 64
+    assert set(plugin.state.health.values()) == {api.UNHEALTHY}
+    assert set(plugin.state.reasons.values()) == {partition.DRAIN_REASON}
+    assert not os.path.exists(ack)              # no health pass yet, no ack
+    plugin.check_health_once()
+    assert set(plugin.state.health.values()) == {api.UNHEALTHY}
+    assert open(ack).read() == "t1"
+    # an ack is never written while some advertised ID is still Healthy
+    os.unlink(ack)
+    plugin._drain_acked = None
+    real = plugin.state.set_health_many
+    plugin.state.set_health_many = lambda updates: real(
+        {k: v for k, v in updates.items() if k != "63"})
+    plugin.state.health["63"] = api.HEALTHY
+    plugin.check_health_once()
+    assert not os.path.exists(ack)
+    plugin.state.set_health_many = real
+    plugin.check_health_once()
+    assert os.path.exists(ack)
+    # drain lifted: the partitions come back Healthy on the next pass
+    mgr._set_drain(None)
+    plugin.check_health_once()
+    assert set(plugin.state.health.values()) == {api.HEALTHY}
+    plugin.monitor.close()
