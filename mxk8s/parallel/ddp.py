@@ -20,7 +20,11 @@ Design (MI355X-first rather than a copy of torch DDP's call pattern):
 * ``reduce_dtype="fp32"``: a bucket is cast to fp32 when it completes and
   reduced in fp32 (2x the bytes on the wire), then rounded to bf16 ONCE; the
   bf16 default rounds the running sum at every ring hop (world - 1 bf16
-  roundings per element at world 8, tests/test_ddp_cpu.py measures both);
+  roundings per element at world 8, tests/test_ddp_cpu.py measures both).
+  The fp32 copies live in a ring of ``stage_slots`` (3) bucket-sized slots,
+  cast in and rounded back on a side stream that also issues the
+  collectives, so neither a full fp32 copy of the gradients nor the casts
+  sit on the compute stream;
 * ``shard_optimizer=True`` (ZeRO-1): buckets are padded to world*64 elements,
   each bucket is REDUCE-SCATTERED instead of all-reduced (rank r keeps chunk
   r), the fp32 master/moments exist only for the rank's shard (12 B/param /
@@ -135,7 +139,7 @@ class FlatParamSpace:
 
 
 class Bucket:
-    __slots__ = ("start", "end", "params", "pending", "handle", "launched", "shard_off")
+    __slots__ = ("start", "end", "params", "pending", "handle", "launched", "shard_off", "index")
 
     def __init__(self, start: int, end: int = 0, params=None):
         self.start = start
@@ -145,6 +149,7 @@ class Bucket:
         self.handle = None
         self.launched = False
         self.shard_off = 0      # offset of this bucket's chunk in the rank's shard
+        self.index = 0          # position in FlatDDP.buckets
 
     def chunk(self, world: int) -> int:
         return (self.end - self.start) // world
@@ -155,7 +160,8 @@ class FlatDDP:
 
     def __init__(self, module: nn.Module, bucket_mb: float = 512.0,
                  process_group=None, broadcast_from: Optional[int] = 0,
-                 shard_optimizer: bool = False, reduce_dtype: str = "bf16"):
+                 shard_optimizer: bool = False, reduce_dtype: str = "bf16",
+                 stage_slots: int = 3):
         if reduce_dtype not in ("bf16", "fp32"):
             raise ValueError(f"reduce_dtype must be bf16 or fp32, got {reduce_dtype!r}")
         self.module = module
@@ -174,6 +180,7 @@ class FlatDDP:
         shard_off = 0
         for start, end, params in self.space.buckets:
             b = Bucket(start, end, params)
+            b.index = len(self.buckets)
             b.shard_off = shard_off
             shard_off += b.chunk(self.world) if self.sharded else 0
             self.buckets.append(b)
@@ -184,16 +191,33 @@ class FlatDDP:
         self.grad_shard = (torch.zeros(shard_off, dtype=self.space.dtype,
                                        device=self.space.grad_buf.device)
                            if self.sharded else None)
-        # fp32 wire format: per-bucket fp32 staging (the whole gradient space,
-        # since every bucket may be in flight at once) and, sharded, an fp32
-        # copy of the rank's shard; only when the gradients are not fp32 already
+        # fp32 wire format: a RING of `stage_slots` fp32 staging slots, each
+        # the size of the largest bucket (not a copy of the whole gradient
+        # space: 32 GB for Llama-3-8B).  A bucket takes slot j % slots; the
+        # slot's previous bucket is finished (its result rounded back to
+        # bf16) first, so at most `stage_slots` buckets are on the wire at
+        # once.  stage_slots=0: one slot per bucket (every bucket in flight).
         self.reduce_fp32 = (reduce_dtype == "fp32" and self.world > 1 and
                             self.space.dtype != torch.float32)
         dev = self.space.grad_buf.device
-        self._f32 = (torch.empty(self.space.numel, dtype=torch.float32, device=dev)
-                     if self.reduce_fp32 else None)
-        self._f32_shard = (torch.empty(shard_off, dtype=torch.float32, device=dev)
-                           if self.reduce_fp32 and self.sharded else None)
+        self.stage_slots = 0
+        self._slots: list = []
+        self._slot_out: list = []
+        self._slot_owner: list = []
+        if self.reduce_fp32:
+            n_slots = len(self.buckets) if stage_slots <= 0 else min(stage_slots, len(self.buckets))
+            big = max(b.end - b.start for b in self.buckets)
+            self.stage_slots = n_slots
+            self._slots = [torch.empty(big, dtype=torch.float32, device=dev) for _ in range(n_slots)]
+            # sharded: the reduce-scatter's fp32 output chunk of each slot
+            self._slot_out = ([torch.empty(big // self.world, dtype=torch.float32, device=dev)
+                               for _ in range(n_slots)] if self.sharded else [])
+            self._slot_owner = [None] * n_slots
+        # the fp32 casts in and out of the slots run on a side stream that the
+        # collectives are issued from, so they ride along with RCCL instead of
+        # serialising on the compute stream behind the backward
+        self._side = (torch.cuda.Stream(device=dev)
+                      if self.reduce_fp32 and dev.type == "cuda" else None)
         self._sync_enabled = True
         self._hooks = []
         if self.world > 1:
@@ -219,36 +243,66 @@ class FlatDDP:
             b.handle = None
             b.launched = False
 
+    def _side_ctx(self):
+        return torch.cuda.stream(self._side) if self._side is not None else contextlib.nullcontext()
+
     def _launch(self, b: Bucket) -> None:
         if b.launched:
             return
         b.launched = True
         g = self.space.grad_buf[b.start:b.end]
-        if self.reduce_fp32:
-            wire = self._f32[b.start:b.end]
+        if not self.reduce_fp32:
+            if self.sharded:
+                c = b.chunk(self.world)
+                out = self.grad_shard[b.shard_off:b.shard_off + c]
+                b.handle = dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM,
+                                                      group=self.group, async_op=True)
+            else:
+                b.handle = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group,
+                                           async_op=True)
+            return
+        k = b.index % self.stage_slots
+        if self._side is not None:
+            ready = torch.cuda.current_stream(g.device).record_event()
+        with self._side_ctx():
+            if self._side is not None:
+                self._side.wait_event(ready)          # bucket b's gradients are complete
+            prev = self._slot_owner[k]
+            if prev is not None:
+                self._round_back(prev)                # frees slot k
+            n = b.end - b.start
+            wire = self._slots[k][:n]
             wire.copy_(g)
-        else:
-            wire = g
+            self._slot_owner[k] = b
+            if self.sharded:
+                out = self._slot_out[k][:b.chunk(self.world)]
+                b.handle = dist.reduce_scatter_tensor(out, wire, op=dist.ReduceOp.SUM,
+                                                      group=self.group, async_op=True)
+            else:
+                b.handle = dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.group,
+                                           async_op=True)
+
+    def _round_back(self, b: Bucket) -> None:
+        """(fp32 wire, on the side stream) wait for b's collective and round
+        its fp32 result to bf16 once, into the gradient buffer / shard."""
+        k = self._slot_owner.index(b)
+        b.handle.wait()
+        b.handle = None
         if self.sharded:
             c = b.chunk(self.world)
-            out = (self._f32_shard if self.reduce_fp32 else self.grad_shard)[b.shard_off:b.shard_off + c]
-            b.handle = dist.reduce_scatter_tensor(out, wire, op=dist.ReduceOp.SUM, group=self.group,
-                                                  async_op=True)
+            self.grad_shard[b.shard_off:b.shard_off + c].copy_(self._slot_out[k][:c])
         else:
-            b.handle = dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self.space.grad_buf[b.start:b.end].copy_(self._slots[k][:b.end - b.start])
+        self._slot_owner[k] = None
 
     def _finish_bucket(self, b: Bucket) -> None:
-        """Wait for bucket b's reduction (a stream wait under RCCL) and, with
-        the fp32 wire format, round its result to bf16 once."""
-        b.handle.wait()
+        """Wait for bucket b's reduction (a stream wait under RCCL); with the
+        fp32 wire format its slot is rounded back on the side stream."""
         if not self.reduce_fp32:
+            b.handle.wait()
             return
-        if self.sharded:
-            c = b.chunk(self.world)
-            self.grad_shard[b.shard_off:b.shard_off + c].copy_(
-                self._f32_shard[b.shard_off:b.shard_off + c])
-        else:
-            self.space.grad_buf[b.start:b.end].copy_(self._f32[b.start:b.end])
+        with self._side_ctx():
+            self._round_back(b)
 
     def _on_grad(self, p) -> None:
         if not self._sync_enabled:
@@ -277,6 +331,9 @@ class FlatDDP:
             for b in self.buckets:
                 if b.handle is not None:
                     self._finish_bucket(b)
+            if self._side is not None:
+                # the optimizer (compute stream) reads what the side stream wrote
+                torch.cuda.current_stream(self._side.device).wait_stream(self._side)
         self._reset_buckets()
 
     def zero_grad(self) -> None:

@@ -51,7 +51,7 @@ def _events_time(fn, iters: int) -> list[float]:
 
 
 def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
-        is_ablation=lambda v: False) -> list[dict]:
+        is_ablation=lambda v: False, pad: int = 0) -> list[dict]:
     dev = device or torch.device("cuda", torch.cuda.current_device())
     L = _lib.lib()
     stream = lambda: _lib.stream_ptr(dev)  # noqa: E731
@@ -60,15 +60,18 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
         M, N, K = n if isinstance(n, tuple) else (n, n, n)
         g = torch.Generator(device=dev)
         g.manual_seed(M * 7 + N * 3 + K)
-        A = (torch.rand((M, K), device=dev, generator=g) * 2 - 1).bfloat16()
-        Bt = (torch.rand((N, K), device=dev, generator=g) * 2 - 1).bfloat16()
+        # pad > 0: operands are [:, :K] views of (rows, K + pad) buffers, so
+        # lda = ldb = K + pad (a diagnostic of power-of-two row strides)
+        A = (torch.rand((M, K + pad), device=dev, generator=g) * 2 - 1).bfloat16()[:, :K]
+        Bt = (torch.rand((N, K + pad), device=dev, generator=g) * 2 - 1).bfloat16()[:, :K]
+        lda = ldb = K + pad
         C = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
         ref = torch.matmul(A, Bt.t())
         kernels = {}
         for v in variants:
             def mk(v=v):
                 st = L.mxk_gemm_bf16_tn_variant(A.data_ptr(), Bt.data_ptr(), C.data_ptr(), M, N, K,
-                                                K, K, N, v, stream())
+                                                lda, ldb, N, v, stream())
                 if st:
                     _lib.check(st, f"gemm variant {v}")
             name = L.mxk_gemm_bf16_tn_variant_name(v)
@@ -106,7 +109,7 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
         flops = 2.0 * M * N * K
         for name, ts in samples.items():
             med = statistics.median(ts)
-            r = {"kernel": name, "M": M, "N": N, "K": K, "dtype": "bf16",
+            r = {"kernel": name, "M": M, "N": N, "K": K, "lda": lda, "dtype": "bf16",
                  "median_ms": med * 1e3, "min_ms": min(ts) * 1e3,
                  "tflops_median": flops / med / 1e12, "tflops_best": flops / min(ts) / 1e12,
                  "samples": len(ts), "data": "uniform[-1,1) random"}
@@ -126,6 +129,7 @@ def main(argv=None) -> int:
     p.add_argument("--rounds", type=int, default=6)
     p.add_argument("--warmup-s", type=float, default=2.0)
     p.add_argument("--device", type=int, default=None)
+    p.add_argument("--pad", type=int, default=0, help="lda = ldb = K + pad (multiple of 8)")
     a = p.parse_args(argv)
     if a.device is not None:
         torch.cuda.set_device(a.device)
@@ -145,7 +149,7 @@ def main(argv=None) -> int:
     sizes = [int(x) for x in a.sizes.split(",")] if a.sizes else []
     sizes += [tuple(int(v) for v in x.split("x")) for x in a.shapes.split(",") if x]
     run(sizes, variants, a.iters, a.warmup_s, a.rounds,
-        is_ablation=lambda v: bool(_lib.lib().mxk_gemm_bf16_tn_is_ablation(v)))
+        is_ablation=lambda v: bool(_lib.lib().mxk_gemm_bf16_tn_is_ablation(v)), pad=a.pad)
     return 0
 
 

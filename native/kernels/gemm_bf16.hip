@@ -75,6 +75,8 @@
 //           DMA reads each row's 128 B in lane order; 38: only the 64-B
 //           halves swapped) - prices the permuted DMA source against the
 //           LDS bank conflicts it removes; 39 / 40: XOR masks 6 / 5
+//  41-43    26 with the XCD sub-block of the super-block tile map 4 x 8 /
+//           2 x 16 / 16 x 2 tiles instead of 8 x 4 (L2-miss A/B)
 //  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
 //           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
 //           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
@@ -1159,7 +1161,7 @@ int mxk_gemm_bf16_tn_ring_launch(int slots, const void* A, const void* Bt, void*
                                  int K, int lda, int ldb, int ldc, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 41;
+constexpr int kNumVariants = 44;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -1168,7 +1170,8 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "w4j_spreadk0", "w4j_hb_bouter", "w4j_hb_prio", "w4j_rot_xcd", "w4j_rot_wg", "pp8",
     "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst", "w4t_trickle", "w4t_trickle_lds", "w4j_ldsst_aln64", "w4j_ldsst_aln64p4",
     "w4j_ldsst_aln64p8", "w4j_ldsst_aln64p12", "w4j_ldsst_linear", "w4j_ldsst_swz_half",
-    "w4j_ldsst_swz6", "w4j_ldsst_swz5"};
+    "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
+    "w4j_ldsst_map16x2"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -1254,6 +1257,9 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 38: launch_w4i<1, 4, 1, 0, 1, 0, 0, 0, 4>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 39: launch_w4i<1, 4, 1, 0, 1, 0, 0, 0, 6>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 40: launch_w4i<1, 4, 1, 0, 1, 0, 0, 0, 5>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 41: launch_w4i<2, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 42: launch_w4i<3, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 43: launch_w4i<4, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 29: mxk_gemm_bf16_tn_ring_launch(4, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 30: mxk_gemm_bf16_tn_ring_launch(5, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 19:

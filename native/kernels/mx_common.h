@@ -142,9 +142,24 @@ __device__ __forceinline__ uint32_t lds_addr32(T* shared_array) {
 //         Cache-sized at 16384^2) instead of every A panel.  Rounds snake over
 //         the super-block grid so consecutive rounds share their A panels.
 //         Needs tiles_m % 16 == tiles_n % 16 == 0; MAP 0 otherwise.
+//  MAP 2 / 3 / 4 (A/B records): the MAP 1 super-block with the XCD sub-block
+//         4 x 8 / 2 x 16 / 16 x 2 tiles (M x N) instead of 8 x 4.
 template <int MAP>
 __device__ __forceinline__ void w4b_tile(int bid, int nwg, int tiles_m, int tiles_n, int* m0,
                                          int* n0) {
+  if (MAP >= 2 && MAP <= 4 && (tiles_m & 15) == 0 && (tiles_n & 15) == 0) {
+    constexpr int SM = MAP == 2 ? 4 : MAP == 3 ? 2 : 16;   // sub-block rows; SM * SN = 32
+    constexpr int XM = 16 / SM;                             // XCD grid: XM x (8 / XM)
+    const int xcd = bid & 7, l = bid >> 3;
+    const int round = l >> 5, pos = l & 31;
+    const int sbn = tiles_n >> 4;
+    const int sm = round / sbn;
+    int sn = round - sm * sbn;
+    if (sm & 1) sn = sbn - 1 - sn;
+    *m0 = (sm * 16 + (xcd % XM) * SM + pos % SM) * 256;
+    *n0 = (sn * 16 + (xcd / XM) * (32 / SM) + pos / SM) * 256;
+    return;
+  }
   if (MAP == 1 && (tiles_m & 15) == 0 && (tiles_n & 15) == 0) {
     const int xcd = bid & 7, l = bid >> 3;
     const int round = l >> 5, pos = l & 31;

@@ -394,11 +394,16 @@ def _zero8_worker(rank, world, port, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = LlamaConfig.tiny()
     out = {}
-    for run, (rdt, overlap) in {"bf16": ("bf16", False), "fp32": ("fp32", False),
-                                "fp32_overlap": ("fp32", True)}.items():
+    for run, (rdt, overlap, slots) in {"bf16": ("bf16", False, 3), "fp32": ("fp32", False, 3),
+                                       "fp32_overlap": ("fp32", True, 3),
+                                       "fp32_full": ("fp32", False, 0)}.items():
         torch.manual_seed(0)
         model = Llama(cfg).to(torch.bfloat16)
-        ddp = FlatDDP(model, bucket_mb=0.05, shard_optimizer=True, reduce_dtype=rdt)
+        ddp = FlatDDP(model, bucket_mb=0.05, shard_optimizer=True, reduce_dtype=rdt,
+                      stage_slots=slots)
+        if rdt == "fp32":
+            out[run + "_staging"] = (sum(t.numel() for t in ddp._slots),
+                                     max(b.end - b.start for b in ddp.buckets), len(ddp.buckets))
         opt = ShardedFlatAdamW(ddp, lr=1e-3)
         seen = {}
         if overlap:
@@ -471,3 +476,54 @@ def test_zero1_eight_ranks_fp32_wire_and_gather_overlap():
         assert set(z[r]["fp32_overlap_waits"]) == set(order)
     for r in range(1, world):
         assert torch.equal(z[r]["fp32_params"], z[0]["fp32_params"])
+    # the fp32 staging is a ring of 3 bucket-sized slots, not a
+    # copy of the whole gradient space, and gives bit-identical results to
+    # staging every bucket at once
+    for r in range(world):
+        staged, biggest, nb = z[r]["fp32_staging"]
+        assert nb > 3 and staged <= 3 * biggest, z[r]["fp32_staging"]
+        assert z[r]["fp32_full_staging"][0] == nb * biggest
+        assert torch.equal(z[r]["fp32_shard"], z[r]["fp32_full_shard"])
+        assert torch.equal(z[r]["fp32_params"], z[r]["fp32_full_params"])
+
+
+def _allreduce_fp32_worker(rank, world, port, outdir):
+    """Replicated (all-reduce) fp32 wire format through the 3-slot ring vs
+    every bucket staged at once, bf16 tiny Llama, 4 gloo ranks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = LlamaConfig.tiny()
+    out = {}
+    for slots in (3, 0):
+        torch.manual_seed(0)
+        model = Llama(cfg).to(torch.bfloat16)
+        ddp = FlatDDP(model, bucket_mb=0.05, reduce_dtype="fp32", stage_slots=slots)
+        with ddp.no_sync():          # the local gradients (the ring rounds results
+            model.loss(_batch(rank * 10, cfg)).backward()    # back during backward)
+        local = ddp.space.grad_buf.clone()
+        ddp.zero_grad()
+        model.loss(_batch(rank * 10, cfg)).backward()
+        ddp.finish_grad_sync()
+        out[slots] = (local, ddp.space.grad_buf.clone(), sum(t.numel() for t in ddp._slots),
+                      max(b.end - b.start for b in ddp.buckets), len(ddp.buckets))
+    torch.save(out, os.path.join(outdir, f"ar{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_allreduce_fp32_wire_ring_staging():
+    world = 4
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_allreduce_fp32_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        z = [torch.load(os.path.join(d, f"ar{i}.pt"), weights_only=True) for i in range(world)]
+    exact = sum(z[r][3][0].double() for r in range(world))
+    for r in range(world):
+        local, reduced, staged, biggest, nb = z[r][3]
+        assert nb > 3 and staged <= 3 * biggest
+        assert torch.equal(reduced, z[r][0][1])                      # ring == all at once
+        assert torch.equal(reduced, z[0][3][1])                      # every rank agrees
+        big = exact.abs() > 1e-3 * exact.abs().max()
+        rel = ((reduced.double() - exact).abs()[big] / exact.abs()[big]).max().item()
+        assert rel <= 2.0 ** -8, rel                                 # one bf16 rounding
