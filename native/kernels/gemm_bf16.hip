@@ -76,7 +76,9 @@
 //           halves swapped) - prices the permuted DMA source against the
 //           LDS bank conflicts it removes; 39 / 40: XOR masks 6 / 5
 //  41-43    26 with the XCD sub-block of the super-block tile map 4 x 8 /
-//           2 x 16 / 16 x 2 tiles instead of 8 x 4 (L2-miss A/B)
+//           2 x 16 / 16 x 2 tiles instead of 8 x 4 (L2-miss A/B); 44: 26 with
+//           the K loop rotated per XCD (17's rotation on the LDS-staged store)
+//  45 DIAG  26 with s_memtime stamps around its waits (mxk_gemm_stamps_read)
 //  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
 //           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
 //           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
@@ -284,19 +286,35 @@ __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
         else mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
         hook(m);
         if (S::a1(m) >= 0) f1a[S::a1(m)] = lds_read_b128(X + aoff(S::a1(m)) + off_k1);
-        if (MODE == 1 && m == S::W1) __builtin_amdgcn_s_waitcnt(0xC07F);
-        if (MODE == 1 && m == S::B1) __builtin_amdgcn_s_barrier();
+        if (MODE == 1 && m == S::W1) {
+          hook.at(0);
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+        }
+        if (MODE == 1 && m == S::B1) {
+          __builtin_amdgcn_s_barrier();
+          hook.at(1);
+        }
         if (MODE == 1 && S::adma(m) >= 0) dma_a.issue(X, S::adma(m), kb2, wave_s);
         if (S::b1(m) >= 0) f1b[S::b1(m)] = lds_read_b128(X + b_base + S::b1(m) * SUB + off_k1);
-        if (MODE == 1 && m == S::W2) __builtin_amdgcn_s_waitcnt(0xC07F);
-        if (MODE == 1 && m == S::B2) __builtin_amdgcn_s_barrier();
+        if (MODE == 1 && m == S::W2) {
+          hook.at(2);
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+        }
+        if (MODE == 1 && m == S::B2) {
+          __builtin_amdgcn_s_barrier();
+          hook.at(3);
+        }
         if (MODE == 1 && S::bdma(m) >= 0)
           dma_b.issue(X + W4B_OP_BYTES, S::bdma(m), kb2, wave_s);
         if (MODE != 3 && m == S::W3) {
+          if (MODE == 1) hook.at(4);
           if constexpr (MODE == 1) vm_wait<S::VM3>();
           else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        if (MODE != 3 && m == S::B3) __builtin_amdgcn_s_barrier();
+        if (MODE != 3 && m == S::B3) {
+          __builtin_amdgcn_s_barrier();
+          if (MODE == 1) hook.at(5);
+        }
         if (MODE != 3 && S::k0(m) >= 0) {
           const int r = S::k0(m);
           if (r < 8) f0b[r] = lds_read_b128(Y + b_base + r * SUB + off_k0);
@@ -477,6 +495,139 @@ mxk_gemm_bf16_tn_w4i(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   } else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
+#ifdef MXK_GEMM_EXPERIMENTS
+// ---------------------------------------------------------------------------
+// w4s (schedule 45, DIAGNOSTIC): schedule 26 with s_memtime stamps around the
+// three waits of every DMA-carrying K-tile (cdna_hip_programming.md §7
+// "In-kernel stamps").  Per wave it sums, in shader cycles: [0] wait #1 +
+// barrier #1 (A k-half-1 reads retired), [1] wait #2 + barrier #2, [2] the
+// stage wait vmcnt + barrier #3, [3] the K-tile period (barrier #3 to
+// barrier #3), [4] the number of K-tiles summed, [5] the whole main loop.
+// The stamps cost cycles themselves (each s_memtime is an SMEM round trip),
+// so the numbers rank the waits; they are not the production kernel's times.
+__device__ unsigned long long g_mxk_gemm_stamps[4096 * 4 * 8];
+
+struct StampHook : mxk::NoHook {
+  unsigned long long* t;      // [0..5] stamps of the current K-tile
+  unsigned long long* sum;    // [0..4] running sums
+  __device__ __forceinline__ void at(int p) const {
+    t[p] = __builtin_amdgcn_s_memtime();
+    if (p == 5) {
+      sum[0] += t[1] - t[0];
+      sum[1] += t[3] - t[2];
+      sum[2] += t[5] - t[4];
+      if (t[6]) sum[3] += t[4] - t[6];
+      t[6] = t[4];
+      sum[4] += 1;
+    }
+  }
+};
+
+template <int PAR>
+__device__ __forceinline__ void w4s_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
+                                          bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
+                                          bf16x8_t (&f1b)[8], char* smem, int a_base, int b_base,
+                                          int off_k0, int off_k1, const DmaK& dma_a,
+                                          const DmaK& dma_b, int kb2, int wave_s,
+                                          const StampHook& h) {
+  w4j_ktile<SchedHB, PAR, 1, 0, 0, false, StampHook>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base,
+                                                     off_k0, off_k1, dma_a, dma_b, kb2, wave_s, 0,
+                                                     0, h);
+}
+
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4s(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
+  int m0, n0;
+  w4b_tile<1>(blockIdx.x, gridDim.x, M / BM, N / BN, &m0, &n0);
+  const DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
+  const DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ ((frow >> 1) & 7);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int ns = K / BK;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_OP_BYTES, p, 0, wave_s);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_a.issue(smem + W4B_STAGE_BYTES, p, BK * 2, wave_s);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_STAGE_BYTES + W4B_OP_BYTES, p, BK * 2, wave_s);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  unsigned long long t[7] = {0, 0, 0, 0, 0, 0, 0}, sum[5] = {0, 0, 0, 0, 0};
+  const StampHook h{{}, t, sum};
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+  int s = 0;
+  int kb = 2 * BK * 2;
+  for (; s + 2 <= ns - 2; s += 2) {
+    w4s_ktile<0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a, dma_b, kb,
+                 wave_s, h);
+    w4s_ktile<1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a, dma_b,
+                 kb + BK * 2, wave_s, h);
+    kb += 2 * BK * 2;
+  }
+  if (s < ns - 2) {
+    w4s_ktile<0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a, dma_b, kb,
+                 wave_s, h);
+    ++s;
+  }
+  ktile_sched<1, 2, 2, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                             dma_b, 0, wave_s, s & 1);
+  ++s;
+  ktile_sched<1, 2, 3, 1, 0>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                             dma_b, 0, wave_s, s & 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  mxk::mfma_drain(acc);
+  const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  mxk::store_block_lds<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane,
+                             smem + wave_s * mxk::kStoreLdsWave);
+  const int slot = static_cast<int>(blockIdx.x) * 4 + wave_s;
+  if (lane == 0 && slot < 4096 * 4) {
+    unsigned long long* o = g_mxk_gemm_stamps + slot * 8;
+    o[0] = sum[0];
+    o[1] = sum[1];
+    o[2] = sum[2];
+    o[3] = sum[3];
+    o[4] = sum[4];
+    o[5] = t_end - t_start;
+    o[6] = t_start;
+    o[7] = t_end;
+  }
+}
+
+// copy the stamps of the last schedule-45 launch: n values (8 per wave)
+MXK_API int mxk_gemm_stamps_read(void* dst, int n) {
+  const int cap = 4096 * 4 * 8;
+  return static_cast<int>(hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_mxk_gemm_stamps),
+                                              sizeof(unsigned long long) * (n < cap ? n : cap)));
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // w4ip (schedule 5): w4i made persistent (grid <= one workgroup per CU,
 // tiles t = blockIdx.x + r * grid).  Between tiles the LDS is free once every
@@ -632,13 +783,13 @@ __device__ __forceinline__ void trickle_ktiles(f32x4_t (&acc)[8][8], bf16x8_t (&
     constexpr int par = decltype(parc)::value;
     using SS = std::conditional_t<q == 0, S0, SchedHBTrk>;
     if constexpr (q < 16) {
-      const mxk::TrickleStore h{buf[q], tp + q * tstride};
+      const mxk::TrickleStore h{{}, buf[q], tp + q * tstride};
       w4j_ktile<SS, par, 1, 0, 0, false, mxk::TrickleStore>(acc, f0a, f0b, f1a, f1b, smem, a_base,
                                                        b_base, off_k0, off_k1, dma_a, dma_b, kbx,
                                                        wave_s, 0, 0, h);
     } else {
       u32x4_t v;
-      const mxk::TrickleLds h{lsrc + (q - 16) * 1024, tp + q * tstride, v};
+      const mxk::TrickleLds h{{}, lsrc + (q - 16) * 1024, tp + q * tstride, v};
       w4j_ktile<SS, par, 1, 0, 0, false, mxk::TrickleLds>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base,
                                                      off_k0, off_k1, dma_a, dma_b, kbx, wave_s, 0,
                                                      0, h);
@@ -1161,7 +1312,7 @@ int mxk_gemm_bf16_tn_ring_launch(int slots, const void* A, const void* Bt, void*
                                  int K, int lda, int ldb, int ldc, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 44;
+constexpr int kNumVariants = 46;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -1171,7 +1322,7 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst", "w4t_trickle", "w4t_trickle_lds", "w4j_ldsst_aln64", "w4j_ldsst_aln64p4",
     "w4j_ldsst_aln64p8", "w4j_ldsst_aln64p12", "w4j_ldsst_linear", "w4j_ldsst_swz_half",
     "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
-    "w4j_ldsst_map16x2"};
+    "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps"};
 
 // compute units of the current device (persistent grids: one workgroup per CU)
 int num_cus() {
@@ -1260,6 +1411,11 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
     case 41: launch_w4i<2, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 42: launch_w4i<3, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 43: launch_w4i<4, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 44: launch_w4i<1, 4, 1, 0, 1, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 45:
+      hipLaunchKernelGGL(mxk_gemm_bf16_tn_w4s, dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c, M, N,
+                         K, lda, ldb, ldc);
+      break;
     case 29: mxk_gemm_bf16_tn_ring_launch(4, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 30: mxk_gemm_bf16_tn_ring_launch(5, A, Bt, C, M, N, K, lda, ldb, ldc, stream); break;
     case 19:

@@ -566,8 +566,8 @@ __device__ __forceinline__ void x2_trickle(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)
                                            uint32_t& sb, uint32_t ka, uint32_t kb, int wave,
                                            const u32x4_t (&buf)[16], uint16_t* tp, size_t tstride) {
   using H = mxk::TrickleStoreT<false>;
-  const H h0{buf[Q], tp + Q * tstride};
-  const H h1{buf[Q + 1], tp + (Q + 1) * tstride};
+  const H h0{{}, buf[Q], tp + Q * tstride};
+  const H h1{{}, buf[Q + 1], tp + (Q + 1) * tstride};
   // K-tile 0: the 16 burst stores and its own trickle store are younger than stage 1
   x2_ktile_s<SCHED, AN, BN, 0, 1, (Q == 0 ? 17 : 1), H>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm,
                                                         wn, sa, sb, wave, 0, h0);

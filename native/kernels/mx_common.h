@@ -281,16 +281,19 @@ __device__ __forceinline__ void vm_wait_n() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// K-tile hook that does nothing (the K-tile bodies call hook(m) after MFMA m)
+// K-tile hook that does nothing (the K-tile bodies call hook(m) after MFMA m,
+// and hook.at(p) around the waits: p 0 / 1 before wait #1 / after barrier #1,
+// 2 / 3 around #2, 4 / 5 around #3)
 struct NoHook {
   __device__ __forceinline__ void operator()(int) const {}
+  __device__ __forceinline__ void at(int) const {}
 };
 
 // ---- trickled C stores (persistent GEMMs, gemm_bf16.hip schedule 31/32 and
 // the layout kernel's x2t): a finished tile's C leaves partly as one
 // whole-line store per K-tile of the next tile.
 template <bool NT = true>
-struct TrickleStoreT {
+struct TrickleStoreT : NoHook {
   u32x4_t v;
   uint16_t* p;
   __device__ __forceinline__ void operator()(int m) const {
@@ -303,7 +306,7 @@ struct TrickleStoreT {
 using TrickleStore = TrickleStoreT<true>;
 
 // LDS-held part (schedule 32): read after MFMA 1, stored after MFMA 9
-struct TrickleLds {
+struct TrickleLds : NoHook {
   const char* src;
   uint16_t* p;
   u32x4_t& v;
