@@ -30,6 +30,13 @@ _fp = ctypes.POINTER(ctypes.c_float)
 
 # name -> (restype, argtypes)
 _SIGNATURES = {
+    "mxk_gemm_set_reserved_cus": (None, [_i]),
+    "mxk_gemm_reserved_cus": (_i, []),
+    "mxk_gemm_available_cus": (_i, []),
+    "mxk_gemm_split_plan": (_i, [_l, _i, _i, ctypes.POINTER(ctypes.c_long)]),
+    "mxk_stream_create_cu_masked": (_i, [_i, _i, _i, ctypes.POINTER(ctypes.c_void_p)]),
+    "mxk_stream_destroy": (_i, [_vp]),
+    "mxk_hbm_stream": (_i, [_vp, _vp, _l, _i, _i, _vp]),
     "mxk_gemm_bf16_tn": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_tn_is_fast": (_i, [_i, _i, _i]),
     "mxk_gemm_bf16_ex": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),

@@ -116,3 +116,38 @@ def gemm_bf16_ex(a: torch.Tensor, b: torch.Tensor, a_kmajor: bool, b_kmajor: boo
         return False
     _lib.check(st, "mxk_gemm_bf16_ex")
     return True
+
+
+# ---- planning for CUs taken by collectives ----------------
+# RCCL's kernels hold some CUs for as long as a collective runs (the ZeRO-1
+# reduce-scatter under the backward, the parameter all-gather under the
+# forward).  The GEMM launchers size their rounds and the split tail for the
+# CUs that are left once told how many are taken (mxk_gemm_set_reserved_cus;
+# env MXK_GEMM_RESERVED_CUS).  scripts/contention_bench.py measures both.
+XBK = 64
+
+
+def split_plan(nwg: int, K: int, cus: int) -> tuple[int, int]:
+    """(whole tiles, tail tiles run as K halves) for ``nwg`` 256^2 output
+    tiles on ``cus`` CUs: the tail of a last round at most half full is split
+    so it occupies the CUs a whole round would, instead of leaving the rest
+    idle.  Mirrors ``mxk_gemm_split_plan`` (gemm_bf16_layouts.hip)."""
+    tail = nwg % cus if nwg > 0 and cus > 0 else 0
+    want = tail > 0 and 2 * tail <= cus and K % (2 * XBK) == 0 and K >= 16 * XBK
+    return (nwg - tail, tail) if want else (nwg, 0)
+
+
+def rounds(nwg: int, K: int, cus: int) -> float:
+    """Chip rounds the plan takes, in whole-tile times: a split tail is one
+    more round of half-depth workgroups (2 x tail <= cus of them)."""
+    whole, tail = split_plan(nwg, K, cus)
+    return whole // cus + 0.5 if tail else float(-(-nwg // cus))
+
+
+def set_reserved_cus(n: int) -> None:
+    """Tell the GEMM planner that ``n`` CUs are taken by other kernels."""
+    _lib.lib().mxk_gemm_set_reserved_cus(int(n))
+
+
+def available_cus() -> int:
+    return int(_lib.lib().mxk_gemm_available_cus())

@@ -23,6 +23,10 @@
 //   (tests/test_gemm_layouts.py).
 // LDS: 2 stages x (A + B) <= 132 KiB, one 4-wave workgroup per CU, 128x128
 // AGPR accumulators per wave, one barrier per 64-deep stage.
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+
 #include "mx_common.h"
 
 #include <cstdlib>
@@ -889,8 +893,18 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
   MXK_RETURN_LAUNCH_STATUS();
 }
 
+// ---- compute units the GEMMs may plan for -------------------------------
+// Every round / split-tail decision below assumes `cus` workgroups run at
+// once.  With collectives in flight (the ZeRO-1 reduce-scatter under the
+// backward, the parameter all-gather under the forward) RCCL's kernels hold
+// some CUs for the whole collective, and a GEMM whose tiles exactly fill the
+// chip then runs one extra, nearly empty round.  mxk_gemm_set_reserved_cus(k)
+// (or MXK_GEMM_RESERVED_CUS=k) tells the planner that k CUs are taken: rounds
+// and the split tail are sized for the CUs that are left.
 namespace {
-int device_cus() {
+std::atomic<int> g_reserved_cus{-1};
+
+int hw_cus() {
   static thread_local int dev_cached = -1, cus = 256;
   int dev = 0;
   if (hipGetDevice(&dev) == hipSuccess && dev != dev_cached) {
@@ -901,6 +915,36 @@ int device_cus() {
   }
   return cus;
 }
+
+int reserved_cus() {
+  int r = g_reserved_cus.load(std::memory_order_relaxed);
+  if (r < 0) {
+    const char* e = std::getenv("MXK_GEMM_RESERVED_CUS");
+    r = e ? std::max(0, std::atoi(e)) : 0;
+    g_reserved_cus.store(r, std::memory_order_relaxed);
+  }
+  return r;
+}
+
+int device_cus() { return std::max(1, hw_cus() - reserved_cus()); }
+}  // namespace
+
+MXK_API void mxk_gemm_set_reserved_cus(int n) { g_reserved_cus.store(std::max(0, n)); }
+MXK_API int mxk_gemm_reserved_cus(void) { return reserved_cus(); }
+MXK_API int mxk_gemm_available_cus(void) { return device_cus(); }
+
+// The split-tail plan for nwg 256^2 output tiles over `cus` CUs and depth K
+// (pure host arithmetic; tests/test_gemm_plan.py checks it on the CPU):
+// returns the number of tail tiles run as K halves (0: no split) and sets
+// *q_full to the tiles that run whole.
+MXK_API int mxk_gemm_split_plan(long nwg, int K, int cus, long* q_full) {
+  const int tail = nwg > 0 && cus > 0 ? static_cast<int>(nwg % cus) : 0;
+  const bool want = tail > 0 && 2 * tail <= cus && K % (2 * XBK) == 0 && K >= 16 * XBK;
+  if (q_full) *q_full = want ? nwg - tail : nwg;
+  return want ? tail : 0;
+}
+
+namespace {
 
 template <bool AN, bool BN>
 void launch_split(int sched, bool wide, int nwg, int q_full, hipStream_t stream, const uint16_t* a,
@@ -923,7 +967,7 @@ void launch_split(int sched, bool wide, int nwg, int q_full, hipStream_t stream,
 // Bytes of fp32 workspace the split tail of an (M, N) output needs at most
 // (half a round of tiles, two partial tiles each).
 MXK_API long mxk_gemm_bf16_split_workspace(void) {
-  return static_cast<long>(device_cus() / 2) * 2 * XBM * XBM * 4;
+  return static_cast<long>(hw_cus() / 2) * 2 * XBM * XBM * 4;   // any reservation fits
 }
 
 // mxk_gemm_bf16_ex (variant 1) with the split tail: when the output's 256^2
@@ -940,9 +984,9 @@ MXK_API int mxk_gemm_bf16_ex_ws(const void* A, const void* B, void* C, int M, in
   if (split) *split = 0;
   const int cus = device_cus();
   const long nwg = M > 0 && N > 0 ? static_cast<long>(M / XBM) * (N / XBM) : 0;
-  const int tail = nwg > 0 ? static_cast<int>(nwg % cus) : 0;
-  const bool want = tail > 0 && 2 * tail <= cus && K % (2 * XBK) == 0 &&
-                    K >= 16 * XBK && ws != nullptr &&
+  long q_plan = nwg;
+  const int tail = static_cast<int>(mxk_gemm_split_plan(nwg, K, cus, &q_plan));
+  const bool want = tail > 0 && ws != nullptr &&
                     ws_bytes >= static_cast<long>(2 * tail) * XBM * XBM * 4 &&
                     reinterpret_cast<uintptr_t>(ws) % 16 == 0;
   if (!want)

@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""1-GPU rehearsal of compute / collective co-residency.
+
+At n > 1 the ZeRO-1 reduce-scatter runs under the backward, and RCCL's
+kernels keep a set of CUs busy for as long as it lasts.  Here a copy kernel
+confined to k CUs (a CU-masked stream, native/kernels/contention.hip) runs
+through every backward of the Llama-3-8B step (seq 2048, micro-batch 8,
+bf16, AdamW - the BASELINE config 5 step at world 1), and the step is timed
+
+  base      no streamer
+  blind     streamer on k CUs, GEMM planner unaware (plans for 256 CUs)
+  aware     streamer on k CUs, mxk_gemm_set_reserved_cus(k): rounds and the
+            split tail are sized for the 256 - k CUs left
+
+for k in --cus.  Prints one RESULT json per (k, mode) with ms/step, the
+slowdown against base, and the ideal k/256 x (backward share) it is judged
+against (<= k/256 + 2 % of the step).
+
+    python scripts/contention_bench.py --cus 16,32,64 [--steps 6] [--layers N]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mxk8s.models.llama import LlamaConfig  # noqa: E402
+from mxk8s.ops import _lib, gemm  # noqa: E402
+from mxk8s.train.ddp_llama import build, use_tuned_gemms  # noqa: E402
+
+
+class Streamer:
+    """HBM copy kernel on a stream confined to CUs [0, k)."""
+
+    def __init__(self, k: int, dev, mib: int = 512):
+        import ctypes
+        self.k = k
+        self.L = _lib.lib()
+        h = ctypes.c_void_p()
+        _lib.check(self.L.mxk_stream_create_cu_masked(0, k, 0, ctypes.byref(h)), "cu-masked stream")
+        self.handle = h.value
+        self.stream = torch.cuda.ExternalStream(self.handle, device=dev)
+        n = mib * 2 ** 20
+        self.src = torch.empty(n, dtype=torch.uint8, device=dev).fill_(1)
+        self.dst = torch.empty(n, dtype=torch.uint8, device=dev)
+        self.nwg = 4 * k
+        self.iters = 1
+
+    def launch(self):
+        _lib.check(self.L.mxk_hbm_stream(self.src.data_ptr(), self.dst.data_ptr(), self.src.numel(),
+                                         self.iters, self.nwg, self.handle), "hbm stream")
+
+    def calibrate(self, target_ms: float):
+        self.iters = 1
+        with torch.cuda.stream(self.stream):
+            self.launch()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(3):
+                self.launch()
+            e.record()
+            e.synchronize()
+        one = s.elapsed_time(e) / 3
+        self.iters = max(1, int(round(target_ms / one)))
+        return one
+
+    def close(self):
+        torch.cuda.synchronize()
+        self.L.mxk_stream_destroy(self.handle)
+
+
+def step(model, ddp, opt, tokens, streamer=None, times=None):
+    cur = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record()
+    loss = model.loss(tokens)
+    ev[1].record()
+    if streamer is not None:
+        streamer.stream.wait_event(ev[1])         # starts with the backward
+        with torch.cuda.stream(streamer.stream):
+            streamer.launch()
+    loss.backward()
+    ddp.finish_grad_sync()
+    ev[2].record()
+    opt.step()
+    ddp.zero_grad()
+    if streamer is not None:
+        cur.wait_stream(streamer.stream)          # like a collective the step waits for
+    if times is not None:
+        times.append(ev)
+    return loss
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--cus", default="16,32,64")
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--layers", type=int, default=None, help="fewer layers (quick check only)")
+    ap.add_argument("--seq-len", type=int, default=2048)
+    ap.add_argument("--micro-batch", type=int, default=8)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    use_tuned_gemms()
+    cfg = LlamaConfig.llama3_8b()
+    if a.layers:
+        cfg.n_layers = a.layers
+    model, ddp, opt = build(cfg, dev, 512.0, zero=False)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    batches = [torch.randint(0, cfg.vocab_size, (a.micro_batch, a.seq_len + 1), device=dev, generator=g)
+               for _ in range(2)]
+
+    def timed(streamer=None):
+        for i in range(a.warmup):
+            step(model, ddp, opt, batches[i % 2], streamer)
+        torch.cuda.synchronize()
+        walls, evs = [], []
+        for i in range(a.steps):
+            t0 = time.perf_counter()
+            step(model, ddp, opt, batches[i % 2], streamer, evs)
+            torch.cuda.synchronize()
+            walls.append((time.perf_counter() - t0) * 1e3)
+        bwd = statistics.median(e[1].elapsed_time(e[2]) for e in evs)
+        return statistics.median(walls), bwd
+
+    gemm.set_reserved_cus(0)
+    base, base_bwd = timed()
+    print("RESULT " + json.dumps({"k": 0, "mode": "base", "ms_per_step": round(base, 2),
+                                  "backward_ms": round(base_bwd, 2), "layers": cfg.n_layers}),
+          flush=True)
+    for k in [int(x) for x in a.cus.split(",") if x]:
+        st = Streamer(k, dev)
+        one = st.calibrate(base_bwd)
+        for mode in ("blind", "aware"):
+            gemm.set_reserved_cus(k if mode == "aware" else 0)
+            ms, bwd = timed(st)
+            ideal = k / 256 * base_bwd / base
+            print("RESULT " + json.dumps({
+                "k": k, "mode": mode, "ms_per_step": round(ms, 2), "backward_ms": round(bwd, 2),
+                "slowdown": round(ms / base - 1, 4), "ideal_slowdown": round(ideal, 4),
+                "criterion": round(k / 256 + 0.02, 4), "streamer_iters": st.iters,
+                "streamer_ms_per_iter_alone": round(one, 3),
+                "available_cus": gemm.available_cus()}), flush=True)
+        gemm.set_reserved_cus(0)
+        st.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
