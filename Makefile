@@ -30,7 +30,7 @@ KERNEL_SRCS := native/kernels/gemm_bf16.hip native/kernels/vector_add.hip \
                native/kernels/fused_ops.hip native/kernels/optim.hip native/kernels/attention.hip \
                native/kernels/gemm_bf16_layouts.hip native/kernels/xent.hip native/kernels/contention.hip
 KERNEL_OBJS := $(patsubst native/kernels/%.hip,$(BUILD)/kernels/%.o,$(KERNEL_SRCS))
-EXP_SRCS    := $(KERNEL_SRCS) native/kernels/gemm_bf16_ring.hip
+EXP_SRCS    := $(KERNEL_SRCS) $(wildcard native/kernels/experiments/*.hip)
 EXP_OBJS    := $(patsubst native/kernels/%.hip,$(BUILD)/exp/%.o,$(EXP_SRCS))
 KERNEL_HDRS := $(wildcard native/kernels/*.h)
 
