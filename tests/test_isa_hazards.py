@@ -70,9 +70,10 @@ def close_accumulator_reads(asm: str) -> dict[str, int]:
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("src", ["gemm_bf16.hip", "gemm_bf16_layouts.hip"])
-def test_no_accumulator_read_right_after_asm_mfma(src, tmp_path):
-    asm = _asm(src, str(tmp_path / (src + ".s")))
+@pytest.mark.parametrize("src,flags", [("gemm_bf16.hip", ()), ("gemm_bf16_layouts.hip", ()),
+                                       ("experiments/gemm_tn_exp.hip", ("-DMXK_GEMM_EXPERIMENTS",))])
+def test_no_accumulator_read_right_after_asm_mfma(src, flags, tmp_path):
+    asm = _asm(src, str(tmp_path / (src.replace("/", "_") + ".s")), flags)
     assert "v_mfma" in asm
     assert close_accumulator_reads(asm) == {}
 
@@ -95,7 +96,7 @@ def test_detector_flags_a_close_accumulator_spill():
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src,flags", [("gemm_bf16.hip", ()), ("gemm_bf16_layouts.hip", ()),
                                        # the trickle-store kernels are experiments-only
-                                       ("gemm_bf16.hip", ("-DMXK_GEMM_EXPERIMENTS",)),
+                                       ("experiments/gemm_tn_exp.hip", ("-DMXK_GEMM_EXPERIMENTS",)),
                                        ("gemm_bf16_layouts.hip", ("-DMXK_GEMM_EXPERIMENTS",))])
 def test_counted_wait_gemms_do_not_spill(src, flags, tmp_path):
     """The GEMM loops wait for their LDS-DMA stages with COUNTED vmcnt waits
@@ -104,14 +105,34 @@ def test_counted_wait_gemms_do_not_spill(src, flags, tmp_path):
     lets the wait pass one DMA piece early (seen: the trickle-store layout
     kernel's wgrad instance at 10 spills gave wrong tiles, the 9 without
     spills were exact).  Every shipped counted-wait GEMM kernel: no spills."""
-    asm = _asm(src, str(tmp_path / (src + ".s")), flags)
+    asm = _asm(src, str(tmp_path / (src.replace("/", "_") + ".s")), flags)
     names = re.findall(r"^\s+\.name:\s+(_Z\S+)", asm, re.M)
     counts = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s+(\d+)", asm)]
     assert len(names) == len(counts) and names
     # production: every counted-wait GEMM; experiments build: the trickle-store
     # kernels (the round-2 persistent w4ip records are known to spill)
     pat = re.compile(r"mxk_gemm_bf16_(tn_w4t|x2t_kernel)" if flags else
-                     r"mxk_gemm_bf16_(tn_w4t|x2t_kernel|tn_w4i|x2_kernel)")
+                     r"mxk_gemm_bf16_(tn_w4t|x2t_kernel|tn_w4j|x2_kernel)")
     checked = {n: c for n, c in zip(names, counts) if pat.search(n)}
     assert checked, "no counted-wait GEMM kernel found"
     assert {n: c for n, c in checked.items() if c} == {}
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_w13_swiglu_spills_stay_out_of_the_dma_loop(tmp_path):
+    """The fused up-projection keeps 3 spill slots for its epilogue; none of
+    them may sit inside the counted-wait K loop (a scratch op there would be a
+    vector-memory op the loop's vmcnt counts do not expect).  The tail
+    K-tiles after the loop wait with vmcnt(0), which also covers a spill."""
+    asm = _asm("gemm_bf16.hip", str(tmp_path / "g.s"))
+    name = re.search(r"^(_Z\S*mxk_gemm_bf16_w13_swiglu\S*):", asm, re.M).group(1)
+    body = asm[asm.index(name + ":"):]
+    body = body[:body.index("s_endpgm")]
+    lines = body.split("\n")
+    heads = [i for i, l in enumerate(lines) if "Inner Loop Header" in l]
+    assert heads, "no K loop found"
+    for h in heads:
+        label = lines[h].split(":")[0]
+        end = next(i for i in range(h + 1, len(lines))
+                   if "s_cbranch" in lines[i] and lines[i].rstrip().endswith(label))
+        assert not [l for l in lines[h:end + 1] if "scratch_" in l], label
