@@ -888,6 +888,10 @@ int mxk_gemm_tn_exp_launch(int v, int nwg, hipStream_t stream, const void* A, co
     // 26 as the full-flag template instantiated it before the production
     // kernel got its own (mxk_gemm_bf16_tn_w4j): same loop, other registers
     case 46: launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
+    case 47:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b,
+                         c, M, N, K, lda, ldb, ldc);
+      break;
     case 31:
     case 32: {
       if (K < (v == 31 ? 18 : 26) * BK) {   // fewer K-tiles than the trickle phase needs

@@ -83,6 +83,9 @@
 //  45 DIAG  26 with s_memtime stamps around its waits (mxk_gemm_stamps_read)
 //  46       26 built from the full-flag experiments template (the same K loop
 //           in other registers: A/B of the production kernel's own template)
+//  47 w4k   ONE barrier per K-tile: A triple-buffered (3 + 2 x 32 KiB = all of
+//           LDS), stage s+2's A refilled early into the slot stage s-1 used,
+//           B right after the barrier (gemm_tn_core.h mxk_gemm_bf16_tn_w4k)
 //  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
 //           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
 //           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
@@ -319,7 +322,7 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                                      int variant, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 47;
+constexpr int kNumVariants = 48;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -329,7 +332,8 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "pp8_prio", "w4j_stag1", "w4j_stag2", "w4j_stag4", "w4j_stag8", "w4j_stag4_st", "w4j_hb_ldsst", "w4j_1bar_ldsst", "w4j_1bar_spread_ldsst", "ring4_ldsst", "ring5_ldsst", "w4t_trickle", "w4t_trickle_lds", "w4j_ldsst_aln64", "w4j_ldsst_aln64p4",
     "w4j_ldsst_aln64p8", "w4j_ldsst_aln64p12", "w4j_ldsst_linear", "w4j_ldsst_swz_half",
     "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
-    "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps", "w4i_ldsst_full_template"};
+    "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps", "w4i_ldsst_full_template",
+    "w4k_1bar_a3_ldsst"};
 
 }  // namespace
 #ifdef MXK_GEMM_EXPERIMENTS

@@ -71,16 +71,18 @@ __device__ __forceinline__ DmaK make_dmak(const uint16_t* src, int ld, int row0,
   return d;
 }
 
-// PAR 0/1: the K-tile reads stage buffer PAR (compile-time LDS bases);
-// PAR 2: runtime parity `par` (the once-per-tile tail: one instantiation per
-// MODE keeps the register assignment of the unrolled loop intact — a
-// runtime-parity branch between two static tails spilled ~1300 VGPRs).
-
 using mxk::SchedHB;
 using mxk::SchedTwoBarrier;
 
 // Table-driven K-tile: S gives, per MFMA index m, the fragment reads, DMA
-// pieces, waits and barriers that follow MFMA m (see w4i_ktile for MODE).
+// pieces, waits and barriers that follow MFMA m.  MODE 1: DMA of stage s+2,
+// counted vmcnt at the stage wait; MODE 2: no DMA, vmcnt(0) (stage s+1 is
+// the last one issued); MODE 3: no DMA, no stage wait, no next-k0 reads (the
+// last K-tile).  PAR 0/1: the K-tile reads stage buffer PAR (compile-time LDS
+// bases); PAR 2: runtime parity `par` (the once-per-tile tail: one
+// instantiation per MODE keeps the register assignment of the unrolled loop
+// intact — a runtime-parity branch between two static tails spilled ~1300
+// VGPRs).
 // SPLITA: A fragments 0-3 at a_base, 4-7 at a_hi (the w13 SwiGLU kernel
 // rotates one wave's row blocks by 4); otherwise a_hi is unused.
 // HOOK(m) runs after MFMA m (the trickle-store kernel's one C store per
@@ -156,8 +158,6 @@ __device__ __forceinline__ void w4j_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
 
 using mxk::store_block_wide;
 using mxk::store_block_narrow;
-
-// K-tile of schedule SCHED (0: w4i knobs LATE/R1, 1: hipBLASLt positions,
 
 // ---------------------------------------------------------------------------
 // The production kernel: 256x256 tile, 4 waves, the three-barrier K-tile at
@@ -255,3 +255,189 @@ mxk_gemm_bf16_tn_w4j(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
+
+// ---------------------------------------------------------------------------
+// w4k: ONE barrier per K-tile (A/B record 47; candidate default).
+//
+// Stamps of the three-barrier K-tile (scripts/gpu/gemm_stamps.py, schedule
+// 45) put ~64 + 64 + 46 cycles per K-tile into its three waits: the MFMA pipe
+// of a wave that waits at a barrier idles (one wave per SIMD).  Two of the
+// three barriers exist only to let the DMA refill a stage in place ("every
+// wave finished reading X.A / X.B").  Here A has THREE 32 KiB slots and B two
+// (3 x 32 + 2 x 32 KiB = the whole 160 KiB LDS): stage s+2's A goes into the
+// slot stage s-1 used, which every wave left before the previous K-tile's
+// barrier, so it is issued early in K-tile s with no barrier at all; stage
+// s+2's B goes into B slot s%2 right after the K-tile's single barrier, by
+// which every wave has read its k-half-1 B fragments of stage s.  Per K-tile
+// (m = MFMA index 0..127):
+//   m  0..14 even  A k-half-1 fragments (A slot s%3)
+//   m 16..30 even  B k-half-1 fragments (B slot s%2)
+//   m 33..61 /4    DMA of stage s+2, A pieces -> A slot (s+2)%3
+//   m  92          lgkmcnt(0) + vmcnt(8) (stage s+1 landed; the 8 A pieces
+//                  of s+2 stay in flight) + the barrier
+//   m 93..123      next K-tile's k-half-0 fragments (stage s+1), SchedHB order
+//   m 94..115      DMA of stage s+2, B pieces -> B slot s%2
+// The stage slots repeat every 6 K-tiles; the loop is unrolled by 6 so every
+// LDS address is a compile-time offset.
+struct SchedA3 {
+  static constexpr int WB = 92;
+  __host__ __device__ static constexpr int a1(int m) { return m < 16 && (m & 1) == 0 ? m >> 1 : -1; }
+  __host__ __device__ static constexpr int b1(int m) {
+    return m >= 16 && m < 32 && (m & 1) == 0 ? (m - 16) >> 1 : -1;
+  }
+  __host__ __device__ static constexpr int adma(int m) {
+    return m >= 33 && m <= 61 && (m - 33) % 4 == 0 ? (m - 33) / 4 : -1;
+  }
+  __host__ __device__ static constexpr int bdma(int m) {
+    return m == 94 ? 0 : m == 96 ? 1 : m == 99 ? 2 : m == 101 ? 3 : m == 104 ? 4 : m == 107 ? 5
+         : m == 110 ? 6 : m == 115 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int k0(int m) { return SchedHB::k0(m); }
+};
+
+constexpr int A3_SLOT = W4B_OP_BYTES;          // 32 KiB
+constexpr int A3_B0 = 3 * A3_SLOT;             // B slots after the three A slots
+constexpr int A3_LDS = 5 * A3_SLOT;            // 160 KiB
+
+// K-tile of stage s with A in slot AS = s % 3 and B in slot BS = s % 2
+// (compile-time; AS/BS = -1: runtime `as`/`bs`, for the two tail K-tiles).
+template <int AS, int BS, int MODE, class HOOK = NoHook>
+__device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
+                                          bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
+                                          bf16x8_t (&f1b)[8], char* smem, int a_base, int b_base,
+                                          int off_k0, int off_k1, const DmaK& dma_a,
+                                          const DmaK& dma_b, int kb2, int wave_s, int as = 0,
+                                          int bs = 0, const HOOK& hook = HOOK{}) {
+  using S = SchedA3;
+  constexpr int SUB = 2048;
+  const int a_cur = AS >= 0 ? AS : as, b_cur = BS >= 0 ? BS : bs;
+  const int a_nxt = a_cur == 2 ? 0 : a_cur + 1;
+  const int a_ref = a_cur == 0 ? 2 : a_cur - 1;
+  char* XA = smem + a_cur * A3_SLOT;
+  char* XB = smem + A3_B0 + b_cur * A3_SLOT;
+  char* YA = smem + a_nxt * A3_SLOT;
+  char* YB = smem + A3_B0 + (b_cur ^ 1) * A3_SLOT;
+  char* RA = smem + a_ref * A3_SLOT;   // refill slot of A (stage s+2)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int m = h * 64 + o * 8 + q;
+        if (h == 0) mfma_16x16x32_agpr(acc[o][q], f0b[q], f0a[o]);
+        else mfma_16x16x32_agpr(acc[o][q], f1b[q], f1a[o]);
+        hook(m);
+        if (S::a1(m) >= 0) f1a[S::a1(m)] = lds_read_b128(XA + a_base + S::a1(m) * SUB + off_k1);
+        if (S::b1(m) >= 0) f1b[S::b1(m)] = lds_read_b128(XB + b_base + S::b1(m) * SUB + off_k1);
+        if (MODE == 1 && S::adma(m) >= 0) dma_a.issue(RA, S::adma(m), kb2, wave_s);
+        if (MODE != 3 && m == S::WB) {
+          hook.at(4);
+          __builtin_amdgcn_s_waitcnt(0xC07F);          // this wave's B k1 reads retired
+          if constexpr (MODE == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          hook.at(5);
+        }
+        if (MODE == 1 && S::bdma(m) >= 0) dma_b.issue(XB, S::bdma(m), kb2, wave_s);
+        if (MODE != 3 && S::k0(m) >= 0) {
+          const int r = S::k0(m);
+          if (r < 8) f0b[r] = lds_read_b128(YB + b_base + r * SUB + off_k0);
+          else f0a[r - 8] = lds_read_b128(YA + a_base + (r - 8) * SUB + off_k0);
+        }
+      }
+    }
+  }
+}
+
+template <int MAP, int EPI>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[A3_LDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
+  int m0, n0;
+  w4b_tile<MAP>(blockIdx.x, gridDim.x, M / BM, N / BN, &m0, &n0);
+  const DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
+  const DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
+
+  const int frow = lane & 15;
+  const int fch = (lane >> 4) ^ ((frow >> 1) & 7);
+  const int off_k0 = frow * 128 + fch * 16;
+  const int off_k1 = frow * 128 + (fch ^ 4) * 16;
+  constexpr int SUB = 2048;
+  const int a_base = wm * 8 * SUB;
+  const int b_base = wn * 8 * SUB;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / BK;
+  // stages 0 and 1: A slots 0, 1 and B slots 0, 1
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) dma_b.issue(smem + A3_B0, p, 0, wave_s);
+  if (ns > 1) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_a.issue(smem + A3_SLOT, p, BK * 2, wave_s);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma_b.issue(smem + A3_B0 + A3_SLOT, p, BK * 2, wave_s);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + A3_B0 + b_base + j * SUB + off_k0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+
+  // K-tiles 0 .. ns-3 carry the DMA of stage s+2 (k offset (s+2)*128 B)
+  int s = 0;
+  int kb = 2 * BK * 2;
+#define MXK_W4K(as_, bs_)                                                                       \
+  w4k_ktile<as_, bs_, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,  \
+                         dma_b, kb, wave_s);                                                    \
+  kb += BK * 2;
+  for (; s + 6 <= ns - 2; s += 6) {
+    MXK_W4K(0, 0) MXK_W4K(1, 1) MXK_W4K(2, 0) MXK_W4K(0, 1) MXK_W4K(1, 0) MXK_W4K(2, 1)
+  }
+  // s % 6 == 0 here: the remaining DMA-carrying K-tiles have compile-time slots
+  const int r = ns - 2 - s;
+  if (r > 0) { MXK_W4K(0, 0) }
+  if (r > 1) { MXK_W4K(1, 1) }
+  if (r > 2) { MXK_W4K(2, 0) }
+  if (r > 3) { MXK_W4K(0, 1) }
+  if (r > 4) { MXK_W4K(1, 0) }
+#undef MXK_W4K
+  s += r > 0 ? r : 0;
+  // the last two K-tiles (or the only one): no DMA, runtime slots
+  if (ns >= 2) {
+    w4k_ktile<-1, -1, 2>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                         dma_b, 0, wave_s, s % 3, s & 1);
+    ++s;
+  }
+  w4k_ktile<-1, -1, 3>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a, dma_b,
+                       0, wave_s, s % 3, s & 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  mxk::mfma_drain(acc);
+
+  if constexpr (EPI == 4) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    mxk::store_block_lds<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane,
+                               smem + wave_s * mxk::kStoreLdsWave);
+  } else if constexpr (EPI == 2) store_block_wide<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+  else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+}
