@@ -892,6 +892,22 @@ int mxk_gemm_tn_exp_launch(int v, int nwg, hipStream_t stream, const void* A, co
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b,
                          c, M, N, K, lda, ldb, ldc);
       break;
+    case 48:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
+                         b, c, M, N, K, lda, ldb, ldc);
+      break;
+    case 49:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 2>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
+                         b, c, M, N, K, lda, ldb, ldc);
+      break;
+    case 50:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
+                         b, c, M, N, K, lda, ldb, ldc);
+      break;
+    case 51:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 7>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
+                         b, c, M, N, K, lda, ldb, ldc);
+      break;
     case 31:
     case 32: {
       if (K < (v == 31 ? 18 : 26) * BK) {   // fewer K-tiles than the trickle phase needs

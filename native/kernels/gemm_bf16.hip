@@ -86,6 +86,8 @@
 //  47 w4k   ONE barrier per K-tile: A triple-buffered (3 + 2 x 32 KiB = all of
 //           LDS), stage s+2's A refilled early into the slot stage s-1 used,
 //           B right after the barrier (gemm_tn_core.h mxk_gemm_bf16_tn_w4k)
+//  48-51 DIAG 47 without its DMA pieces / fragment reads / waits and barrier /
+//           all three (timing ablations, wrong outputs)
 //  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
 //           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
 //           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
@@ -322,7 +324,7 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                                      int variant, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 48;
+constexpr int kNumVariants = 52;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -333,7 +335,8 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "w4j_ldsst_aln64p8", "w4j_ldsst_aln64p12", "w4j_ldsst_linear", "w4j_ldsst_swz_half",
     "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
     "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps", "w4i_ldsst_full_template",
-    "w4k_1bar_a3_ldsst"};
+    "w4k_1bar_a3_ldsst", "diag_w4k_nodma", "diag_w4k_noreads", "diag_w4k_nowait",
+    "diag_w4k_mfma_only"};
 
 }  // namespace
 #ifdef MXK_GEMM_EXPERIMENTS
@@ -403,7 +406,9 @@ MXK_API const char* mxk_gemm_bf16_tn_variant_name(int variant) {
 }
 MXK_API int mxk_gemm_bf16_tn_variant_built(int variant) { return variant_built(variant); }
 // Variant 10 is a timing ablation (no C store): never correctness-checked or used.
-MXK_API int mxk_gemm_bf16_tn_is_ablation(int variant) { return variant == 10; }
+MXK_API int mxk_gemm_bf16_tn_is_ablation(int variant) {
+  return variant == 10 || (variant >= 48 && variant <= 51);
+}
 
 MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,
                              int lda, int ldb, int ldc, hipStream_t stream) {

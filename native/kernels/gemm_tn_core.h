@@ -301,7 +301,10 @@ constexpr int A3_LDS = 5 * A3_SLOT;            // 160 KiB
 
 // K-tile of stage s with A in slot AS = s % 3 and B in slot BS = s % 2
 // (compile-time; AS/BS = -1: runtime `as`/`bs`, for the two tail K-tiles).
-template <int AS, int BS, int MODE, class HOOK = NoHook>
+// ABL (timing ablations only, wrong outputs; experiments variants 48-51):
+// bit 0 skips the DMA pieces, bit 1 the fragment reads, bit 2 the waits and
+// the barrier.
+template <int AS, int BS, int MODE, class HOOK = NoHook, int ABL = 0>
 __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                           bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                           bf16x8_t (&f1b)[8], char* smem, int a_base, int b_base,
@@ -328,10 +331,12 @@ __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
         if (h == 0) mfma_16x16x32_agpr(acc[o][q], f0b[q], f0a[o]);
         else mfma_16x16x32_agpr(acc[o][q], f1b[q], f1a[o]);
         hook(m);
-        if (S::a1(m) >= 0) f1a[S::a1(m)] = lds_read_b128(XA + a_base + S::a1(m) * SUB + off_k1);
-        if (S::b1(m) >= 0) f1b[S::b1(m)] = lds_read_b128(XB + b_base + S::b1(m) * SUB + off_k1);
-        if (MODE == 1 && S::adma(m) >= 0) dma_a.issue(RA, S::adma(m), kb2, wave_s);
-        if (MODE != 3 && m == S::WB) {
+        if (!(ABL & 2) && S::a1(m) >= 0)
+          f1a[S::a1(m)] = lds_read_b128(XA + a_base + S::a1(m) * SUB + off_k1);
+        if (!(ABL & 2) && S::b1(m) >= 0)
+          f1b[S::b1(m)] = lds_read_b128(XB + b_base + S::b1(m) * SUB + off_k1);
+        if (!(ABL & 1) && MODE == 1 && S::adma(m) >= 0) dma_a.issue(RA, S::adma(m), kb2, wave_s);
+        if (!(ABL & 4) && MODE != 3 && m == S::WB) {
           hook.at(4);
           __builtin_amdgcn_s_waitcnt(0xC07F);          // this wave's B k1 reads retired
           if constexpr (MODE == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -339,8 +344,8 @@ __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
           __builtin_amdgcn_s_barrier();
           hook.at(5);
         }
-        if (MODE == 1 && S::bdma(m) >= 0) dma_b.issue(XB, S::bdma(m), kb2, wave_s);
-        if (MODE != 3 && S::k0(m) >= 0) {
+        if (!(ABL & 1) && MODE == 1 && S::bdma(m) >= 0) dma_b.issue(XB, S::bdma(m), kb2, wave_s);
+        if (!(ABL & 2) && MODE != 3 && S::k0(m) >= 0) {
           const int r = S::k0(m);
           if (r < 8) f0b[r] = lds_read_b128(YB + b_base + r * SUB + off_k0);
           else f0a[r - 8] = lds_read_b128(YA + a_base + (r - 8) * SUB + off_k0);
@@ -350,7 +355,7 @@ __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
   }
 }
 
-template <int MAP, int EPI>
+template <int MAP, int EPI, int ABL = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -407,8 +412,8 @@ mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   int s = 0;
   int kb = 2 * BK * 2;
 #define MXK_W4K(as_, bs_)                                                                       \
-  w4k_ktile<as_, bs_, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,  \
-                         dma_b, kb, wave_s);                                                    \
+  w4k_ktile<as_, bs_, 1, NoHook, ABL>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,     \
+                                      off_k1, dma_a, dma_b, kb, wave_s);                        \
   kb += BK * 2;
   for (; s + 6 <= ns - 2; s += 6) {
     MXK_W4K(0, 0) MXK_W4K(1, 1) MXK_W4K(2, 0) MXK_W4K(0, 1) MXK_W4K(1, 0) MXK_W4K(2, 1)

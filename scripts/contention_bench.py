@@ -3,9 +3,11 @@
 
 At n > 1 the ZeRO-1 reduce-scatter runs under the backward, and RCCL's
 kernels keep a set of CUs busy for as long as it lasts.  Here a copy kernel
-confined to k CUs (a CU-masked stream, native/kernels/contention.hip) runs
-through every backward of the Llama-3-8B step (seq 2048, micro-batch 8,
-bf16, AdamW - the BASELINE config 5 step at world 1), and the step is timed
+holding k CUs (native/kernels/contention.hip; --placement spread: k
+workgroups dealt over the XCDs like RCCL's channels, masked: a CU-masked
+stream on CUs [0, k)) runs through every backward of the Llama-3-8B step
+(seq 2048, micro-batch 8, bf16, AdamW - the BASELINE config 5 step at world
+1), and the step is timed
 
   base      no streamer
   blind     streamer on k CUs, GEMM planner unaware (plans for 256 CUs)
@@ -34,20 +36,33 @@ from mxk8s.train.ddp_llama import build, use_tuned_gemms  # noqa: E402
 
 
 class Streamer:
-    """HBM copy kernel on a stream confined to CUs [0, k)."""
+    """HBM copy kernel holding k CUs.
 
-    def __init__(self, k: int, dev, mib: int = 512):
+    placement "spread" (default, what RCCL's kernels look like): k
+    workgroups of 256 threads on an ordinary high-priority stream; workgroups
+    are dealt round-robin over the 8 XCDs, so k/8 CUs of every XCD are held.
+    placement "masked": 4k workgroups on a stream CU-masked to CUs [0, k) -
+    all of them on the first XCD(s), the worst case for a GEMM whose tiles
+    are dealt evenly over the XCDs (that XCD then finishes last)."""
+
+    def __init__(self, k: int, dev, mib: int = 512, placement: str = "spread"):
         import ctypes
         self.k = k
         self.L = _lib.lib()
-        h = ctypes.c_void_p()
-        _lib.check(self.L.mxk_stream_create_cu_masked(0, k, 0, ctypes.byref(h)), "cu-masked stream")
-        self.handle = h.value
-        self.stream = torch.cuda.ExternalStream(self.handle, device=dev)
+        self.owned = placement == "masked"
+        if self.owned:
+            h = ctypes.c_void_p()
+            _lib.check(self.L.mxk_stream_create_cu_masked(0, k, 0, ctypes.byref(h)), "cu-masked stream")
+            self.handle = h.value
+            self.stream = torch.cuda.ExternalStream(self.handle, device=dev)
+            self.nwg = 4 * k
+        else:
+            self.stream = torch.cuda.Stream(device=dev, priority=-1)
+            self.handle = self.stream.cuda_stream
+            self.nwg = k
         n = mib * 2 ** 20
         self.src = torch.empty(n, dtype=torch.uint8, device=dev).fill_(1)
         self.dst = torch.empty(n, dtype=torch.uint8, device=dev)
-        self.nwg = 4 * k
         self.iters = 1
 
     def launch(self):
@@ -71,7 +86,8 @@ class Streamer:
 
     def close(self):
         torch.cuda.synchronize()
-        self.L.mxk_stream_destroy(self.handle)
+        if self.owned:
+            self.L.mxk_stream_destroy(self.handle)
 
 
 def step(model, ddp, opt, tokens, streamer=None, times=None):
@@ -104,6 +120,7 @@ def main() -> int:
     ap.add_argument("--layers", type=int, default=None, help="fewer layers (quick check only)")
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--micro-batch", type=int, default=8)
+    ap.add_argument("--placement", default="spread", help="comma list: spread, masked")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -135,21 +152,22 @@ def main() -> int:
     print("RESULT " + json.dumps({"k": 0, "mode": "base", "ms_per_step": round(base, 2),
                                   "backward_ms": round(base_bwd, 2), "layers": cfg.n_layers}),
           flush=True)
-    for k in [int(x) for x in a.cus.split(",") if x]:
-        st = Streamer(k, dev)
-        one = st.calibrate(base_bwd)
-        for mode in ("blind", "aware"):
-            gemm.set_reserved_cus(k if mode == "aware" else 0)
-            ms, bwd = timed(st)
-            ideal = k / 256 * base_bwd / base
-            print("RESULT " + json.dumps({
-                "k": k, "mode": mode, "ms_per_step": round(ms, 2), "backward_ms": round(bwd, 2),
-                "slowdown": round(ms / base - 1, 4), "ideal_slowdown": round(ideal, 4),
-                "criterion": round(k / 256 + 0.02, 4), "streamer_iters": st.iters,
-                "streamer_ms_per_iter_alone": round(one, 3),
-                "available_cus": gemm.available_cus()}), flush=True)
-        gemm.set_reserved_cus(0)
-        st.close()
+    for placement in a.placement.split(","):
+        for k in [int(x) for x in a.cus.split(",") if x]:
+            st = Streamer(k, dev, placement=placement)
+            one = st.calibrate(base_bwd)
+            for mode in ("blind", "aware"):
+                gemm.set_reserved_cus(k if mode == "aware" else 0)
+                ms, bwd = timed(st)
+                ideal = k / 256 * base_bwd / base
+                print("RESULT " + json.dumps({
+                    "k": k, "placement": placement, "mode": mode, "ms_per_step": round(ms, 2),
+                    "backward_ms": round(bwd, 2), "slowdown": round(ms / base - 1, 4),
+                    "ideal_slowdown": round(ideal, 4), "criterion": round(k / 256 + 0.02, 4),
+                    "streamer_iters": st.iters, "streamer_ms_per_iter_alone": round(one, 3),
+                    "available_cus": gemm.available_cus()}), flush=True)
+            gemm.set_reserved_cus(0)
+            st.close()
     return 0
 
 

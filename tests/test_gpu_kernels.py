@@ -61,10 +61,13 @@ def test_gemm_narrow_c_stride(cuda_device):
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 4096, 256), (1024, 768, 512), (512, 512, 64),
-                                   (512, 768, 128), (768, 512, 192)])
+                                   (512, 768, 128), (768, 512, 192), (512, 512, 320),
+                                   (512, 256, 448), (256, 512, 832), (512, 512, 1216)])
 def test_gemm_every_schedule_vs_fp32(cuda_device, M, N, K):
     """Every non-ablation schedule of the 256x256 kernel; 4096^2 puts the
-    XCD super-block map (16x16 tiles) in play, 1024x768 its MAP-0 fallback."""
+    XCD super-block map (16x16 tiles) in play, 1024x768 its MAP-0 fallback;
+    K = 64 .. 1216 gives 1-19 K-tiles, every remainder of the one-barrier
+    schedule's 6-K-tile slot cycle (47: 3 A slots x 2 B slots)."""
     from mxk8s.ops import _lib
     L = _lib.lib()
     a = _rand((M, K), cuda_device, 23).bfloat16()
