@@ -88,6 +88,8 @@
 //           B right after the barrier (gemm_tn_core.h mxk_gemm_bf16_tn_w4k)
 //  48-51 DIAG 47 without its DMA pieces / fragment reads / waits and barrier /
 //           all three (timing ablations, wrong outputs)
+//  52 w4k   47 with the B fragment as the outer MFMA loop (srcA held for 8
+//           MFMAs, hipBLASLt's operand order)
 //  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
 //           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
 //           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
@@ -324,7 +326,7 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                                      int variant, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 52;
+constexpr int kNumVariants = 53;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -336,7 +338,7 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
     "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps", "w4i_ldsst_full_template",
     "w4k_1bar_a3_ldsst", "diag_w4k_nodma", "diag_w4k_noreads", "diag_w4k_nowait",
-    "diag_w4k_mfma_only"};
+    "diag_w4k_mfma_only", "w4k_border"};
 
 }  // namespace
 #ifdef MXK_GEMM_EXPERIMENTS

@@ -304,7 +304,9 @@ constexpr int A3_LDS = 5 * A3_SLOT;            // 160 KiB
 // ABL (timing ablations only, wrong outputs; experiments variants 48-51):
 // bit 0 skips the DMA pieces, bit 1 the fragment reads, bit 2 the waits and
 // the barrier.
-template <int AS, int BS, int MODE, class HOOK = NoHook, int ABL = 0>
+// ORDER 1: the B fragment is the outer MFMA loop (srcA held for 8 MFMAs,
+// srcB changing - hipBLASLt's operand order) instead of the A fragment.
+template <int AS, int BS, int MODE, class HOOK = NoHook, int ABL = 0, int ORDER = 0>
 __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                           bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                           bf16x8_t (&f1b)[8], char* smem, int a_base, int b_base,
@@ -328,8 +330,9 @@ __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int m = h * 64 + o * 8 + q;
-        if (h == 0) mfma_16x16x32_agpr(acc[o][q], f0b[q], f0a[o]);
-        else mfma_16x16x32_agpr(acc[o][q], f1b[q], f1a[o]);
+        const int i = ORDER ? q : o, j = ORDER ? o : q;
+        if (h == 0) mfma_16x16x32_agpr(acc[i][j], f0b[j], f0a[i]);
+        else mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
         hook(m);
         if (!(ABL & 2) && S::a1(m) >= 0)
           f1a[S::a1(m)] = lds_read_b128(XA + a_base + S::a1(m) * SUB + off_k1);
@@ -355,7 +358,7 @@ __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
   }
 }
 
-template <int MAP, int EPI, int ABL = 0>
+template <int MAP, int EPI, int ABL = 0, int ORDER = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -412,7 +415,7 @@ mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   int s = 0;
   int kb = 2 * BK * 2;
 #define MXK_W4K(as_, bs_)                                                                       \
-  w4k_ktile<as_, bs_, 1, NoHook, ABL>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,     \
+  w4k_ktile<as_, bs_, 1, NoHook, ABL, ORDER>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,     \
                                       off_k1, dma_a, dma_b, kb, wave_s);                        \
   kb += BK * 2;
   for (; s + 6 <= ns - 2; s += 6) {
@@ -429,11 +432,11 @@ mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   s += r > 0 ? r : 0;
   // the last two K-tiles (or the only one): no DMA, runtime slots
   if (ns >= 2) {
-    w4k_ktile<-1, -1, 2>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+    w4k_ktile<-1, -1, 2, NoHook, 0, ORDER>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
                          dma_b, 0, wave_s, s % 3, s & 1);
     ++s;
   }
-  w4k_ktile<-1, -1, 3>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a, dma_b,
+  w4k_ktile<-1, -1, 3, NoHook, 0, ORDER>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a, dma_b,
                        0, wave_s, s % 3, s & 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   mxk::mfma_drain(acc);
