@@ -35,6 +35,7 @@ _SIGNATURES = {
     "mxk_gemm_available_cus": (_i, []),
     "mxk_gemm_split_plan": (_i, [_l, _i, _i, ctypes.POINTER(ctypes.c_long)]),
     "mxk_stream_create_cu_masked": (_i, [_i, _i, _i, ctypes.POINTER(ctypes.c_void_p)]),
+    "mxk_stream_create_cu_masked_groups": (_i, [_i, _i, _i, ctypes.POINTER(ctypes.c_void_p)]),
     "mxk_stream_destroy": (_i, [_vp]),
     "mxk_hbm_stream": (_i, [_vp, _vp, _l, _i, _i, _vp]),
     "mxk_gemm_bf16_tn": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp]),

@@ -62,6 +62,26 @@ MXK_API int mxk_stream_create_cu_masked(int first, int n, int invert, void** out
   return static_cast<int>(e);
 }
 
+// A stream on the CUs c with c % group < per_group (invert = 0) or on every
+// other CU (invert = 1).  group = CUs per XCD spreads the set evenly over the
+// XCDs when the mask's bit order is XCD-major (the `xcd` placement of
+// scripts/contention_bench.py checks that it is: an unbalanced set makes the
+// GEMMs' XCD finish last).
+MXK_API int mxk_stream_create_cu_masked_groups(int per_group, int group, int invert, void** out) {
+  const int cus = hw_cus();
+  if (!out || group <= 0 || per_group < 0 || per_group > group || cus % group)
+    return static_cast<int>(hipErrorInvalidValue);
+  std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+  for (int c = 0; c < cus; ++c) {
+    const bool in = c % group < per_group;
+    if (in != (invert != 0)) mask[c / 32] |= 1u << (c % 32);
+  }
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data());
+  *out = s;
+  return static_cast<int>(e);
+}
+
 MXK_API int mxk_stream_destroy(void* s) {
   return static_cast<int>(hipStreamDestroy(static_cast<hipStream_t>(s)));
 }

@@ -908,6 +908,10 @@ int mxk_gemm_tn_exp_launch(int v, int nwg, hipStream_t stream, const void* A, co
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 0, 1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
                          b, c, M, N, K, lda, ldb, ldc);
       break;
+    case 53:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 8>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
+                         b, c, M, N, K, lda, ldb, ldc);
+      break;
     case 51:
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 7>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
                          b, c, M, N, K, lda, ldb, ldc);

@@ -326,7 +326,7 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                                      int variant, hipStream_t stream);
 
 namespace {
-constexpr int kNumVariants = 53;
+constexpr int kNumVariants = 54;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -338,7 +338,7 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
     "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps", "w4i_ldsst_full_template",
     "w4k_1bar_a3_ldsst", "diag_w4k_nodma", "diag_w4k_noreads", "diag_w4k_nowait",
-    "diag_w4k_mfma_only", "w4k_border"};
+    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore"};
 
 }  // namespace
 #ifdef MXK_GEMM_EXPERIMENTS
@@ -409,7 +409,7 @@ MXK_API const char* mxk_gemm_bf16_tn_variant_name(int variant) {
 MXK_API int mxk_gemm_bf16_tn_variant_built(int variant) { return variant_built(variant); }
 // Variant 10 is a timing ablation (no C store): never correctness-checked or used.
 MXK_API int mxk_gemm_bf16_tn_is_ablation(int variant) {
-  return variant == 10 || (variant >= 48 && variant <= 51);
+  return variant == 10 || (variant >= 48 && variant <= 51) || variant == 53;
 }
 
 MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,

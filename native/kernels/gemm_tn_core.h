@@ -303,7 +303,7 @@ constexpr int A3_LDS = 5 * A3_SLOT;            // 160 KiB
 // (compile-time; AS/BS = -1: runtime `as`/`bs`, for the two tail K-tiles).
 // ABL (timing ablations only, wrong outputs; experiments variants 48-51):
 // bit 0 skips the DMA pieces, bit 1 the fragment reads, bit 2 the waits and
-// the barrier.
+// the barrier, bit 3 the C store (the epilogue's price).
 // ORDER 1: the B fragment is the outer MFMA loop (srcA held for 8 MFMAs,
 // srcB changing - hipBLASLt's operand order) instead of the A fragment.
 template <int AS, int BS, int MODE, class HOOK = NoHook, int ABL = 0, int ORDER = 0>
@@ -441,7 +441,9 @@ mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   mxk::mfma_drain(acc);
 
-  if constexpr (EPI == 4) {
+  if constexpr (ABL & 8) {
+    return;
+  } else if constexpr (EPI == 4) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     mxk::store_block_lds<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane,

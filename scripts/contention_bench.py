@@ -43,16 +43,24 @@ class Streamer:
     are dealt round-robin over the 8 XCDs, so k/8 CUs of every XCD are held.
     placement "masked": 4k workgroups on a stream CU-masked to CUs [0, k) -
     all of them on the first XCD(s), the worst case for a GEMM whose tiles
-    are dealt evenly over the XCDs (that XCD then finishes last)."""
+    are dealt evenly over the XCDs (that XCD then finishes last).
+    placement "xcd": 4k workgroups on a stream CU-masked to the first k/8 CUs
+    of every 32 (of every XCD when the mask's bit order is XCD-major) - how
+    a collective confined to a CU partition would sit."""
 
     def __init__(self, k: int, dev, mib: int = 512, placement: str = "spread"):
         import ctypes
         self.k = k
         self.L = _lib.lib()
-        self.owned = placement == "masked"
+        self.owned = placement in ("masked", "xcd")
         if self.owned:
             h = ctypes.c_void_p()
-            _lib.check(self.L.mxk_stream_create_cu_masked(0, k, 0, ctypes.byref(h)), "cu-masked stream")
+            if placement == "xcd":
+                assert k % 8 == 0, "xcd placement needs k % 8 == 0"
+                _lib.check(self.L.mxk_stream_create_cu_masked_groups(k // 8, 32, 0, ctypes.byref(h)),
+                           "cu-masked stream")
+            else:
+                _lib.check(self.L.mxk_stream_create_cu_masked(0, k, 0, ctypes.byref(h)), "cu-masked stream")
             self.handle = h.value
             self.stream = torch.cuda.ExternalStream(self.handle, device=dev)
             self.nwg = 4 * k
@@ -120,7 +128,7 @@ def main() -> int:
     ap.add_argument("--layers", type=int, default=None, help="fewer layers (quick check only)")
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--micro-batch", type=int, default=8)
-    ap.add_argument("--placement", default="spread", help="comma list: spread, masked")
+    ap.add_argument("--placement", default="spread", help="comma list: spread, xcd, masked")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)

@@ -16,7 +16,7 @@
 #   attn_ab       attention fwd/bwd timing                 [ATTN_ARGS]
 #   prof_ddp      kernel trace + roctx breakdown of the DDP step [STEPS]
 #   pmc_gemm      PMC counters of the TN GEMM              [VARIANTS, SIZES, COUNTERS]
-#   contention    DDP step beside a CU-pinned HBM streamer  [CONT_CUS]
+#   contention    DDP step beside a CU-pinned HBM streamer  [CONT_CUS, CONT_PLACE]
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 R=$PWD
@@ -81,7 +81,7 @@ for step in "$@"; do
         -d "$O/pmc_gemm" -o run -- python3 -m mxk8s.validate.gemm --sizes "${SIZES:-8192}" \
         --variants "${VARIANTS:-26}" --iters 6 --rounds 2 --warmup-s 0.5 ;;
     contention)
-      run contention 900 python3 -u scripts/contention_bench.py --cus "${CONT_CUS:-0,16,32,64}" ;;
+      run contention 900 python3 -u scripts/contention_bench.py --cus "${CONT_CUS:-16,32,64}" --placement "${CONT_PLACE:-spread,xcd}" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
