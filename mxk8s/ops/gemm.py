@@ -151,3 +151,31 @@ def set_reserved_cus(n: int) -> None:
 
 def available_cus() -> int:
     return int(_lib.lib().mxk_gemm_available_cus())
+
+
+# ---- staggered rounds (gemm_bf16.hip schedule 54) --------------------------
+def stagger_plan(T: int, K: int, cus: int) -> int:
+    """Split tiles per XCD of the staggered-round schedule, 0 when it does not
+    apply.  Mirrors ``mxk_gemm_stagger_plan`` (gemm_bf16.hip)."""
+    if T <= 0 or T % 8 or cus < 16 or K % (2 * XBK) or K < 4 * XBK:
+        return 0
+    tx, cx = T // 8, cus // 8
+    sx = cx // 2
+    return sx if sx > 0 and tx >= 2 * cx else 0
+
+
+def stagger_part(b: int, T: int, sx: int) -> tuple[int, int, int]:
+    """(virtual tile, part, slot) of workgroup ``b``: part 0 a whole tile, 1
+    the first K half of a split tile (its fp32 partial goes to ``slot``), 2
+    the second half (waits for ``slot``).  Mirrors ``stagger_part``
+    (gemm_tn_core.h)."""
+    x, i = b & 7, b >> 3
+    tx = T >> 3
+    f = tx - sx
+    if i < 2 * sx and i & 1:
+        return x + 8 * (f + (i >> 1)), 1, x * sx + (i >> 1)
+    if i < 2 * sx:
+        return x + 8 * (i >> 1), 0, -1
+    if i < tx:
+        return x + 8 * (i - sx), 0, -1
+    return x + 8 * (f + i - tx), 2, x * sx + (i - tx)

@@ -99,7 +99,10 @@
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
 // stay in profiles/r1_gemm_*/ (numbered by the old ids: old 34 = 0,
 // 31 = 1, 29 = 2, 30 = 3, 32 = 4, 35 = 5, 36 = 6).
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "gemm_tn_core.h"
 
@@ -325,8 +328,31 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
                                      int lda, int ldb, int ldc, int a_kmajor, int b_kmajor,
                                      int variant, hipStream_t stream);
 
+MXK_API int mxk_gemm_available_cus(void);   // gemm_bf16_layouts.hip
+
+// Staggered-round plan (schedule 54, mxk_gemm_bf16_tn_w4j_stag): split tiles
+// per XCD (half the XCD's CUs), or 0 when it does not apply - T % 8, fewer
+// than two whole rounds, or K halves shorter than two K-tiles / not whole
+// K-tiles.  Pure host arithmetic (tests/test_gemm_plan.py).
+MXK_API int mxk_gemm_stagger_plan(long T, int K, int cus) {
+  if (T <= 0 || T % 8 || cus < 16 || K % (2 * BK) || K < 4 * BK) return 0;
+  const long tx = T / 8;
+  const int cx = cus / 8;
+  const int sx = cx / 2;
+  if (sx <= 0 || tx < 2 * cx) return 0;
+  return sx;
+}
+
+// stagger_part() of workgroup b on the host: out = {virtual tile, part, slot}
+MXK_API void mxk_gemm_stagger_part(int b, int T, int sx, int* out) {
+  const StaggerPart p = stagger_part(b, T, sx);
+  out[0] = p.vtile;
+  out[1] = p.part;
+  out[2] = p.slot;
+}
+
 namespace {
-constexpr int kNumVariants = 54;
+constexpr int kNumVariants = 55;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -338,7 +364,7 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
     "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps", "w4i_ldsst_full_template",
     "w4k_1bar_a3_ldsst", "diag_w4k_nodma", "diag_w4k_noreads", "diag_w4k_nowait",
-    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore"};
+    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore", "w4j_stagger"};
 
 }  // namespace
 #ifdef MXK_GEMM_EXPERIMENTS
@@ -355,9 +381,60 @@ void launch_w4j(int nwg, hipStream_t stream, const void* a, const void* b, void*
                      static_cast<uint16_t*>(c), M, N, K, lda, ldb, ldc);
 }
 
+// Per-(device, stream) workspace of the staggered schedule: fp32 partial
+// tiles and their flags in uncached memory (a first half and its second half
+// meet through memory, not through an L2), flags zeroed once and reset by
+// every consumer, so graph replays need no re-initialisation.
+struct StagWs {
+  float* ws = nullptr;
+  int* flags = nullptr;
+  int slots = 0;
+};
+std::mutex g_stag_mu;
+std::map<std::pair<int, hipStream_t>, StagWs> g_stag;
+
+const StagWs* stag_ws(hipStream_t stream, int slots) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_stag_mu);
+  StagWs& w = g_stag[{dev, stream}];
+  if (w.slots >= slots) return &w;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+    return nullptr;                     // no allocation inside a capture: plain schedule
+  if (w.ws) (void)hipFree(w.ws);
+  if (w.flags) (void)hipFree(w.flags);
+  w = StagWs{};
+  void *ws = nullptr, *fl = nullptr;
+  if (hipExtMallocWithFlags(&ws, static_cast<size_t>(slots) * BM * BN * 4, hipDeviceMallocUncached) !=
+          hipSuccess ||
+      hipExtMallocWithFlags(&fl, static_cast<size_t>(slots) * 4, hipDeviceMallocUncached) != hipSuccess ||
+      hipMemsetAsync(fl, 0, static_cast<size_t>(slots) * 4, stream) != hipSuccess) {
+    if (ws) (void)hipFree(ws);
+    if (fl) (void)hipFree(fl);
+    return nullptr;
+  }
+  w.ws = static_cast<float*>(ws);
+  w.flags = static_cast<int*>(fl);
+  w.slots = slots;
+  return &w;
+}
+
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
                 int N, int K, int lda, int ldb, int ldc) {
   switch (v) {
+    case 54: {
+      const int sx = mxk_gemm_stagger_plan(nwg, K, mxk_gemm_available_cus());
+      const StagWs* w = sx > 0 ? stag_ws(stream, 8 * sx) : nullptr;
+      if (!w) {
+        launch_w4j<4>(nwg, stream, A, Bt, C, M, N, K, lda, ldb, ldc);
+        break;
+      }
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j_stag<1, 4>), dim3(nwg + 8 * sx), dim3(W4_THREADS), 0,
+                         stream, static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
+                         static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc, w->ws, w->flags, sx);
+      break;
+    }
     case 1: launch_w4j<0>(nwg, stream, A, Bt, C, M, N, K, lda, ldb, ldc); break;
     case 6: launch_w4j<2>(nwg, stream, A, Bt, C, M, N, K, lda, ldb, ldc); break;
     case 9:
@@ -381,7 +458,7 @@ bool variant_built(int v) {
 #ifdef MXK_GEMM_EXPERIMENTS
   return v >= 0 && v < kNumVariants;
 #else
-  return v == 1 || v == 6 || v == 9 || v == 26;
+  return v == 1 || v == 6 || v == 9 || v == 26 || v == 54;
 #endif
 }
 

@@ -165,18 +165,15 @@ using mxk::store_block_narrow;
 // 4 = C staged through LDS and stored as whole lines (default, schedule 26),
 // 2 = non-temporal widened stores (schedule 6), 0 = 8-byte stores (schedule 1:
 // C not 16-B aligned or ldc % 8 != 0).
-template <int MAP, int EPI>
-__global__ void __launch_bounds__(W4_THREADS, 1)
-mxk_gemm_bf16_tn_w4j(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
-                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+// The K loop of one 256x256 tile over ns K-tiles (A / Bt at the first k of
+// the range, rows m0 / n0): prologue DMA of stages 0 and 1, the unrolled
+// three-barrier K-tiles, the two DMA-free tail K-tiles and the MFMA drain.
+__device__ __forceinline__ void w4j_mainloop(f32x4_t (&acc)[8][8], char* smem,
+                                             const uint16_t* __restrict__ A,
+                                             const uint16_t* __restrict__ Bt, int lda, int ldb,
+                                             int m0, int n0, int ns, int lane, int wave_s) {
   const int wm = wave_s >> 1;
   const int wn = wave_s & 1;
-  int m0, n0;
-  w4b_tile<MAP>(blockIdx.x, gridDim.x, M / BM, N / BN, &m0, &n0);
   const DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
   const DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
 
@@ -188,13 +185,11 @@ mxk_gemm_bf16_tn_w4j(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   const int a_base = wm * 8 * SUB;
   const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
 
-  f32x4_t acc[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int ns = K / BK;
 #pragma unroll
   for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
 #pragma unroll
@@ -243,7 +238,14 @@ mxk_gemm_bf16_tn_w4j(const uint16_t* __restrict__ A, const uint16_t* __restrict_
                         dma_b, 0, wave_s, s & 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   mxk::mfma_drain(acc);
+}
 
+template <int EPI>
+__device__ __forceinline__ void w4j_epilogue(f32x4_t (&acc)[8][8], char* smem,
+                                             uint16_t* __restrict__ C, int ldc, int m0, int n0,
+                                             int lane, int wave_s) {
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
   if constexpr (EPI == 4) {
     // whole-line stores through LDS; every wave's last fragment reads retired first
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -253,6 +255,122 @@ mxk_gemm_bf16_tn_w4j(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   } else if constexpr (EPI == 1) store_block_wide<false>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else if constexpr (EPI == 2) store_block_wide<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+}
+
+template <int MAP, int EPI>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4j(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int lane = threadIdx.x & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int m0, n0;
+  w4b_tile<MAP>(blockIdx.x, gridDim.x, M / BM, N / BN, &m0, &n0);
+  f32x4_t acc[8][8];
+  w4j_mainloop(acc, smem, A, Bt, lda, ldb, m0, n0, K / BK, lane, wave_s);
+  w4j_epilogue<EPI>(acc, smem, C, ldc, m0, n0, lane, wave_s);
+}
+
+// ---------------------------------------------------------------------------
+// Staggered rounds (schedule 54).  With T tiles over the CUs in whole rounds,
+// every CU finishes its tile at the same moment and all of them store their
+// C tiles at once: a 32 MB burst per round at 8192^3 (three times that for
+// the SwiGLU epilogues) that HBM drains while the matrix cores idle.  Here
+// half the CUs of every XCD start with HALF a tile: tiles are split into K
+// halves for sx tiles per XCD; the first halves run in the first wave of
+// workgroups (alternating with whole tiles), so those CUs run half a tile
+// out of phase for the whole kernel, and the second halves run last, where
+// the first-half CUs free up half a tile early.  A first half leaves its
+// fp32 partial in ws (uncached memory) and raises flags[slot]; the matching
+// second half (dispatched later on the same XCD, so the wait cannot
+// deadlock) waits for the flag, adds the partial and stores the tile.
+// Workgroup b runs on XCD b % 8; its local index i = b / 8 on that XCD:
+//   i < 2 sx, even   whole tile i / 2
+//   i < 2 sx, odd    first K half of split tile i / 2 (slot x sx + i / 2)
+//   2 sx <= i < tx   whole tile i - sx
+//   tx <= i          second K half of split tile i - tx
+// (tx = T / 8 tiles per XCD; the split tiles are the XCD's last sx tiles of
+// the map).  Virtual tile v = x + 8 * (local tile) keeps the map's XCD.
+struct StaggerPart {
+  int vtile;   // tile index fed to the tile map
+  int part;    // 0 whole tile, 1 first K half, 2 second K half
+  int slot;    // partial slot (parts 1, 2), else -1
+};
+
+__host__ __device__ inline StaggerPart stagger_part(int b, int T, int sx) {
+  const int x = b & 7, i = b >> 3;
+  const int tx = T >> 3, f = tx - sx;
+  StaggerPart r;
+  if (i < 2 * sx && (i & 1)) {
+    r.part = 1; r.slot = x * sx + (i >> 1); r.vtile = x + 8 * (f + (i >> 1));
+  } else if (i < 2 * sx) {
+    r.part = 0; r.slot = -1; r.vtile = x + 8 * (i >> 1);
+  } else if (i < tx) {
+    r.part = 0; r.slot = -1; r.vtile = x + 8 * (i - sx);
+  } else {
+    r.part = 2; r.slot = x * sx + (i - tx); r.vtile = x + 8 * (f + i - tx);
+  }
+  return r;
+}
+
+// fp32 partial of one tile in accumulator order: wave w's acc[i][j] of lane l
+// at float4 index ((w * 64 + i * 8 + j) * 64 + l) of the slot (256 KiB)
+__device__ __forceinline__ void partial_store(const f32x4_t (&acc)[8][8], float* ws, int slot,
+                                              int wave_s, int lane) {
+  f32x4_t* p = reinterpret_cast<f32x4_t*>(ws) + (static_cast<size_t>(slot) * 4 + wave_s) * 4096 + lane;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[(i * 8 + j) * 64] = acc[i][j];
+}
+
+template <int MAP, int EPI>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4j_stag(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                          uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc,
+                          float* __restrict__ ws, int* __restrict__ flags, int sx) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  const int lane = threadIdx.x & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int T = (M / BM) * (N / BN);
+  const StaggerPart sp = stagger_part(blockIdx.x, T, sx);
+  int m0, n0;
+  w4b_tile<MAP>(sp.vtile, T, M / BM, N / BN, &m0, &n0);
+  int ns = K / BK;
+  int k0 = 0;
+  if (sp.part) {
+    ns >>= 1;
+    if (sp.part == 2) k0 = ns * BK;
+  }
+  f32x4_t acc[8][8];
+  w4j_mainloop(acc, smem, A + k0, Bt + k0, lda, ldb, m0, n0, ns, lane, wave_s);
+  if (sp.part == 1) {
+    partial_store(acc, ws, sp.slot, wave_s, lane);
+    __builtin_amdgcn_s_waitcnt(0);             // this wave's partial reached memory
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(flags + sp.slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  static_assert(EPI == 4, "the staggered schedule adds the partial in the LDS-staged store");
+  const int wm = wave_s >> 1, wn = wave_s & 1;
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  if (sp.part == 2) {
+    if (threadIdx.x == 0)
+      while (__hip_atomic_load(flags + sp.slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        __builtin_amdgcn_s_sleep(4);
+    __syncthreads();
+    const f32x4_t* add =
+        reinterpret_cast<const f32x4_t*>(ws) + (static_cast<size_t>(sp.slot) * 4 + wave_s) * 4096 + lane;
+    mxk::store_block_lds<true, true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane,
+                                     smem + wave_s * mxk::kStoreLdsWave, 0, add);
+    if (threadIdx.x == 0)
+      __hip_atomic_store(flags + sp.slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  __builtin_amdgcn_s_barrier();
+  mxk::store_block_lds<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane,
+                             smem + wave_s * mxk::kStoreLdsWave);
 }
 
 

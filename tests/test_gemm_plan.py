@@ -62,3 +62,63 @@ def test_set_reserved_cus_roundtrip():
         assert L.mxk_gemm_reserved_cus() == 0
     finally:
         gemm.set_reserved_cus(0)
+
+
+# ---- staggered rounds (schedule 54) ----------------------------------------
+def _simulate(T, sx, cus, dur):
+    """Greedy in-order dispatch per XCD (workgroup b on XCD b % 8, the next
+    one to the first free CU): finish time of the grid, and the times at
+    which tiles end (C stores)."""
+    import heapq
+    cx = cus // 8
+    free = [[0.0] * cx for _ in range(8)]
+    for q in free:
+        heapq.heapify(q)
+    end, stores = 0.0, []
+    for b in range(T + 8 * sx):
+        _, part, _ = gemm.stagger_part(b, T, sx)
+        t0 = heapq.heappop(free[b & 7])
+        t1 = t0 + (dur if part == 0 else dur / 2)
+        heapq.heappush(free[b & 7], t1)
+        end = max(end, t1)
+        if part != 1:
+            stores.append(t1)
+    return end, stores
+
+
+@pytest.mark.parametrize("T,K", [(1024, 8192), (4096, 16384), (64 * 112, 4096), (64 * 56, 4096),
+                                 (64 * 24, 4096), (64 * 16, 4096), (256, 8192), (1000, 4096)])
+@pytest.mark.parametrize("cus", [256, 240, 192])
+def test_stagger_plan_and_parts(T, K, cus):
+    sx = gemm.stagger_plan(T, K, cus)
+    assert sx == _lib.lib().mxk_gemm_stagger_plan(T, K, cus)
+    if T % 8 or T // 8 < 2 * (cus // 8):
+        assert sx == 0
+        return
+    assert sx == cus // 16
+    out = (ctypes.c_int * 3)()
+    whole, first, second = {}, {}, {}
+    for b in range(T + 8 * sx):
+        p = gemm.stagger_part(b, T, sx)
+        _lib.lib().mxk_gemm_stagger_part(b, T, sx, out)
+        assert tuple(out) == p
+        v, part, slot = p
+        assert v % 8 == b % 8                      # the tile map keeps the XCD
+        {0: whole, 1: first, 2: second}[part].setdefault(v, []).append((b, slot))
+    # every tile exactly once: whole, or a first and a second half
+    assert set(whole) | set(first) == set(range(T))
+    assert not set(whole) & set(first) and set(first) == set(second)
+    assert all(len(v) == 1 for d in (whole, first, second) for v in d.values())
+    slots = sorted(first[v][0][1] for v in first)
+    assert slots == list(range(8 * sx))
+    for v in first:
+        (bp, sp), (bc, sc) = first[v][0], second[v][0]
+        assert sp == sc and bp < bc and bp % 8 == bc % 8   # producer dispatched first, same XCD
+    # whole rounds stay whole (ideal makespan) and the stores no longer
+    # coincide: half of them fall half a tile out of phase
+    cx = cus // 8
+    if (T // 8) % cx == 0:
+        end, stores = _simulate(T, sx, cus, 1.0)
+        assert end == pytest.approx(T / 8 / cx)
+        frac = [t % 1.0 for t in stores]
+        assert sum(abs(f - 0.5) < 1e-9 for f in frac) >= len(stores) // 2 - 8 * sx
