@@ -168,10 +168,14 @@ using mxk::store_block_narrow;
 // The K loop of one 256x256 tile over ns K-tiles (A / Bt at the first k of
 // the range, rows m0 / n0): prologue DMA of stages 0 and 1, the unrolled
 // three-barrier K-tiles, the two DMA-free tail K-tiles and the MFMA drain.
+// INIT: the accumulators start from init[(i * 8 + j) * 64] (this lane's fp32
+// partial of acc[i][j], the staggered schedule's first K half) instead of 0.
+template <bool INIT = false>
 __device__ __forceinline__ void w4j_mainloop(f32x4_t (&acc)[8][8], char* smem,
                                              const uint16_t* __restrict__ A,
                                              const uint16_t* __restrict__ Bt, int lda, int ldb,
-                                             int m0, int n0, int ns, int lane, int wave_s) {
+                                             int m0, int n0, int ns, int lane, int wave_s,
+                                             const f32x4_t* init = nullptr) {
   const int wm = wave_s >> 1;
   const int wn = wave_s & 1;
   const DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
@@ -188,7 +192,11 @@ __device__ __forceinline__ void w4j_mainloop(f32x4_t (&acc)[8][8], char* smem,
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (INIT) acc[i][j] = init[(i * 8 + j) * 64];
+      else acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+  if constexpr (INIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // before the counted DMA waits
 
 #pragma unroll
   for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
@@ -336,41 +344,33 @@ mxk_gemm_bf16_tn_w4j_stag(const uint16_t* __restrict__ A, const uint16_t* __rest
   const StaggerPart sp = stagger_part(blockIdx.x, T, sx);
   int m0, n0;
   w4b_tile<MAP>(sp.vtile, T, M / BM, N / BN, &m0, &n0);
-  int ns = K / BK;
-  int k0 = 0;
-  if (sp.part) {
-    ns >>= 1;
-    if (sp.part == 2) k0 = ns * BK;
-  }
+  const int ns = sp.part ? (K / BK) >> 1 : K / BK;
   f32x4_t acc[8][8];
-  w4j_mainloop(acc, smem, A + k0, Bt + k0, lda, ldb, m0, n0, ns, lane, wave_s);
-  if (sp.part == 1) {
-    partial_store(acc, ws, sp.slot, wave_s, lane);
-    __builtin_amdgcn_s_waitcnt(0);             // this wave's partial reached memory
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store(flags + sp.slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  static_assert(EPI == 4, "the staggered schedule adds the partial in the LDS-staged store");
-  const int wm = wave_s >> 1, wn = wave_s & 1;
-  __builtin_amdgcn_s_waitcnt(0xC07F);
   if (sp.part == 2) {
+    // second K half: start from the first half's partial (written half a
+    // tile after the kernel began, by a workgroup dispatched earlier on this
+    // XCD), then run the upper K range and store the tile as usual
     if (threadIdx.x == 0)
       while (__hip_atomic_load(flags + sp.slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
         __builtin_amdgcn_s_sleep(4);
     __syncthreads();
-    const f32x4_t* add =
+    const f32x4_t* init =
         reinterpret_cast<const f32x4_t*>(ws) + (static_cast<size_t>(sp.slot) * 4 + wave_s) * 4096 + lane;
-    mxk::store_block_lds<true, true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane,
-                                     smem + wave_s * mxk::kStoreLdsWave, 0, add);
+    w4j_mainloop<true>(acc, smem, A + ns * BK, Bt + ns * BK, lda, ldb, m0, n0, ns, lane, wave_s, init);
     if (threadIdx.x == 0)
       __hip_atomic_store(flags + sp.slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
+  } else {
+    w4j_mainloop(acc, smem, A, Bt, lda, ldb, m0, n0, ns, lane, wave_s);
+    if (sp.part == 1) {
+      partial_store(acc, ws, sp.slot, wave_s, lane);
+      __builtin_amdgcn_s_waitcnt(0);             // this wave's partial reached memory
+      __syncthreads();
+      if (threadIdx.x == 0)
+        __hip_atomic_store(flags + sp.slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
   }
-  __builtin_amdgcn_s_barrier();
-  mxk::store_block_lds<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane,
-                             smem + wave_s * mxk::kStoreLdsWave);
+  w4j_epilogue<EPI>(acc, smem, C, ldc, m0, n0, lane, wave_s);
 }
 
 

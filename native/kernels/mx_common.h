@@ -243,12 +243,10 @@ constexpr int kStoreLdsRow = 272;
 constexpr int kStoreLdsWave = 64 * kStoreLdsRow;
 // rot 1: acc[4p..4p+3] hold rows 64 (p ^ 1) .. (the w13 SwiGLU kernel's
 // rotated up waves); the two passes then write each other's rows.
-// ADD: add[(i * 8 + j) * 64] (this lane's fp32 partial of acc[i][j], the
-// staggered GEMM's first K half) is added before the conversion.
-template <bool NT = true, bool ADD = false>
+template <bool NT = true>
 __device__ __forceinline__ void store_block_lds(const f32x4_t (&acc)[8][8], uint16_t* C, int ldc,
                                                 int row0, int col0, int lane, char* lds,
-                                                int rot = 0, const f32x4_t* add = nullptr) {
+                                                int rot = 0) {
   const int crow = lane & 15, q = lane >> 4;
   const int rr = lane >> 4, cc = (lane & 15) * 8;
 #pragma unroll
@@ -257,11 +255,9 @@ __device__ __forceinline__ void store_block_lds(const f32x4_t (&acc)[8][8], uint
     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        f32x4_t a = acc[4 * p + ii][j];
-        if constexpr (ADD) a += add[((4 * p + ii) * 8 + j) * 64];
         uint2 pk;
-        pk.x = pack2bf(a[0], a[1]);
-        pk.y = pack2bf(a[2], a[3]);
+        pk.x = pack2bf(acc[4 * p + ii][j][0], acc[4 * p + ii][j][1]);
+        pk.y = pack2bf(acc[4 * p + ii][j][2], acc[4 * p + ii][j][3]);
         *reinterpret_cast<uint2*>(lds + (ii * 16 + crow) * kStoreLdsRow + (j * 16 + q * 4) * 2) = pk;
       }
 #pragma unroll
