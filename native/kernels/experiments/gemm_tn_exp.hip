@@ -2,6 +2,9 @@
 // (`make gemm-exp` -> libmxkernels_exp.so; -DMXK_GEMM_EXPERIMENTS), reached
 // through mxk_gemm_bf16_tn_variant (gemm_bf16.hip) -> mxk_gemm_tn_exp_launch.
 // The schedule list and what each measured is in gemm_bf16.hip's header.
+#include <map>
+#include <mutex>
+#include <tuple>
 #include "gemm_tn_core.h"
 
 // ---------------------------------------------------------------------------
@@ -877,6 +880,65 @@ void launch_w4i(int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* 
 }  // namespace
 
 // Launch A/B record `v` (any schedule the production build does not carry);
+// ---- staggered rounds (schedules 54 / 55, mxk_gemm_bf16_tn_w4j_stag in
+// gemm_tn_core.h): per-(device, stream) workspace of fp32 partial tiles and
+// their flags, zeroed once and reset by every consumer.  54: uncached memory
+// (the two halves meet through memory, whatever XCD each runs on); 55: plain
+// device memory (the halves meet in their XCD's L2 - correct only while
+// workgroup b runs on XCD b % 8, an A/B of the uncached traffic's price).
+MXK_API int mxk_gemm_stagger_plan(long T, int K, int cus);
+MXK_API int mxk_gemm_available_cus(void);
+
+namespace {
+struct StagWs {
+  float* ws = nullptr;
+  int* flags = nullptr;
+  int slots = 0;
+};
+std::mutex g_stag_mu;
+std::map<std::tuple<int, hipStream_t, bool>, StagWs> g_stag;
+
+const StagWs* stag_ws(hipStream_t stream, int slots, bool uncached) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_stag_mu);
+  StagWs& w = g_stag[{dev, stream, uncached}];
+  if (w.slots >= slots) return &w;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+    return nullptr;                     // no allocation inside a capture: plain schedule
+  if (w.ws) (void)hipFree(w.ws);
+  if (w.flags) (void)hipFree(w.flags);
+  w = StagWs{};
+  const unsigned fl_kind = uncached ? hipDeviceMallocUncached : hipDeviceMallocDefault;
+  void *ws = nullptr, *fl = nullptr;
+  if (hipExtMallocWithFlags(&ws, static_cast<size_t>(slots) * BM * BN * 4, fl_kind) != hipSuccess ||
+      hipExtMallocWithFlags(&fl, static_cast<size_t>(slots) * 4, fl_kind) != hipSuccess ||
+      hipMemsetAsync(fl, 0, static_cast<size_t>(slots) * 4, stream) != hipSuccess) {
+    if (ws) (void)hipFree(ws);
+    if (fl) (void)hipFree(fl);
+    return nullptr;
+  }
+  w.ws = static_cast<float*>(ws);
+  w.flags = static_cast<int*>(fl);
+  w.slots = slots;
+  return &w;
+}
+
+void launch_stag(bool uncached, int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b,
+                 uint16_t* c, int M, int N, int K, int lda, int ldb, int ldc) {
+  const int sx = mxk_gemm_stagger_plan(nwg, K, mxk_gemm_available_cus());
+  const StagWs* w = sx > 0 ? stag_ws(stream, 8 * sx, uncached) : nullptr;
+  if (!w) {
+    hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j<1, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc);
+    return;
+  }
+  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j_stag<1, 4>), dim3(nwg + 8 * sx), dim3(W4_THREADS), 0,
+                     stream, a, b, c, M, N, K, lda, ldb, ldc, w->ws, w->flags, sx);
+}
+}  // namespace
+
 // returns 0, or -1 when v is not an experiments schedule.
 int mxk_gemm_tn_exp_launch(int v, int nwg, hipStream_t stream, const void* A, const void* Bt,
                            void* C, int M, int N, int K, int lda, int ldb, int ldc) {
@@ -888,10 +950,6 @@ int mxk_gemm_tn_exp_launch(int v, int nwg, hipStream_t stream, const void* A, co
     // 26 as the full-flag template instantiated it before the production
     // kernel got its own (mxk_gemm_bf16_tn_w4j): same loop, other registers
     case 46: launch_w4i<1, 4, 1, 0, 1>(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
-    case 47:
-      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b,
-                         c, M, N, K, lda, ldb, ldc);
-      break;
     case 48:
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
                          b, c, M, N, K, lda, ldb, ldc);
@@ -904,10 +962,8 @@ int mxk_gemm_tn_exp_launch(int v, int nwg, hipStream_t stream, const void* A, co
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
                          b, c, M, N, K, lda, ldb, ldc);
       break;
-    case 52:
-      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 0, 1>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
-                         b, c, M, N, K, lda, ldb, ldc);
-      break;
+    case 54:
+    case 55: launch_stag(v == 54, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 53:
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 8>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
                          b, c, M, N, K, lda, ldb, ldc);

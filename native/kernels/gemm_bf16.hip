@@ -33,7 +33,8 @@
 //
 // Schedules (mxk_gemm_bf16_tn_variant, A/B-timed by python -m
 // mxk8s.validate.gemm --variants all).  The production library builds 1, 6,
-// 9 and 26 (mxk_gemm_bf16_tn_w4j, gemm_tn_core.h); every other schedule is
+// 9, 26 (mxk_gemm_bf16_tn_w4j) and 47 / 52 (mxk_gemm_bf16_tn_w4k, both in
+// gemm_tn_core.h); every other schedule is
 // an A/B record in experiments/gemm_tn_exp.hip, compiled only into `make
 // gemm-exp`'s libmxkernels_exp.so (-DMXK_GEMM_EXPERIMENTS):
 //   0 w4i   super-block map, non-temporal widened stores, late barrier #3
@@ -90,6 +91,12 @@
 //           all three (timing ablations, wrong outputs)
 //  52 w4k   47 with the B fragment as the outer MFMA loop (srcA held for 8
 //           MFMAs, hipBLASLt's operand order)
+//  53 DIAG  47 without the C store (prices the epilogue: ~2 % at 8192^3)
+//  54-55    26 with staggered rounds (mxk_gemm_bf16_tn_w4j_stag): half of
+//           each XCD's CUs start with a K-half tile so the C-store bursts fall
+//           half a tile apart; 54 exchanges the fp32 partials through
+//           uncached memory (-8 % at 8192^3, profiles/r4_gemm/), 55 through
+//           plain memory (same-XCD L2; A/B of the uncached traffic)
 //  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
 //           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
 //           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
@@ -99,10 +106,7 @@
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
 // stay in profiles/r1_gemm_*/ (numbered by the old ids: old 34 = 0,
 // 31 = 1, 29 = 2, 30 = 3, 32 = 4, 35 = 5, 36 = 6).
-#include <map>
-#include <mutex>
 #include <type_traits>
-#include <utility>
 
 #include "gemm_tn_core.h"
 
@@ -352,7 +356,7 @@ MXK_API void mxk_gemm_stagger_part(int b, int T, int sx, int* out) {
 }
 
 namespace {
-constexpr int kNumVariants = 55;
+constexpr int kNumVariants = 56;
 constexpr int kDefaultVariant = 26;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -364,7 +368,7 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
     "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps", "w4i_ldsst_full_template",
     "w4k_1bar_a3_ldsst", "diag_w4k_nodma", "diag_w4k_noreads", "diag_w4k_nowait",
-    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore", "w4j_stagger"};
+    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore", "w4j_stagger", "w4j_stagger_cached"};
 
 }  // namespace
 #ifdef MXK_GEMM_EXPERIMENTS
@@ -381,60 +385,19 @@ void launch_w4j(int nwg, hipStream_t stream, const void* a, const void* b, void*
                      static_cast<uint16_t*>(c), M, N, K, lda, ldb, ldc);
 }
 
-// Per-(device, stream) workspace of the staggered schedule: fp32 partial
-// tiles and their flags in uncached memory (a first half and its second half
-// meet through memory, not through an L2), flags zeroed once and reset by
-// every consumer, so graph replays need no re-initialisation.
-struct StagWs {
-  float* ws = nullptr;
-  int* flags = nullptr;
-  int slots = 0;
-};
-std::mutex g_stag_mu;
-std::map<std::pair<int, hipStream_t>, StagWs> g_stag;
-
-const StagWs* stag_ws(hipStream_t stream, int slots) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(g_stag_mu);
-  StagWs& w = g_stag[{dev, stream}];
-  if (w.slots >= slots) return &w;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
-    return nullptr;                     // no allocation inside a capture: plain schedule
-  if (w.ws) (void)hipFree(w.ws);
-  if (w.flags) (void)hipFree(w.flags);
-  w = StagWs{};
-  void *ws = nullptr, *fl = nullptr;
-  if (hipExtMallocWithFlags(&ws, static_cast<size_t>(slots) * BM * BN * 4, hipDeviceMallocUncached) !=
-          hipSuccess ||
-      hipExtMallocWithFlags(&fl, static_cast<size_t>(slots) * 4, hipDeviceMallocUncached) != hipSuccess ||
-      hipMemsetAsync(fl, 0, static_cast<size_t>(slots) * 4, stream) != hipSuccess) {
-    if (ws) (void)hipFree(ws);
-    if (fl) (void)hipFree(fl);
-    return nullptr;
-  }
-  w.ws = static_cast<float*>(ws);
-  w.flags = static_cast<int*>(fl);
-  w.slots = slots;
-  return &w;
-}
-
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
                 int N, int K, int lda, int ldb, int ldc) {
   switch (v) {
-    case 54: {
-      const int sx = mxk_gemm_stagger_plan(nwg, K, mxk_gemm_available_cus());
-      const StagWs* w = sx > 0 ? stag_ws(stream, 8 * sx) : nullptr;
-      if (!w) {
-        launch_w4j<4>(nwg, stream, A, Bt, C, M, N, K, lda, ldb, ldc);
-        break;
-      }
-      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j_stag<1, 4>), dim3(nwg + 8 * sx), dim3(W4_THREADS), 0,
-                         stream, static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
-                         static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc, w->ws, w->flags, sx);
+    case 47:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream,
+                         static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
+                         static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
       break;
-    }
+    case 52:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 0, 1>), dim3(nwg), dim3(W4_THREADS), 0, stream,
+                         static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
+                         static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
+      break;
     case 1: launch_w4j<0>(nwg, stream, A, Bt, C, M, N, K, lda, ldb, ldc); break;
     case 6: launch_w4j<2>(nwg, stream, A, Bt, C, M, N, K, lda, ldb, ldc); break;
     case 9:
@@ -458,7 +421,7 @@ bool variant_built(int v) {
 #ifdef MXK_GEMM_EXPERIMENTS
   return v >= 0 && v < kNumVariants;
 #else
-  return v == 1 || v == 6 || v == 9 || v == 26 || v == 54;
+  return v == 1 || v == 6 || v == 9 || v == 26 || v == 47 || v == 52;
 #endif
 }
 
@@ -486,7 +449,7 @@ MXK_API const char* mxk_gemm_bf16_tn_variant_name(int variant) {
 MXK_API int mxk_gemm_bf16_tn_variant_built(int variant) { return variant_built(variant); }
 // Variant 10 is a timing ablation (no C store): never correctness-checked or used.
 MXK_API int mxk_gemm_bf16_tn_is_ablation(int variant) {
-  return variant == 10 || (variant >= 48 && variant <= 51) || variant == 53;
+  return variant == 10 || variant == 45 || (variant >= 48 && variant <= 51) || variant == 53;
 }
 
 MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K,

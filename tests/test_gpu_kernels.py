@@ -86,9 +86,9 @@ def test_gemm_every_schedule_vs_fp32(cuda_device, M, N, K):
         assert err <= tol, (v, err)
 
 
-@pytest.mark.parametrize("M,N,K,variants", [(8192, 8192, 8192, (26, 6, 54)),
-                                            (16384, 16384, 512, (26, 54)),
-                                            (16384, 6144, 4096, (26, 6, 54))])
+@pytest.mark.parametrize("M,N,K,variants", [(8192, 8192, 8192, (26, 6, 47, 52)),
+                                            (16384, 16384, 512, (26, 52)),
+                                            (16384, 6144, 4096, (26, 6, 52))])
 def test_gemm_headline_shapes_full_output_vs_fp32(cuda_device, M, N, K, variants):
     """The long-K headline shape and the XCD super-block map at 64x64 tiles,
     the WHOLE output against an fp32 GEMM (tolerance 2^-7 max|ref|)."""
@@ -107,15 +107,19 @@ def test_gemm_headline_shapes_full_output_vs_fp32(cuda_device, M, N, K, variants
         assert err <= tol, (v, err, tol)
 
 
+@pytest.mark.parametrize("variant", [54, 55])
 @pytest.mark.parametrize("reserved", [0, 64])
 @pytest.mark.parametrize("M,N,K", [(8192, 4096, 256), (4096, 8192, 1152), (8192, 8192, 2048)])
-def test_gemm_staggered_rounds_vs_fp32(cuda_device, M, N, K, reserved):
-    """Schedule 54: half of each XCD's CUs start with half a tile (K-split
-    tiles whose halves meet through uncached memory and a flag).  Whole
-    output against fp32, three launches back to back on one stream (the
-    consumers reset the flags), also with the plan sized for 192 CUs."""
+def test_gemm_staggered_rounds_vs_fp32(cuda_device, M, N, K, reserved, variant):
+    """Schedules 54 / 55 (experiments library): half of each XCD's CUs start
+    with half a tile (K-split tiles whose halves meet through uncached / plain
+    memory and a flag).  Whole output against fp32, three launches back to
+    back on one stream (the consumers reset the flags), also with the plan
+    sized for 192 CUs."""
     from mxk8s.ops import _lib, gemm
     L = _lib.lib()
+    if not L.mxk_gemm_bf16_tn_variant_built(variant):
+        pytest.skip("experiments library only")
     T = (M // 256) * (N // 256)
     a = _rand((M, K), cuda_device, 41).bfloat16()
     bt = _rand((N, K), cuda_device, 42).bfloat16()
@@ -128,7 +132,8 @@ def test_gemm_staggered_rounds_vs_fp32(cuda_device, M, N, K, reserved):
         for _ in range(3):
             c = torch.full((M, N), float("nan"), device=cuda_device, dtype=torch.bfloat16)
             _lib.check(L.mxk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K,
-                                                  K, K, N, 54, _lib.stream_ptr(cuda_device)), "v54")
+                                                  K, K, N, variant, _lib.stream_ptr(cuda_device)),
+                       f"v{variant}")
             outs.append(c)
         torch.cuda.synchronize()
     finally:
