@@ -40,6 +40,9 @@ _SIGNATURES = {
     "mxk_stream_create_cu_masked_groups": (_i, [_i, _i, _i, ctypes.POINTER(ctypes.c_void_p)]),
     "mxk_stream_destroy": (_i, [_vp]),
     "mxk_hbm_stream": (_i, [_vp, _vp, _l, _i, _i, _vp]),
+    "mxk_hbm_stream_paced": (_i, [_vp, _vp, _l, _i, _i, _i, _vp]),
+    "mxk_cu_probe": (_i, [_vp, _i, _i, _vp]),
+    "mxk_stream_create_cu_masked_bits": (_i, [ctypes.POINTER(ctypes.c_int), _i, ctypes.POINTER(ctypes.c_void_p)]),
     "mxk_gemm_bf16_tn": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp]),
     "mxk_gemm_bf16_tn_is_fast": (_i, [_i, _i, _i]),
     "mxk_gemm_bf16_ex": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),

@@ -64,7 +64,7 @@
 //  21-24 w4j schedule 6 with a staggered first round (four CU groups start
 //           1/2/4/8 x ~1024 clocks apart, so C store bursts do not coincide)
 //  25 w4j   variant 23 with plain (temporal) widened stores
-//  26 w4j   default: schedule 6 with the C tile stored through LDS, read
+//  26 w4j   round-2/3 default: schedule 6 with the C tile stored through LDS, read
 //           back row-major so every store covers whole lines (4 rows x 256 B
 //           per wave-instruction instead of 16 x 64 B): +1.3 / +3.0 / +0.4 %
 //           over 6 at 8192^3 / 4096^3 / 16384^3 (profiles/r2_gemm_ab/)
@@ -89,8 +89,10 @@
 //           B right after the barrier (gemm_tn_core.h mxk_gemm_bf16_tn_w4k)
 //  48-51 DIAG 47 without its DMA pieces / fragment reads / waits and barrier /
 //           all three (timing ablations, wrong outputs)
-//  52 w4k   47 with the B fragment as the outer MFMA loop (srcA held for 8
-//           MFMAs, hipBLASLt's operand order)
+//  52 w4k   DEFAULT (round 4): 47 with the B fragment as the outer MFMA loop
+//           (srcA held for 8 MFMAs, hipBLASLt's operand order); against 26
+//           on two boxes: +1.8 / +0.5 % at 8192^3, 0 % at 4096^3, +0.2 % at
+//           16384^3, -0.2 / +2.5 % at 4096x4096x16384 (profiles/r4_gemm/)
 //  53 DIAG  47 without the C store (prices the epilogue: ~2 % at 8192^3)
 //  54-55    26 with staggered rounds (mxk_gemm_bf16_tn_w4j_stag): half of
 //           each XCD's CUs start with a K-half tile so the C-store bursts fall
@@ -357,7 +359,7 @@ MXK_API void mxk_gemm_stagger_part(int b, int T, int sx, int* out) {
 
 namespace {
 constexpr int kNumVariants = 56;
-constexpr int kDefaultVariant = 26;
+constexpr int kDefaultVariant = 52;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
     "w4i", "w4i_narrow", "w4i_b3_91", "w4i_b3_96", "w4i_r1", "w4ip", "w4j_hb", "w4j_2bar",
@@ -413,8 +415,9 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
   }
 }
 
-// Production builds carry the default (26), its non-LDS-store base (6), the
-// 8-byte-store fallback (1, same K-tile) and the layout kernel (9); every
+// Production builds carry the default (52), its ORDER-0 twin (47), the
+// round-3 default (26) and its non-LDS-store base (6), the 8-byte-store
+// fallback (1, 26's K-tile) and the layout kernel (9); every
 // other schedule is an A/B record in experiments/gemm_tn_exp.hip, built only
 // with -DMXK_GEMM_EXPERIMENTS (`make gemm-exp` -> libmxkernels_exp.so).
 bool variant_built(int v) {

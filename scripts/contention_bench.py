@@ -14,11 +14,16 @@ stream on CUs [0, k)) runs through every backward of the Llama-3-8B step
   aware     streamer on k CUs, mxk_gemm_set_reserved_cus(k): rounds and the
             split tail are sized for the 256 - k CUs left
 
-for k in --cus.  Prints one RESULT json per (k, mode) with ms/step, the
-slowdown against base, and the ideal k/256 x (backward share) it is judged
-against (<= k/256 + 2 % of the step).
+for k in --cus.  The streamer is paced to --gbps (copy traffic, read +
+write; default 700 GB/s, what an 8-rank ring reduce-scatter of the bf16
+gradient buckets puts on one GPU's HBM over xGMI) so that it takes CUs the
+way a collective does without also taking most of HBM; --gbps 0 lets it run
+flat out (a bandwidth hog, not a collective).  Prints one RESULT json per
+(k, placement, mode): ms/step, the backward's ms (the streamer runs beside
+it) and both slowdowns against base.  The criterion is the
+backward slowdown <= k/256 + 2 %.
 
-    python scripts/contention_bench.py --cus 16,32,64 [--steps 6] [--layers N]
+    python scripts/contention_bench.py --cus 16,32,64 [--gbps 700] [--steps 6] [--layers N]
 """
 import argparse
 import json
@@ -35,6 +40,39 @@ from mxk8s.ops import _lib, gemm  # noqa: E402
 from mxk8s.train.ddp_llama import build, use_tuned_gemms  # noqa: E402
 
 
+def cu_mask_map(dev) -> dict:
+    """mask bit -> (XCC, SE, SH, CU) of the CU it names: a one-bit CU-masked
+    stream per bit runs mxk_cu_probe (contention.hip) and reads back HW_ID /
+    XCC_ID of where its workgroups landed."""
+    import ctypes
+    L = _lib.lib()
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    out = torch.zeros(2 * 4, dtype=torch.int32, device=dev)
+    res = {}
+    for b in range(cus):
+        h = ctypes.c_void_p()
+        bits = (ctypes.c_int * 1)(b)
+        _lib.check(L.mxk_stream_create_cu_masked_bits(bits, 1, ctypes.byref(h)), "masked stream")
+        _lib.check(L.mxk_cu_probe(out.data_ptr(), 4, 2000, h.value), "cu probe")
+        torch.cuda.synchronize()
+        L.mxk_stream_destroy(h.value)
+        v = out.cpu().tolist()
+        places = {(v[2 * i + 1] & 0xF, (v[2 * i] >> 13) & 7, (v[2 * i] >> 12) & 1, (v[2 * i] >> 8) & 15)
+                  for i in range(4)}
+        res[b] = sorted(places)
+    return res
+
+
+def xcd_balanced_bits(k: int, cmap: dict) -> list:
+    """k mask bits, k/8 on each XCC, from the probed map (one CU per bit)."""
+    per = {}
+    for b in sorted(cmap):
+        if len(cmap[b]) == 1:
+            per.setdefault(cmap[b][0][0], []).append(b)
+    assert len(per) == 8 and all(len(v) >= k // 8 for v in per.values()), per.keys()
+    return sorted(b for x in sorted(per) for b in per[x][:k // 8])
+
+
 class Streamer:
     """HBM copy kernel holding k CUs.
 
@@ -44,11 +82,11 @@ class Streamer:
     placement "masked": 4k workgroups on a stream CU-masked to CUs [0, k) -
     all of them on the first XCD(s), the worst case for a GEMM whose tiles
     are dealt evenly over the XCDs (that XCD then finishes last).
-    placement "xcd": 4k workgroups on a stream CU-masked to the first k/8 CUs
-    of every 32 (of every XCD when the mask's bit order is XCD-major) - how
-    a collective confined to a CU partition would sit."""
+    placement "xcd": 4k workgroups on a stream CU-masked to k/8 CUs of every
+    XCD, the bits chosen from the probed mask -> CU map (cu_mask_map) - how a
+    collective confined to a CU partition would sit."""
 
-    def __init__(self, k: int, dev, mib: int = 512, placement: str = "spread"):
+    def __init__(self, k: int, dev, mib: int = 512, placement: str = "spread", cmap=None):
         import ctypes
         self.k = k
         self.L = _lib.lib()
@@ -57,7 +95,9 @@ class Streamer:
             h = ctypes.c_void_p()
             if placement == "xcd":
                 assert k % 8 == 0, "xcd placement needs k % 8 == 0"
-                _lib.check(self.L.mxk_stream_create_cu_masked_groups(k // 8, 32, 0, ctypes.byref(h)),
+                bits = xcd_balanced_bits(k, cmap if cmap is not None else cu_mask_map(dev))
+                arr = (ctypes.c_int * len(bits))(*bits)
+                _lib.check(self.L.mxk_stream_create_cu_masked_bits(arr, len(bits), ctypes.byref(h)),
                            "cu-masked stream")
             else:
                 _lib.check(self.L.mxk_stream_create_cu_masked(0, k, 0, ctypes.byref(h)), "cu-masked stream")
@@ -72,12 +112,15 @@ class Streamer:
         self.src = torch.empty(n, dtype=torch.uint8, device=dev).fill_(1)
         self.dst = torch.empty(n, dtype=torch.uint8, device=dev)
         self.iters = 1
+        self.pace = 0
 
     def launch(self):
-        _lib.check(self.L.mxk_hbm_stream(self.src.data_ptr(), self.dst.data_ptr(), self.src.numel(),
-                                         self.iters, self.nwg, self.handle), "hbm stream")
+        _lib.check(self.L.mxk_hbm_stream_paced(self.src.data_ptr(), self.dst.data_ptr(),
+                                               self.src.numel(), self.iters, self.nwg, self.pace,
+                                               self.handle), "hbm stream")
 
-    def calibrate(self, target_ms: float):
+    def time_one(self) -> float:
+        """ms of one pass over the buffer, alone on the GPU."""
         self.iters = 1
         with torch.cuda.stream(self.stream):
             self.launch()
@@ -88,7 +131,31 @@ class Streamer:
                 self.launch()
             e.record()
             e.synchronize()
-        one = s.elapsed_time(e) / 3
+        return s.elapsed_time(e) / 3
+
+    def gbps(self, ms: float) -> float:
+        return 2 * self.src.numel() / ms / 1e6
+
+    def calibrate(self, target_ms: float, gbps: float = 0.0):
+        """Pace to <= gbps (0: unpaced), then enough passes to cover target_ms."""
+        self.pace = 0
+        one = self.time_one()
+        if gbps > 0 and self.gbps(one) > gbps:
+            lo, hi = 0, 1
+            while True:
+                self.pace = hi
+                one = self.time_one()
+                if self.gbps(one) <= gbps or hi >= 4096:
+                    break
+                lo, hi = hi, hi * 2
+            while hi - lo > 1:                 # smallest pace within the target
+                self.pace = (lo + hi) // 2
+                t = self.time_one()
+                if self.gbps(t) <= gbps:
+                    hi, one = self.pace, t
+                else:
+                    lo = self.pace
+            self.pace = hi
         self.iters = max(1, int(round(target_ms / one)))
         return one
 
@@ -129,9 +196,24 @@ def main() -> int:
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--micro-batch", type=int, default=8)
     ap.add_argument("--placement", default="spread", help="comma list: spread, xcd, masked")
+    ap.add_argument("--map-only", action="store_true", help="print the CU-mask bit map and exit")
+    ap.add_argument("--gbps", type=float, default=700.0,
+                    help="streamer copy traffic (read + write, GB/s); 0: unpaced")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    cmap = None
+    if a.map_only or "xcd" in a.placement:
+        cmap = cu_mask_map(dev)
+        xccs = {}
+        for b, pl in cmap.items():
+            for p in pl:
+                xccs.setdefault(p[0], set()).add(b)
+        print("CUMAP " + json.dumps({"bits_per_xcc": {x: len(v) for x, v in sorted(xccs.items())},
+                                     "first_64": {b: cmap[b] for b in range(min(64, len(cmap)))}}),
+              flush=True)
+        if a.map_only:
+            return 0
     use_tuned_gemms()
     cfg = LlamaConfig.llama3_8b()
     if a.layers:
@@ -162,16 +244,19 @@ def main() -> int:
           flush=True)
     for placement in a.placement.split(","):
         for k in [int(x) for x in a.cus.split(",") if x]:
-            st = Streamer(k, dev, placement=placement)
-            one = st.calibrate(base_bwd)
+            st = Streamer(k, dev, placement=placement, cmap=cmap)
+            one = st.calibrate(base_bwd, a.gbps)
             for mode in ("blind", "aware"):
                 gemm.set_reserved_cus(k if mode == "aware" else 0)
                 ms, bwd = timed(st)
                 ideal = k / 256 * base_bwd / base
+                bslow = bwd / base_bwd - 1
                 print("RESULT " + json.dumps({
                     "k": k, "placement": placement, "mode": mode, "ms_per_step": round(ms, 2),
                     "backward_ms": round(bwd, 2), "slowdown": round(ms / base - 1, 4),
-                    "ideal_slowdown": round(ideal, 4), "criterion": round(k / 256 + 0.02, 4),
+                    "backward_slowdown": round(bslow, 4), "ideal_slowdown": round(ideal, 4),
+                    "criterion": round(k / 256 + 0.02, 4), "meets": bslow <= k / 256 + 0.02,
+                    "streamer_gbps_alone": round(st.gbps(one), 1), "streamer_pace": st.pace,
                     "streamer_iters": st.iters, "streamer_ms_per_iter_alone": round(one, 3),
                     "available_cus": gemm.available_cus()}), flush=True)
             gemm.set_reserved_cus(0)

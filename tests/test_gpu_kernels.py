@@ -76,7 +76,7 @@ def test_gemm_every_schedule_vs_fp32(cuda_device, M, N, K):
     tol = ref.abs().max().item() * 2 ** -7 + 1e-3
     built = [v for v in range(L.mxk_gemm_bf16_tn_num_variants())
              if L.mxk_gemm_bf16_tn_variant_built(v) and not L.mxk_gemm_bf16_tn_is_ablation(v)]
-    assert 26 in built and 1 in built            # the default and the narrow-C fallback
+    assert 52 in built and 26 in built and 1 in built   # default, round-3 default, narrow-C fallback
     for v in built:
         c = torch.full((M, N), float("nan"), device=cuda_device, dtype=torch.bfloat16)
         st = L.mxk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
