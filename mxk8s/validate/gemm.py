@@ -51,7 +51,7 @@ def _events_time(fn, iters: int) -> list[float]:
 
 
 def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
-        is_ablation=lambda v: False, pad: int = 0) -> list[dict]:
+        is_ablation=lambda v: False, pad: int = 0, cold: int = 1) -> list[dict]:
     dev = device or torch.device("cuda", torch.cuda.current_device())
     L = _lib.lib()
     stream = lambda: _lib.stream_ptr(dev)  # noqa: E731
@@ -62,22 +62,42 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
         g.manual_seed(M * 7 + N * 3 + K)
         # pad > 0: operands are [:, :K] views of (rows, K + pad) buffers, so
         # lda = ldb = K + pad (a diagnostic of power-of-two row strides)
-        A = (torch.rand((M, K + pad), device=dev, generator=g) * 2 - 1).bfloat16()[:, :K]
-        Bt = (torch.rand((N, K + pad), device=dev, generator=g) * 2 - 1).bfloat16()[:, :K]
+        # cold > 1: that many operand pairs, each launch takes the next one, so
+        # with cold x (A + B) beyond the 256 MB Infinity Cache every launch
+        # streams its operands from HBM as in a training step (back-to-back
+        # launches of one pair run from the cache)
+        pairs = [((torch.rand((M, K + pad), device=dev, generator=g) * 2 - 1).bfloat16()[:, :K],
+                  (torch.rand((N, K + pad), device=dev, generator=g) * 2 - 1).bfloat16()[:, :K])
+                 for _ in range(max(1, cold))]
+        A, Bt = pairs[0]
         lda = ldb = K + pad
         C = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
         ref = torch.matmul(A, Bt.t())
         kernels = {}
+        turn = [0]
+
+        def nxt():
+            turn[0] += 1
+            return pairs[turn[0] % len(pairs)]
         for v in variants:
             def mk(v=v):
-                st = L.mxk_gemm_bf16_tn_variant(A.data_ptr(), Bt.data_ptr(), C.data_ptr(), M, N, K,
+                a, b = nxt()
+                st = L.mxk_gemm_bf16_tn_variant(a.data_ptr(), b.data_ptr(), C.data_ptr(), M, N, K,
                                                 lda, ldb, N, v, stream())
                 if st:
                     _lib.check(st, f"gemm variant {v}")
             name = L.mxk_gemm_bf16_tn_variant_name(v)
             kernels[f"mxk_v{v}_{name.decode() if name else '?'}"] = mk
-        kernels["mxk_default"] = lambda: gemm_bf16_tn(A, Bt, C)
-        kernels["hipblaslt"] = lambda: torch.matmul(A, Bt.t(), out=C)
+
+        def default():
+            a, b = nxt()
+            gemm_bf16_tn(a, b, C)
+
+        def lib():
+            a, b = nxt()
+            torch.matmul(a, b.t(), out=C)
+        kernels["mxk_default"] = default
+        kernels["hipblaslt"] = lib
         # correctness of every hand-written schedule
         checks = {}
         ablations = set(k for k in kernels if k.startswith("mxk_v") and
@@ -86,6 +106,7 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
             if name == "hipblaslt" or name in ablations:
                 continue
             C.zero_()
+            turn[0] = len(pairs) - 1          # the next launch takes pair 0
             fn()
             torch.cuda.synchronize()
             rel = ((C.float() - ref.float()).norm() / ref.float().norm()).item()
@@ -112,7 +133,7 @@ def run(sizes, variants, iters: int, warmup_s: float, rounds: int, device=None,
             r = {"kernel": name, "M": M, "N": N, "K": K, "lda": lda, "dtype": "bf16",
                  "median_ms": med * 1e3, "min_ms": min(ts) * 1e3,
                  "tflops_median": flops / med / 1e12, "tflops_best": flops / min(ts) / 1e12,
-                 "samples": len(ts), "data": "uniform[-1,1) random"}
+                 "samples": len(ts), "data": "uniform[-1,1) random", "cold_pairs": len(pairs)}
             if name in checks:
                 r["rel_err_vs_hipblaslt"], r["max_abs_err_subblock_vs_fp32"] = checks[name]
             results.append(r)
@@ -130,6 +151,8 @@ def main(argv=None) -> int:
     p.add_argument("--warmup-s", type=float, default=2.0)
     p.add_argument("--device", type=int, default=None)
     p.add_argument("--pad", type=int, default=0, help="lda = ldb = K + pad (multiple of 8)")
+    p.add_argument("--cold", type=int, default=1,
+                   help="operand pairs cycled per launch (beyond the Infinity Cache: HBM-cold)")
     a = p.parse_args(argv)
     if a.device is not None:
         torch.cuda.set_device(a.device)
@@ -149,7 +172,8 @@ def main(argv=None) -> int:
     sizes = [int(x) for x in a.sizes.split(",")] if a.sizes else []
     sizes += [tuple(int(v) for v in x.split("x")) for x in a.shapes.split(",") if x]
     run(sizes, variants, a.iters, a.warmup_s, a.rounds,
-        is_ablation=lambda v: bool(_lib.lib().mxk_gemm_bf16_tn_is_ablation(v)), pad=a.pad)
+        is_ablation=lambda v: bool(_lib.lib().mxk_gemm_bf16_tn_is_ablation(v)), pad=a.pad,
+        cold=a.cold)
     return 0
 
 

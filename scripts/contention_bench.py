@@ -26,6 +26,7 @@ backward slowdown <= k/256 + 2 %.
     python scripts/contention_bench.py --cus 16,32,64 [--gbps 700] [--steps 6] [--layers N]
 """
 import argparse
+import itertools
 import json
 import os
 import statistics
@@ -47,18 +48,19 @@ def cu_mask_map(dev) -> dict:
     import ctypes
     L = _lib.lib()
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    out = torch.zeros(2 * 4, dtype=torch.int32, device=dev)
+    nw = 16
+    out = torch.zeros(2 * nw, dtype=torch.int32, device=dev)
     res = {}
     for b in range(cus):
         h = ctypes.c_void_p()
         bits = (ctypes.c_int * 1)(b)
         _lib.check(L.mxk_stream_create_cu_masked_bits(bits, 1, ctypes.byref(h)), "masked stream")
-        _lib.check(L.mxk_cu_probe(out.data_ptr(), 4, 2000, h.value), "cu probe")
+        _lib.check(L.mxk_cu_probe(out.data_ptr(), nw, 20000, h.value), "cu probe")
         torch.cuda.synchronize()
         L.mxk_stream_destroy(h.value)
         v = out.cpu().tolist()
         places = {(v[2 * i + 1] & 0xF, (v[2 * i] >> 13) & 7, (v[2 * i] >> 12) & 1, (v[2 * i] >> 8) & 15)
-                  for i in range(4)}
+                  for i in range(nw)}
         res[b] = sorted(places)
     return res
 
@@ -67,9 +69,11 @@ def xcd_balanced_bits(k: int, cmap: dict) -> list:
     """k mask bits, k/8 on each XCC, from the probed map (one CU per bit)."""
     per = {}
     for b in sorted(cmap):
-        if len(cmap[b]) == 1:
+        if len({p[0] for p in cmap[b]}) == 1:
             per.setdefault(cmap[b][0][0], []).append(b)
-    assert len(per) == 8 and all(len(v) >= k // 8 for v in per.values()), per.keys()
+    if len(per) != 8 or any(len(v) < k // 8 for v in per.values()):
+        raise SystemExit("CU mask bits do not name single XCDs on this device (see CUMAP); "
+                         "no xcd placement")
     return sorted(b for x in sorted(per) for b in per[x][:k // 8])
 
 
@@ -197,8 +201,9 @@ def main() -> int:
     ap.add_argument("--micro-batch", type=int, default=8)
     ap.add_argument("--placement", default="spread", help="comma list: spread, xcd, masked")
     ap.add_argument("--map-only", action="store_true", help="print the CU-mask bit map and exit")
-    ap.add_argument("--gbps", type=float, default=700.0,
-                    help="streamer copy traffic (read + write, GB/s); 0: unpaced")
+    ap.add_argument("--gbps", default="700",
+                    help="comma list of streamer copy rates (read + write, GB/s); 0: unpaced. "
+                         "A few GB/s isolates the CUs the streamer holds from the HBM it takes")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -210,8 +215,7 @@ def main() -> int:
             for p in pl:
                 xccs.setdefault(p[0], set()).add(b)
         print("CUMAP " + json.dumps({"bits_per_xcc": {x: len(v) for x, v in sorted(xccs.items())},
-                                     "first_64": {b: cmap[b] for b in range(min(64, len(cmap)))}}),
-              flush=True)
+                                     "map": {b: cmap[b] for b in range(len(cmap))}}), flush=True)
         if a.map_only:
             return 0
     use_tuned_gemms()
@@ -242,25 +246,27 @@ def main() -> int:
     print("RESULT " + json.dumps({"k": 0, "mode": "base", "ms_per_step": round(base, 2),
                                   "backward_ms": round(base_bwd, 2), "layers": cfg.n_layers}),
           flush=True)
-    for placement in a.placement.split(","):
-        for k in [int(x) for x in a.cus.split(",") if x]:
-            st = Streamer(k, dev, placement=placement, cmap=cmap)
-            one = st.calibrate(base_bwd, a.gbps)
-            for mode in ("blind", "aware"):
-                gemm.set_reserved_cus(k if mode == "aware" else 0)
-                ms, bwd = timed(st)
-                ideal = k / 256 * base_bwd / base
-                bslow = bwd / base_bwd - 1
-                print("RESULT " + json.dumps({
-                    "k": k, "placement": placement, "mode": mode, "ms_per_step": round(ms, 2),
-                    "backward_ms": round(bwd, 2), "slowdown": round(ms / base - 1, 4),
-                    "backward_slowdown": round(bslow, 4), "ideal_slowdown": round(ideal, 4),
-                    "criterion": round(k / 256 + 0.02, 4), "meets": bslow <= k / 256 + 0.02,
-                    "streamer_gbps_alone": round(st.gbps(one), 1), "streamer_pace": st.pace,
-                    "streamer_iters": st.iters, "streamer_ms_per_iter_alone": round(one, 3),
-                    "available_cus": gemm.available_cus()}), flush=True)
-            gemm.set_reserved_cus(0)
-            st.close()
+    for placement, gbps, k in itertools.product(a.placement.split(","),
+                                                [float(x) for x in a.gbps.split(",") if x],
+                                                [int(x) for x in a.cus.split(",") if x]):
+        st = Streamer(k, dev, placement=placement, cmap=cmap)
+        one = st.calibrate(base_bwd, gbps)
+        for mode in ("blind", "aware"):
+            gemm.set_reserved_cus(k if mode == "aware" else 0)
+            ms, bwd = timed(st)
+            ideal = k / 256 * base_bwd / base
+            bslow = bwd / base_bwd - 1
+            print("RESULT " + json.dumps({
+                "k": k, "placement": placement, "gbps_target": gbps, "mode": mode,
+                "ms_per_step": round(ms, 2),
+                "backward_ms": round(bwd, 2), "slowdown": round(ms / base - 1, 4),
+                "backward_slowdown": round(bslow, 4), "ideal_slowdown": round(ideal, 4),
+                "criterion": round(k / 256 + 0.02, 4), "meets": bslow <= k / 256 + 0.02,
+                "streamer_gbps_alone": round(st.gbps(one), 1), "streamer_pace": st.pace,
+                "streamer_iters": st.iters, "streamer_ms_per_iter_alone": round(one, 3),
+                "available_cus": gemm.available_cus()}), flush=True)
+        gemm.set_reserved_cus(0)
+        st.close()
     return 0
 
 

@@ -81,7 +81,7 @@ for step in "$@"; do
         -d "$O/pmc_gemm" -o run -- python3 -m mxk8s.validate.gemm --sizes "${SIZES:-8192}" \
         --variants "${VARIANTS:-26}" --iters 6 --rounds 2 --warmup-s 0.5 ;;
     contention)
-      run contention 900 python3 -u scripts/contention_bench.py --cus "${CONT_CUS:-16,32,64}" --placement "${CONT_PLACE:-spread,xcd}" ;;
+      run contention 900 python3 -u scripts/contention_bench.py --cus "${CONT_CUS:-16,32,64}" --placement "${CONT_PLACE:-spread}" --gbps "${CONT_GBPS:-5,700}" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
