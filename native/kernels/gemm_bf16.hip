@@ -99,6 +99,8 @@
 //           half a tile apart; 54 exchanges the fp32 partials through
 //           uncached memory (-8 % at 8192^3, profiles/r4_gemm/), 55 through
 //           plain memory (same-XCD L2; A/B of the uncached traffic)
+//  56 w4j   26 with an L2 prefetch of stage s+4 per K-tile (gemm_tn_core.h
+//           L2Prefetch; for HBM-cold operands)
 //  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
 //           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
 //           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
@@ -358,7 +360,7 @@ MXK_API void mxk_gemm_stagger_part(int b, int T, int sx, int* out) {
 }
 
 namespace {
-constexpr int kNumVariants = 56;
+constexpr int kNumVariants = 57;
 constexpr int kDefaultVariant = 52;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -370,7 +372,7 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
     "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps", "w4i_ldsst_full_template",
     "w4k_1bar_a3_ldsst", "diag_w4k_nodma", "diag_w4k_noreads", "diag_w4k_nowait",
-    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore", "w4j_stagger", "w4j_stagger_cached"};
+    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore", "w4j_stagger", "w4j_stagger_cached", "w4j_l2pf"};
 
 }  // namespace
 #ifdef MXK_GEMM_EXPERIMENTS
@@ -390,6 +392,11 @@ void launch_w4j(int nwg, hipStream_t stream, const void* a, const void* b, void*
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
                 int N, int K, int lda, int ldb, int ldc) {
   switch (v) {
+    case 56:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j<1, 4, true>), dim3(nwg), dim3(W4_THREADS), 0, stream,
+                         static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
+                         static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
+      break;
     case 47:
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream,
                          static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
@@ -424,7 +431,7 @@ bool variant_built(int v) {
 #ifdef MXK_GEMM_EXPERIMENTS
   return v >= 0 && v < kNumVariants;
 #else
-  return v == 1 || v == 6 || v == 9 || v == 26 || v == 47 || v == 52;
+  return v == 1 || v == 6 || v == 9 || v == 26 || v == 47 || v == 52 || v == 56;
 #endif
 }
 

@@ -170,7 +170,57 @@ using mxk::store_block_narrow;
 // three-barrier K-tiles, the two DMA-free tail K-tiles and the MFMA drain.
 // INIT: the accumulators start from init[(i * 8 + j) * 64] (this lane's fp32
 // partial of acc[i][j], the staggered schedule's first K half) instead of 0.
-template <bool INIT = false>
+// ---- L2 prefetch (schedule 56) ---------------------------------------------
+// With the operands HBM-cold (a training step: every GEMM reads activations
+// another kernel just wrote and weights nothing has touched since the last
+// step) the three-barrier K-tile's last B piece has ~0.75 K-tile (~0.9 us)
+// before its wait, about one HBM miss under load: 16384x4096x4096 runs 3.4 %
+// and 16384x6144x4096 4.7 % slower cold than cache-warm, hipBLASLt 1.4-1.8 %
+// (profiles/r4_gemm/cold_vs_warm.log).  Each K-tile therefore also pulls
+// stage s+4 into L2 with one dword per 128-B line (buffer_load_dword ... lds
+// into a 1 KiB LDS sink nobody reads: no VGPR is written, so no register
+// hazard), issued after stage s+2's last piece: it is older than stage s+3,
+// so K-tile s+2's stage wait covers it (~1.75 K-tiles of lead) and stage
+// s+4's real DMA in K-tile s+2 hits L2.  The 32 workgroups of an XCD's
+// 8 x 4 sub-block share 8 A and 4 B panels: waves 0-1 take a quarter of the
+// workgroup's A panel (by its sub-block column), waves 2-3 an eighth of its B
+// panel (by its row), so each line is pulled about once per XCD.
+constexpr int kPfSink = 2 * W4B_STAGE_BYTES;      // LDS byte offset of the sink
+constexpr int kPfLds = kPfSink + 4 * 256;         // LDS bytes of a prefetching kernel
+
+struct SchedHBPf : SchedHB {
+  static constexpr int PF = 125;                 // after stage s+2's last piece (m 124)
+  static constexpr int VM3 = SchedHB::VM3 + 1;   // the previous K-tile's prefetch is younger
+};
+
+struct L2Prefetch : NoHook {
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t voff;
+  char* sink;
+  int kb;
+  __device__ __forceinline__ void operator()(int m) const {
+    if (m == SchedHBPf::PF)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)sink, 4, voff, kb, 0, 0);
+  }
+};
+
+__device__ __forceinline__ L2Prefetch make_l2pf(const DmaK& dma_a, const DmaK& dma_b, int lda,
+                                                int ldb, char* smem, int lane, int wave_s) {
+  const int pos = (blockIdx.x >> 3) & 31;         // MAP 1 sub-block position
+  L2Prefetch h;
+  if (wave_s < 2) {   // A rows [64 (pos >> 3) + 32 wave, +32): lanes 32..63 repeat 0..31
+    h.rsrc = dma_a.rsrc;
+    h.voff = static_cast<uint32_t>((64 * (pos >> 3) + 32 * wave_s + (lane & 31)) * lda * 2);
+  } else {            // B rows [32 (pos & 7) + 16 (wave - 2), +16)
+    h.rsrc = dma_b.rsrc;
+    h.voff = static_cast<uint32_t>((32 * (pos & 7) + 16 * (wave_s - 2) + (lane & 15)) * ldb * 2);
+  }
+  h.sink = smem + kPfSink + wave_s * 256;
+  h.kb = 0;
+  return h;
+}
+
+template <bool INIT = false, bool PF = false>
 __device__ __forceinline__ void w4j_mainloop(f32x4_t (&acc)[8][8], char* smem,
                                              const uint16_t* __restrict__ A,
                                              const uint16_t* __restrict__ Bt, int lda, int ldb,
@@ -224,17 +274,42 @@ __device__ __forceinline__ void w4j_mainloop(f32x4_t (&acc)[8][8], char* smem,
   // K-tiles 0 .. ns-3 carry the DMA of stage s+2 (k offset kb = (s+2)*128 B)
   int s = 0;
   int kb = 2 * BK * 2;
-  for (; s + 2 <= ns - 2; s += 2) {
-    w4j_ktile<SchedHB, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                          dma_b, kb, wave_s);
-    w4j_ktile<SchedHB, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                          dma_b, kb + BK * 2, wave_s);
-    kb += 2 * BK * 2;
-  }
-  if (s < ns - 2) {   // s even
-    w4j_ktile<SchedHB, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                          dma_b, kb, wave_s);
-    ++s;
+  if constexpr (PF) {
+    // stage s+4's lines into L2; past the last stage the last one again (an
+    // L2 hit), so every K-tile issues the same number of vector-memory ops
+    L2Prefetch pf = make_l2pf(dma_a, dma_b, lda, ldb, smem, lane, wave_s);
+    const int kb_last = (ns - 1) * BK * 2;
+    for (; s + 2 <= ns - 2; s += 2) {
+      pf.kb = min(kb + 2 * BK * 2, kb_last);
+      w4j_ktile<SchedHBPf, 0, 1, 0, 0, false, L2Prefetch>(acc, f0a, f0b, f1a, f1b, smem, a_base,
+                                                          b_base, off_k0, off_k1, dma_a, dma_b, kb,
+                                                          wave_s, 0, 0, pf);
+      pf.kb = min(kb + 3 * BK * 2, kb_last);
+      w4j_ktile<SchedHBPf, 1, 1, 0, 0, false, L2Prefetch>(acc, f0a, f0b, f1a, f1b, smem, a_base,
+                                                          b_base, off_k0, off_k1, dma_a, dma_b,
+                                                          kb + BK * 2, wave_s, 0, 0, pf);
+      kb += 2 * BK * 2;
+    }
+    if (s < ns - 2) {   // s even
+      pf.kb = min(kb + 2 * BK * 2, kb_last);
+      w4j_ktile<SchedHBPf, 0, 1, 0, 0, false, L2Prefetch>(acc, f0a, f0b, f1a, f1b, smem, a_base,
+                                                          b_base, off_k0, off_k1, dma_a, dma_b, kb,
+                                                          wave_s, 0, 0, pf);
+      ++s;
+    }
+  } else {
+    for (; s + 2 <= ns - 2; s += 2) {
+      w4j_ktile<SchedHB, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                            dma_b, kb, wave_s);
+      w4j_ktile<SchedHB, 1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                            dma_b, kb + BK * 2, wave_s);
+      kb += 2 * BK * 2;
+    }
+    if (s < ns - 2) {   // s even
+      w4j_ktile<SchedHB, 0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
+                            dma_b, kb, wave_s);
+      ++s;
+    }
   }
   // the last two K-tiles (or the only one): no DMA
   if (ns >= 2) {
@@ -265,17 +340,17 @@ __device__ __forceinline__ void w4j_epilogue(f32x4_t (&acc)[8][8], char* smem,
   else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
-template <int MAP, int EPI>
+template <int MAP, int EPI, bool PF = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4j(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                      uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[PF ? kPfLds : 2 * W4B_STAGE_BYTES];
   const int lane = threadIdx.x & 63;
   const int wave_s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int m0, n0;
   w4b_tile<MAP>(blockIdx.x, gridDim.x, M / BM, N / BN, &m0, &n0);
   f32x4_t acc[8][8];
-  w4j_mainloop(acc, smem, A, Bt, lda, ldb, m0, n0, K / BK, lane, wave_s);
+  w4j_mainloop<false, PF>(acc, smem, A, Bt, lda, ldb, m0, n0, K / BK, lane, wave_s);
   w4j_epilogue<EPI>(acc, smem, C, ldc, m0, n0, lane, wave_s);
 }
 

@@ -38,6 +38,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mxk8s.models.llama import LlamaConfig  # noqa: E402
 from mxk8s.ops import _lib, gemm  # noqa: E402
+from mxk8s.utils import roctx  # noqa: E402
 from mxk8s.train.ddp_llama import build, use_tuned_gemms  # noqa: E402
 
 
@@ -201,6 +202,10 @@ def main() -> int:
     ap.add_argument("--micro-batch", type=int, default=8)
     ap.add_argument("--placement", default="spread", help="comma list: spread, xcd, masked")
     ap.add_argument("--map-only", action="store_true", help="print the CU-mask bit map and exit")
+    ap.add_argument("--modes", default="blind,aware", help="comma list: blind, aware")
+    ap.add_argument("--base-steps", type=int, default=None,
+                    help="steps of the base run (default --steps; its backward time calibrates "
+                         "the streamer)")
     ap.add_argument("--gbps", default="700",
                     help="comma list of streamer copy rates (read + write, GB/s); 0: unpaced. "
                          "A few GB/s isolates the CUs the streamer holds from the HBM it takes")
@@ -228,16 +233,17 @@ def main() -> int:
     batches = [torch.randint(0, cfg.vocab_size, (a.micro_batch, a.seq_len + 1), device=dev, generator=g)
                for _ in range(2)]
 
-    def timed(streamer=None):
+    def timed(streamer=None, label="base"):
         for i in range(a.warmup):
             step(model, ddp, opt, batches[i % 2], streamer)
         torch.cuda.synchronize()
         walls, evs = [], []
-        for i in range(a.steps):
-            t0 = time.perf_counter()
-            step(model, ddp, opt, batches[i % 2], streamer, evs)
-            torch.cuda.synchronize()
-            walls.append((time.perf_counter() - t0) * 1e3)
+        with roctx.range(f"contention.{label}"):     # kernel traces split by these ranges
+            for i in range(a.steps):
+                t0 = time.perf_counter()
+                step(model, ddp, opt, batches[i % 2], streamer, evs)
+                torch.cuda.synchronize()
+                walls.append((time.perf_counter() - t0) * 1e3)
         bwd = statistics.median(e[1].elapsed_time(e[2]) for e in evs)
         return statistics.median(walls), bwd
 
@@ -251,9 +257,9 @@ def main() -> int:
                                                 [int(x) for x in a.cus.split(",") if x]):
         st = Streamer(k, dev, placement=placement, cmap=cmap)
         one = st.calibrate(base_bwd, gbps)
-        for mode in ("blind", "aware"):
+        for mode in a.modes.split(","):
             gemm.set_reserved_cus(k if mode == "aware" else 0)
-            ms, bwd = timed(st)
+            ms, bwd = timed(st, f"k{k}.{placement}.{gbps:g}.{mode}")
             ideal = k / 256 * base_bwd / base
             bslow = bwd / base_bwd - 1
             print("RESULT " + json.dumps({

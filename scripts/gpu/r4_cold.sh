@@ -7,7 +7,7 @@ O=gpurun_out/r4cold; mkdir -p $O
 export PYTHONPATH=.
 for c in 1 4; do
   timeout -k 10 300 python3 -u -m mxk8s.validate.gemm --sizes 8192 --shapes 16384x4096x4096,16384x6144x4096,16384x4096x14336 \
-    --variants 26,52 --iters 48 --rounds 12 --cold $c > $O/cold$c.log 2>&1 || exit $?
+    --variants ${VARIANTS:-26,52,56} --iters 48 --rounds 12 --cold $c > $O/cold$c.log 2>&1 || exit $?
 done
 for c in 1 4; do
   grep RESULT $O/cold$c.log | python3 -c "
