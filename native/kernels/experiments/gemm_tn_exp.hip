@@ -962,6 +962,10 @@ int mxk_gemm_tn_exp_launch(int v, int nwg, hipStream_t stream, const void* A, co
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
                          b, c, M, N, K, lda, ldb, ldc);
       break;
+    case 56:
+      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j<1, 4, true>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
+                         b, c, M, N, K, lda, ldb, ldc);
+      break;
     case 54:
     case 55: launch_stag(v == 54, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 53:

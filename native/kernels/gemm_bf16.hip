@@ -100,7 +100,8 @@
 //           uncached memory (-8 % at 8192^3, profiles/r4_gemm/), 55 through
 //           plain memory (same-XCD L2; A/B of the uncached traffic)
 //  56 w4j   26 with an L2 prefetch of stage s+4 per K-tile (gemm_tn_core.h
-//           L2Prefetch; for HBM-cold operands)
+//           L2Prefetch; for HBM-cold operands): -1.5..-3 % warm, -1.7 % cold
+//           (profiles/r4_gemm/cold_vs_warm_prefetch56.txt)
 //  29-30    gemm_bf16_ring.hip: a ring of 4 / 5 32-deep k slots, one
 //           barrier per k-step, refills 4-5 steps ahead: -9 % at 8192^3,
 //           -23 % at 16384^3 (a k32 slot row is half a 128-B line, so each
@@ -392,11 +393,6 @@ void launch_w4j(int nwg, hipStream_t stream, const void* a, const void* b, void*
 void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* Bt, void* C, int M,
                 int N, int K, int lda, int ldb, int ldc) {
   switch (v) {
-    case 56:
-      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j<1, 4, true>), dim3(nwg), dim3(W4_THREADS), 0, stream,
-                         static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
-                         static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
-      break;
     case 47:
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream,
                          static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
@@ -431,7 +427,7 @@ bool variant_built(int v) {
 #ifdef MXK_GEMM_EXPERIMENTS
   return v >= 0 && v < kNumVariants;
 #else
-  return v == 1 || v == 6 || v == 9 || v == 26 || v == 47 || v == 52 || v == 56;
+  return v == 1 || v == 6 || v == 9 || v == 26 || v == 47 || v == 52;
 #endif
 }
 
