@@ -31,6 +31,8 @@ _fp = ctypes.POINTER(ctypes.c_float)
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "mxk_gemm_set_reserved_cus": (None, [_i]),
+    "mxk_gemm_set_exclusive": (None, [_i]),
+    "mxk_gemm_exclusive": (_i, []),
     "mxk_gemm_reserved_cus": (_i, []),
     "mxk_gemm_available_cus": (_i, []),
     "mxk_gemm_split_plan": (_i, [_l, _i, _i, ctypes.POINTER(ctypes.c_long)]),

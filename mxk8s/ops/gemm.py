@@ -153,6 +153,16 @@ def available_cus() -> int:
     return int(_lib.lib().mxk_gemm_available_cus())
 
 
+def set_exclusive(on: bool) -> None:
+    """GEMM launches claim the whole LDS of their CU (no other kernel's
+    workgroup can share a CU with a GEMM tile; mx_common.h mxk_excl_lds)."""
+    _lib.lib().mxk_gemm_set_exclusive(int(bool(on)))
+
+
+def exclusive() -> bool:
+    return bool(_lib.lib().mxk_gemm_exclusive())
+
+
 # ---- staggered rounds (gemm_bf16.hip schedule 54) --------------------------
 def stagger_plan(T: int, K: int, cus: int) -> int:
     """Split tiles per XCD of the staggered-round schedule, 0 when it does not

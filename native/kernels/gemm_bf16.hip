@@ -385,7 +385,7 @@ namespace {
 template <int EPI>
 void launch_w4j(int nwg, hipStream_t stream, const void* a, const void* b, void* c, int M, int N,
                 int K, int lda, int ldb, int ldc) {
-  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j<1, EPI>), dim3(nwg), dim3(W4_THREADS), 0, stream,
+  MXK_LAUNCH_GEMM((mxk_gemm_bf16_tn_w4j<1, EPI>), dim3(nwg), dim3(W4_THREADS), stream,
                      static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b),
                      static_cast<uint16_t*>(c), M, N, K, lda, ldb, ldc);
 }
@@ -394,12 +394,12 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
                 int N, int K, int lda, int ldb, int ldc) {
   switch (v) {
     case 47:
-      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream,
+      MXK_LAUNCH_GEMM((mxk_gemm_bf16_tn_w4k<1, 4>), dim3(nwg), dim3(W4_THREADS), stream,
                          static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
                          static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
       break;
     case 52:
-      hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4k<1, 4, 0, 1>), dim3(nwg), dim3(W4_THREADS), 0, stream,
+      MXK_LAUNCH_GEMM((mxk_gemm_bf16_tn_w4k<1, 4, 0, 1>), dim3(nwg), dim3(W4_THREADS), stream,
                          static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
                          static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
       break;
@@ -489,7 +489,10 @@ MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, v
       static_cast<long>(F + 128) * ldw * 2 >= (1L << 31))
     return static_cast<int>(hipErrorInvalidValue);
   const int nwg = (M / BM) * (F / 128);
-  hipLaunchKernelGGL(mxk_gemm_bf16_w13_swiglu, dim3(nwg), dim3(W4_THREADS), 0, stream,
+  using W13Kernel = void (*)(const uint16_t*, const uint16_t*, uint16_t*, uint16_t*, int, int, int,
+                            int, int, int, int);
+  const W13Kernel w13k = mxk_gemm_bf16_w13_swiglu;   // the kernel, not this host entry point
+  hipLaunchKernelGGL(w13k, dim3(nwg), dim3(W4_THREADS), mxk_excl_lds(reinterpret_cast<const void*>(w13k)), stream,
                      static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
                      static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu,
                      ldh);

@@ -23,6 +23,8 @@
 //   (tests/test_gemm_layouts.py).
 // LDS: 2 stages x (A + B) <= 132 KiB, one 4-wave workgroup per CU, 128x128
 // AGPR accumulators per wave, one barrier per 64-deep stage.
+#include <mutex>
+#include <map>
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -738,19 +740,19 @@ static void launch_x(int sched, bool wide, int nwg, hipStream_t stream, const ui
                      int ldc) {
   // sched: -1 = the one-barrier x kernel, 0 = x2, 1 = x2 at hipBLASLt positions
   if (sched < 0)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x_kernel<AN, BN>), dim3(nwg), dim3(XT), 0, stream, a, b, c,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x_kernel<AN, BN>), dim3(nwg), dim3(XT), stream, a, b, c,
                        M, N, K, lda, ldb, ldc);
   else if (sched == 1 && wide)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 1, 1>), dim3(nwg), dim3(XT), 0, stream, a,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, 1, 1>), dim3(nwg), dim3(XT), stream, a,
                        b, c, M, N, K, lda, ldb, ldc);
   else if (sched == 1)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 1>), dim3(nwg), dim3(XT), 0, stream, a,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 1>), dim3(nwg), dim3(XT), stream, a,
                        b, c, M, N, K, lda, ldb, ldc);
   else if (wide)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 1>), dim3(nwg), dim3(XT), 0, stream, a, b,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, 1>), dim3(nwg), dim3(XT), stream, a, b,
                        c, M, N, K, lda, ldb, ldc);
   else
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 0>), dim3(nwg), dim3(XT), 0, stream, a, b,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, 0>), dim3(nwg), dim3(XT), stream, a, b,
                        c, M, N, K, lda, ldb, ldc);
 }
 
@@ -777,10 +779,10 @@ static void launch_xt(int sched, int nwg, hipStream_t stream, const uint16_t* a,
   const int cus = device_cus();
   const int grid = nwg < cus ? nwg : cus;
   if (sched == 1)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2t_kernel<AN, BN, 1>), dim3(grid), dim3(XT), 0, stream, a, b,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2t_kernel<AN, BN, 1>), dim3(grid), dim3(XT), stream, a, b,
                        c, M, N, K, lda, ldb, ldc);
   else
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2t_kernel<AN, BN, 0>), dim3(grid), dim3(XT), 0, stream, a, b,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2t_kernel<AN, BN, 0>), dim3(grid), dim3(XT), stream, a, b,
                        c, M, N, K, lda, ldb, ldc);
 }
 
@@ -876,17 +878,17 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
   const bool wide = wide_mode != 0 && reinterpret_cast<uintptr_t>(gu) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(dgu) % 16 == 0;
   if (wide && wide_mode == 3)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<false, true, 3, 0>), dim3(nwg), dim3(XT), 0, stream,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 3, 0>), dim3(nwg), dim3(XT), stream,
                        static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
                        static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
                        static_cast<const uint16_t*>(gu));
   else if (wide)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<false, true, 4, 0>), dim3(nwg), dim3(XT), 0, stream,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 4, 0>), dim3(nwg), dim3(XT), stream,
                        static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
                        static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
                        static_cast<const uint16_t*>(gu));
   else
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<false, true, 2, 0>), dim3(nwg), dim3(XT), 0, stream,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 2, 0>), dim3(nwg), dim3(XT), stream,
                        static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
                        static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
                        static_cast<const uint16_t*>(gu));
@@ -927,7 +929,41 @@ int reserved_cus() {
 }
 
 int device_cus() { return std::max(1, hw_cus() - reserved_cus()); }
+
+std::atomic<int> g_exclusive{-1};
+int exclusive() {
+  int e = g_exclusive.load(std::memory_order_relaxed);
+  if (e < 0) {
+    const char* v = std::getenv("MXK_GEMM_EXCLUSIVE");
+    e = v && std::atoi(v) ? 1 : 0;
+    g_exclusive.store(e, std::memory_order_relaxed);
+  }
+  return e;
+}
+std::mutex g_excl_mu;
+std::map<std::pair<int, const void*>, size_t> g_excl;
 }  // namespace
+
+size_t mxk_excl_lds(const void* kernel) {
+  if (!exclusive()) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(g_excl_mu);
+  auto it = g_excl.find({dev, kernel});
+  if (it != g_excl.end()) return it->second;
+  hipFuncAttributes fa{};
+  int max_lds = 0;
+  size_t add = 0;
+  if (hipFuncGetAttributes(&fa, kernel) == hipSuccess &&
+      hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
+      fa.sharedSizeBytes < static_cast<size_t>(max_lds))
+    add = static_cast<size_t>(max_lds) - fa.sharedSizeBytes;
+  g_excl[{dev, kernel}] = add;
+  return add;
+}
+
+MXK_API void mxk_gemm_set_exclusive(int on) { g_exclusive.store(on ? 1 : 0); }
+MXK_API int mxk_gemm_exclusive(void) { return exclusive(); }
 
 MXK_API void mxk_gemm_set_reserved_cus(int n) { g_reserved_cus.store(std::max(0, n)); }
 MXK_API int mxk_gemm_reserved_cus(void) { return reserved_cus(); }
@@ -954,10 +990,10 @@ void launch_split(int sched, bool wide, int nwg, int q_full, hipStream_t stream,
   if (q_full > 0) launch_x<AN, BN>(sched, wide, q_full, stream, a, b, c, M, N, K, lda, ldb, ldc);
   const dim3 grid(2 * (nwg - q_full));
   if (sched == 1)
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 1, true>), grid, dim3(XT), 0, stream, a,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 1, true>), grid, dim3(XT), stream, a,
                        b, c, M, N, K, lda, ldb, ldc, nullptr, ws, q_full);
   else
-    hipLaunchKernelGGL((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 0, true>), grid, dim3(XT), 0, stream, a,
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 0, true>), grid, dim3(XT), stream, a,
                        b, c, M, N, K, lda, ldb, ldc, nullptr, ws, q_full);
   hipLaunchKernelGGL(mxk_gemm_split_fixup, dim3(XBM * XBM / (256 * 8), nwg - q_full), dim3(256), 0,
                      stream, ws, c, M, N, ldc, q_full);

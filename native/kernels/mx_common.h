@@ -8,6 +8,17 @@
 
 #define MXK_API extern "C" __attribute__((visibility("default")))
 
+// Dynamic LDS to add to a one-workgroup-per-CU GEMM launch so that it claims
+// the CU's whole LDS while exclusive mode is on (mxk_gemm_set_exclusive,
+// MXK_GEMM_EXCLUSIVE=1; gemm_bf16_layouts.hip): then no other kernel's
+// workgroup (an RCCL collective's, say) can share a CU with a GEMM tile and
+// slow it; it takes a CU between tiles instead, and the planner sized for
+// the CUs left (mxk_gemm_set_reserved_cus) absorbs that.  0 when off.
+size_t mxk_excl_lds(const void* kernel);
+#define MXK_LAUNCH_GEMM(kern, grid, block, stream, ...)                                         \
+  hipLaunchKernelGGL(kern, grid, block, mxk_excl_lds(reinterpret_cast<const void*>(kern)), stream, \
+                     __VA_ARGS__)
+
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short bf16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));

@@ -13,6 +13,10 @@ stream on CUs [0, k)) runs through every backward of the Llama-3-8B step
   blind     streamer on k CUs, GEMM planner unaware (plans for 256 CUs)
   aware     streamer on k CUs, mxk_gemm_set_reserved_cus(k): rounds and the
             split tail are sized for the 256 - k CUs left
+  excl_*    the same with the GEMMs in exclusive mode (mxk_gemm_set_exclusive:
+            each GEMM workgroup claims its CU's whole LDS, so the streamer's
+            workgroups cannot share a CU with a GEMM tile and slow it; they
+            take whole CUs between tiles instead)
 
 for k in --cus.  The streamer is paced to --gbps (copy traffic, read +
 write; default 700 GB/s, what an 8-rank ring reduce-scatter of the bf16
@@ -202,7 +206,8 @@ def main() -> int:
     ap.add_argument("--micro-batch", type=int, default=8)
     ap.add_argument("--placement", default="spread", help="comma list: spread, xcd, masked")
     ap.add_argument("--map-only", action="store_true", help="print the CU-mask bit map and exit")
-    ap.add_argument("--modes", default="blind,aware", help="comma list: blind, aware")
+    ap.add_argument("--modes", default="blind,aware,excl_blind,excl_aware",
+                    help="comma list: blind, aware, excl_blind, excl_aware")
     ap.add_argument("--base-steps", type=int, default=None,
                     help="steps of the base run (default --steps; its backward time calibrates "
                          "the streamer)")
@@ -258,7 +263,8 @@ def main() -> int:
         st = Streamer(k, dev, placement=placement, cmap=cmap)
         one = st.calibrate(base_bwd, gbps)
         for mode in a.modes.split(","):
-            gemm.set_reserved_cus(k if mode == "aware" else 0)
+            gemm.set_reserved_cus(k if mode.endswith("aware") else 0)
+            gemm.set_exclusive(mode.startswith("excl"))
             ms, bwd = timed(st, f"k{k}.{placement}.{gbps:g}.{mode}")
             ideal = k / 256 * base_bwd / base
             bslow = bwd / base_bwd - 1
@@ -272,6 +278,7 @@ def main() -> int:
                 "streamer_iters": st.iters, "streamer_ms_per_iter_alone": round(one, 3),
                 "available_cus": gemm.available_cus()}), flush=True)
         gemm.set_reserved_cus(0)
+        gemm.set_exclusive(False)
         st.close()
     return 0
 

@@ -122,3 +122,13 @@ def test_stagger_plan_and_parts(T, K, cus):
         assert end == pytest.approx(T / 8 / cx)
         frac = [t % 1.0 for t in stores]
         assert sum(abs(f - 0.5) < 1e-9 for f in frac) >= len(stores) // 2 - 8 * sx
+
+
+def test_set_exclusive_roundtrip():
+    try:
+        gemm.set_exclusive(True)
+        assert gemm.exclusive()
+        gemm.set_exclusive(False)
+        assert not gemm.exclusive()
+    finally:
+        gemm.set_exclusive(False)

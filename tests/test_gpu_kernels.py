@@ -440,3 +440,30 @@ def test_qkv_rope_matches_split_rope(cuda_device):
     dk32 = rope_ref(gk.float(), cos, sin, sign=-1.0)
     want_g = torch.cat([dq32.reshape(B, S, -1), dk32.reshape(B, S, -1), gv.float().reshape(B, S, -1)], -1)
     assert (qkv.grad.float() - want_g).abs().max().item() <= 2 ** -7 * 2.0
+
+
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(1, 1), (1, 0), (0, 0)])
+def test_gemm_exclusive_mode_vs_fp32(cuda_device, a_kmajor, b_kmajor):
+    """Exclusive mode (each GEMM workgroup claims its CU's whole LDS through
+    extra dynamic LDS) leaves the results unchanged: TN, dgrad and wgrad
+    layouts and the fused SwiGLU up-projection."""
+    from mxk8s.ops import gemm, linear
+    M, N, K = 2048, 1024, 512
+    a = _rand((M, K) if a_kmajor else (K, M), cuda_device, 51).bfloat16()
+    b = _rand((N, K) if b_kmajor else (K, N), cuda_device, 52).bfloat16()
+    ref = (a.float() if a_kmajor else a.float().t()) @ (b.float().t() if b_kmajor else b.float())
+    try:
+        gemm.set_exclusive(True)
+        out = torch.empty((M, N), device=cuda_device, dtype=torch.bfloat16)
+        assert gemm.gemm_bf16_ex(a, b, bool(a_kmajor), bool(b_kmajor), out)
+        x = _rand((M, K), cuda_device, 53).bfloat16()
+        w13 = _rand((2 * 512, K), cuda_device, 54).bfloat16()
+        r = linear.w13_swiglu(x, w13)
+        torch.cuda.synchronize()
+    finally:
+        gemm.set_exclusive(False)
+    tol = ref.abs().max().item() * 2 ** -7 + 1e-3
+    assert (out.float() - ref).abs().max().item() <= tol
+    assert r is not None
+    gu_ref = x.float() @ w13.float().t()
+    assert (r[0].float() - gu_ref).abs().max().item() <= gu_ref.abs().max().item() * 2 ** -7 + 1e-3
