@@ -111,6 +111,8 @@
 // loop-exit accumulator copies racing the inline-asm MFMAs; their A/B logs
 // stay in profiles/r1_gemm_*/ (numbered by the old ids: old 34 = 0,
 // 31 = 1, 29 = 2, 30 = 3, 32 = 4, 35 = 5, 36 = 6).
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
 #include "gemm_tn_core.h"
@@ -140,11 +142,15 @@ __device__ __forceinline__ void w13_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
                                             off_k1, dma_a, dma_b, kb2, wave_s, par, a_hi);
 }
 
+// ONEBAR: the K loop of the default TN schedule 52 (gemm_tn_core.h
+// w4k_mainloop: one barrier per K-tile, A in three LDS slots) instead of the
+// three-barrier w4j loop; MXK_W13_SCHED=1 selects it (A/B in the step).
+template <bool ONEBAR>
 __global__ void __launch_bounds__(W4_THREADS, 1)
-mxk_gemm_bf16_w13_swiglu(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W13,
-                         uint16_t* __restrict__ GU, uint16_t* __restrict__ H, int M, int F, int K,
-                         int ldx, int ldw, int ldgu, int ldh) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * W4B_STAGE_BYTES];
+mxk_gemm_bf16_w13_swiglu_k(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W13,
+                           uint16_t* __restrict__ GU, uint16_t* __restrict__ H, int M, int F, int K,
+                           int ldx, int ldw, int ldgu, int ldh) {
+  __shared__ __attribute__((aligned(16))) char smem[ONEBAR ? A3_LDS : 2 * W4B_STAGE_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -174,58 +180,65 @@ mxk_gemm_bf16_w13_swiglu(const uint16_t* __restrict__ X, const uint16_t* __restr
   const int b_base = W4B_OP_BYTES + wn * 8 * SUB;
 
   f32x4_t acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
   const int ns = K / BK;
-#pragma unroll
-  for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_OP_BYTES, p, 0, wave_s);
-  if (ns > 1) {
-#pragma unroll
-    for (int p = 0; p < 8; ++p) dma_a.issue(smem + W4B_STAGE_BYTES, p, BK * 2, wave_s);
-#pragma unroll
-    for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_STAGE_BYTES + W4B_OP_BYTES, p, BK * 2, wave_s);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  if constexpr (ONEBAR) {
+    w4k_mainloop<0, 1, true>(acc, smem, dma_a, dma_b, a_lo, a_hi, wn * 8 * SUB, ns, lane, wave_s);
   } else {
+    f32x4_t acc[8][8];
+  #pragma unroll
+    for (int i = 0; i < 8; ++i)
+  #pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int ns = K / BK;
+  #pragma unroll
+    for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+  #pragma unroll
+    for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_OP_BYTES, p, 0, wave_s);
+    if (ns > 1) {
+  #pragma unroll
+      for (int p = 0; p < 8; ++p) dma_a.issue(smem + W4B_STAGE_BYTES, p, BK * 2, wave_s);
+  #pragma unroll
+      for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_STAGE_BYTES + W4B_OP_BYTES, p, BK * 2, wave_s);
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+
+    bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+  #pragma unroll
+    for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
+  #pragma unroll
+    for (int i = 0; i < 8; ++i)
+      f0a[i] = lds_read_b128(smem + (i < 4 ? a_lo + i * SUB : a_hi + (i - 4) * SUB) + off_k0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+
+    int s = 0;
+    int kb = 2 * BK * 2;
+    for (; s + 2 <= ns - 2; s += 2) {
+      w13_ktile<0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
+                      kb, wave_s);
+      w13_ktile<1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
+                      kb + BK * 2, wave_s);
+      kb += 2 * BK * 2;
+    }
+    if (s < ns - 2) {
+      w13_ktile<0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
+                      kb, wave_s);
+      ++s;
+    }
+    if (ns >= 2) {
+      w13_ktile<2, 2>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
+                      0, wave_s, s & 1);
+      ++s;
+    }
+    w13_ktile<2, 3>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b, 0,
+                    wave_s, s & 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mxk::mfma_drain(acc);
   }
-  __builtin_amdgcn_s_barrier();
 
-  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    f0a[i] = lds_read_b128(smem + (i < 4 ? a_lo + i * SUB : a_hi + (i - 4) * SUB) + off_k0);
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-
-  int s = 0;
-  int kb = 2 * BK * 2;
-  for (; s + 2 <= ns - 2; s += 2) {
-    w13_ktile<0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
-                    kb, wave_s);
-    w13_ktile<1, 1>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
-                    kb + BK * 2, wave_s);
-    kb += 2 * BK * 2;
-  }
-  if (s < ns - 2) {
-    w13_ktile<0, 1>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
-                    kb, wave_s);
-    ++s;
-  }
-  if (ns >= 2) {
-    w13_ktile<2, 2>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b,
-                    0, wave_s, s & 1);
-    ++s;
-  }
-  w13_ktile<2, 3>(acc, f0a, f0b, f1a, f1b, smem, a_lo, a_hi, b_base, off_k0, off_k1, dma_a, dma_b, 0,
-                  wave_s, s & 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  mxk::mfma_drain(acc);
 
   // 1. gu: each wave its half (gate -> columns g0.., up -> F + g0..), its two
   //    64-row passes swapped back for the rotated up waves
@@ -431,6 +444,17 @@ bool variant_built(int v) {
 #endif
 }
 
+// MXK_TN_VARIANT=v: another built schedule as the default (same-box A/B of
+// the training step; the validator times schedules directly)
+int default_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("MXK_TN_VARIANT");
+    const int x = e ? std::atoi(e) : kDefaultVariant;
+    return variant_built(x) && x != kNarrowCVariant ? x : kDefaultVariant;
+  }();
+  return v;
+}
+
 // every schedule but 1 stores 16 B per lane: C 16-B aligned, ldc % 8 == 0
 bool wide_c_ok(const void* C, int ldc) {
   return (ldc % 8 == 0) && (reinterpret_cast<uintptr_t>(C) % 16 == 0);
@@ -467,7 +491,7 @@ MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int 
                     (reinterpret_cast<uintptr_t>(Bt) % 16 == 0) &&
                     (reinterpret_cast<uintptr_t>(C) % 8 == 0);
   if (fast) {
-    launch_256(wide_c_ok(C, ldc) ? kDefaultVariant : kNarrowCVariant, (M / BM) * (N / BN), stream,
+    launch_256(wide_c_ok(C, ldc) ? default_variant() : kNarrowCVariant, (M / BM) * (N / BN), stream,
                A, Bt, C, M, N, K, lda, ldb, ldc);
   } else {
     dim3 grid((N + 63) / 64, (M + 63) / 64);
@@ -480,6 +504,23 @@ MXK_API int mxk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int 
 
 // gu = x . W13^T and h = silu(gu[:, :F]) * gu[:, F:] in one launch (see the
 // kernel).  M % 256, F % 128, K % 64, 16-B aligned operands, ld* % 8.
+namespace {
+std::atomic<int> g_w13_sched{-1};
+int w13_sched() {
+  int v = g_w13_sched.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("MXK_W13_SCHED");
+    v = e ? std::atoi(e) : 0;
+    g_w13_sched.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+}  // namespace
+
+// K loop of the fused up-projection: 0 three-barrier w4j (default), 1 the
+// one-barrier loop of TN schedule 52 (env MXK_W13_SCHED)
+MXK_API void mxk_gemm_w13_set_sched(int v) { g_w13_sched.store(v == 1 ? 1 : 0); }
+
 MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, void* h, int M,
                                      int F, int K, int ldx, int ldw, int ldgu, int ldh,
                                      hipStream_t stream) {
@@ -489,13 +530,14 @@ MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, v
       static_cast<long>(F + 128) * ldw * 2 >= (1L << 31))
     return static_cast<int>(hipErrorInvalidValue);
   const int nwg = (M / BM) * (F / 128);
-  using W13Kernel = void (*)(const uint16_t*, const uint16_t*, uint16_t*, uint16_t*, int, int, int,
-                            int, int, int, int);
-  const W13Kernel w13k = mxk_gemm_bf16_w13_swiglu;   // the kernel, not this host entry point
-  hipLaunchKernelGGL(w13k, dim3(nwg), dim3(W4_THREADS), mxk_excl_lds(reinterpret_cast<const void*>(w13k)), stream,
-                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
-                     static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu,
-                     ldh);
+  if (w13_sched() == 1)
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_w13_swiglu_k<true>), dim3(nwg), dim3(W4_THREADS), stream,
+                    static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
+                    static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu, ldh);
+  else
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_w13_swiglu_k<false>), dim3(nwg), dim3(W4_THREADS), stream,
+                    static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
+                    static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu, ldh);
   MXK_RETURN_LAUNCH_STATUS();
 }
 

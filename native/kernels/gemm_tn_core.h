@@ -499,15 +499,18 @@ constexpr int A3_LDS = 5 * A3_SLOT;            // 160 KiB
 // the barrier, bit 3 the C store (the epilogue's price).
 // ORDER 1: the B fragment is the outer MFMA loop (srcA held for 8 MFMAs,
 // srcB changing - hipBLASLt's operand order) instead of the A fragment.
-template <int AS, int BS, int MODE, class HOOK = NoHook, int ABL = 0, int ORDER = 0>
+// SPLITA: A fragments 0-3 at a_base, 4-7 at a_hi (the w13 SwiGLU kernel).
+template <int AS, int BS, int MODE, class HOOK = NoHook, int ABL = 0, int ORDER = 0,
+          bool SPLITA = false>
 __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                           bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                           bf16x8_t (&f1b)[8], char* smem, int a_base, int b_base,
                                           int off_k0, int off_k1, const DmaK& dma_a,
                                           const DmaK& dma_b, int kb2, int wave_s, int as = 0,
-                                          int bs = 0, const HOOK& hook = HOOK{}) {
+                                          int bs = 0, const HOOK& hook = HOOK{}, int a_hi = 0) {
   using S = SchedA3;
   constexpr int SUB = 2048;
+  auto aoff = [&](int r) { return SPLITA && r >= 4 ? a_hi + (r - 4) * SUB : a_base + r * SUB; };
   const int a_cur = AS >= 0 ? AS : as, b_cur = BS >= 0 ? BS : bs;
   const int a_nxt = a_cur == 2 ? 0 : a_cur + 1;
   const int a_ref = a_cur == 0 ? 2 : a_cur - 1;
@@ -528,7 +531,7 @@ __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
         else mfma_16x16x32_agpr(acc[i][j], f1b[j], f1a[i]);
         hook(m);
         if (!(ABL & 2) && S::a1(m) >= 0)
-          f1a[S::a1(m)] = lds_read_b128(XA + a_base + S::a1(m) * SUB + off_k1);
+          f1a[S::a1(m)] = lds_read_b128(XA + aoff(S::a1(m)) + off_k1);
         if (!(ABL & 2) && S::b1(m) >= 0)
           f1b[S::b1(m)] = lds_read_b128(XB + b_base + S::b1(m) * SUB + off_k1);
         if (!(ABL & 1) && MODE == 1 && S::adma(m) >= 0) dma_a.issue(RA, S::adma(m), kb2, wave_s);
@@ -544,43 +547,33 @@ __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
         if (!(ABL & 2) && MODE != 3 && S::k0(m) >= 0) {
           const int r = S::k0(m);
           if (r < 8) f0b[r] = lds_read_b128(YB + b_base + r * SUB + off_k0);
-          else f0a[r - 8] = lds_read_b128(YA + a_base + (r - 8) * SUB + off_k0);
+          else f0a[r - 8] = lds_read_b128(YA + aoff(r - 8) + off_k0);
         }
       }
     }
   }
 }
 
-template <int MAP, int EPI, int ABL = 0, int ORDER = 0>
-__global__ void __launch_bounds__(W4_THREADS, 1)
-mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
-                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
-  __shared__ __attribute__((aligned(16))) char smem[A3_LDS];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave_s >> 1;
-  const int wn = wave_s & 1;
-  int m0, n0;
-  w4b_tile<MAP>(blockIdx.x, gridDim.x, M / BM, N / BN, &m0, &n0);
-  const DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
-  const DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
-
+// The one-barrier K loop over ns K-tiles into acc (zeroed here): prologue DMA
+// of stages 0 and 1, the K-tiles unrolled by the 6-K-tile slot cycle, the two
+// DMA-free tail K-tiles, the MFMA drain.  smem: A3_LDS bytes; b_base relative
+// to a B slot.
+template <int ABL = 0, int ORDER = 0, bool SPLITA = false>
+__device__ __forceinline__ void w4k_mainloop(f32x4_t (&acc)[8][8], char* smem, const DmaK& dma_a,
+                                             const DmaK& dma_b, int a_base, int a_hi, int b_base,
+                                             int ns, int lane, int wave_s) {
   const int frow = lane & 15;
   const int fch = (lane >> 4) ^ ((frow >> 1) & 7);
   const int off_k0 = frow * 128 + fch * 16;
   const int off_k1 = frow * 128 + (fch ^ 4) * 16;
   constexpr int SUB = 2048;
-  const int a_base = wm * 8 * SUB;
-  const int b_base = wn * 8 * SUB;
+  auto aoff = [&](int r) { return SPLITA && r >= 4 ? a_hi + (r - 4) * SUB : a_base + r * SUB; };
 
-  f32x4_t acc[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int ns = K / BK;
   // stages 0 and 1: A slots 0, 1 and B slots 0, 1
 #pragma unroll
   for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
@@ -601,15 +594,16 @@ mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 #pragma unroll
   for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + A3_B0 + b_base + j * SUB + off_k0);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + a_base + i * SUB + off_k0);
+  for (int i = 0; i < 8; ++i) f0a[i] = lds_read_b128(smem + aoff(i) + off_k0);
   __builtin_amdgcn_s_waitcnt(0xC07F);
 
   // K-tiles 0 .. ns-3 carry the DMA of stage s+2 (k offset (s+2)*128 B)
   int s = 0;
   int kb = 2 * BK * 2;
 #define MXK_W4K(as_, bs_)                                                                       \
-  w4k_ktile<as_, bs_, 1, NoHook, ABL, ORDER>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0,     \
-                                      off_k1, dma_a, dma_b, kb, wave_s);                        \
+  w4k_ktile<as_, bs_, 1, NoHook, ABL, ORDER, SPLITA>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, \
+                                                     off_k0, off_k1, dma_a, dma_b, kb, wave_s, 0, 0, \
+                                                     NoHook{}, a_hi);                            \
   kb += BK * 2;
   for (; s + 6 <= ns - 2; s += 6) {
     MXK_W4K(0, 0) MXK_W4K(1, 1) MXK_W4K(2, 0) MXK_W4K(0, 1) MXK_W4K(1, 0) MXK_W4K(2, 1)
@@ -625,14 +619,36 @@ mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   s += r > 0 ? r : 0;
   // the last two K-tiles (or the only one): no DMA, runtime slots
   if (ns >= 2) {
-    w4k_ktile<-1, -1, 2, NoHook, 0, ORDER>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a,
-                         dma_b, 0, wave_s, s % 3, s & 1);
+    w4k_ktile<-1, -1, 2, NoHook, 0, ORDER, SPLITA>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base,
+                                                   off_k0, off_k1, dma_a, dma_b, 0, wave_s, s % 3,
+                                                   s & 1, NoHook{}, a_hi);
     ++s;
   }
-  w4k_ktile<-1, -1, 3, NoHook, 0, ORDER>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base, off_k0, off_k1, dma_a, dma_b,
-                       0, wave_s, s % 3, s & 1);
+  w4k_ktile<-1, -1, 3, NoHook, 0, ORDER, SPLITA>(acc, f0a, f0b, f1a, f1b, smem, a_base, b_base,
+                                                 off_k0, off_k1, dma_a, dma_b, 0, wave_s, s % 3,
+                                                 s & 1, NoHook{}, a_hi);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   mxk::mfma_drain(acc);
+}
+
+template <int MAP, int EPI, int ABL = 0, int ORDER = 0>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[A3_LDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
+  int m0, n0;
+  w4b_tile<MAP>(blockIdx.x, gridDim.x, M / BM, N / BN, &m0, &n0);
+  const DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
+  const DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
+  constexpr int SUB = 2048;
+  f32x4_t acc[8][8];
+  w4k_mainloop<ABL, ORDER>(acc, smem, dma_a, dma_b, wm * 8 * SUB, 0, wn * 8 * SUB, K / BK, lane,
+                           wave_s);
 
   if constexpr (ABL & 8) {
     return;

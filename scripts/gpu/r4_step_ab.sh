@@ -1,0 +1,19 @@
+# Same-box A/B of the Llama-3-8B step (bench.py --mode ddp): TN default 52 vs
+# the round-3 default 26 (MXK_TN_VARIANT) and the w13 SwiGLU kernel on the
+# one-barrier loop (MXK_W13_SCHED=1), interleaved twice.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+O=gpurun_out/r4step; mkdir -p $O
+export PYTHONPATH=.
+run() {  # name env...
+  local n=$1; shift
+  timeout -k 10 240 env "$@" python3 bench.py --mode ddp --steps 8 --warmup 3 > $O/$n.out 2> $O/$n.err || return $?
+  python3 -c "
+import json,sys
+for l in open('$O/$n.out'):
+    if l.startswith('{'):
+        d=json.loads(l); print('$n', d['value'], d['ms_per_step'])"
+}
+for r in 1 2; do
+  run base$r MXK_NOP=1 && run tn26_$r MXK_TN_VARIANT=26 && run w13one_$r MXK_W13_SCHED=1 || exit $?
+done

@@ -13,14 +13,23 @@ def dev():
     return torch.device("cuda", 0)
 
 
+@pytest.mark.parametrize("sched", [0, 1])
 @pytest.mark.parametrize("M,F,K", [(256, 128, 64), (512, 384, 256), (2048, 1792, 1024),
-                                   (16384, 14336, 4096)])
-def test_w13_swiglu_vs_fp32(dev, M, F, K):
+                                   (512, 256, 448), (16384, 14336, 4096)])
+def test_w13_swiglu_vs_fp32(dev, M, F, K, sched):
+    """Both K loops (0: three-barrier w4j, 1: the one-barrier loop of TN
+    schedule 52, whose 6-K-tile slot cycle K = 448 leaves at a remainder)."""
+    from mxk8s.ops import _lib
     from mxk8s.ops.linear import w13_swiglu
     g = torch.Generator(device=dev).manual_seed(M + F + K)
     x = (torch.randn((M, K), device=dev, generator=g) * 0.5).bfloat16()
     w = (torch.randn((2 * F, K), device=dev, generator=g) * K ** -0.5).bfloat16()
-    r = w13_swiglu(x, w)
+    try:
+        _lib.lib().mxk_gemm_w13_set_sched(sched)
+        r = w13_swiglu(x, w)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().mxk_gemm_w13_set_sched(0)
     assert r is not None, "fused kernel did not take the shape"
     gu, h = r
     ref = x.float() @ w.float().t()

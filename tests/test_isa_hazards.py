@@ -126,14 +126,16 @@ def test_epilogue_spills_stay_out_of_the_dma_loop(kernel, tmp_path):
     vector-memory op the loop's vmcnt counts do not expect).  The tail
     K-tiles after the loop wait with vmcnt(0), which also covers a spill."""
     asm = _asm("gemm_bf16.hip", str(tmp_path / "g.s"))
-    name = re.search(r"^(_Z\S*mxk_gemm_bf16_%s\S*):" % kernel, asm, re.M).group(1)
-    body = asm[asm.index(name + ":"):]
-    body = body[:body.index("s_endpgm")]
-    lines = body.split("\n")
-    heads = [i for i, l in enumerate(lines) if "Inner Loop Header" in l]
-    assert heads, "no K loop found"
-    for h in heads:
-        label = lines[h].split(":")[0]
-        end = next(i for i in range(h + 1, len(lines))
-                   if "s_cbranch" in lines[i] and lines[i].rstrip().endswith(label))
-        assert not [l for l in lines[h:end + 1] if "scratch_" in l], label
+    names = re.findall(r"^(_Z\S*mxk_gemm_bf16_%s\S*):" % kernel, asm, re.M)
+    assert names
+    for name in names:
+        body = asm[asm.index(name + ":"):]
+        body = body[:body.index("s_endpgm")]
+        lines = body.split("\n")
+        heads = [i for i, l in enumerate(lines) if "Inner Loop Header" in l]
+        assert heads, "no K loop found"
+        for h in heads:
+            label = lines[h].split(":")[0]
+            end = next(i for i in range(h + 1, len(lines))
+                       if "s_cbranch" in lines[i] and lines[i].rstrip().endswith(label))
+            assert not [l for l in lines[h:end + 1] if "scratch_" in l], (name, label)
