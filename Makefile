@@ -21,7 +21,7 @@ OUT_LIB   := mxk8s/_lib
 OUT_BIN   := bin
 BUILD     := build
 
-HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wshadow -Wno-unused-function \
              -Inative/kernels
 CXXFLAGS  := -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -Inative/libmxnode -I$(ROCM)/include
 LDLIBS_NODE := -ldl -lpthread

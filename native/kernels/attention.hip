@@ -493,20 +493,20 @@ mxk_attn_fwd_dma_kernel(const uint16_t* __restrict__ q, const uint16_t* __restri
 #pragma unroll
   for (int db = 0; db < 4; ++db) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int g0 = 2 * k, g1 = 2 * k + 1;
+    for (int kk = 0; kk < 2; ++kk) {
+      const int g0 = 2 * kk, g1 = 2 * kk + 1;
       const uint32_t x0 = mxk::pack2bf(acc[db][4 * g0] * inv, acc[db][4 * g0 + 1] * inv);
       const uint32_t x1 = mxk::pack2bf(acc[db][4 * g0 + 2] * inv, acc[db][4 * g0 + 3] * inv);
       const uint32_t y0 = mxk::pack2bf(acc[db][4 * g1] * inv, acc[db][4 * g1 + 1] * inv);
       const uint32_t y1 = mxk::pack2bf(acc[db][4 * g1 + 2] * inv, acc[db][4 * g1 + 3] * inv);
       const auto p0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
       const auto p1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
-      uint4 v;
-      v.x = p0[0];
-      v.y = p1[0];
-      v.z = p0[1];
-      v.w = p1[1];
-      *reinterpret_cast<uint4*>(orow + 32 * db + 16 * k + 8 * h) = v;
+      uint4 ov;
+      ov.x = p0[0];
+      ov.y = p1[0];
+      ov.z = p0[1];
+      ov.w = p1[1];
+      *reinterpret_cast<uint4*>(orow + 32 * db + 16 * kk + 8 * h) = ov;
     }
   }
   if (h == 0) lse[(static_cast<long>(b) * Hq + hq) * S + myq] = m * scale + logf(lt);
@@ -1056,20 +1056,20 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
 #pragma unroll
   for (int db = 0; db < 4; ++db) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int g0 = 2 * k, g1 = 2 * k + 1;
+    for (int kk = 0; kk < 2; ++kk) {
+      const int g0 = 2 * kk, g1 = 2 * kk + 1;
       const uint32_t x0 = mxk::pack2bf(acc[db][4 * g0] * scale, acc[db][4 * g0 + 1] * scale);
       const uint32_t x1 = mxk::pack2bf(acc[db][4 * g0 + 2] * scale, acc[db][4 * g0 + 3] * scale);
       const uint32_t y0 = mxk::pack2bf(acc[db][4 * g1] * scale, acc[db][4 * g1 + 1] * scale);
       const uint32_t y1 = mxk::pack2bf(acc[db][4 * g1 + 2] * scale, acc[db][4 * g1 + 3] * scale);
       const auto p0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
       const auto p1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
-      uint4 v;
-      v.x = p0[0];
-      v.y = p1[0];
-      v.z = p0[1];
-      v.w = p1[1];
-      *reinterpret_cast<uint4*>(row + 32 * db + 16 * k + 8 * h) = v;
+      uint4 ov;
+      ov.x = p0[0];
+      ov.y = p1[0];
+      ov.z = p0[1];
+      ov.w = p1[1];
+      *reinterpret_cast<uint4*>(row + 32 * db + 16 * kk + 8 * h) = ov;
     }
   }
 }

@@ -128,10 +128,10 @@ mxk_rmsnorm_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restri
         o[e] = rs * (a[e] * g[e] - b[e] * rs * rs * mean_gx);
       }
       if (dres) {   // fused residual: gradient flowing around the norm
-        float r[8];
-        load8(dres + off + c, r);
+        float rv[8];
+        load8(dres + off + c, rv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] += r[e];
+        for (int e = 0; e < 8; ++e) o[e] += rv[e];
       }
       store8(dx + off + c, o);
 #pragma unroll

@@ -184,21 +184,18 @@ mxk_gemm_bf16_w13_swiglu_k(const uint16_t* __restrict__ X, const uint16_t* __res
   if constexpr (ONEBAR) {
     w4k_mainloop<0, 1, true>(acc, smem, dma_a, dma_b, a_lo, a_hi, wn * 8 * SUB, ns, lane, wave_s);
   } else {
-    f32x4_t acc[8][8];
-  #pragma unroll
+#pragma unroll
     for (int i = 0; i < 8; ++i)
-  #pragma unroll
+#pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-    const int ns = K / BK;
-  #pragma unroll
+#pragma unroll
     for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
-  #pragma unroll
+#pragma unroll
     for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_OP_BYTES, p, 0, wave_s);
     if (ns > 1) {
-  #pragma unroll
+#pragma unroll
       for (int p = 0; p < 8; ++p) dma_a.issue(smem + W4B_STAGE_BYTES, p, BK * 2, wave_s);
-  #pragma unroll
+#pragma unroll
       for (int p = 0; p < 8; ++p) dma_b.issue(smem + W4B_STAGE_BYTES + W4B_OP_BYTES, p, BK * 2, wave_s);
       asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     } else {
@@ -207,9 +204,9 @@ mxk_gemm_bf16_w13_swiglu_k(const uint16_t* __restrict__ X, const uint16_t* __res
     __builtin_amdgcn_s_barrier();
 
     bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
-  #pragma unroll
+#pragma unroll
     for (int j = 0; j < 8; ++j) f0b[j] = lds_read_b128(smem + b_base + j * SUB + off_k0);
-  #pragma unroll
+#pragma unroll
     for (int i = 0; i < 8; ++i)
       f0a[i] = lds_read_b128(smem + (i < 4 ? a_lo + i * SUB : a_hi + (i - 4) * SUB) + off_k0);
     __builtin_amdgcn_s_waitcnt(0xC07F);

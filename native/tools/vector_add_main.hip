@@ -166,7 +166,7 @@ int main(int argc, char** argv) {
     if (hipDeviceGetPCIBusId(bus, sizeof(bus), d) == hipSuccess) bdfs.insert(norm_bdf(bus));
   }
   std::set<std::string> want_bdfs;
-  for (const auto& b : split_csv(std::getenv("AMD_GPU_BDFS"))) want_bdfs.insert(norm_bdf(b));
+  for (const auto& bdf : split_csv(std::getenv("AMD_GPU_BDFS"))) want_bdfs.insert(norm_bdf(bdf));
   const auto nodes = render_nodes();
   std::set<std::string> want_nodes;
   for (const auto& r : split_csv(std::getenv("AMD_GPU_RENDER_NODES"))) want_nodes.insert(r);
