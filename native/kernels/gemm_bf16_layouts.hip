@@ -442,6 +442,25 @@ __device__ __forceinline__ void x2_ktile_s(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)
 // C.  A separate kernel (not a branch of the whole-tile one): with both
 // epilogues in one body the allocator spilled accumulators, and a spill
 // store of an AGPR right behind its inline-asm MFMA reads a stale value.
+// EPI 4 (SwiGLU backward): pass 0's g / u rows of each wave by LDS-DMA into
+// the stage the last K-tile does not read, issued right after the second-to-
+// last K-tile's stage barrier (m 96; that stage is free everywhere by then):
+// 16 pieces per wave (8 of g, 8 of u), each 4 rows x 256 B, one per MFMA from
+// m 97.  The epilogue's vmcnt(0) + barrier covers them.
+struct GuPrefetch : mxk::NoHook {
+  mxk::u32x4 rsrc;
+  uint32_t voff;     // this lane's (row, column) of piece 0, bytes
+  uint32_t rowstep;  // 4 rows, bytes
+  uint32_t fbytes;   // F columns (g -> u), bytes
+  uint32_t lds;      // LDS address of this wave's 16 KiB
+  __device__ __forceinline__ void operator()(int m) const {
+    if (m >= 97 && m < 113) {
+      const int q = m - 97, u = q >> 3, i = q & 7;
+      mxk::dma16m(rsrc, lds + u * 8192 + i * 1024, voff + i * rowstep + u * fbytes, 0);
+    }
+  }
+};
+
 template <bool AN, bool BN, int EPI, int SCHED = 0, bool SPLIT = false>
 __global__ void __launch_bounds__(XT, 1)
 mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
@@ -450,7 +469,12 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
                         int q_full = 0) {
   constexpr int A_BYTES = XOp<AN>::BYTES;
   constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  // EPI 4: 1 KiB more, so the epilogue's acc slices (4 x kSwigluLdsWave from
+  // the last K-tile's stage) and the g / u prefetch (64 KiB at the other
+  // stage + 1 KiB) never overlap, whichever stage is which
+  static_assert(EPI != 4 || (4 * mxk::kSwigluLdsWave <= STAGE + 1024 && 65536 + 1024 <= STAGE),
+                "EPI 4 LDS plan");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (EPI == 4 ? 1024 : 0)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -517,7 +541,22 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     ++s;
   }
   if (ns >= 2) {
-    x2_ktile_s<SCHED, AN, BN, 2, 2>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
+    if constexpr (EPI == 4 && SCHED == 0 && !SPLIT) {
+      // stage s & 1 is read by this K-tile; the last one reads the other
+      GuPrefetch pf;
+      pf.rsrc = mxk::make_rsrc(aux, 0xFFFFFFF0u);
+      const int rr = lane >> 4, cc = (lane & 15) * 8;
+      pf.voff = static_cast<uint32_t>(
+          (static_cast<long>(m0 + wm * 128 + rr) * ldc + n0 + wn * 128 + cc) * 2);
+      pf.rowstep = static_cast<uint32_t>(4L * ldc * 2);
+      pf.fbytes = static_cast<uint32_t>(N * 2);
+      pf.lds = mxk::lds_addr32(smem) + (s & 1) * STAGE + 1024 + wave * 16384;
+      x2_ktile<AN, BN, 2, 2, -1, GuPrefetch>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0,
+                                              wave, s & 1, pf);
+    } else {
+      x2_ktile_s<SCHED, AN, BN, 2, 2>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave,
+                                      s & 1);
+    }
     ++s;
   }
   x2_ktile_s<SCHED, AN, BN, 2, 3>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave, s & 1);
@@ -542,8 +581,14 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     // every wave's last-stage fragment reads retired before any slice is written
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
-    mxk::swiglu_bwd_block_lds(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane,
-                              smem + wave * mxk::kSwigluLdsWave);
+    // acc slices in the stage the last K-tile read (s & 1); the g / u rows of
+    // pass 0 were prefetched into the other one (ns >= 2)
+    // (the launcher takes EPI 4 only for K >= 2 * XBK, so that K-tile ran)
+    char* last = smem + (s & 1) * STAGE;
+    const char* gul = smem + ((s & 1) ^ 1) * STAGE + 1024 + wave * 16384;
+    mxk::swiglu_bwd_block_lds<SCHED == 0 && !SPLIT>(acc, aux, C, ldc, N, m0 + wm * 128,
+                                                    n0 + wn * 128, lane,
+                                                    last + wave * mxk::kSwigluLdsWave, gul);
   }
   else if constexpr (EPI == 1) {
     // whole-line stores through LDS (as the TN kernel's default schedule);
@@ -876,7 +921,7 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
     return e ? std::atoi(e) : 4;
   }();
   const bool wide = wide_mode != 0 && reinterpret_cast<uintptr_t>(gu) % 16 == 0 &&
-                    reinterpret_cast<uintptr_t>(dgu) % 16 == 0;
+                    reinterpret_cast<uintptr_t>(dgu) % 16 == 0 && K >= 2 * XBK;
   if (wide && wide_mode == 3)
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 3, 0>), dim3(nwg), dim3(XT), stream,
                        static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),

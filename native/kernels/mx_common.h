@@ -491,10 +491,14 @@ __device__ __forceinline__ void swiglu_bwd_block_wide(const f32x4_t (&acc)[8][8]
 // ds_write_b128 group land 4 banks apart).
 constexpr int kSwigluLdsRow = 528;
 constexpr int kSwigluLdsWave = 32 * kSwigluLdsRow;
+// gu_lds (optional): this wave's pass-0 g / u rows already in LDS (32 rows x
+// 256 B of g, then 32 x 256 B of u; the layout GEMM DMAs them during its last
+// K-tiles, x2 EPI 4), so pass 0 does not wait for HBM after the K loop.
+template <bool PF = false>
 __device__ __forceinline__ void swiglu_bwd_block_lds(const f32x4_t (&acc)[8][8],
                                                      const uint16_t* gu, uint16_t* dgu, long ld,
                                                      int F, int row0, int col0, int lane,
-                                                     char* lds) {
+                                                     char* lds, const char* gu_lds = nullptr) {
   typedef float f2_t __attribute__((ext_vector_type(2)));
   const int crow = lane & 15, q = lane >> 4;
   const int rr = lane >> 4, cc = (lane & 15) * 8;   // read phase: row rr of 4, 8 columns
@@ -507,7 +511,16 @@ __device__ __forceinline__ void swiglu_bwd_block_lds(const f32x4_t (&acc)[8][8],
       uw[b][it] = *reinterpret_cast<const uint4*>(gu + off + F);
     }
   };
-  load(0, 0);
+  if constexpr (PF) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const char* gp = gu_lds + (it * 4 + rr) * 256 + cc * 2;
+      gw[0][it] = *reinterpret_cast<const uint4*>(gp);
+      uw[0][it] = *reinterpret_cast<const uint4*>(gp + 8192);
+    }
+  } else {
+    load(0, 0);
+  }
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int b = p & 1;
