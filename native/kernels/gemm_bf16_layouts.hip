@@ -576,6 +576,13 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     mxk::swiglu_bwd_block(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane);
   else if constexpr (EPI == 3)
     mxk::swiglu_bwd_block_wide(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane);
+  else if constexpr (EPI == 5) {
+    // EPI 4 without the g / u prefetch (A/B: MXK_SWIGLU_WIDE=5)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    mxk::swiglu_bwd_block_lds(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane,
+                              smem + wave * mxk::kSwigluLdsWave);
+  }
   else if constexpr (EPI == 4) {
     static_assert(4 * mxk::kSwigluLdsWave <= 2 * STAGE, "LDS slice per wave");
     // every wave's last-stage fragment reads retired before any slice is written
@@ -914,15 +921,22 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
                   reinterpret_cast<uintptr_t>(dgu) % 8 == 0;
   if (!ok) return static_cast<int>(hipErrorInvalidValue);
   const int nwg = (M / XBM) * (F / XBM);
-  // 16-B g/u accesses: EPI 4 (LDS-staged, whole lines) by default, EPI 3
-  // (permlane pairs) with MXK_SWIGLU_WIDE=3, the 8-B form with =0 (A/B)
+  // 16-B g/u accesses: EPI 4 (LDS-staged, whole lines, pass 0's g/u
+  // prefetched during the last K-tiles) by default, EPI 5 (the same without
+  // the prefetch) with MXK_SWIGLU_WIDE=5, EPI 3 (permlane pairs) with =3, the
+  // 8-B form with =0 (A/B)
   static const int wide_mode = [] {
     const char* e = std::getenv("MXK_SWIGLU_WIDE");
     return e ? std::atoi(e) : 4;
   }();
   const bool wide = wide_mode != 0 && reinterpret_cast<uintptr_t>(gu) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(dgu) % 16 == 0 && K >= 2 * XBK;
-  if (wide && wide_mode == 3)
+  if (wide && wide_mode == 5)
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 5, 0>), dim3(nwg), dim3(XT), stream,
+                    static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
+                    static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
+                    static_cast<const uint16_t*>(gu));
+  else if (wide && wide_mode == 3)
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 3, 0>), dim3(nwg), dim3(XT), stream,
                        static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
                        static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
