@@ -666,13 +666,18 @@ mxk_attn_bwd_delta_kernel(const uint16_t* __restrict__ o, const uint16_t* __rest
 // kernel's piece mapping, destinations bound to M0) instead of register
 // staging - frees the 32 staging VGPRs that made this kernel spill at two
 // waves per SIMD, and the ds_writes.  Requires S * token_stride * 2 < 2^32.
-template <bool CAUSAL, bool DMA = false, bool PIPE = false, bool UNROLL = false>
+// FOLD (backward variant 5): the delta pass folded in - each query row's
+// delta = dO . O is computed here from the row's own dO fragments and O (the
+// two lanes of a row hold 64 columns each) and written to delta_w for the
+// dK/dV kernel, which then runs after this one; no separate delta kernel.
+template <bool CAUSAL, bool DMA = false, bool PIPE = false, bool UNROLL = false, bool FOLD = false>
 __global__ void __launch_bounds__(NT, 2)
 mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                        const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
                        const float* __restrict__ lse, const float* __restrict__ delta,
                        uint16_t* __restrict__ dq, int S, int Hq, int Hkv, long q_tok, long k_tok,
-                       long v_tok, float scale) {
+                       long v_tok, float scale, const uint16_t* __restrict__ o = nullptr,
+                       float* __restrict__ delta_w = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[2][2 * TILE_BYTES];   // [buf][K | V]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -703,7 +708,23 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   const float c = scale * 1.4426950408889634f;
   const long lrow = (static_cast<long>(b) * Hq + hq) * S + myq;
   const float lse2 = lse[lrow] * 1.4426950408889634f;
-  const float dlt = delta[lrow];
+  float dlt;
+  if constexpr (FOLD) {
+    const uint16_t* ob_ptr = o + static_cast<long>(b) * S * Hq * D + static_cast<long>(hq) * D;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const bf16x8_t of = *reinterpret_cast<const bf16x8_t*>(ob_ptr + static_cast<long>(myq) * Hq * D +
+                                                              16 * s + 8 * h);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        part += mxk::bf2f(static_cast<uint16_t>(dof[s][e])) * mxk::bf2f(static_cast<uint16_t>(of[e]));
+    }
+    dlt = part + __shfl_xor(part, 32);       // the row's other 64 columns
+    if (h == 0) delta_w[lrow] = dlt;
+  } else {
+    dlt = delta[lrow];
+  }
 
   const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
   const int nkv = kv_end / BKV;
@@ -1704,7 +1725,7 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
                                  long q_tok, long k_tok, long v_tok, long dk_tok, long dv_tok,
                                  float scale, int causal, int variant, hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv || q_tok % 8 ||
-      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 4 ||
+      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 5 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
        reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
@@ -1721,9 +1742,24 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
   const auto* dO = static_cast<const uint16_t*>(dout);
   auto* dK = static_cast<uint16_t*>(dk);
   auto* dV = static_cast<uint16_t*>(dv);
-  hipLaunchKernelGGL(mxk_attn_bwd_delta_kernel, dim3((rows * 16 + 255) / 256), dim3(256), 0,
-                     stream, static_cast<const uint16_t*>(o), dO, delta, S, Hq, rows);
   const int nwg = B * Hq * (S / BQ);
+  const long span0 = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
+  if (variant == 5 && span0 < (1L << 32)) {
+    // delta folded into the dQ kernel, which therefore runs first
+    auto* dQ5 = static_cast<uint16_t*>(dq);
+    const auto* O5 = static_cast<const uint16_t*>(o);
+    if (causal)
+      hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<true, true, true, false, true>), dim3(nwg), dim3(NT),
+                         0, stream, Q, K, V, dO, lse, delta, dQ5, S, Hq, Hkv, q_tok, k_tok, v_tok,
+                         scale, O5, delta);
+    else
+      hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<false, true, true, false, true>), dim3(nwg),
+                         dim3(NT), 0, stream, Q, K, V, dO, lse, delta, dQ5, S, Hq, Hkv, q_tok, k_tok,
+                         v_tok, scale, O5, delta);
+  } else {
+    hipLaunchKernelGGL(mxk_attn_bwd_delta_kernel, dim3((rows * 16 + 255) / 256), dim3(256), 0,
+                       stream, static_cast<const uint16_t*>(o), dO, delta, S, Hq, rows);
+  }
   const int nwg_kv = B * Hkv * (S / BQ);
   const long qspan = static_cast<long>(S) * (q_tok > static_cast<long>(Hq) * D ? q_tok : Hq * D) * 2;
   if (variant >= 3 && causal && qspan < (1L << 32)) {
@@ -1763,7 +1799,9 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
   const long span = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
   const bool dq_dma = variant >= 2 && span < (1L << 32);
   auto* dQ = static_cast<uint16_t*>(dq);
-  if (causal && dq_dma && variant == 4)
+  if (variant == 5 && dq_dma) {
+    // dQ already done (with delta) above
+  } else if (causal && dq_dma && variant == 4)
     hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<true, true, true, true>), dim3(nwg), dim3(NT), 0,
                        stream, Q, K, V, dO, lse, delta, dQ, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
   else if (causal && dq_dma && variant == 3)

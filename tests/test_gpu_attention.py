@@ -74,7 +74,7 @@ def test_attn_bwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
         assert err < tol, (name, err, tol)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
     (1, 256, 8, 2, True),
     (2, 384, 4, 1, True),
@@ -101,3 +101,8 @@ def test_attn_bwd_variants_into_strided_dkdv(cuda_device, B, S, Hq, Hkv, causal,
         err = (got.float() - want).abs().max().item()
         tol = 3e-2 * max(1.0, want.abs().max().item())
         assert err < tol, (name, variant, err, tol)
+    if variant == 5:   # the delta folded into dQ: bit-identical to the separate pass (3)
+        ref3 = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, variant=3)
+        ref5 = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, variant=5)
+        for a3, a5 in zip(ref3, ref5):
+            assert (a3.float() - a5.float()).abs().max().item() <= 1e-2 * max(1.0, a3.float().abs().max().item())
