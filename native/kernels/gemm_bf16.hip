@@ -145,7 +145,9 @@ __device__ __forceinline__ void w13_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
 // ONEBAR: the K loop of the default TN schedule 52 (gemm_tn_core.h
 // w4k_mainloop: one barrier per K-tile, A in three LDS slots) instead of the
 // three-barrier w4j loop; MXK_W13_SCHED=1 selects it (A/B in the step).
-template <bool ONEBAR>
+// GUNT: gu (read again only by the backward, a step later) stored
+// non-temporally so it does not displace the A/B panels; MXK_W13_SCHED=2.
+template <bool ONEBAR, bool GUNT = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_w13_swiglu_k(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W13,
                            uint16_t* __restrict__ GU, uint16_t* __restrict__ H, int M, int F, int K,
@@ -241,7 +243,7 @@ mxk_gemm_bf16_w13_swiglu_k(const uint16_t* __restrict__ X, const uint16_t* __res
   //    64-row passes swapped back for the rotated up waves
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
-  mxk::store_block_lds<false>(acc, GU, ldgu, m0 + wm * 128, (wn ? F : 0) + g0, lane,
+  mxk::store_block_lds<GUNT>(acc, GU, ldgu, m0 + wm * 128, (wn ? F : 0) + g0, lane,
                               smem + wave_s * mxk::kStoreLdsWave, wn);
   __builtin_amdgcn_s_barrier();            // every staging slice is free again
   // 2. hand acc[4..7] to the partner (gate: g of rows 64-127, up: u of rows
@@ -515,8 +517,9 @@ int w13_sched() {
 }  // namespace
 
 // K loop of the fused up-projection: 0 three-barrier w4j (default), 1 the
-// one-barrier loop of TN schedule 52 (env MXK_W13_SCHED)
-MXK_API void mxk_gemm_w13_set_sched(int v) { g_w13_sched.store(v == 1 ? 1 : 0); }
+// one-barrier loop of TN schedule 52, 2 = 0 with non-temporal gu stores
+// (env MXK_W13_SCHED)
+MXK_API void mxk_gemm_w13_set_sched(int v) { g_w13_sched.store(v == 1 || v == 2 ? v : 0); }
 
 MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, void* h, int M,
                                      int F, int K, int ldx, int ldw, int ldgu, int ldh,
@@ -527,7 +530,11 @@ MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, v
       static_cast<long>(F + 128) * ldw * 2 >= (1L << 31))
     return static_cast<int>(hipErrorInvalidValue);
   const int nwg = (M / BM) * (F / 128);
-  if (w13_sched() == 1)
+  if (w13_sched() == 2)
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_w13_swiglu_k<false, true>), dim3(nwg), dim3(W4_THREADS), stream,
+                    static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
+                    static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu, ldh);
+  else if (w13_sched() == 1)
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_w13_swiglu_k<true>), dim3(nwg), dim3(W4_THREADS), stream,
                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
                     static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu, ldh);

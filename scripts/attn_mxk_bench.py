@@ -42,6 +42,7 @@ def main():
     res["mxk_fwd"] = bench(lambda: A.attn_fwd(q, k, v, causal=True))
     res["mxk_fwd_v0"] = bench(lambda: A.attn_fwd(q, k, v, causal=True, variant=0))
     res["mxk_fwd_v2"] = bench(lambda: A.attn_fwd(q, k, v, causal=True, variant=2))
+    res["mxk_fwd_v4"] = bench(lambda: A.attn_fwd(q, k, v, causal=True, variant=4))
     qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
     with torch.no_grad():
         res["sdpa_fwd"] = bench(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=True,
@@ -60,10 +61,11 @@ def main():
     res["sdpa_fwd_bwd"] = bench(sdpa_fb)
     res["mxk_fwd_bwd"] = res["mxk_fwd"] + res["mxk_bwd"]
     # useful FLOPs: fwd 2 products, bwd 5 products (causal halves all)
-    mult = {"mxk_fwd": 1.0, "mxk_fwd_v0": 1.0, "mxk_fwd_v2": 1.0, "sdpa_fwd": 1.0, "mxk_bwd": 2.5, "sdpa_fwd_bwd": 3.5, "mxk_fwd_bwd": 3.5}
+    def mult(name):
+        return 3.5 if name.endswith("fwd_bwd") else 2.5 if "_bwd" in name else 1.0
     for name, ms in res.items():
-        print("RESULT " + json.dumps({"kernel": name, "ms": round(ms, 4), "S": S,
-                                      "tflops": round(mult[name] * flops_fwd / ms / 1e9, 1)}),
+        print("RESULT " + json.dumps({"kernel": name, "ms": round(ms, 4), "S": S, "B": B,
+                                      "tflops": round(mult(name) * flops_fwd / ms / 1e9, 1)}),
               flush=True)
 
 

@@ -16,5 +16,5 @@ for l in open('$O/$n.out'):
         d=json.loads(l); print('$n', d['value'], d['ms_per_step'])"
 }
 for r in 1 2; do
-  run base$r MXK_NOP=1 && run tn26_$r MXK_TN_VARIANT=26 && run w13one_$r MXK_W13_SCHED=1 && run swnopf_$r MXK_SWIGLU_WIDE=5 || exit $?
+  run base$r MXK_NOP=1 && run tn26_$r MXK_TN_VARIANT=26 && run w13one_$r MXK_W13_SCHED=1 && run swnopf_$r MXK_SWIGLU_WIDE=5 && run w13nt_$r MXK_W13_SCHED=2 || exit $?
 done

@@ -13,7 +13,7 @@ def dev():
     return torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("sched", [0, 1])
+@pytest.mark.parametrize("sched", [0, 1, 2])
 @pytest.mark.parametrize("M,F,K", [(256, 128, 64), (512, 384, 256), (2048, 1792, 1024),
                                    (512, 256, 448), (16384, 14336, 4096)])
 def test_w13_swiglu_vs_fp32(dev, M, F, K, sched):
