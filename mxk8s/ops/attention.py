@@ -76,7 +76,7 @@ def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None, variant: 
     return o, lse
 
 
-_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "3"))
+_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "5"))
 
 
 def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = None,
@@ -85,7 +85,10 @@ def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = N
 
     ``dk``/``dv`` may be preallocated views (e.g. slices of a fused dQKV
     buffer) with a token stride; by default they are fresh contiguous tensors.
-    ``variant`` 3 (default): variant 2 with explicitly software-pipelined
+    ``variant`` 5 (default): variant 3 with the delta pass (dO . O per query
+    row) folded into the dQ kernel, which then runs before dK/dV: no separate
+    delta kernel, 1.042 vs 1.064 ms per Llama-3-8B layer at B 8
+    (profiles/r4_final/attention_b8.log).  3: variant 2 with explicitly software-pipelined
     dK/dV and dQ bodies (LDS operands read a group ahead instead of one
     lgkmcnt(0) per MFMA), bit-identical to 2 and 15 % faster (1.070 vs 1.262
     ms per Llama-3-8B layer at B 8: profiles/r2_attention/); 2: dK/dV
