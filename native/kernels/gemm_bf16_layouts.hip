@@ -472,9 +472,11 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
   // EPI 4: 1 KiB more, so the epilogue's acc slices (4 x kSwigluLdsWave from
   // the last K-tile's stage) and the g / u prefetch (64 KiB at the other
   // stage + 1 KiB) never overlap, whichever stage is which
-  static_assert(EPI != 4 || (4 * mxk::kSwigluLdsWave <= STAGE + 1024 && 65536 + 1024 <= STAGE),
+  // EPI 6: EPI 4 with the SwiGLU math removed (timing ablation, wrong values)
+  constexpr bool PFEPI = EPI == 4 || EPI == 6;
+  static_assert(!PFEPI || (4 * mxk::kSwigluLdsWave <= STAGE + 1024 && 65536 + 1024 <= STAGE),
                 "EPI 4 LDS plan");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (EPI == 4 ? 1024 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (PFEPI ? 1024 : 0)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -541,7 +543,7 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     ++s;
   }
   if (ns >= 2) {
-    if constexpr (EPI == 4 && SCHED == 0 && !SPLIT) {
+    if constexpr (PFEPI && SCHED == 0 && !SPLIT) {
       // stage s & 1 is read by this K-tile; the last one reads the other
       GuPrefetch pf;
       pf.rsrc = mxk::make_rsrc(aux, 0xFFFFFFF0u);
@@ -583,7 +585,7 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     mxk::swiglu_bwd_block_lds(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128, lane,
                               smem + wave * mxk::kSwigluLdsWave);
   }
-  else if constexpr (EPI == 4) {
+  else if constexpr (PFEPI) {
     static_assert(4 * mxk::kSwigluLdsWave <= 2 * STAGE, "LDS slice per wave");
     // every wave's last-stage fragment reads retired before any slice is written
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -593,7 +595,7 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     // (the launcher takes EPI 4 only for K >= 2 * XBK, so that K-tile ran)
     char* last = smem + (s & 1) * STAGE;
     const char* gul = smem + ((s & 1) ^ 1) * STAGE + 1024 + wave * 16384;
-    mxk::swiglu_bwd_block_lds<SCHED == 0 && !SPLIT>(acc, aux, C, ldc, N, m0 + wm * 128,
+    mxk::swiglu_bwd_block_lds<SCHED == 0 && !SPLIT, EPI == 6>(acc, aux, C, ldc, N, m0 + wm * 128,
                                                     n0 + wn * 128, lane,
                                                     last + wave * mxk::kSwigluLdsWave, gul);
   }
@@ -905,6 +907,22 @@ MXK_API int mxk_gemm_bf16_ex_variant(const void* A, const void* B, void* C, int 
   MXK_RETURN_LAUNCH_STATUS();
 }
 
+namespace {
+std::atomic<int> g_swiglu_epi{-1};
+int swiglu_epi() {
+  int v = g_swiglu_epi.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("MXK_SWIGLU_WIDE");
+    v = e ? std::atoi(e) : 4;
+    g_swiglu_epi.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+}  // namespace
+
+// dgrad-SwiGLU epilogue mode (MXK_SWIGLU_WIDE; see mxk_gemm_bf16_dgrad_swiglu)
+MXK_API void mxk_gemm_swiglu_set_epi(int v) { g_swiglu_epi.store(v); }
+
 // Down-projection input gradient with the SwiGLU backward fused into the
 // epilogue: d(act) = dy W2 (dy [M][K] K-major, W2 [K][F] F-major) never
 // reaches memory; dgu [M][2F] = d[g | u] is written from gu [M][2F].
@@ -924,14 +942,16 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
   // 16-B g/u accesses: EPI 4 (LDS-staged, whole lines, pass 0's g/u
   // prefetched during the last K-tiles) by default, EPI 5 (the same without
   // the prefetch) with MXK_SWIGLU_WIDE=5, EPI 3 (permlane pairs) with =3, the
-  // 8-B form with =0 (A/B)
-  static const int wide_mode = [] {
-    const char* e = std::getenv("MXK_SWIGLU_WIDE");
-    return e ? std::atoi(e) : 4;
-  }();
+  // 8-B form with =0 (A/B); 6 = EPI 4 without the SwiGLU math (timing only)
+  const int wide_mode = swiglu_epi();
   const bool wide = wide_mode != 0 && reinterpret_cast<uintptr_t>(gu) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(dgu) % 16 == 0 && K >= 2 * XBK;
-  if (wide && wide_mode == 5)
+  if (wide && wide_mode == 6)
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 6, 0>), dim3(nwg), dim3(XT), stream,
+                    static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
+                    static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
+                    static_cast<const uint16_t*>(gu));
+  else if (wide && wide_mode == 5)
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 5, 0>), dim3(nwg), dim3(XT), stream,
                     static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
                     static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,

@@ -494,7 +494,9 @@ constexpr int kSwigluLdsWave = 32 * kSwigluLdsRow;
 // gu_lds (optional): this wave's pass-0 g / u rows already in LDS (32 rows x
 // 256 B of g, then 32 x 256 B of u; the layout GEMM DMAs them during its last
 // K-tiles, x2 EPI 4), so pass 0 does not wait for HBM after the K loop.
-template <bool PF = false>
+// NOMATH (timing ablation, wrong values): dg = d u, du = d g - the same
+// memory traffic without the sigmoid's exp / rcp and its products.
+template <bool PF = false, bool NOMATH = false>
 __device__ __forceinline__ void swiglu_bwd_block_lds(const f32x4_t (&acc)[8][8],
                                                      const uint16_t* gu, uint16_t* dgu, long ld,
                                                      int F, int row0, int col0, int lane,
@@ -547,12 +549,18 @@ __device__ __forceinline__ void swiglu_bwd_block_lds(const f32x4_t (&acc)[8][8],
         const f2_t g = {__uint_as_float(gp[h] << 16), __uint_as_float(gp[h] & 0xFFFF0000u)};
         const f2_t u = {__uint_as_float(up[h] << 16), __uint_as_float(up[h] & 0xFFFF0000u)};
         const f2_t dd = {d[2 * h], d[2 * h + 1]};
-        const f2_t x = g * -1.44269504f;
-        const f2_t sg = {__builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[0])),
-                         __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[1]))};
-        const f2_t t = dd * sg;
-        const f2_t du = t * g;
-        const f2_t dg = t * u * ((g + 1.f) - g * sg);
+        f2_t dg, du;
+        if constexpr (NOMATH) {
+          dg = dd * u;
+          du = dd * g;
+        } else {
+          const f2_t x = g * -1.44269504f;
+          const f2_t sg = {__builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[0])),
+                           __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[1]))};
+          const f2_t t = dd * sg;
+          du = t * g;
+          dg = t * u * ((g + 1.f) - g * sg);
+        }
         pg[h] = pack2bf(dg[0], dg[1]);
         pu[h] = pack2bf(du[0], du[1]);
       }
