@@ -34,6 +34,7 @@ _SIGNATURES = {
     "mxk_gemm_set_exclusive": (None, [_i]),
     "mxk_gemm_w13_set_sched": (None, [_i]),
     "mxk_gemm_swiglu_set_epi": (None, [_i]),
+    "mxk_gemm_x2_set_order": (None, [_i]),
     "mxk_gemm_exclusive": (_i, []),
     "mxk_gemm_reserved_cus": (_i, []),
     "mxk_gemm_available_cus": (_i, []),

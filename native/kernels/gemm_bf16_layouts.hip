@@ -308,7 +308,8 @@ mxk_gemm_bf16_x_kernel(const uint16_t* __restrict__ A, const uint16_t* __restric
 // ---------------------------------------------------------------------------
 // VMX >= 0 replaces the stage wait's vmcnt (the trickle kernel's C stores
 // sit among the DMA pieces); HOOK(m) runs after MFMA m.
-template <bool AN, bool BN, int PAR, int MODE, int VMX = -1, class HOOK = mxk::NoHook>
+template <bool AN, bool BN, int PAR, int MODE, int VMX = -1, class HOOK = mxk::NoHook,
+          int ORDER = 0>
 __device__ __forceinline__ void x2_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                          bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                          bf16x8_t (&f1b)[8], char* smem, const XOp<AN>& oa,
@@ -324,10 +325,12 @@ __device__ __forceinline__ void x2_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int o = 0; o < 8; ++o) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = h * 64 + i * 8 + j;
+      for (int q = 0; q < 8; ++q) {
+        const int m = h * 64 + o * 8 + q;
+        // ORDER 0: A fragment outer; 1: B outer (srcA held for 8 MFMAs)
+        const int i = ORDER ? q : o, j = ORDER ? o : q;
         if (h == 0) xmfma(acc[i][j], f0b[j], f0a[i]);
         else xmfma(acc[i][j], f1b[j], f1a[i]);
         hook(m);
@@ -363,7 +366,8 @@ __device__ __forceinline__ void x2_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8
 
 // SCHED 1: the same K-tile at hipBLASLt's instruction positions
 // (mxk::SchedHB; a "read" is one operand fragment as above).
-template <class S, bool AN, bool BN, int PAR, int MODE, int VMX = -1, class HOOK = mxk::NoHook>
+template <class S, bool AN, bool BN, int PAR, int MODE, int VMX = -1, class HOOK = mxk::NoHook,
+          int ORDER = 0>
 __device__ __forceinline__ void x2_ktile_tab(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[8],
                                              bf16x8_t (&f0b)[8], bf16x8_t (&f1a)[8],
                                              bf16x8_t (&f1b)[8], char* smem, const XOp<AN>& oa,
@@ -378,10 +382,12 @@ __device__ __forceinline__ void x2_ktile_tab(f32x4_t (&acc)[8][8], bf16x8_t (&f0
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int o = 0; o < 8; ++o) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = h * 64 + i * 8 + j;
+      for (int q = 0; q < 8; ++q) {
+        const int m = h * 64 + o * 8 + q;
+        // ORDER 0: A fragment outer; 1: B outer (srcA held for 8 MFMAs)
+        const int i = ORDER ? q : o, j = ORDER ? o : q;
         if (h == 0) xmfma(acc[i][j], f0b[j], f0a[i]);
         else xmfma(acc[i][j], f1b[j], f1a[i]);
         hook(m);
@@ -420,12 +426,14 @@ __device__ __forceinline__ void x2_ktile_s(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)
                                            const XOp<BN>& ob, int wm, int wn, uint32_t soa,
                                            uint32_t sob, int wave, int par = 0,
                                            const HOOK& hook = HOOK{}) {
-  if constexpr (SCHED == 1)
-    x2_ktile_tab<mxk::SchedHB, AN, BN, PAR, MODE, (VMD ? mxk::SchedHB::VM3 + VMD : -1), HOOK>(
-        acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, soa, sob, wave, par, hook);
+  // SCHED bit 0: hipBLASLt's positions (x2_ktile_tab); bit 1: B-outer MFMA order
+  if constexpr ((SCHED & 1) == 1)
+    x2_ktile_tab<mxk::SchedHB, AN, BN, PAR, MODE, (VMD ? mxk::SchedHB::VM3 + VMD : -1), HOOK,
+                 (SCHED >> 1) & 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, soa, sob, wave,
+                                   par, hook);
   else
-    x2_ktile<AN, BN, PAR, MODE, (VMD ? 15 + VMD : -1), HOOK>(acc, f0a, f0b, f1a, f1b, smem, oa, ob,
-                                                           wm, wn, soa, sob, wave, par, hook);
+    x2_ktile<AN, BN, PAR, MODE, (VMD ? 15 + VMD : -1), HOOK, (SCHED >> 1) & 1>(
+        acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, soa, sob, wave, par, hook);
 }
 
 // EPI 0: 8-B stores, 1: 16-B stores through LDS (whole lines), 2: SwiGLU backward, 3: SwiGLU
@@ -543,7 +551,7 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     ++s;
   }
   if (ns >= 2) {
-    if constexpr (PFEPI && SCHED == 0 && !SPLIT) {
+    if constexpr (PFEPI && (SCHED & 1) == 0 && !SPLIT) {
       // stage s & 1 is read by this K-tile; the last one reads the other
       GuPrefetch pf;
       pf.rsrc = mxk::make_rsrc(aux, 0xFFFFFFF0u);
@@ -553,7 +561,8 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
       pf.rowstep = static_cast<uint32_t>(4L * ldc * 2);
       pf.fbytes = static_cast<uint32_t>(N * 2);
       pf.lds = mxk::lds_addr32(smem) + (s & 1) * STAGE + 1024 + wave * 16384;
-      x2_ktile<AN, BN, 2, 2, -1, GuPrefetch>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0,
+      x2_ktile<AN, BN, 2, 2, -1, GuPrefetch, (SCHED >> 1) & 1>(acc, f0a, f0b, f1a, f1b, smem, oa, ob,
+                                                               wm, wn, 0, 0,
                                               wave, s & 1, pf);
     } else {
       x2_ktile_s<SCHED, AN, BN, 2, 2>(acc, f0a, f0b, f1a, f1b, smem, oa, ob, wm, wn, 0, 0, wave,
@@ -595,7 +604,7 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     // (the launcher takes EPI 4 only for K >= 2 * XBK, so that K-tile ran)
     char* last = smem + (s & 1) * STAGE;
     const char* gul = smem + ((s & 1) ^ 1) * STAGE + 1024 + wave * 16384;
-    mxk::swiglu_bwd_block_lds<SCHED == 0 && !SPLIT, EPI == 6>(acc, aux, C, ldc, N, m0 + wm * 128,
+    mxk::swiglu_bwd_block_lds<(SCHED & 1) == 0 && !SPLIT, EPI == 6>(acc, aux, C, ldc, N, m0 + wm * 128,
                                                     n0 + wn * 128, lane,
                                                     last + wave * mxk::kSwigluLdsWave, gul);
   }
@@ -788,26 +797,45 @@ mxk_gemm_split_fixup(const float* __restrict__ ws, uint16_t* __restrict__ C, int
   *reinterpret_cast<uint2*>(cp + 4) = hi;
 }
 
+namespace {
+std::atomic<int> g_x2_order{-1};
+int x2_order() {
+  int v = g_x2_order.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("MXK_X2_ORDER");
+    v = e && std::atoi(e) == 1 ? 1 : 0;
+    g_x2_order.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+}  // namespace
+
+// MFMA order of the layout kernel's K-tile: 0 A-fragment outer (default), 1
+// B-fragment outer (env MXK_X2_ORDER)
+MXK_API void mxk_gemm_x2_set_order(int v) { g_x2_order.store(v == 1 ? 1 : 0); }
+
 template <bool AN, bool BN>
 static void launch_x(int sched, bool wide, int nwg, hipStream_t stream, const uint16_t* a,
                      const uint16_t* b, uint16_t* c, int M, int N, int K, int lda, int ldb,
                      int ldc) {
-  // sched: -1 = the one-barrier x kernel, 0 = x2, 1 = x2 at hipBLASLt positions
-  if (sched < 0)
+  // sched: -1 = the one-barrier x kernel, 0 = x2, 1 = x2 at hipBLASLt positions;
+  // x2_order() adds bit 1 (B-outer MFMA order, MXK_X2_ORDER=1)
+  if (sched < 0) {
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_x_kernel<AN, BN>), dim3(nwg), dim3(XT), stream, a, b, c,
-                       M, N, K, lda, ldb, ldc);
-  else if (sched == 1 && wide)
-    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, 1, 1>), dim3(nwg), dim3(XT), stream, a,
-                       b, c, M, N, K, lda, ldb, ldc);
-  else if (sched == 1)
-    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, 0, 1>), dim3(nwg), dim3(XT), stream, a,
-                       b, c, M, N, K, lda, ldb, ldc);
-  else if (wide)
-    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, 1>), dim3(nwg), dim3(XT), stream, a, b,
-                       c, M, N, K, lda, ldb, ldc);
-  else
-    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, 0>), dim3(nwg), dim3(XT), stream, a, b,
-                       c, M, N, K, lda, ldb, ldc);
+                    M, N, K, lda, ldb, ldc);
+    return;
+  }
+  switch ((sched | (x2_order() ? 2 : 0)) * 2 + (wide ? 1 : 0)) {
+#define MXK_X2_CASE(S, W)                                                                        \
+  case S * 2 + W:                                                                                \
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<AN, BN, W, S>), dim3(nwg), dim3(XT), stream, a, b, c, \
+                    M, N, K, lda, ldb, ldc);                                                     \
+    break;
+    MXK_X2_CASE(0, 0) MXK_X2_CASE(0, 1) MXK_X2_CASE(1, 0) MXK_X2_CASE(1, 1)
+    MXK_X2_CASE(2, 0) MXK_X2_CASE(2, 1) MXK_X2_CASE(3, 0) MXK_X2_CASE(3, 1)
+#undef MXK_X2_CASE
+    default: break;
+  }
 }
 
 // 1 if layout-kernel variant v is in this build (4, x2t: experiments only)
@@ -961,6 +989,11 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
                        static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
                        static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
                        static_cast<const uint16_t*>(gu));
+  else if (wide && x2_order())
+    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 4, 2>), dim3(nwg), dim3(XT), stream,
+                    static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
+                    static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
+                    static_cast<const uint16_t*>(gu));
   else if (wide)
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 4, 0>), dim3(nwg), dim3(XT), stream,
                        static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),

@@ -1,7 +1,9 @@
 # Same-box A/B of the Llama-3-8B step (bench.py --mode ddp): TN default 52 vs
 # the round-3 default 26 (MXK_TN_VARIANT) and the w13 SwiGLU kernel on the
 # one-barrier loop (MXK_W13_SCHED=1) and the dgrad-SwiGLU epilogue without its
-# g/u prefetch (MXK_SWIGLU_WIDE=5), interleaved twice.
+# g/u prefetch (MXK_SWIGLU_WIDE=5), interleaved twice.  Second set: layout
+# kernel B-outer order (MXK_X2_ORDER=1), w13 non-temporal gu stores
+# (MXK_W13_SCHED=2), attention backward variant 3 (MXK_ATTN_BWD_VARIANT=3).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 O=gpurun_out/r4step; mkdir -p $O
@@ -16,5 +18,5 @@ for l in open('$O/$n.out'):
         d=json.loads(l); print('$n', d['value'], d['ms_per_step'])"
 }
 for r in 1 2; do
-  run base$r MXK_NOP=1 && run tn26_$r MXK_TN_VARIANT=26 && run w13one_$r MXK_W13_SCHED=1 && run swnopf_$r MXK_SWIGLU_WIDE=5 && run w13nt_$r MXK_W13_SCHED=2 || exit $?
+  run base$r MXK_NOP=1 && run x2ord_$r MXK_X2_ORDER=1 && run w13nt_$r MXK_W13_SCHED=2 && run bwd3_$r MXK_ATTN_BWD_VARIANT=3 || exit $?
 done

@@ -471,3 +471,38 @@ def test_gemm_exclusive_mode_vs_fp32(cuda_device, a_kmajor, b_kmajor):
     assert r is not None
     gu_ref = x.float() @ w13.float().t()
     assert (r[0].float() - gu_ref).abs().max().item() <= gu_ref.abs().max().item() * 2 ** -7 + 1e-3
+
+
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(1, 0), (0, 0), (0, 1)])
+def test_gemm_layouts_b_outer_order_vs_fp32(cuda_device, a_kmajor, b_kmajor):
+    """The layout kernel's K-tile with the B fragment as the outer MFMA loop
+    (mxk_gemm_x2_set_order(1), MXK_X2_ORDER=1) against fp32, and the fused
+    dgrad-SwiGLU GEMM under the same order against the default order."""
+    from mxk8s.ops import _lib, gemm
+    L = _lib.lib()
+    M, N, K = 2048, 1024, 1088
+    a = _rand((M, K) if a_kmajor else (K, M), cuda_device, 61).bfloat16()
+    b = _rand((N, K) if b_kmajor else (K, N), cuda_device, 62).bfloat16()
+    ref = (a.float() if a_kmajor else a.float().t()) @ (b.float().t() if b_kmajor else b.float())
+    T, F, KD = 1024, 512, 1024
+    dy = _rand((T, KD), cuda_device, 63).bfloat16()
+    w2 = _rand((KD, F), cuda_device, 64, 0.05).bfloat16()
+    gu = _rand((T, 2 * F), cuda_device, 65, 3.0).bfloat16()
+    outs = []
+    try:
+        for order in (1, 0):
+            L.mxk_gemm_x2_set_order(order)
+            out = torch.empty((M, N), device=cuda_device, dtype=torch.bfloat16)
+            assert gemm.gemm_bf16_ex(a, b, bool(a_kmajor), bool(b_kmajor), out)
+            dgu = torch.empty_like(gu)
+            _lib.check(L.mxk_gemm_bf16_dgrad_swiglu(dy.data_ptr(), w2.data_ptr(), gu.data_ptr(),
+                                                    dgu.data_ptr(), T, F, KD, KD, F,
+                                                    _lib.stream_ptr(cuda_device)), "dgrad_swiglu")
+            torch.cuda.synchronize()
+            outs.append((out, dgu))
+    finally:
+        L.mxk_gemm_x2_set_order(0)
+    tol = ref.abs().max().item() * 2 ** -7 + 1e-3
+    assert (outs[0][0].float() - ref).abs().max().item() <= tol
+    d1, d0 = outs[0][1].float(), outs[1][1].float()
+    assert (d1 - d0).abs().max().item() <= 2 ** -7 * d0.abs().max().item() + 1e-3
