@@ -41,6 +41,7 @@ _SIGNATURES = {
     "mxk_gemm_split_plan": (_i, [_l, _i, _i, ctypes.POINTER(ctypes.c_long)]),
     "mxk_gemm_stagger_plan": (_i, [_l, _i, _i]),
     "mxk_gemm_stagger_part": (None, [_i, _i, _i, ctypes.POINTER(ctypes.c_int)]),
+    "mxk_gemm_stagger_part_xcd": (None, [_i, _i, _i, ctypes.POINTER(ctypes.c_int)]),
     "mxk_stream_create_cu_masked": (_i, [_i, _i, _i, ctypes.POINTER(ctypes.c_void_p)]),
     "mxk_stream_create_cu_masked_groups": (_i, [_i, _i, _i, ctypes.POINTER(ctypes.c_void_p)]),
     "mxk_stream_destroy": (_i, [_vp]),

@@ -189,3 +189,19 @@ def stagger_part(b: int, T: int, sx: int) -> tuple[int, int, int]:
     if i < tx:
         return x + 8 * (i - sx), 0, -1
     return x + 8 * (f + i - tx), 2, x * sx + (i - tx)
+
+
+def stagger_part_xcd(b: int, T: int, cx: int) -> tuple[int, int, int]:
+    """(virtual tile, part, slot) of workgroup ``b`` in the XCD-group stagger
+    (schedule 57): XCDs 0-3 whole tiles, XCDs 4-7 start with cx first K halves
+    and end with their second halves; part -1: an idle workgroup.  Mirrors
+    ``stagger_part_xcd`` (gemm_tn_core.h)."""
+    x, i = b & 7, b >> 3
+    tx = T >> 3
+    if x < 4:
+        return (x + 8 * i, 0, -1) if i < tx else (x, -1, -1)
+    if i < cx:
+        return x + 8 * i, 1, (x - 4) * cx + i
+    if i < tx:
+        return x + 8 * i, 0, -1
+    return x + 8 * (i - tx), 2, (x - 4) * cx + (i - tx)

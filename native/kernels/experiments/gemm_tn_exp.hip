@@ -925,6 +925,21 @@ const StagWs* stag_ws(hipStream_t stream, int slots, bool uncached) {
   return &w;
 }
 
+void launch_stag_xcd(int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b, uint16_t* c,
+                     int M, int N, int K, int lda, int ldb, int ldc) {
+  const int cx = mxk_gemm_available_cus() / 8;
+  const long tx = nwg / 8;
+  const bool ok = nwg % 8 == 0 && cx > 0 && tx >= 2 * cx && K % (2 * BK) == 0 && K >= 4 * BK;
+  const StagWs* w = ok ? stag_ws(stream, 4 * cx, true) : nullptr;
+  if (!w) {
+    hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j<1, 4>), dim3(nwg), dim3(W4_THREADS), 0, stream, a, b, c,
+                       M, N, K, lda, ldb, ldc);
+    return;
+  }
+  hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j_stag<1, 4, 1>), dim3(nwg + 8 * cx), dim3(W4_THREADS), 0,
+                     stream, a, b, c, M, N, K, lda, ldb, ldc, w->ws, w->flags, cx);
+}
+
 void launch_stag(bool uncached, int nwg, hipStream_t stream, const uint16_t* a, const uint16_t* b,
                  uint16_t* c, int M, int N, int K, int lda, int ldb, int ldc) {
   const int sx = mxk_gemm_stagger_plan(nwg, K, mxk_gemm_available_cus());
@@ -966,6 +981,7 @@ int mxk_gemm_tn_exp_launch(int v, int nwg, hipStream_t stream, const void* A, co
       hipLaunchKernelGGL((mxk_gemm_bf16_tn_w4j<1, 4, true>), dim3(nwg), dim3(W4_THREADS), 0, stream, a,
                          b, c, M, N, K, lda, ldb, ldc);
       break;
+    case 57: launch_stag_xcd(nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 54:
     case 55: launch_stag(v == 54, nwg, stream, a, b, c, M, N, K, lda, ldb, ldc); break;
     case 53:

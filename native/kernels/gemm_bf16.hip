@@ -99,6 +99,8 @@
 //           half a tile apart; 54 exchanges the fp32 partials through
 //           uncached memory (-8 % at 8192^3, profiles/r4_gemm/), 55 through
 //           plain memory (same-XCD L2; A/B of the uncached traffic)
+//  57 w4j   staggered by XCD group (stagger_part_xcd): XCDs 4-7 half a tile
+//           out of phase with XCDs 0-3, every CU of an XCD in phase
 //  56 w4j   26 with an L2 prefetch of stage s+4 per K-tile (gemm_tn_core.h
 //           L2Prefetch; for HBM-cold operands): -1.5..-3 % warm, -1.7 % cold
 //           (profiles/r4_gemm/cold_vs_warm_prefetch56.txt)
@@ -372,8 +374,15 @@ MXK_API void mxk_gemm_stagger_part(int b, int T, int sx, int* out) {
   out[2] = p.slot;
 }
 
+MXK_API void mxk_gemm_stagger_part_xcd(int b, int T, int cx, int* out) {
+  const StaggerPart p = stagger_part_xcd(b, T, cx);
+  out[0] = p.vtile;
+  out[1] = p.part;
+  out[2] = p.slot;
+}
+
 namespace {
-constexpr int kNumVariants = 57;
+constexpr int kNumVariants = 58;
 constexpr int kDefaultVariant = 52;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -385,7 +394,7 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
     "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps", "w4i_ldsst_full_template",
     "w4k_1bar_a3_ldsst", "diag_w4k_nodma", "diag_w4k_noreads", "diag_w4k_nowait",
-    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore", "w4j_stagger", "w4j_stagger_cached", "w4j_l2pf"};
+    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore", "w4j_stagger", "w4j_stagger_cached", "w4j_l2pf", "w4j_stagger_xcd"};
 
 }  // namespace
 #ifdef MXK_GEMM_EXPERIMENTS

@@ -396,6 +396,37 @@ __host__ __device__ inline StaggerPart stagger_part(int b, int T, int sx) {
   return r;
 }
 
+// XCD-group stagger (schedule 57): the PMC of the per-CU stagger above shows
+// +43 % fetch beyond L2 at 8192^3 - half of an XCD's CUs half a tile out of
+// phase no longer read each panel slice together, so the XCD's L2 stops
+// sharing it.  Here whole XCDs are out of phase instead: XCDs 0-3 run whole
+// tiles, XCDs 4-7 start with the first K halves of their first cx tiles (one
+// per CU) and end with the second halves.  Inside an XCD every CU stays in
+// phase (L2 reuse kept); XCDs 0-3 and 4-7 share no A panel of the super-block
+// (rows x >> 2) and their shared B panels are half a tile apart (MALL hits);
+// the C-store bursts of the two halves of the chip alternate.  Workgroup b on
+// XCD x = b & 7, local index i = b >> 3, tx = T / 8, grid 8 (tx + cx):
+//   x < 4:  i < tx whole tile i; i >= tx nothing (part -1)
+//   x >= 4: i < cx first half of tile i (slot (x - 4) cx + i); cx <= i < tx
+//           whole tile i; tx <= i second half of tile i - tx
+__host__ __device__ inline StaggerPart stagger_part_xcd(int b, int T, int cx) {
+  const int x = b & 7, i = b >> 3;
+  const int tx = T >> 3;
+  StaggerPart r;
+  r.slot = -1;
+  if (x < 4) {
+    r.part = i < tx ? 0 : -1;
+    r.vtile = x + 8 * (i < tx ? i : 0);
+  } else if (i < cx) {
+    r.part = 1; r.slot = (x - 4) * cx + i; r.vtile = x + 8 * i;
+  } else if (i < tx) {
+    r.part = 0; r.vtile = x + 8 * i;
+  } else {
+    r.part = 2; r.slot = (x - 4) * cx + (i - tx); r.vtile = x + 8 * (i - tx);
+  }
+  return r;
+}
+
 // fp32 partial of one tile in accumulator order: wave w's acc[i][j] of lane l
 // at float4 index ((w * 64 + i * 8 + j) * 64 + l) of the slot (256 KiB)
 __device__ __forceinline__ void partial_store(const f32x4_t (&acc)[8][8], float* ws, int slot,
@@ -407,7 +438,9 @@ __device__ __forceinline__ void partial_store(const f32x4_t (&acc)[8][8], float*
     for (int j = 0; j < 8; ++j) p[(i * 8 + j) * 64] = acc[i][j];
 }
 
-template <int MAP, int EPI>
+// STYLE 0: stagger_part (per CU, sx split tiles per XCD); 1: stagger_part_xcd
+// (sx = CUs per XCD).
+template <int MAP, int EPI, int STYLE = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4j_stag(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                           uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc,
@@ -416,7 +449,8 @@ mxk_gemm_bf16_tn_w4j_stag(const uint16_t* __restrict__ A, const uint16_t* __rest
   const int lane = threadIdx.x & 63;
   const int wave_s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int T = (M / BM) * (N / BN);
-  const StaggerPart sp = stagger_part(blockIdx.x, T, sx);
+  const StaggerPart sp = STYLE ? stagger_part_xcd(blockIdx.x, T, sx) : stagger_part(blockIdx.x, T, sx);
+  if (sp.part < 0) return;
   int m0, n0;
   w4b_tile<MAP>(sp.vtile, T, M / BM, N / BN, &m0, &n0);
   const int ns = sp.part ? (K / BK) >> 1 : K / BK;

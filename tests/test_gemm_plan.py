@@ -132,3 +132,49 @@ def test_set_exclusive_roundtrip():
         assert not gemm.exclusive()
     finally:
         gemm.set_exclusive(False)
+
+
+@pytest.mark.parametrize("T,cus", [(1024, 256), (4096, 256), (64 * 56, 256), (1024, 192)])
+def test_stagger_by_xcd_parts(T, cus):
+    """Schedule 57: every tile once (whole, or two halves on one XCD of 4-7,
+    producer dispatched first); XCDs 0-3 and 4-7 finish together and store
+    half a tile apart."""
+    cx = cus // 8
+    out = (ctypes.c_int * 3)()
+    seen = {}
+    for b in range(T + 8 * cx):
+        p = gemm.stagger_part_xcd(b, T, cx)
+        _lib.lib().mxk_gemm_stagger_part_xcd(b, T, cx, out)
+        assert tuple(out) == p
+        v, part, slot = p
+        if part < 0:
+            assert b & 7 < 4
+            continue
+        assert v % 8 == b % 8
+        seen.setdefault(v, []).append((part, b, slot))
+    assert set(seen) == set(range(T))
+    for v, ps in seen.items():
+        kinds = sorted(p for p, _, _ in ps)
+        assert kinds in ([0], [1, 2])
+        if kinds == [1, 2]:
+            (p1, b1, s1), (p2, b2, s2) = sorted(ps)
+            assert v % 8 >= 4 and s1 == s2 and b1 < b2 and b1 % 8 == b2 % 8
+    # dispatch simulation (unit tile time): both XCD groups end at T / 8 / cx,
+    # and group 4-7 stores half a tile out of phase with group 0-3
+    import heapq
+    free = [[0.0] * cx for _ in range(8)]
+    ends = {0: [], 1: []}
+    for b in range(T + 8 * cx):
+        v, part, _ = gemm.stagger_part_xcd(b, T, cx)
+        if part < 0:
+            continue
+        q = free[b & 7]
+        t0 = heapq.heappop(q)
+        t1 = t0 + (1.0 if part == 0 else 0.5)
+        heapq.heappush(q, t1)
+        if part != 1:
+            ends[(b & 7) >= 4].append(t1)
+    if (T // 8) % cx == 0:
+        assert max(ends[0]) == pytest.approx(T / 8 / cx) == max(ends[1])
+        assert all(abs(t % 1.0) < 1e-9 for t in ends[0])
+        assert sum(abs(t % 1.0 - 0.5) < 1e-9 for t in ends[1]) >= len(ends[1]) - 2 * 4 * cx

@@ -107,7 +107,7 @@ def test_gemm_headline_shapes_full_output_vs_fp32(cuda_device, M, N, K, variants
         assert err <= tol, (v, err, tol)
 
 
-@pytest.mark.parametrize("variant", [54, 55])
+@pytest.mark.parametrize("variant", [54, 55, 57])
 @pytest.mark.parametrize("reserved", [0, 64])
 @pytest.mark.parametrize("M,N,K", [(8192, 4096, 256), (4096, 8192, 1152), (8192, 8192, 2048)])
 def test_gemm_staggered_rounds_vs_fp32(cuda_device, M, N, K, reserved, variant):
@@ -127,7 +127,11 @@ def test_gemm_staggered_rounds_vs_fp32(cuda_device, M, N, K, reserved, variant):
     tol = ref.abs().max().item() * 2 ** -7 + 1e-3
     try:
         gemm.set_reserved_cus(reserved)
-        assert gemm.stagger_plan(T, K, gemm.available_cus()) > 0
+        if variant == 57:
+            cx = gemm.available_cus() // 8
+            assert T % 8 == 0 and T // 8 >= 2 * cx, "shape too small for schedule 57"
+        else:
+            assert gemm.stagger_plan(T, K, gemm.available_cus()) > 0
         outs = []
         for _ in range(3):
             c = torch.full((M, N), float("nan"), device=cuda_device, dtype=torch.bfloat16)
