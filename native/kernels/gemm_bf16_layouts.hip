@@ -469,12 +469,20 @@ struct GuPrefetch : mxk::NoHook {
   }
 };
 
-template <bool AN, bool BN, int EPI, int SCHED = 0, bool SPLIT = false>
+// STAG (EPI 4 only, the down projection's dgrad-SwiGLU): rounds staggered by
+// XCD group (mx_common.h stagger_part_xcd; TN schedule 57's mapping): XCDs 4-7
+// run half a tile out of phase with XCDs 0-3, so the two halves of the chip
+// take turns with the epilogue's HBM traffic (1.9 GB per Llama-3-8B layer,
+// +19 % over a plain store when every CU bursts at once,
+// profiles/r4_step/swiglu_epilogue_price.log) instead of all bursting at once.
+// A first K half leaves d as fp32 rows in ws[slot] and raises flags[slot]; the
+// second half (later on the same XCD) waits for it, adds it in the epilogue.
+template <bool AN, bool BN, int EPI, int SCHED = 0, bool SPLIT = false, bool STAG = false>
 __global__ void __launch_bounds__(XT, 1)
 mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                         uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc,
                         const uint16_t* __restrict__ aux = nullptr, float* __restrict__ ws = nullptr,
-                        int q_full = 0) {
+                        int q_full = 0, int* __restrict__ flags = nullptr, int stag_cx = 0) {
   constexpr int A_BYTES = XOp<AN>::BYTES;
   constexpr int STAGE = A_BYTES + XOp<BN>::BYTES;
   // EPI 4: 1 KiB more, so the epilogue's acc slices (4 x kSwigluLdsWave from
@@ -495,6 +503,17 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     tile = q_full + (static_cast<int>(blockIdx.x) >> 1);
     klen = K >> 1;
     kbeg = (blockIdx.x & 1) * klen;
+  }
+  mxk::StaggerPart sp{static_cast<int>(blockIdx.x), 0, -1};
+  if constexpr (STAG) {
+    static_assert(EPI == 4 && !SPLIT, "STAG: the dgrad-SwiGLU epilogue only");
+    sp = mxk::stagger_part_xcd(blockIdx.x, (M / XBM) * (N / XBM), stag_cx);
+    if (sp.part < 0) return;
+    tile = sp.vtile;
+    if (sp.part) {
+      klen = K >> 1;
+      kbeg = sp.part == 2 ? klen : 0;
+    }
   }
   int m0, n0;
   mxk::w4b_tile<1>(tile, (M / XBM) * (N / XBM), M / XBM, N / XBM, &m0, &n0);
@@ -604,9 +623,31 @@ mxk_gemm_bf16_x2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     // (the launcher takes EPI 4 only for K >= 2 * XBK, so that K-tile ran)
     char* last = smem + (s & 1) * STAGE;
     const char* gul = smem + ((s & 1) ^ 1) * STAGE + 1024 + wave * 16384;
-    mxk::swiglu_bwd_block_lds<(SCHED & 1) == 0 && !SPLIT, EPI == 6>(acc, aux, C, ldc, N, m0 + wm * 128,
-                                                    n0 + wn * 128, lane,
-                                                    last + wave * mxk::kSwigluLdsWave, gul);
+    constexpr bool PFX = (SCHED & 1) == 0 && !SPLIT;
+    if constexpr (STAG) {
+      float* part = ws + static_cast<size_t>(sp.slot) * (XBM * XBM) + wave * (128 * 128);
+      if (sp.part == 1) {
+        mxk::swiglu_bwd_block_lds<PFX, false, 1>(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128,
+                                                 lane, last + wave * mxk::kSwigluLdsWave, gul, part);
+        __builtin_amdgcn_s_waitcnt(0);            // this wave's partial reached memory
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flags + sp.slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      if (sp.part == 2) {
+        if (tid == 0)
+          while (__hip_atomic_load(flags + sp.slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            __builtin_amdgcn_s_sleep(4);
+        __syncthreads();
+        mxk::swiglu_bwd_block_lds<PFX, false, 2>(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128,
+                                                 lane, last + wave * mxk::kSwigluLdsWave, gul, part);
+        __syncthreads();                          // every wave read its partial
+        if (tid == 0) __hip_atomic_store(flags + sp.slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+    }
+    mxk::swiglu_bwd_block_lds<PFX, EPI == 6>(acc, aux, C, ldc, N, m0 + wm * 128, n0 + wn * 128,
+                                             lane, last + wave * mxk::kSwigluLdsWave, gul);
   }
   else if constexpr (EPI == 1) {
     // whole-line stores through LDS (as the TN kernel's default schedule);
@@ -951,6 +992,46 @@ int swiglu_epi() {
 // dgrad-SwiGLU epilogue mode (MXK_SWIGLU_WIDE; see mxk_gemm_bf16_dgrad_swiglu)
 MXK_API void mxk_gemm_swiglu_set_epi(int v) { g_swiglu_epi.store(v); }
 
+namespace {
+// Per-(device, stream) uncached workspace of the staggered dgrad-SwiGLU GEMM:
+// fp32 partial tiles (256 KiB each) and their flags, zeroed once; each
+// consumer resets its flag, so later launches and graph replays start clean.
+struct SwigluStagWs {
+  float* ws = nullptr;
+  int* flags = nullptr;
+  int slots = 0;
+};
+std::mutex g_sstag_mu;
+std::map<std::pair<int, hipStream_t>, SwigluStagWs> g_sstag;
+
+const SwigluStagWs* swiglu_stag_ws(hipStream_t stream, int slots) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_sstag_mu);
+  SwigluStagWs& w = g_sstag[{dev, stream}];
+  if (w.slots >= slots) return &w;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+    return nullptr;
+  if (w.ws) (void)hipFree(w.ws);
+  if (w.flags) (void)hipFree(w.flags);
+  w = SwigluStagWs{};
+  void *ws = nullptr, *fl = nullptr;
+  if (hipExtMallocWithFlags(&ws, static_cast<size_t>(slots) * XBM * XBM * 4,
+                            hipDeviceMallocUncached) != hipSuccess ||
+      hipExtMallocWithFlags(&fl, static_cast<size_t>(slots) * 4, hipDeviceMallocUncached) != hipSuccess ||
+      hipMemsetAsync(fl, 0, static_cast<size_t>(slots) * 4, stream) != hipSuccess) {
+    if (ws) (void)hipFree(ws);
+    if (fl) (void)hipFree(fl);
+    return nullptr;
+  }
+  w.ws = static_cast<float*>(ws);
+  w.flags = static_cast<int*>(fl);
+  w.slots = slots;
+  return &w;
+}
+}  // namespace
+
 // Down-projection input gradient with the SwiGLU backward fused into the
 // epilogue: d(act) = dy W2 (dy [M][K] K-major, W2 [K][F] F-major) never
 // reaches memory; dgu [M][2F] = d[g | u] is written from gu [M][2F].
@@ -970,10 +1051,26 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
   // 16-B g/u accesses: EPI 4 (LDS-staged, whole lines, pass 0's g/u
   // prefetched during the last K-tiles) by default, EPI 5 (the same without
   // the prefetch) with MXK_SWIGLU_WIDE=5, EPI 3 (permlane pairs) with =3, the
-  // 8-B form with =0 (A/B); 6 = EPI 4 without the SwiGLU math (timing only)
+  // 8-B form with =0 (A/B); 6 = EPI 4 without the SwiGLU math (timing only);
+  // 8 = EPI 4 staggered by XCD group (STAG)
   const int wide_mode = swiglu_epi();
   const bool wide = wide_mode != 0 && reinterpret_cast<uintptr_t>(gu) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(dgu) % 16 == 0 && K >= 2 * XBK;
+  if (wide && wide_mode == 8) {
+    // staggered by XCD group (x2 STAG); the plain EPI 4 launch when the shape
+    // has fewer than two rounds or no workspace can be had
+    const int cx = device_cus() / 8;
+    const long T = nwg;
+    const bool fits = T % 8 == 0 && cx > 0 && T / 8 >= 2 * cx && K % (2 * XBK) == 0;
+    const SwigluStagWs* w = fits ? swiglu_stag_ws(stream, 4 * cx) : nullptr;
+    if (w) {
+      MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 4, 0, false, true>), dim3(nwg + 8 * cx),
+                      dim3(XT), stream, static_cast<const uint16_t*>(dy),
+                      static_cast<const uint16_t*>(w2), static_cast<uint16_t*>(dgu), M, F, K, ld_dy,
+                      ld_w2, 2 * F, static_cast<const uint16_t*>(gu), w->ws, 0, w->flags, cx);
+      MXK_RETURN_LAUNCH_STATUS();
+    }
+  }
   if (wide && wide_mode == 6)
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 6, 0>), dim3(nwg), dim3(XT), stream,
                     static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),

@@ -44,6 +44,8 @@ __device__ __forceinline__ void vm_wait() {
 
 using mxk::w4b_tile;
 }  // namespace
+using mxk::StaggerPart;
+using mxk::stagger_part_xcd;
 
 struct DmaK {
   __amdgpu_buffer_rsrc_t rsrc;   // 256-row panel, whole K
@@ -374,12 +376,6 @@ mxk_gemm_bf16_tn_w4j(const uint16_t* __restrict__ A, const uint16_t* __restrict_
 //   tx <= i          second K half of split tile i - tx
 // (tx = T / 8 tiles per XCD; the split tiles are the XCD's last sx tiles of
 // the map).  Virtual tile v = x + 8 * (local tile) keeps the map's XCD.
-struct StaggerPart {
-  int vtile;   // tile index fed to the tile map
-  int part;    // 0 whole tile, 1 first K half, 2 second K half
-  int slot;    // partial slot (parts 1, 2), else -1
-};
-
 __host__ __device__ inline StaggerPart stagger_part(int b, int T, int sx) {
   const int x = b & 7, i = b >> 3;
   const int tx = T >> 3, f = tx - sx;
@@ -392,37 +388,6 @@ __host__ __device__ inline StaggerPart stagger_part(int b, int T, int sx) {
     r.part = 0; r.slot = -1; r.vtile = x + 8 * (i - sx);
   } else {
     r.part = 2; r.slot = x * sx + (i - tx); r.vtile = x + 8 * (f + i - tx);
-  }
-  return r;
-}
-
-// XCD-group stagger (schedule 57): the PMC of the per-CU stagger above shows
-// +43 % fetch beyond L2 at 8192^3 - half of an XCD's CUs half a tile out of
-// phase no longer read each panel slice together, so the XCD's L2 stops
-// sharing it.  Here whole XCDs are out of phase instead: XCDs 0-3 run whole
-// tiles, XCDs 4-7 start with the first K halves of their first cx tiles (one
-// per CU) and end with the second halves.  Inside an XCD every CU stays in
-// phase (L2 reuse kept); XCDs 0-3 and 4-7 share no A panel of the super-block
-// (rows x >> 2) and their shared B panels are half a tile apart (MALL hits);
-// the C-store bursts of the two halves of the chip alternate.  Workgroup b on
-// XCD x = b & 7, local index i = b >> 3, tx = T / 8, grid 8 (tx + cx):
-//   x < 4:  i < tx whole tile i; i >= tx nothing (part -1)
-//   x >= 4: i < cx first half of tile i (slot (x - 4) cx + i); cx <= i < tx
-//           whole tile i; tx <= i second half of tile i - tx
-__host__ __device__ inline StaggerPart stagger_part_xcd(int b, int T, int cx) {
-  const int x = b & 7, i = b >> 3;
-  const int tx = T >> 3;
-  StaggerPart r;
-  r.slot = -1;
-  if (x < 4) {
-    r.part = i < tx ? 0 : -1;
-    r.vtile = x + 8 * (i < tx ? i : 0);
-  } else if (i < cx) {
-    r.part = 1; r.slot = (x - 4) * cx + i; r.vtile = x + 8 * i;
-  } else if (i < tx) {
-    r.part = 0; r.vtile = x + 8 * i;
-  } else {
-    r.part = 2; r.slot = (x - 4) * cx + (i - tx); r.vtile = x + 8 * (i - tx);
   }
   return r;
 }

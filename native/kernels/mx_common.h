@@ -193,6 +193,45 @@ __device__ __forceinline__ void w4b_tile(int bid, int nwg, int tiles_m, int tile
   *n0 = (in_group / gsize) * 256;
 }
 
+// ---- staggered rounds (gemm_tn_core.h schedules 54-57; the dgrad-SwiGLU
+// layout GEMM) ----------------------------------------------------------------
+struct StaggerPart {
+  int vtile;   // tile index fed to the tile map
+  int part;    // 0 whole tile, 1 first K half, 2 second K half, -1 idle
+  int slot;    // partial slot (parts 1, 2), else -1
+};
+
+// XCD-group stagger (schedule 57): the PMC of the per-CU stagger above shows
+// +43 % fetch beyond L2 at 8192^3 - half of an XCD's CUs half a tile out of
+// phase no longer read each panel slice together, so the XCD's L2 stops
+// sharing it.  Here whole XCDs are out of phase instead: XCDs 0-3 run whole
+// tiles, XCDs 4-7 start with the first K halves of their first cx tiles (one
+// per CU) and end with the second halves.  Inside an XCD every CU stays in
+// phase (L2 reuse kept); XCDs 0-3 and 4-7 share no A panel of the super-block
+// (rows x >> 2) and their shared B panels are half a tile apart (MALL hits);
+// the C-store bursts of the two halves of the chip alternate.  Workgroup b on
+// XCD x = b & 7, local index i = b >> 3, tx = T / 8, grid 8 (tx + cx):
+//   x < 4:  i < tx whole tile i; i >= tx nothing (part -1)
+//   x >= 4: i < cx first half of tile i (slot (x - 4) cx + i); cx <= i < tx
+//           whole tile i; tx <= i second half of tile i - tx
+__host__ __device__ inline StaggerPart stagger_part_xcd(int b, int T, int cx) {
+  const int x = b & 7, i = b >> 3;
+  const int tx = T >> 3;
+  StaggerPart r;
+  r.slot = -1;
+  if (x < 4) {
+    r.part = i < tx ? 0 : -1;
+    r.vtile = x + 8 * (i < tx ? i : 0);
+  } else if (i < cx) {
+    r.part = 1; r.slot = (x - 4) * cx + i; r.vtile = x + 8 * i;
+  } else if (i < tx) {
+    r.part = 0; r.vtile = x + 8 * i;
+  } else {
+    r.part = 2; r.slot = (x - 4) * cx + (i - tx); r.vtile = x + 8 * (i - tx);
+  }
+  return r;
+}
+
 // bf16 store of a wave's 128x128 accumulator block, widened to dwordx4 by
 // v_permlane16_swap (w4b EPI 1).  NT: non-temporal stores (C is written once
 // and not re-read by this kernel; keeps it from displacing A/B panels).
@@ -496,11 +535,15 @@ constexpr int kSwigluLdsWave = 32 * kSwigluLdsRow;
 // K-tiles, x2 EPI 4), so pass 0 does not wait for HBM after the K loop.
 // NOMATH (timing ablation, wrong values): dg = d u, du = d g - the same
 // memory traffic without the sigmoid's exp / rcp and its products.
-template <bool PF = false, bool NOMATH = false>
+// PM (staggered dgrad-SwiGLU, x2 STAG): 1 = this is a first K half: store d
+// as fp32 rows to part (this wave's [128][128] block, row-major) and nothing
+// else; 2 = a second K half: d += part before the SwiGLU backward.
+template <bool PF = false, bool NOMATH = false, int PM = 0>
 __device__ __forceinline__ void swiglu_bwd_block_lds(const f32x4_t (&acc)[8][8],
                                                      const uint16_t* gu, uint16_t* dgu, long ld,
                                                      int F, int row0, int col0, int lane,
-                                                     char* lds, const char* gu_lds = nullptr) {
+                                                     char* lds, const char* gu_lds = nullptr,
+                                                     float* part = nullptr) {
   typedef float f2_t __attribute__((ext_vector_type(2)));
   const int crow = lane & 15, q = lane >> 4;
   const int rr = lane >> 4, cc = (lane & 15) * 8;   // read phase: row rr of 4, 8 columns
@@ -513,7 +556,8 @@ __device__ __forceinline__ void swiglu_bwd_block_lds(const f32x4_t (&acc)[8][8],
       uw[b][it] = *reinterpret_cast<const uint4*>(gu + off + F);
     }
   };
-  if constexpr (PF) {
+  if constexpr (PM == 1) {
+  } else if constexpr (PF) {
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const char* gp = gu_lds + (it * 4 + rr) * 256 + cc * 2;
@@ -526,7 +570,7 @@ __device__ __forceinline__ void swiglu_bwd_block_lds(const f32x4_t (&acc)[8][8],
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int b = p & 1;
-    if (p + 1 < 4) load(p + 1, b ^ 1);
+    if (PM != 1 && p + 1 < 4) load(p + 1, b ^ 1);
     // d rows [32p, 32p + 32) = accumulator rows i = 2p, 2p + 1
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii)
@@ -538,8 +582,17 @@ __device__ __forceinline__ void swiglu_bwd_block_lds(const f32x4_t (&acc)[8][8],
     for (int it = 0; it < 8; ++it) {
       const int r = it * 4 + rr;
       const char* dp = lds + r * kSwigluLdsRow + cc * 4;
-      const f32x4_t d0 = *reinterpret_cast<const f32x4_t*>(dp);
-      const f32x4_t d1 = *reinterpret_cast<const f32x4_t*>(dp + 16);
+      f32x4_t d0 = *reinterpret_cast<const f32x4_t*>(dp);
+      f32x4_t d1 = *reinterpret_cast<const f32x4_t*>(dp + 16);
+      float* pp = part + (p * 32 + r) * 128 + cc;
+      if constexpr (PM == 1) {
+        *reinterpret_cast<f32x4_t*>(pp) = d0;
+        *reinterpret_cast<f32x4_t*>(pp + 4) = d1;
+        continue;
+      } else if constexpr (PM == 2) {
+        d0 += *reinterpret_cast<const f32x4_t*>(pp);
+        d1 += *reinterpret_cast<const f32x4_t*>(pp + 4);
+      }
       const float d[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
       const uint32_t gp[4] = {gw[b][it].x, gw[b][it].y, gw[b][it].z, gw[b][it].w};
       const uint32_t up[4] = {uw[b][it].x, uw[b][it].y, uw[b][it].z, uw[b][it].w};

@@ -4,6 +4,7 @@
 # g/u prefetch (MXK_SWIGLU_WIDE=5), interleaved twice.  Second set: layout
 # kernel B-outer order (MXK_X2_ORDER=1), w13 non-temporal gu stores
 # (MXK_W13_SCHED=2), attention backward variant 3 (MXK_ATTN_BWD_VARIANT=3).
+# Set 3: the dgrad-SwiGLU GEMM staggered by XCD group (MXK_SWIGLU_WIDE=8).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 O=gpurun_out/r4step; mkdir -p $O
@@ -18,5 +19,5 @@ for l in open('$O/$n.out'):
         d=json.loads(l); print('$n', d['value'], d['ms_per_step'])"
 }
 for r in 1 2; do
-  run base$r MXK_NOP=1 && run x2ord_$r MXK_X2_ORDER=1 && run w13nt_$r MXK_W13_SCHED=2 && run bwd3_$r MXK_ATTN_BWD_VARIANT=3 || exit $?
+  run base$r MXK_NOP=1 && run swstag_$r MXK_SWIGLU_WIDE=8 || exit $?
 done

@@ -8,6 +8,7 @@ interleaved over rounds, in one process:
   epi5     epi4 without the prefetch
   epi6     epi4 without the SwiGLU math (same memory traffic; wrong values)
   epi3     the permlane-pair epilogue
+  epi8     epi4 with the rounds staggered by XCD group
 
 Prints one RESULT json per kernel (median ms, TF/s of the GEMM part)."""
 import json
@@ -41,7 +42,8 @@ def main() -> int:
         return f
 
     kernels = {"plain": lambda: gemm.gemm_bf16_ex(dy, w2, True, False, dh),
-               "epi4": fused(4), "epi5": fused(5), "epi6": fused(6), "epi3": fused(3)}
+               "epi4": fused(4), "epi5": fused(5), "epi6": fused(6), "epi3": fused(3),
+               "epi8": fused(8)}
     for fn in kernels.values():
         for _ in range(3):
             fn()

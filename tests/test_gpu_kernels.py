@@ -510,3 +510,44 @@ def test_gemm_layouts_b_outer_order_vs_fp32(cuda_device, a_kmajor, b_kmajor):
     assert (outs[0][0].float() - ref).abs().max().item() <= tol
     d1, d0 = outs[0][1].float(), outs[1][1].float()
     assert (d1 - d0).abs().max().item() <= 2 ** -7 * d0.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("reserved", [0, 64])
+def test_dgrad_swiglu_staggered_vs_default(cuda_device, reserved):
+    """Epilogue mode 8: the dgrad-SwiGLU GEMM with its rounds staggered by XCD
+    group (first K halves hand fp32 partials to their second halves through
+    uncached memory and flags).  Against the default epilogue (mode 4) and an
+    fp32 reference, launched three times back to back (flags reset)."""
+    from mxk8s.ops import _lib, gemm
+    L = _lib.lib()
+    T, F, K = 4096, 8192, 1024
+    dy = _rand((T, K), cuda_device, 71).bfloat16()
+    w2 = _rand((K, F), cuda_device, 72, 0.05).bfloat16()
+    gu = _rand((T, 2 * F), cuda_device, 73, 3.0).bfloat16()
+    outs = {}
+    try:
+        gemm.set_reserved_cus(reserved)
+        for mode in (8, 4):
+            L.mxk_gemm_swiglu_set_epi(mode)
+            runs = []
+            for _ in range(3 if mode == 8 else 1):
+                dgu = torch.full_like(gu, float("nan"))
+                _lib.check(L.mxk_gemm_bf16_dgrad_swiglu(dy.data_ptr(), w2.data_ptr(), gu.data_ptr(),
+                                                        dgu.data_ptr(), T, F, K, K, F,
+                                                        _lib.stream_ptr(cuda_device)), f"mode {mode}")
+                runs.append(dgu)
+            torch.cuda.synchronize()
+            outs[mode] = runs
+    finally:
+        L.mxk_gemm_swiglu_set_epi(4)
+        gemm.set_reserved_cus(0)
+    d = dy.float() @ w2.float()
+    g, u = gu.float().chunk(2, -1)
+    sg = torch.sigmoid(g)
+    ref = torch.cat([d * u * sg * (1 + g * (1 - sg)), d * g * sg], -1)
+    tol = 2 ** -6 * ref.abs().max().item() + 1e-3
+    for dgu in outs[8]:
+        assert not torch.isnan(dgu).any()
+        assert (dgu.float() - ref).abs().max().item() <= tol
+        assert torch.equal(dgu, outs[8][0])
+    assert (outs[8][0].float() - outs[4][0].float()).abs().max().item() <= tol
