@@ -539,6 +539,9 @@ MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, v
       static_cast<long>(F + 128) * ldw * 2 >= (1L << 31))
     return static_cast<int>(hipErrorInvalidValue);
   const int nwg = (M / BM) * (F / 128);
+#ifdef MXK_GEMM_EXPERIMENTS
+  // A/B records (experiments library): 1 = one-barrier K loop, 2 = non-temporal
+  // gu stores; both step-neutral (profiles/r4_step/)
   if (w13_sched() == 2)
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_w13_swiglu_k<false, true>), dim3(nwg), dim3(W4_THREADS), stream,
                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
@@ -548,6 +551,7 @@ MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, v
                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
                     static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu, ldh);
   else
+#endif
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_w13_swiglu_k<false>), dim3(nwg), dim3(W4_THREADS), stream,
                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
                     static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu, ldh);

@@ -841,6 +841,9 @@ mxk_gemm_split_fixup(const float* __restrict__ ws, uint16_t* __restrict__ C, int
 namespace {
 std::atomic<int> g_x2_order{-1};
 int x2_order() {
+#ifndef MXK_GEMM_EXPERIMENTS
+  return 0;   // the B-outer order is built into the experiments library only
+#endif
   int v = g_x2_order.load(std::memory_order_relaxed);
   if (v < 0) {
     const char* e = std::getenv("MXK_X2_ORDER");
@@ -873,7 +876,10 @@ static void launch_x(int sched, bool wide, int nwg, hipStream_t stream, const ui
                     M, N, K, lda, ldb, ldc);                                                     \
     break;
     MXK_X2_CASE(0, 0) MXK_X2_CASE(0, 1) MXK_X2_CASE(1, 0) MXK_X2_CASE(1, 1)
+#ifdef MXK_GEMM_EXPERIMENTS
+    // B-outer order: step-neutral (profiles/r4_step/step_ab_set2.txt), A/B only
     MXK_X2_CASE(2, 0) MXK_X2_CASE(2, 1) MXK_X2_CASE(3, 0) MXK_X2_CASE(3, 1)
+#endif
 #undef MXK_X2_CASE
     default: break;
   }
@@ -992,6 +998,7 @@ int swiglu_epi() {
 // dgrad-SwiGLU epilogue mode (MXK_SWIGLU_WIDE; see mxk_gemm_bf16_dgrad_swiglu)
 MXK_API void mxk_gemm_swiglu_set_epi(int v) { g_swiglu_epi.store(v); }
 
+#ifdef MXK_GEMM_EXPERIMENTS
 namespace {
 // Per-(device, stream) uncached workspace of the staggered dgrad-SwiGLU GEMM:
 // fp32 partial tiles (256 KiB each) and their flags, zeroed once; each
@@ -1031,6 +1038,7 @@ const SwigluStagWs* swiglu_stag_ws(hipStream_t stream, int slots) {
   return &w;
 }
 }  // namespace
+#endif
 
 // Down-projection input gradient with the SwiGLU backward fused into the
 // epilogue: d(act) = dy W2 (dy [M][K] K-major, W2 [K][F] F-major) never
@@ -1056,9 +1064,11 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
   const int wide_mode = swiglu_epi();
   const bool wide = wide_mode != 0 && reinterpret_cast<uintptr_t>(gu) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(dgu) % 16 == 0 && K >= 2 * XBK;
+#ifdef MXK_GEMM_EXPERIMENTS
+  // A/B records (experiments library): 8 = staggered by XCD group (+0.8 %,
+  // profiles/r4_step/swiglu_epilogue_stagger.log), 6 = no SwiGLU math (timing
+  // ablation), 5 = no g/u prefetch, and the B-outer MFMA order
   if (wide && wide_mode == 8) {
-    // staggered by XCD group (x2 STAG); the plain EPI 4 launch when the shape
-    // has fewer than two rounds or no workspace can be had
     const int cx = device_cus() / 8;
     const long T = nwg;
     const bool fits = T % 8 == 0 && cx > 0 && T / 8 >= 2 * cx && K % (2 * XBK) == 0;
@@ -1071,26 +1081,30 @@ MXK_API int mxk_gemm_bf16_dgrad_swiglu(const void* dy, const void* w2, const voi
       MXK_RETURN_LAUNCH_STATUS();
     }
   }
-  if (wide && wide_mode == 6)
-    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 6, 0>), dim3(nwg), dim3(XT), stream,
-                    static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
-                    static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
-                    static_cast<const uint16_t*>(gu));
-  else if (wide && wide_mode == 5)
-    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 5, 0>), dim3(nwg), dim3(XT), stream,
-                    static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
-                    static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
-                    static_cast<const uint16_t*>(gu));
-  else if (wide && wide_mode == 3)
+  if (wide && (wide_mode == 6 || wide_mode == 5 || x2_order())) {
+    if (wide_mode == 6)
+      MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 6, 0>), dim3(nwg), dim3(XT), stream,
+                      static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
+                      static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
+                      static_cast<const uint16_t*>(gu));
+    else if (wide_mode == 5)
+      MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 5, 0>), dim3(nwg), dim3(XT), stream,
+                      static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
+                      static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
+                      static_cast<const uint16_t*>(gu));
+    else
+      MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 4, 2>), dim3(nwg), dim3(XT), stream,
+                      static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
+                      static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
+                      static_cast<const uint16_t*>(gu));
+    MXK_RETURN_LAUNCH_STATUS();
+  }
+#endif
+  if (wide && wide_mode == 3)
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 3, 0>), dim3(nwg), dim3(XT), stream,
                        static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
                        static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
                        static_cast<const uint16_t*>(gu));
-  else if (wide && x2_order())
-    MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 4, 2>), dim3(nwg), dim3(XT), stream,
-                    static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),
-                    static_cast<uint16_t*>(dgu), M, F, K, ld_dy, ld_w2, 2 * F,
-                    static_cast<const uint16_t*>(gu));
   else if (wide)
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_x2_kernel<false, true, 4, 0>), dim3(nwg), dim3(XT), stream,
                        static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w2),

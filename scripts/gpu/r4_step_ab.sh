@@ -9,6 +9,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 O=gpurun_out/r4step; mkdir -p $O
 export PYTHONPATH=.
+# the A/B switches below are built into the experiments library only
+export MXK_KERNELS_LIB=$PWD/mxk8s/_lib/libmxkernels_exp.so
 run() {  # name env...
   local n=$1; shift
   timeout -k 10 240 env "$@" python3 bench.py --mode ddp --steps 8 --warmup 3 > $O/$n.out 2> $O/$n.err || return $?

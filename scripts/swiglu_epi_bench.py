@@ -10,6 +10,9 @@ interleaved over rounds, in one process:
   epi3     the permlane-pair epilogue
   epi8     epi4 with the rounds staggered by XCD group
 
+(modes 5, 6 and 8 are A/B records: run with
+MXK_KERNELS_LIB=mxk8s/_lib/libmxkernels_exp.so, or they time the default)
+
 Prints one RESULT json per kernel (median ms, TF/s of the GEMM part)."""
 import json
 import os

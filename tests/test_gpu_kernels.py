@@ -480,10 +480,13 @@ def test_gemm_exclusive_mode_vs_fp32(cuda_device, a_kmajor, b_kmajor):
 @pytest.mark.parametrize("a_kmajor,b_kmajor", [(1, 0), (0, 0), (0, 1)])
 def test_gemm_layouts_b_outer_order_vs_fp32(cuda_device, a_kmajor, b_kmajor):
     """The layout kernel's K-tile with the B fragment as the outer MFMA loop
-    (mxk_gemm_x2_set_order(1), MXK_X2_ORDER=1) against fp32, and the fused
-    dgrad-SwiGLU GEMM under the same order against the default order."""
+    (mxk_gemm_x2_set_order(1), MXK_X2_ORDER=1; experiments library) against
+    fp32, and the fused dgrad-SwiGLU GEMM under the same order against the
+    default order."""
     from mxk8s.ops import _lib, gemm
     L = _lib.lib()
+    if not L.mxk_gemm_bf16_tn_variant_built(54):
+        pytest.skip("A/B record: experiments library only")
     M, N, K = 2048, 1024, 1088
     a = _rand((M, K) if a_kmajor else (K, M), cuda_device, 61).bfloat16()
     b = _rand((N, K) if b_kmajor else (K, N), cuda_device, 62).bfloat16()
@@ -516,10 +519,13 @@ def test_gemm_layouts_b_outer_order_vs_fp32(cuda_device, a_kmajor, b_kmajor):
 def test_dgrad_swiglu_staggered_vs_default(cuda_device, reserved):
     """Epilogue mode 8: the dgrad-SwiGLU GEMM with its rounds staggered by XCD
     group (first K halves hand fp32 partials to their second halves through
-    uncached memory and flags).  Against the default epilogue (mode 4) and an
-    fp32 reference, launched three times back to back (flags reset)."""
+    uncached memory and flags; experiments library).  Against the default
+    epilogue (mode 4) and an fp32 reference, launched three times back to back
+    (flags reset)."""
     from mxk8s.ops import _lib, gemm
     L = _lib.lib()
+    if not L.mxk_gemm_bf16_tn_variant_built(54):
+        pytest.skip("A/B record: experiments library only")
     T, F, K = 4096, 8192, 1024
     dy = _rand((T, K), cuda_device, 71).bfloat16()
     w2 = _rand((K, F), cuda_device, 72, 0.05).bfloat16()
