@@ -145,8 +145,9 @@ class Streamer:
     def gbps(self, ms: float) -> float:
         return 2 * self.src.numel() / ms / 1e6
 
-    def calibrate(self, target_ms: float, gbps: float = 0.0):
-        """Pace to <= gbps (0: unpaced), then enough passes to cover target_ms."""
+    def calibrate(self, target_ms: float, gbps: float = 0.0, gb_per_step: float = 0.0):
+        """Pace to <= gbps (0: unpaced), then enough passes to cover target_ms,
+        or (gb_per_step > 0) to move that many GB of copy traffic per step."""
         self.pace = 0
         one = self.time_one()
         if gbps > 0 and self.gbps(one) > gbps:
@@ -165,7 +166,10 @@ class Streamer:
                 else:
                     lo = self.pace
             self.pace = hi
-        self.iters = max(1, int(round(target_ms / one)))
+        if gb_per_step > 0:
+            self.iters = max(1, int(round(gb_per_step * 1e9 / (2 * self.src.numel()))))
+        else:
+            self.iters = max(1, int(round(target_ms / one)))
         return one
 
     def close(self):
@@ -206,6 +210,10 @@ def main() -> int:
     ap.add_argument("--micro-batch", type=int, default=8)
     ap.add_argument("--placement", default="spread", help="comma list: spread, xcd, masked")
     ap.add_argument("--map-only", action="store_true", help="print the CU-mask bit map and exit")
+    ap.add_argument("--gb-per-step", type=float, default=0.0,
+                    help="streamer traffic per step in GB (read + write); 0: it runs through the "
+                         "whole backward.  28 is an 8-rank ZeRO-1 gradient reduce-scatter of "
+                         "Llama-3-8B (16 GB of bf16 gradients, 7/8 of it read and written once)")
     ap.add_argument("--modes", default="blind,aware,excl_blind,excl_aware",
                     help="comma list: blind, aware, excl_blind, excl_aware")
     ap.add_argument("--base-steps", type=int, default=None,
@@ -261,7 +269,7 @@ def main() -> int:
                                                 [float(x) for x in a.gbps.split(",") if x],
                                                 [int(x) for x in a.cus.split(",") if x]):
         st = Streamer(k, dev, placement=placement, cmap=cmap)
-        one = st.calibrate(base_bwd, gbps)
+        one = st.calibrate(base_bwd, gbps, a.gb_per_step)
         for mode in a.modes.split(","):
             gemm.set_reserved_cus(k if mode.endswith("aware") else 0)
             gemm.set_exclusive(mode.startswith("excl"))
@@ -270,6 +278,7 @@ def main() -> int:
             bslow = bwd / base_bwd - 1
             print("RESULT " + json.dumps({
                 "k": k, "placement": placement, "gbps_target": gbps, "mode": mode,
+                "gb_per_step": a.gb_per_step or None,
                 "ms_per_step": round(ms, 2),
                 "backward_ms": round(bwd, 2), "slowdown": round(ms / base - 1, 4),
                 "backward_slowdown": round(bslow, 4), "ideal_slowdown": round(ideal, 4),
