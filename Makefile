@@ -87,7 +87,7 @@ $(BUILD)/tools/%.o: native/tools/%.hip $(KERNEL_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/tools/allreduce_perf.o: native/rccl_bench/allreduce_perf.cc
+$(BUILD)/tools/allreduce_perf.o: native/rccl_bench/allreduce_perf.cc native/rccl_bench/sweep_plan.h
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 

@@ -179,16 +179,34 @@ def allreduce_sizes(args, world) -> list[int]:
     return out
 
 
+def allreduce_iters(nbytes: int) -> int:
+    """Timed calls per sweep size: ~4 GiB of data per size, 3..50 calls."""
+    return max(3, min(50, (4 << 30) // max(nbytes, 1)))
+
+
+AR_WARM_CALLS = 2   # untimed calls per size before its timed calls
+
+
+def allreduce_plan(args, world) -> list[tuple[int, int]]:
+    """(bytes, timed calls) per sweep size, in sweep order (per dtype)."""
+    return [(b, allreduce_iters(b)) for b in allreduce_sizes(args, world)]
+
+
 def run_allreduce(args, dev, world, rank) -> dict:
     """Real collective (RCCL at every N on GPUs): an exact-sum check per dtype,
     then the size sweep, each size timed with an event pair around its
-    iterations (hipEvents on a GPU), slowest rank's time."""
+    iterations (hipEvents on a GPU), slowest rank's time.
+
+    The sweep buffer holds zeros, the fixed point of an in-place sum over
+    ranks: every timed call reduces finite data (a buffer of ones would be
+    multiplied by N at every call and reach inf after ~43 calls at N = 8),
+    and the buffer is checked to be all zero after each dtype's sweep."""
     import torch
     import torch.distributed as dist
 
     dtypes = {"bf16": torch.bfloat16, "fp32": torch.float32}
     names = [d for d in args.allreduce_dtypes.split(",") if d]
-    sizes = allreduce_sizes(args, world)
+    plan = allreduce_plan(args, world)
     timer = _Timer(dev)
     sweep = []
     for name in names:
@@ -203,12 +221,11 @@ def run_allreduce(args, dev, world, rank) -> dict:
         if bad:
             raise SystemExit(f"{name} all-reduce check failed on rank {rank}: {bad} elements != {want}")
         del probe
-        buf = torch.ones(max(sizes) // esz, device=dev, dtype=dt_)
-        for nbytes in sizes:
+        buf = torch.zeros(max(b for b, _ in plan) // esz, device=dev, dtype=dt_)
+        for nbytes, iters in plan:
             n = max(1, nbytes // esz)
             x = buf[:n]
-            iters = max(3, min(50, (4 << 30) // max(nbytes, 1)))
-            for _ in range(2):
+            for _ in range(AR_WARM_CALLS):
                 dist.all_reduce(x)
             _sync(dev)
             _barrier(dev)
@@ -225,6 +242,11 @@ def run_allreduce(args, dev, world, rank) -> dict:
                           # a 1-rank all-reduce moves nothing: no bandwidth to report
                           "algbw_GBps": round(algbw, 2) if world > 1 else None,
                           "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2)})
+        _sync(dev)
+        nonzero = int(torch.count_nonzero(buf).item())
+        if nonzero:
+            raise SystemExit(f"{name} all-reduce sweep buffer on rank {rank}: {nonzero} elements "
+                             "left the zero fixed point")
         del buf
     head = next((s for s in sweep if s["bytes"] == args.allreduce_mib << 20 and s["dtype"] == names[0]),
                 sweep[-1] if sweep else None)
@@ -233,6 +255,7 @@ def run_allreduce(args, dev, world, rank) -> dict:
         "backend": dist.get_backend(),
         "rccl_ranks": dist.get_world_size(),
         "dtypes": names, "op": "sum", "check": "exact (sum of rank+1) per dtype",
+        "sweep_data": "zeros, the in-place sum's fixed point (all zero after each sweep: checked)",
         "timing": "event pair around the iterations of each size (hipEvents on GPUs), slowest rank",
         "bytes": head["bytes"] if head else None,
         "ms": head["ms"] if head else None,

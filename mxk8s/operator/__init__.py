@@ -141,6 +141,30 @@ def is_subset(want, have, key: str = "", injected: tuple = INJECTED_NAME_PREFIXE
     return False
 
 
+def drift_names(want, have, injected: tuple = INJECTED_NAME_PREFIXES, path: str = "") -> list:
+    """Named list items that differ between ``want`` and ``have``, as
+    ``"<path>: +name"`` (only live) / ``"<path>: -name"`` (only rendered):
+    what an admin adds to ``--injected-name`` when a mutating admission
+    policy, not the chart, put the ``+`` items there."""
+    out = []
+    if isinstance(want, dict) and isinstance(have, dict):
+        for k, v in want.items():
+            if k in have:
+                out += drift_names(v, have[k], injected, f"{path}.{k}" if path else k)
+    elif isinstance(want, list) and isinstance(have, list) and _named(want):
+        live = [x for x in have if isinstance(x, dict) and isinstance(x.get("name"), str)
+                and not x["name"].startswith(injected)]
+        wn = {w["name"] for w in want}
+        ln = {x["name"] for x in live}
+        out += [f"{path}: +{n}" for n in sorted(ln - wn)]
+        out += [f"{path}: -{n}" for n in sorted(wn - ln)]
+        by_name = {x["name"]: x for x in live}
+        for w in want:
+            if w["name"] in by_name:
+                out += drift_names(w, by_name[w["name"]], injected, f"{path}[{w['name']}]")
+    return out
+
+
 @dataclasses.dataclass
 class ReconcileResult:
     state: str
@@ -155,8 +179,16 @@ class ReconcileResult:
 class Controller:
     def __init__(self, client: KubeClient, namespace: str = "amd-gpu",
                  release: str = "amd-gpu-stack", chart_dir: str = chart_render.CHART_DIR,
-                 delete_wait_s: float = 5.0, injected: Sequence[str] = ()):
+                 delete_wait_s: float = 5.0, injected: Sequence[str] = (),
+                 replace_backoff_s: float = 1.0, replace_backoff_max_s: float = 300.0):
         self.client = client
+        # consecutive replaces of one object back off exponentially: a
+        # mutating admission policy that re-adds an item after every replace
+        # would otherwise make each reconcile replace it again, and the
+        # MODIFIED event wake the loop again (a hot loop)
+        self.replace_backoff_s = replace_backoff_s
+        self.replace_backoff_max_s = replace_backoff_max_s
+        self._replaces: dict = {}     # path -> [consecutive replaces, next allowed, names logged]
         self.injected = tuple(INJECTED_NAME_PREFIXES) + tuple(injected)
         self.namespace = namespace
         self.release = release
@@ -207,9 +239,23 @@ class Controller:
             log.info("creating %s", name, extra={"event": "operand_created", "component": name})
             return self.client.create(coll, obj)
         if is_subset(obj, live, injected=self.injected):
+            self._replaces.pop(path, None)
             return live
         if obj["kind"] == "Job":    # pod template is immutable: re-create
             return self._recreate_job(path, name, obj, live, res)
+        st = self._replaces.setdefault(path, [0, 0.0, None])
+        now = time.monotonic()
+        if now < st[1]:
+            res.pending.append(name)      # backing off: retried on a later pass
+            return live
+        names = drift_names(obj, live, self.injected)
+        if names and names != st[2]:
+            log.warning("%s drift in named items %s; if an admission controller adds them, "
+                        "pass --injected-name", name, ", ".join(names),
+                        extra={"event": "operand_drift_names", "component": name})
+            st[2] = names
+        st[0] += 1
+        st[1] = now + min(self.replace_backoff_max_s, self.replace_backoff_s * 2 ** (st[0] - 1))
         new = copy.deepcopy(obj)
         new["metadata"]["resourceVersion"] = live.get("metadata", {}).get("resourceVersion", "")
         res.updated.append(name)

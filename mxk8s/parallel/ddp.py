@@ -171,7 +171,11 @@ class FlatDDP:
         # ZeRO-1: gradients are reduce-scattered (each rank keeps 1/world of
         # every bucket) and the optimizer state is sharded the same way
         self.sharded = shard_optimizer and self.world > 1
-        esz = next(p for p in module.parameters() if p.requires_grad).element_size()
+        trainable = [p for p in module.parameters() if p.requires_grad]
+        if not trainable:
+            raise ValueError("FlatDDP: the module has no trainable parameters (nothing to "
+                             "bucket, reduce or stage)")
+        esz = trainable[0].element_size()
         cap = max(1, int(bucket_mb * 2 ** 20 / esz))
         self.space = FlatParamSpace(module, bucket_elems=cap,
                                     pad=ALIGN * (self.world if self.sharded else 1))
@@ -204,7 +208,7 @@ class FlatDDP:
         self._slots: list = []
         self._slot_out: list = []
         self._slot_owner: list = []
-        if self.reduce_fp32:
+        if self.reduce_fp32 and self.buckets:     # no trainable params: no ring
             n_slots = len(self.buckets) if stage_slots <= 0 else min(stage_slots, len(self.buckets))
             big = max(b.end - b.start for b in self.buckets)
             self.stage_slots = n_slots

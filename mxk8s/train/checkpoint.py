@@ -100,13 +100,38 @@ def _read_meta(ckpt_dir: str) -> Optional[dict]:
         return None
 
 
-def _history(prev: Optional[dict], current: str, keep: int) -> list[str]:
+def _complete_dirs(ckpt_dir: str) -> list[str]:
+    """Step directories that hold a complete-looking shard set (params plus
+    at least one optimizer shard), oldest first (zero-padded step names)."""
+    out = []
+    for d in sorted(os.listdir(ckpt_dir)):
+        full = os.path.join(ckpt_dir, d)
+        if not (d.startswith("step-") and os.path.isdir(full)):
+            continue
+        names = os.listdir(full)
+        if "params.safetensors" in names and any(n.startswith("optim-rank") and
+                                                  n.endswith(".safetensors") for n in names):
+            out.append(d)
+    return out
+
+
+def _history(prev: Optional[dict], current: str, keep: int,
+             ckpt_dir: Optional[str] = None) -> list[str]:
     """Committed step directories, oldest first, ending with ``current``:
     the previous commit record's history (or its single ``path`` for records
-    written before the history existed), truncated to the ``keep`` newest."""
+    written before the history existed), truncated to the ``keep`` newest.
+    When no usable record exists (missing, unreadable, another format, or a
+    record without ``history``) and ``ckpt_dir`` is given, fall back to the
+    newest ``keep`` directories with a complete shard set, so a lost
+    meta.json never makes the prune delete every earlier commit."""
     hist = []
-    if prev and prev.get("format") == FORMAT:
-        hist = list(prev.get("history") or ([prev["path"]] if prev.get("path") else []))
+    if prev and prev.get("format") == FORMAT and prev.get("history"):
+        hist = list(prev["history"])
+    else:
+        if prev and prev.get("format") == FORMAT and prev.get("path"):
+            hist = [prev["path"]]
+        if ckpt_dir is not None:
+            hist = sorted(set(hist) | set(_complete_dirs(ckpt_dir)))
     hist = [h for h in hist if h != current] + [current]
     return hist[-max(1, keep):]
 
@@ -115,11 +140,20 @@ def _prune(ckpt_dir: str, history: list[str]) -> None:
     """Remove every step directory that is not one of the retained COMMITTED
     ones: older commits beyond ``keep`` and uncommitted directories left by
     an interrupted save (never counted toward ``keep``, whatever their step
-    number)."""
+    number).  Deleting more than one complete-looking directory at once is
+    logged: that only happens after ``keep`` was lowered or a record was
+    lost."""
     import shutil
-    for d in os.listdir(ckpt_dir):
-        if d.startswith("step-") and d not in history and os.path.isdir(os.path.join(ckpt_dir, d)):
-            shutil.rmtree(os.path.join(ckpt_dir, d), ignore_errors=True)
+    import sys
+    victims = [d for d in os.listdir(ckpt_dir)
+               if d.startswith("step-") and d not in history
+               and os.path.isdir(os.path.join(ckpt_dir, d))]
+    complete = set(_complete_dirs(ckpt_dir)) & set(victims)
+    if len(complete) > 1:
+        print(f"mxk8s.checkpoint: pruning {len(complete)} complete step directories "
+              f"{sorted(complete)} (retained: {history})", file=sys.stderr)
+    for d in victims:
+        shutil.rmtree(os.path.join(ckpt_dir, d), ignore_errors=True)
 
 
 def save(ckpt_dir: str, ddp, opt, step: int, keep: int = 2) -> None:
@@ -142,7 +176,7 @@ def save(ckpt_dir: str, ddp, opt, step: int, keep: int = 2) -> None:
     # every shard is on disk before the commit record names this step
     mxdist.barrier()
     if rank == 0:
-        history = _history(_read_meta(ckpt_dir), sub, keep)
+        history = _history(_read_meta(ckpt_dir), sub, keep, ckpt_dir)
         _write_meta(ckpt_dir, {"step": step, "optimizer_step": opt.step_count, "world_size": world,
                                "sharded": sharded, "layout": fp, "numel": ddp.space.numel,
                                "format": FORMAT, "path": sub, "history": history})

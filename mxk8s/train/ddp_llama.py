@@ -31,6 +31,15 @@ TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning",
                            "tunableop_mi355x_llama3_8b.csv")
 
 
+def library_gemms_in_step() -> bool:
+    """True when an A/B switch routes some product of the step to torch's
+    hipBLASLt / rocBLAS GEMMs (``MXK_WGRAD=0``, ``MXK_DGRAD=0``,
+    ``MXK_FWD_LIB=1``); by default every product runs on the hand-written
+    kernels and no library GEMM is called."""
+    from ..ops import linear
+    return not (linear._USE_MXK_WGRAD and linear._USE_MXK_DGRAD and not linear._FWD_LIB)
+
+
 def use_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
     """Load the PyTorch TunableOp table of the Llama-3-8B step's hipBLASLt /
     rocBLAS GEMMs (fastest solution per shape, found once with
@@ -127,7 +136,10 @@ def run_ddp_bench(args) -> dict:
         model_name = "tiny-llama (test)"
     seq, mb = args.seq_len, args.micro_batch
     bucket_mb = getattr(args, "bucket_mb", 512.0)
-    tuned = False if getattr(args, "no_tuned_gemms", False) else use_tuned_gemms()
+    # the TunableOp table only matters when a library GEMM runs in the step
+    lib_gemms = library_gemms_in_step()
+    tuned = (use_tuned_gemms() if lib_gemms and not getattr(args, "no_tuned_gemms", False)
+             else False)
     zero = not getattr(args, "no_zero", False)
     reduce_dtype = getattr(args, "grad_reduce", "bf16")
     model, ddp, opt = build(cfg, dev, bucket_mb, zero=zero, reduce_dtype=reduce_dtype)
@@ -196,7 +208,7 @@ def run_ddp_bench(args) -> dict:
         "grad_reduce_dtype": reduce_dtype,
         "param_gather": ("overlapped with the next forward" if getattr(opt, "_module_buckets", None)
                          else "in step()") if ddp.sharded else None,
-        "tuned_gemms": tuned,
+        "library_gemms": ({"tunableop_table": tuned} if lib_gemms else None),
         "grad_norm_last": float(opt.last_grad_norm.item()),
         "losses": [round(float(x), 6) for x in torch.stack(losses).float().tolist()] if losses else [],
     }

@@ -63,10 +63,6 @@ class KubeClient:
                 return json.loads(r.read() or b"{}")
         except urllib.error.HTTPError as e:
             raise KubeError(e.code, e.read().decode(errors="replace")[:500]) from None
-        except (OSError, ValueError, AttributeError):
-            if not cancelled:
-                raise
-            return      # cancelled by the caller (connection shut down under the read)
 
     def get(self, path: str) -> dict:
         return self._req("GET", path)
@@ -122,6 +118,10 @@ class KubeClient:
                         yield json.loads(line)
         except urllib.error.HTTPError as e:
             raise KubeError(e.code, e.read().decode(errors="replace")[:500]) from None
+        except (OSError, ValueError, AttributeError):
+            if not cancelled:
+                raise
+            return      # cancelled by the caller (connection shut down under the read)
 
     def create(self, collection: str, obj: dict) -> dict:
         return self._req("POST", collection, obj)

@@ -1745,16 +1745,19 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
   const int nwg = B * Hq * (S / BQ);
   const long span0 = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
   if (variant == 5 && span0 < (1L << 32)) {
-    // delta folded into the dQ kernel, which therefore runs first
+    // delta folded into the dQ kernel, which therefore runs first; its
+    // read-only `delta` argument is null (FOLD writes delta_w, never reads
+    // delta: passing the same buffer as both __restrict__ pointers would be
+    // undefined behaviour the day the kernel reads it)
     auto* dQ5 = static_cast<uint16_t*>(dq);
     const auto* O5 = static_cast<const uint16_t*>(o);
     if (causal)
       hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<true, true, true, false, true>), dim3(nwg), dim3(NT),
-                         0, stream, Q, K, V, dO, lse, delta, dQ5, S, Hq, Hkv, q_tok, k_tok, v_tok,
+                         0, stream, Q, K, V, dO, lse, nullptr, dQ5, S, Hq, Hkv, q_tok, k_tok, v_tok,
                          scale, O5, delta);
     else
       hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<false, true, true, false, true>), dim3(nwg),
-                         dim3(NT), 0, stream, Q, K, V, dO, lse, delta, dQ5, S, Hq, Hkv, q_tok, k_tok,
+                         dim3(NT), 0, stream, Q, K, V, dO, lse, nullptr, dQ5, S, Hq, Hkv, q_tok, k_tok,
                          v_tok, scale, O5, delta);
   } else {
     hipLaunchKernelGGL(mxk_attn_bwd_delta_kernel, dim3((rows * 16 + 255) / 256), dim3(256), 0,

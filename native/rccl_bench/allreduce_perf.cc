@@ -49,6 +49,8 @@
 
 #include <unistd.h>
 
+#include "sweep_plan.h"
+
 namespace {
 
 #define CHECK_HIP(x)                                                              \
@@ -68,41 +70,10 @@ namespace {
     }                                                                             \
   } while (0)
 
-enum class Op { AllReduce, ReduceScatter, AllGather, AllToAll };
-
-const char* op_name(Op op) {
-  switch (op) {
-    case Op::AllReduce: return "allreduce";
-    case Op::ReduceScatter: return "reducescatter";
-    case Op::AllGather: return "allgather";
-    default: return "alltoall";
-  }
-}
-
-double bus_factor(Op op, int n) {
-  if (n <= 1) return 0.0;
-  return op == Op::AllReduce ? 2.0 * (n - 1) / n : double(n - 1) / n;
-}
-
-size_t parse_size(const char* s) {
-  char* end = nullptr;
-  double v = std::strtod(s, &end);
-  switch (end && *end ? *end : ' ') {
-    case 'K': case 'k': v *= 1024.0; break;
-    case 'M': case 'm': v *= 1024.0 * 1024.0; break;
-    case 'G': case 'g': v *= 1024.0 * 1024.0 * 1024.0; break;
-    default: break;
-  }
-  return static_cast<size_t>(v);
-}
-
-std::vector<int> parse_list(const char* s) {
-  std::vector<int> v;
-  std::stringstream ss(s);
-  std::string x;
-  while (std::getline(ss, x, ',')) if (!x.empty()) v.push_back(std::atoi(x.c_str()));
-  return v;
-}
+using mxrb::Op;
+using mxrb::Shape;
+using mxrb::bus_factor;
+using mxrb::op_name;
 
 __global__ void fill_value(void* p, size_t n, float v, int is_bf16) {
   for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
@@ -145,38 +116,14 @@ unsigned long long mismatches(Op op, const void* rb, size_t recv, size_t count, 
   unsigned long long h = 0;
   CHECK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(h), st));
   CHECK_HIP(hipMemsetAsync(d, 0, sizeof(h), st));
-  const size_t chunk = (op == Op::AllReduce || op == Op::ReduceScatter) ? 0 : count;
-  hipLaunchKernelGGL(count_mismatch, dim3(1024), dim3(256), 0, st, rb, recv, chunk,
-                     n * (n + 1) / 2.0f, int(bf16), d);
+  const mxrb::CheckParams c = mxrb::check_params(op, Shape{count, 0, recv}, n);
+  hipLaunchKernelGGL(count_mismatch, dim3(1024), dim3(256), 0, st, rb, recv, c.chunk, c.sum,
+                     int(bf16), d);
   CHECK_HIP(hipGetLastError());
   CHECK_HIP(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, st));
   CHECK_HIP(hipFreeAsync(d, st));
   CHECK_HIP(hipStreamSynchronize(st));
   return h;
-}
-
-int iters_for(size_t bytes, int base) {
-  // keep a point under ~1 s: large messages need fewer iterations
-  if (bytes >= (size_t(1) << 31)) return std::max(3, base / 4);
-  if (bytes >= (size_t(1) << 29)) return std::max(5, base / 2);
-  return base;
-}
-
-// Element counts of one sweep point: `chunk` = per-peer block, send/recv =
-// per-rank buffer elements; `count` is what the RCCL call takes.
-struct Shape {
-  size_t count, send, recv;
-};
-
-Shape shape_for(Op op, size_t bytes, size_t esz, int n) {
-  size_t elems = std::max<size_t>(1, bytes / esz);
-  if (op == Op::AllReduce) return {elems, elems, elems};
-  const size_t chunk = std::max<size_t>(1, elems / n);
-  switch (op) {
-    case Op::ReduceScatter: return {chunk, chunk * n, chunk};
-    case Op::AllGather: return {chunk, chunk, chunk * n};
-    default: return {chunk, chunk * n, chunk * n};   // all-to-all: count per pair
-  }
 }
 
 void issue(Op op, const void* sb, void* rb, const Shape& s, ncclDataType_t dt, ncclComm_t comm,
@@ -230,9 +177,8 @@ bool sweep_single(const Opts& o, Op op, int n, double* peak_busbw) {
   bool ok = true;
   std::printf("# %s n=%d  %14s %8s %12s %12s %12s %6s\n", op_name(op), n, "bytes", "type",
               "time(us)", "algbw(GB/s)", "busbw(GB/s)", "check");
-  for (size_t bytes = o.minb; bytes <= o.maxb; bytes *= o.factor) {
-    const Shape s = shape_for(op, bytes, esz, n);
-    if (std::max(s.send, s.recv) * esz > o.maxb) continue;   // tiny sizes x many ranks
+  for (const mxrb::Point& pt : mxrb::sweep_points(op, o.minb, o.maxb, o.factor, esz, n, o.iters)) {
+    const Shape& s = pt.shape;
     auto launch = [&]() {
       CHECK_NCCL(ncclGroupStart());
       for (int g = 0; g < n; ++g) issue(op, sb[g], rb[g], s, o.dt(), comms[g], st[g]);
@@ -243,7 +189,7 @@ bool sweep_single(const Opts& o, Op op, int n, double* peak_busbw) {
     };
     for (int w = 0; w < o.warmup; ++w) launch();
     sync();
-    const int it = iters_for(bytes, o.iters);
+    const int it = pt.iters;
     roctxRangePushA(op_name(op));
     auto t0 = std::chrono::steady_clock::now();
     for (int i = 0; i < it; ++i) launch();
@@ -256,10 +202,9 @@ bool sweep_single(const Opts& o, Op op, int n, double* peak_busbw) {
       good &= check_recv(op, rb[g], s, n, o.bf16, st[g]);
     }
     ok &= good;
-    const size_t sbytes = std::max(s.send, s.recv) * esz;
+    const size_t sbytes = pt.reported;
     *peak_busbw = std::max(*peak_busbw, double(sbytes) / t / 1e9 * bus_factor(op, n));
     print_point(op, n, "single", sbytes, o, t, good);
-    if (bytes > o.maxb / o.factor) break;
   }
   for (int g = 0; g < n; ++g) {
     CHECK_HIP(hipSetDevice(g));
@@ -362,12 +307,12 @@ bool sweep_multiproc(const Opts& o, int rank, int world, int local) {
   bool ok = true;
   for (Op op : o.ops) {
     double peak = 0;
-    for (size_t bytes = o.minb; bytes <= o.maxb; bytes *= o.factor) {
-      const Shape s = shape_for(op, bytes, esz, world);
-      if (std::max(s.send, s.recv) * esz > o.maxb) continue;
+    for (const mxrb::Point& pt : mxrb::sweep_points(op, o.minb, o.maxb, o.factor, esz, world,
+                                                   o.iters)) {
+      const Shape& s = pt.shape;
       for (int w = 0; w < o.warmup; ++w) issue(op, sb, rb, s, o.dt(), comm, st);
       CHECK_HIP(hipStreamSynchronize(st));
-      const int it = iters_for(bytes, o.iters);
+      const int it = pt.iters;
       roctxRangePushA(op_name(op));
       auto t0 = std::chrono::steady_clock::now();
       for (int i = 0; i < it; ++i) issue(op, sb, rb, s, o.dt(), comm, st);
@@ -388,10 +333,9 @@ bool sweep_multiproc(const Opts& o, int rank, int world, int local) {
       }
       const bool good = bad == 0;
       ok &= good;
-      const size_t sbytes = std::max(s.send, s.recv) * esz;
+      const size_t sbytes = pt.reported;
       peak = std::max(peak, double(sbytes) / t / 1e9 * bus_factor(op, world));
       if (rank == 0) print_point(op, world, "multiproc", sbytes, o, t, good);
-      if (bytes > o.maxb / o.factor) break;
     }
     if (rank == 0)
       std::printf("RESULT {\"test\":\"%s_summary\",\"ngpus\":%d,\"peak_busbw_GBps\":%.3f}\n",
@@ -404,41 +348,23 @@ bool sweep_multiproc(const Opts& o, int rank, int world, int local) {
   return ok;
 }
 
-bool parse_ops(const char* s, std::vector<Op>* out) {
-  out->clear();
-  std::stringstream ss(s);
-  std::string x;
-  while (std::getline(ss, x, ',')) {
-    if (x == "all") {
-      *out = {Op::AllReduce, Op::ReduceScatter, Op::AllGather, Op::AllToAll};
-      return true;
-    }
-    if (x == "allreduce") out->push_back(Op::AllReduce);
-    else if (x == "reducescatter") out->push_back(Op::ReduceScatter);
-    else if (x == "allgather") out->push_back(Op::AllGather);
-    else if (x == "alltoall") out->push_back(Op::AllToAll);
-    else return false;
-  }
-  return !out->empty();
-}
-
 }  // namespace
 
 int main(int argc, char** argv) {
   Opts o;
   for (int i = 1; i < argc; ++i) {
-    if (!std::strcmp(argv[i], "-b") && i + 1 < argc) o.minb = parse_size(argv[++i]);
-    else if (!std::strcmp(argv[i], "-e") && i + 1 < argc) o.maxb = parse_size(argv[++i]);
+    if (!std::strcmp(argv[i], "-b") && i + 1 < argc) o.minb = mxrb::parse_size(argv[++i]);
+    else if (!std::strcmp(argv[i], "-e") && i + 1 < argc) o.maxb = mxrb::parse_size(argv[++i]);
     else if (!std::strcmp(argv[i], "-f") && i + 1 < argc) o.factor = std::max(2, std::atoi(argv[++i]));
     else if (!std::strcmp(argv[i], "-g") && i + 1 < argc) o.ngpus = std::atoi(argv[++i]);
-    else if (!std::strcmp(argv[i], "--scaling") && i + 1 < argc) o.scaling = parse_list(argv[++i]);
+    else if (!std::strcmp(argv[i], "--scaling") && i + 1 < argc) o.scaling = mxrb::parse_list(argv[++i]);
     else if (!std::strcmp(argv[i], "--dtype") && i + 1 < argc) o.bf16 = !std::strcmp(argv[++i], "bf16");
     else if (!std::strcmp(argv[i], "--iters") && i + 1 < argc) o.iters = std::max(1, std::atoi(argv[++i]));
     else if (!std::strcmp(argv[i], "--warmup") && i + 1 < argc) o.warmup = std::max(0, std::atoi(argv[++i]));
     else if (!std::strcmp(argv[i], "--id-file") && i + 1 < argc) o.id_file = argv[++i];
     else if (!std::strcmp(argv[i], "--nonce") && i + 1 < argc) o.nonce = argv[++i];
     else if (!std::strcmp(argv[i], "--op") && i + 1 < argc) {
-      if (!parse_ops(argv[++i], &o.ops)) { std::fprintf(stderr, "bad --op %s\n", argv[i]); return 2; }
+      if (!mxrb::parse_ops(argv[++i], &o.ops)) { std::fprintf(stderr, "bad --op %s\n", argv[i]); return 2; }
     } else { std::fprintf(stderr, "unknown argument %s\n", argv[i]); return 2; }
   }
   if (o.minb < 1 || o.maxb < o.minb) { std::fprintf(stderr, "bad size range\n"); return 2; }

@@ -527,3 +527,31 @@ def test_allreduce_fp32_wire_ring_staging():
         big = exact.abs() > 1e-3 * exact.abs().max()
         rel = ((reduced.double() - exact).abs()[big] / exact.abs()[big]).max().item()
         assert rel <= 2.0 ** -8, rel                                 # one bf16 rounding
+
+
+def _frozen_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = torch.nn.Linear(4, 4).to(torch.bfloat16)
+    for p in m.parameters():
+        p.requires_grad_(False)
+    try:
+        FlatDDP(m, reduce_dtype="fp32", stage_slots=3)
+        msg = "constructed"
+    except ValueError as e:                 # a clear error, not a max() of an empty list
+        msg = str(e)
+    torch.save({"msg": msg}, os.path.join(outdir, f"f{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_fp32_wire_without_trainable_params():
+    """no trainable parameters means no buckets; the fp32 staging
+    ring must not be sized from the empty list (a clear ValueError instead)."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_frozen_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        z = [torch.load(os.path.join(d, f"f{i}.pt"), weights_only=True) for i in range(world)]
+    assert all("no trainable parameters" in r["msg"] for r in z), z

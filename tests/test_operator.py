@@ -333,3 +333,38 @@ def test_wait_for_change_leaves_no_watch_threads_behind(api):
         assert ctl.wait_for_change(60.0).startswith("watch:")
         assert live() == [], live()
     assert ctl.wait_for_change(0.5) == "resync" and live() == []
+
+
+def test_mutating_policy_replace_loop_backs_off_and_names_drift(api, caplog):
+    """A mutating admission policy (Kyverno-style) re-adds a container env var
+    after every replace: the controller replaces once, then backs off
+    (pending) instead of replacing on every pass, and logs which names
+    drifted so the admin can pass --injected-name."""
+    import logging
+    _policy(api)
+    ctl = op.Controller(KubeClient(api.url), NS, replace_backoff_s=0.3)
+    ctl.reconcile_once()
+    path = f"{DS}/amd-gpu-stack-device-plugin"
+    name = "DaemonSet/amd-gpu-stack-device-plugin"
+
+    def mutate():
+        c = api.objects[path]["spec"]["template"]["spec"]["containers"][0]
+        c.setdefault("env", []).append({"name": "KYVERNO_INJECTED", "value": "1"})
+
+    mutate()
+    with caplog.at_level(logging.WARNING):
+        r1 = ctl.reconcile_once()
+    assert name in r1.updated
+    assert any("KYVERNO_INJECTED" in rec.getMessage() for rec in caplog.records)
+    mutate()                                   # the webhook mutates the replaced object again
+    r2 = ctl.reconcile_once()
+    assert name not in r2.updated and name in r2.pending
+    time.sleep(0.35)
+    r3 = ctl.reconcile_once()                  # backoff expired: replaced again
+    assert name in r3.updated
+    mutate()
+    r4 = ctl.reconcile_once()                  # second backoff is twice as long
+    assert name in r4.pending
+    # with the name allow-listed there is no drift at all
+    ctl2 = op.Controller(KubeClient(api.url), NS, injected=["KYVERNO_"])
+    assert name not in ctl2.reconcile_once().updated

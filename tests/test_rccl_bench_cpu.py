@@ -36,3 +36,22 @@ def test_multiproc_requires_nonce(tmp_path):
     p = subprocess.run([BIN, "--id-file", str(tmp_path / "id")], env=env, capture_output=True,
                        text=True, timeout=60)
     assert p.returncode == 1 and "no job nonce" in p.stderr
+
+
+def test_sweep_plan_all_ops_host(tmp_path):
+    """mx-allreduce-perf's size list, shapes, bus factors, iteration counts
+    and whole-buffer mismatch chunking for all four ops at n = 1, 2, 4, 8
+    (native/rccl_bench/sweep_plan.h, the logic the first 8-GPU run takes),
+    compiled for the host under ASan + UBSan and run against collectives
+    simulated from their definitions."""
+    import shutil
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no host C++ compiler")
+    exe = str(tmp_path / "test_sweep_plan")
+    src = os.path.join(REPO, "native", "rccl_bench", "tests", "test_sweep_plan.cc")
+    subprocess.run([cxx, "-std=c++17", "-O1", "-Wall", "-Wextra", "-Werror",
+                    "-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-o", exe, src],
+                   check=True, timeout=300)
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "PASS sweep_plan" in p.stdout, p.stderr[-3000:]
