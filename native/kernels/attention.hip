@@ -670,7 +670,11 @@ mxk_attn_bwd_delta_kernel(const uint16_t* __restrict__ o, const uint16_t* __rest
 // delta = dO . O is computed here from the row's own dO fragments and O (the
 // two lanes of a row hold 64 columns each) and written to delta_w for the
 // dK/dV kernel, which then runs after this one; no separate delta kernel.
-template <bool CAUSAL, bool DMA = false, bool PIPE = false, bool UNROLL = false, bool FOLD = false>
+// ROWC (with FOLD; backward variant 6): instead of delta, write the row
+// pair {-lse/scale, -delta} that the 256-key dK/dV kernel
+// (attention_bwd256.hip) loads as the initial S' / dP' accumulators.
+template <bool CAUSAL, bool DMA = false, bool PIPE = false, bool UNROLL = false, bool FOLD = false,
+          bool ROWC = false>
 __global__ void __launch_bounds__(NT, 2)
 mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                        const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
@@ -721,7 +725,12 @@ mxk_attn_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
         part += mxk::bf2f(static_cast<uint16_t>(dof[s][e])) * mxk::bf2f(static_cast<uint16_t>(of[e]));
     }
     dlt = part + __shfl_xor(part, 32);       // the row's other 64 columns
-    if (h == 0) delta_w[lrow] = dlt;
+    if constexpr (ROWC) {
+      if (h == 0)
+        *reinterpret_cast<float2*>(delta_w + 2 * lrow) = make_float2(-lse[lrow] / scale, -dlt);
+    } else {
+      if (h == 0) delta_w[lrow] = dlt;
+    }
   } else {
     dlt = delta[lrow];
   }
@@ -1705,6 +1714,7 @@ mxk_attn_bwd_gqa_reduce_kernel(const float* __restrict__ dk_p, const float* __re
 // variant 0, the per-query-head dK/dV kernel).
 MXK_API long mxk_attn_bwd_workspace_variant(int B, int S, int Hq, int variant) {
   const long rows = static_cast<long>(B) * Hq * S;
+  if (variant == 6) return rows * 8;   // {-lse/scale, -delta} row pairs
   return rows * 4 + (variant == 0 ? 2 * rows * D * 4 : 0);
 }
 MXK_API long mxk_attn_bwd_workspace(int B, int S, int Hq) {
@@ -1725,7 +1735,7 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
                                  long q_tok, long k_tok, long v_tok, long dk_tok, long dv_tok,
                                  float scale, int causal, int variant, hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv || q_tok % 8 ||
-      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 5 ||
+      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 6 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
        reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
@@ -1744,6 +1754,29 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
   auto* dV = static_cast<uint16_t*>(dv);
   const int nwg = B * Hq * (S / BQ);
   const long span0 = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
+  if (variant == 6) {
+    // dQ with the delta pass folded in, writing {-lse/scale, -delta} rows,
+    // then dK / dV with 256 keys per workgroup (attention_bwd256.hip)
+    const long qspan6 = static_cast<long>(S) * (q_tok > static_cast<long>(Hq) * D ? q_tok : Hq * D) * 2;
+    if (S % 256 == 0 && span0 < (1L << 32) && qspan6 < (1L << 32)) {
+      float* rowc = static_cast<float*>(workspace);
+      auto* dQ6 = static_cast<uint16_t*>(dq);
+      const auto* O6 = static_cast<const uint16_t*>(o);
+      if (causal)
+        hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<true, true, true, false, true, true>), dim3(nwg),
+                           dim3(NT), 0, stream, Q, K, V, dO, lse, nullptr, dQ6, S, Hq, Hkv, q_tok,
+                           k_tok, v_tok, scale, O6, rowc);
+      else
+        hipLaunchKernelGGL((mxk_attn_bwd_dq_kernel<false, true, true, false, true, true>),
+                           dim3(nwg), dim3(NT), 0, stream, Q, K, V, dO, lse, nullptr, dQ6, S, Hq,
+                           Hkv, q_tok, k_tok, v_tok, scale, O6, rowc);
+      const int st = static_cast<int>(hipGetLastError());
+      if (st) return st;
+      return mxk_attn_bwd_dkdv256(q, k, v, dout, rowc, dk, dv, B, S, Hq, Hkv, q_tok, k_tok, v_tok,
+                                  dk_tok, dv_tok, scale, causal, stream);
+    }
+    variant = 5;   // layout the 256-key kernel does not take
+  }
   if (variant == 5 && span0 < (1L << 32)) {
     // delta folded into the dQ kernel, which therefore runs first; its
     // read-only `delta` argument is null (FOLD writes delta_w, never reads

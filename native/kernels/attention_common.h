@@ -119,3 +119,9 @@ __device__ __forceinline__ void map_block_xcd(int w, int nwg, int nqb, int grp, 
 namespace {
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 }
+
+// dK / dV with 256 keys per workgroup (attention_bwd256.hip; backward variant 6)
+MXK_API int mxk_attn_bwd_dkdv256(const void* q, const void* k, const void* v, const void* dout,
+                                 const float* rowc, void* dk, void* dv, int B, int S, int Hq,
+                                 int Hkv, long q_tok, long k_tok, long v_tok, long dk_tok,
+                                 long dv_tok, float scale, int causal, hipStream_t stream);

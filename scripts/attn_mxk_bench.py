@@ -52,6 +52,7 @@ def main():
     res["mxk_bwd"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True))
     res["mxk_bwd_v3"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=3))
     res["mxk_bwd_v5"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=5))
+    res["mxk_bwd_v6"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=6))
     qg, kg, vg = (t.detach().transpose(1, 2).requires_grad_() for t in (q, k, v))
     dot = do.transpose(1, 2)
 

@@ -74,7 +74,7 @@ def test_attn_bwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
         assert err < tol, (name, err, tol)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
     (1, 256, 8, 2, True),
     (2, 384, 4, 1, True),
@@ -106,3 +106,43 @@ def test_attn_bwd_variants_into_strided_dkdv(cuda_device, B, S, Hq, Hkv, causal,
         ref5 = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, variant=5)
         for a3, a5 in zip(ref3, ref5):
             assert (a3.float() - a5.float()).abs().max().item() <= 1e-2 * max(1.0, a3.float().abs().max().item())
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
+    (1, 256, 4, 4, False),     # one key block, no GQA
+    (2, 512, 8, 2, True),      # two key blocks: a masked wave per diagonal slice
+    (1, 1024, 8, 1, True),     # MQA: all 8 query heads swept by one workgroup
+    (1, 768, 4, 2, False),     # three key blocks, full attention
+    (1, 2048, 32, 8, True),    # the Llama-3-8B shape (B = 1)
+])
+def test_attn_bwd_dkdv256_v6(cuda_device, B, S, Hq, Hkv, causal):
+    """Backward variant 6: the 256-key-per-workgroup dK/dV kernel
+    (attention_bwd256.hip, dK^T / dV^T in the accumulator file, S / dP with
+    the key on the lane, -LSE/scale and -delta as the initial accumulators)
+    after the delta-folded dQ kernel.  dK / dV vs the fp32 reference into
+    strided slices of a fused buffer; bit-identical across two runs (no
+    atomics anywhere); dQ bit-identical to variant 5 (same kernel, only the
+    row constants it stores differ)."""
+    q, k, v = _qkv(B, S, Hq, Hkv, cuda_device, seed=11, fused=True)
+    o, lse = A.attn_fwd(q, k, v, causal=causal)
+    g = torch.Generator(device=cuda_device).manual_seed(13)
+    dout = torch.randn(B, S, Hq, 128, device=cuda_device, generator=g).bfloat16()
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    A.attention_ref(qr, kr, vr, causal=causal).backward(dout.float())
+    fused = torch.full((B, S, (Hq + 2 * Hkv) * 128), float("nan"), device=cuda_device,
+                       dtype=torch.bfloat16)
+    dk = fused[..., Hq * 128:(Hq + Hkv) * 128].view(B, S, Hkv, 128)
+    dv = fused[..., (Hq + Hkv) * 128:].view(B, S, Hkv, 128)
+    dq, _, _ = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, dk=dk, dv=dv, variant=6)
+    for name, got, want in (("dq", dq, qr.grad), ("dk", dk, kr.grad), ("dv", dv, vr.grad)):
+        assert not torch.isnan(got).any(), name
+        err = (got.float() - want).abs().max().item()
+        tol = 3e-2 * max(1.0, want.abs().max().item())
+        assert err < tol, (name, err, tol)
+    again = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, variant=6)
+    assert torch.equal(again[0], dq) and torch.equal(again[1], dk) and torch.equal(again[2], dv)
+    v5 = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, variant=5)
+    assert torch.equal(v5[0], dq)
+    for a5, a6 in zip(v5[1:], (dk, dv)):       # same math, other summation order
+        scale_ = max(1.0, a5.float().abs().max().item())
+        assert (a5.float() - a6.float()).abs().max().item() <= 1e-2 * scale_

@@ -69,6 +69,72 @@ def close_accumulator_reads(asm: str) -> dict[str, int]:
     return bad
 
 
+def _regs(text: str) -> set[int]:
+    out = set()
+    for m in re.finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", text):
+        lo = int(m.group(1) or m.group(3))
+        hi = int(m.group(2) or m.group(3))
+        out.update(range(lo, hi + 1))
+    return out
+
+
+def close_vgpr_result_reads(asm: str, states: int = 12) -> dict[str, int]:
+    """Reads of an MFMA's VGPR result (``v_mfma ... v[a:b], ...``) by any
+    instruction other than the next MFMA of its chain within ``states`` wait
+    states (``s_nop N`` counts N + 1).  The 256-key attention backward keeps
+    S / dP in VGPRs through inline-asm MFMAs, which hipcc does not pad: the
+    VALU softmax must not read them early (8-pass XDL -> VALU: 12 states)."""
+    bad = {}
+    for name in re.findall(r"^(_Z[^\s:]+):", asm, re.M):
+        i = asm.find(name + ":")
+        j = asm.find(".Lfunc_end", i)
+        body = [ln.split(";")[0].strip() for ln in asm[i:j].split("\n")]
+        body = [ln for ln in body if ln and not ln.startswith(".") and not ln.endswith(":")]
+        pend: dict[int, int] = {}
+        n = 0
+        for ln in body:
+            op, _, rest = ln.partition(" ")
+            if op.startswith("v_mfma"):
+                dst, _, srcs = rest.partition(",")
+                # the chain's next MFMA may take the result whole as C
+                pend = {r: c + 1 for r, c in pend.items() if r not in _regs(srcs.rsplit(",", 1)[0])
+                        or c >= states}
+                if dst.strip().startswith("v"):
+                    for r in _regs(dst):
+                        pend[r] = 0
+                continue
+            m = re.match(r"s_nop (\d+)", ln)
+            step = int(m.group(1)) + 1 if m else 1
+            if any(pend.get(r, states) < states for r in _regs(rest)):
+                n += 1
+            pend = {r: c + step for r, c in pend.items() if c + step < states}
+        if n:
+            bad[name] = n
+    return bad
+
+
+def test_detector_flags_a_close_vgpr_result_read():
+    asm = ("_Zbaz:\n\tv_mfma_f32_32x32x16_bf16 v[0:15], v[16:19], v[20:23], v[0:15]\n"
+           "\tv_mfma_f32_32x32x16_bf16 v[0:15], v[24:27], v[28:31], v[0:15]\n"
+           "\tv_mul_f32_e32 v40, 0x3fb8aa3b, v3\n.Lfunc_end0:\n")
+    assert close_vgpr_result_reads(asm) == {"_Zbaz": 1}
+    safe = asm.replace("\tv_mul", "\ts_nop 7\n\ts_nop 4\n\tv_mul")
+    assert close_vgpr_result_reads(safe) == {}
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_attention_bwd256_asm_mfma_hazards_and_spills(tmp_path):
+    """attention_bwd256.hip: dK^T / dV^T pinned to AGPRs and S / dP to VGPRs
+    by inline-asm MFMAs; no early read of either, and no spill (its Q / dO
+    ring waits are counted vmcnt waits)."""
+    asm = _asm("attention_bwd256.hip", str(tmp_path / "b256.s"))
+    assert "v_mfma" in asm
+    assert close_accumulator_reads(asm) == {}
+    assert close_vgpr_result_reads(asm) == {}
+    counts = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s+(\d+)", asm)]
+    assert counts and not any(counts)
+
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src,flags", [("gemm_bf16.hip", ()), ("gemm_bf16_layouts.hip", ()),
                                        ("experiments/gemm_tn_exp.hip", ("-DMXK_GEMM_EXPERIMENTS",))])
