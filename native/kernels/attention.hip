@@ -1715,6 +1715,7 @@ mxk_attn_bwd_gqa_reduce_kernel(const float* __restrict__ dk_p, const float* __re
 MXK_API long mxk_attn_bwd_workspace_variant(int B, int S, int Hq, int variant) {
   const long rows = static_cast<long>(B) * Hq * S;
   if (variant == 6) return rows * 8;   // {-lse/scale, -delta} row pairs
+  if (variant == 7 || variant == 8) return mxk_attn_bwd_onepass_workspace(B, S, Hq, variant == 8);
   return rows * 4 + (variant == 0 ? 2 * rows * D * 4 : 0);
 }
 MXK_API long mxk_attn_bwd_workspace(int B, int S, int Hq) {
@@ -1735,7 +1736,7 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
                                  long q_tok, long k_tok, long v_tok, long dk_tok, long dv_tok,
                                  float scale, int causal, int variant, hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv || q_tok % 8 ||
-      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 6 ||
+      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 8 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
        reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
@@ -1754,6 +1755,13 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
   auto* dV = static_cast<uint16_t*>(dv);
   const int nwg = B * Hq * (S / BQ);
   const long span0 = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
+  if ((variant == 7 || variant == 8) && S % 256 == 0) {
+    // one pass (attention_bwd256.hip): dQ by fp32 (7) or packed-bf16 (8)
+    // atomics from the 256-key workgroups; not bit-reproducible
+    return mxk_attn_bwd_onepass(q, k, v, o, dout, lse, dq, dk, dv, workspace, B, S, Hq, Hkv, q_tok,
+                                k_tok, v_tok, dk_tok, dv_tok, scale, causal, variant == 8, stream);
+  }
+  if (variant == 7 || variant == 8) variant = 5;
   if (variant == 6) {
     // dQ with the delta pass folded in, writing {-lse/scale, -delta} rows,
     // then dK / dV with 256 keys per workgroup (attention_bwd256.hip)

@@ -58,6 +58,11 @@ constexpr int KIMG = KBLK * 256;              // 64 KiB
 // ring first: every ring offset (< 49920) fits a ds_read's 16-bit immediate
 constexpr int KOFF = NSLOT * SLOT;             // K image after the ring
 constexpr int LDS_BYTES = KOFF + KIMG;
+// one-pass variants (DQ != 0): the workgroup's dS (32 queries x 256 keys,
+// bf16) is exchanged through a double-buffered LDS image for the dQ product
+constexpr int DSOFF = KOFF + KIMG;
+constexpr int DSIMG = QS * 512;               // 16 KiB: [32 q][256 key positions]
+constexpr int LDS_BYTES_DQ = DSOFF + 2 * DSIMG;
 
 __device__ __forceinline__ void dma4m(const mxk::u32x4& rsrc, uint32_t lds_addr, uint32_t voff,
                                       uint32_t soff) {
@@ -100,6 +105,9 @@ __device__ __forceinline__ void mfma_v(f32x16_t& acc, const bf16x8_t& a, const b
 __device__ __forceinline__ void mfma_result_fence(f32x16_t& x, f32x16_t& y) {
   asm volatile("s_nop 7\n\ts_nop 4" : "+v"(x), "+v"(y));
 }
+__device__ __forceinline__ void mfma_result_fence1(f32x16_t& x) {
+  asm volatile("s_nop 7\n\ts_nop 4" : "+v"(x));
+}
 __device__ __forceinline__ void mfma_operands_ready(const bf16x8_t (&pf)[2], const bf16x8_t (&sf)[2]) {
   asm volatile("s_nop 2" ::"v"(pf[0]), "v"(pf[1]), "v"(sf[0]), "v"(sf[1]));
 }
@@ -115,6 +123,37 @@ __device__ __forceinline__ void mfma_drain_acc(f32x16_t (&x)[NI][NJ], f32x16_t (
     for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(x[i][j]), "+a"(y[i][j]));
 }
 
+// s_waitcnt vmcnt(n) for the few counts the ring uses (n: ring pieces plus
+// the dQ atomics issued after the awaited piece); anything else waits for all
+__device__ __forceinline__ void vm_wait_n(int n) {
+  switch (n) {
+    case 4: vm_wait<4>(); break;
+    case 5: vm_wait<5>(); break;
+    case 8: vm_wait<8>(); break;
+    case 12: vm_wait<12>(); break;
+    case 13: vm_wait<13>(); break;
+    case 16: vm_wait<16>(); break;
+    case 20: vm_wait<20>(); break;
+    case 21: vm_wait<21>(); break;
+    case 32: vm_wait<32>(); break;
+    case 36: vm_wait<36>(); break;
+    case 37: vm_wait<37>(); break;
+    default: vm_wait<0>(); break;
+  }
+}
+// the ring's barrier: LDS traffic retired, then s_barrier (no vmcnt wait:
+// __syncthreads() would drain the dQ atomics, and with them the DMA ring)
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+}
+// key position in the dS image: bits 2 and 3 of the key swapped, so that a
+// row read of 8 consecutive positions yields the keys in the order the
+// transposed K reads (the V^T pattern of the forward) deliver them
+__device__ __forceinline__ int dspos(int key) {
+  return (key & ~12) | ((key & 4) << 1) | ((key & 8) >> 1);
+}
+
 __device__ __forceinline__ void zero16(f32x16_t& x) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) x[r] = 0.f;
@@ -125,14 +164,23 @@ __device__ __forceinline__ void zero16(f32x16_t& x) {
 // Heaviest key blocks first (causal: block kb has S - 256 kb query rows per
 // head): with two rounds of workgroups per CU that is the longest-job-first
 // order, which balances exactly at Llama's 8 key blocks.
-template <bool CAUSAL>
+//
+// DQ (one-pass variants 7 / 8): the same workgroup also computes its 256
+// keys' share of dQ = dS K: each wave writes its dS (bf16) into an LDS image
+// [32 queries][256 key positions], and one item later (after the item's
+// barrier) wave w multiplies the whole 256-key dS by K[., 32 w .. 32 w + 31]
+// (transposed reads of the resident K image) and adds the 32 x 32 result to
+// global memory: DQ 1 fp32 atomics into dq_acc [B, S, Hq, 128] (then a
+// convert pass), DQ 2 packed-bf16 atomics straight into dq (scaled here).
+template <bool CAUSAL, int DQ = 0>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                             const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
                             const float* __restrict__ rowc, uint16_t* __restrict__ dk,
                             uint16_t* __restrict__ dv, int S, int Hq, int Hkv, long q_tok,
-                            long k_tok, long v_tok, long dk_tok, long dv_tok, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+                            long k_tok, long v_tok, long dk_tok, long dv_tok, float scale,
+                            void* __restrict__ dqo = nullptr) {
+  __shared__ __attribute__((aligned(16))) char smem[DQ ? LDS_BYTES_DQ : LDS_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -252,6 +300,86 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     roff[s] = swz(r32, 2 * s + h);
     koff[s] = KOFF + wave * KW * 256 + roff[s];
   }
+  // DQ: dS image writes (per key tile kt and row class j & 3; + (2 s2 +
+  // (j >> 2)) * 4096 immediates), reads of the A operand of dQ (per key
+  // step class s'' & 3; + (s'' >> 2) * 128), transposed reads of K as the B
+  // operand (d = 32 wave + r32; + s'' * 4096)
+  int dsw[2][4] = {}, dsr[4] = {}, ktr0 = 0, ktr1 = 0;
+  if constexpr (DQ != 0) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int pos = dspos(wave * KW + 32 * kt + r32);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int q7 = jj + 4 * h;
+        dsw[kt][jj] = DSOFF + q7 * 512 + (((pos >> 3) ^ q7) << 4) + (pos & 7) * 2;
+      }
+    }
+    const int m = (r32 >> 1) & 3;
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl)
+      dsr[sl] = DSOFF + r32 * 512 + ((2 * (sl ^ m) + (h ^ (r32 & 1))) << 4);
+    ktr0 = KOFF + swz(tr_row, 4 * wave + tr_ch) + tr_byte;
+    ktr1 = KOFF + swz(tr_row + 8, 4 * wave + tr_ch) + tr_byte;
+  }
+
+  // DQ: item j's share of dQ - rows qs0 .. qs0 + 31 of head gq, columns
+  // 32 wave .. + 31 - from the whole workgroup's dS image (buffer j & 1)
+  auto dq_item = [&](int j) {
+    const int gq = j / nsl;
+    const int qs0 = q_begin + (j - gq * nsl) * QS;
+    const int buf = (j & 1) * DSIMG;
+    // key steps holding an unmasked key (a fully masked wave wrote nothing)
+    const int s_end = CAUSAL ? min(16, (qs0 + QS - k0 + 15) >> 4) : 16;
+    f32x16_t acc;
+    zero16(acc);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (t < s_end) {
+        const bf16x8_t a = lds_b128(smem + buf + dsr[t & 3] + (t >> 2) * 128);
+        const bf16x8_t bk = cat8(lds_tr_b64(smem + ktr0 + t * 4096), lds_tr_b64(smem + ktr1 + t * 4096));
+        if (t == 0) mfma_v<true>(acc, a, bk);
+        else mfma_v(acc, a, bk);
+      }
+      if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // bound the operand look-ahead
+    }
+    mfma_result_fence1(acc);
+    // wave-uniform row base + one lane offset, so the atomics take the
+    // SGPR-base + VGPR-offset form (no 64-bit address per register)
+    const long row0 = (static_cast<long>(b) * S + qs0) * Hq + hq0 + gq;   // (b, qs0, head)
+    const long rstride = static_cast<long>(Hq) * D;                       // elements per token
+    if constexpr (DQ == 1) {
+      float* rb = static_cast<float*>(dqo) + row0 * D;
+      const uint32_t lo = static_cast<uint32_t>(4 * h * rstride + 32 * wave + r32);
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        __hip_atomic_fetch_add(rb + ((r & 3) + 8 * (r >> 2)) * rstride + lo, acc[r],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      // packed bf16 pairs: lanes 2m and 2m + 1 swap one value of a register
+      // pair, so the even lane holds columns (2m, 2m + 1) of row crow(r) and
+      // the odd lane the same columns of row crow(r + 1)
+      typedef short s2_t __attribute__((ext_vector_type(2)));
+      uint16_t* rb = static_cast<uint16_t*>(dqo) + row0 * D;
+      const bool odd = r32 & 1;
+      const uint32_t lo = static_cast<uint32_t>((4 * h + (odd ? 1 : 0)) * rstride + 32 * wave +
+                                                (r32 & ~1));
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float x = odd ? acc[r] : acc[r + 1];
+        const float y = __builtin_bit_cast(
+            float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, true));
+        const float vlo = odd ? y : acc[r];
+        const float vhi = odd ? acc[r + 1] : y;
+        const uint32_t pk = mxk::pack2bf(vlo * scale, vhi * scale);
+        __builtin_amdgcn_global_atomic_fadd_v2bf16(
+            reinterpret_cast<s2_t*>(rb + ((r & 3) + 8 * (r >> 2)) * rstride + lo),
+            __builtin_bit_cast(s2_t, pk));
+      }
+    }
+  };
+  constexpr int NATOM = DQ == 1 ? 16 : DQ == 2 ? 8 : 0;   // atomics per dq_item
 
   // softmax of one 32-key tile: P = exp2(c S'), dS = P dP' (causal mask on
   // the diagonal slices), converted to the bf16 B operands of the two
@@ -295,6 +423,9 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     constexpr int SL = decltype(slot_c)::value;   // == i % NSLOT
     // slot (i + 2) % 3 was last read in item i - 1 (barrier-certified)
     if (i + 2 < niter) issue(i + 2);
+    if constexpr (DQ != 0) {
+      if (i > 0) dq_item(i - 1);    // its dS image was completed before this item's barrier
+    }
     const int gq = i / nsl;
     const int qs0 = q_begin + (i - gq * nsl) * QS;
     if (!CAUSAL || qs0 + QS - 1 >= kw0) {     // else every key of this wave is masked
@@ -353,16 +484,28 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
       // phase D: dK / dV of tile 1
       dkdv(qt, dt, 1, pf1, sf1);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DQ != 0) {
+        // dS into the image (buffer i & 1; its previous item's dQ reads
+        // ended before the last barrier): element j of sf[kt][s2] is row
+        // crow(8 s2 + j, h) = (j & 3) + 4 h + 8 (2 s2 + (j >> 2))
+        char* dsb = smem + (i & 1) * DSIMG;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int imm = (2 * s2 + (j >> 2)) * 4096;
+            *reinterpret_cast<short*>(dsb + dsw[0][j & 3] + imm) = sf0[s2][j];
+            *reinterpret_cast<short*>(dsb + dsw[1][j & 3] + imm) = sf1[s2][j];
+          }
+      }
     }
-    // item i + 1 landed (own pieces); the barrier publishes every wave's
-    // pieces and certifies slot i % 3 is no longer read
-    if (i + 2 < niter) {
-      if (wave == 0) vm_wait<5>();
-      else vm_wait<4>();
-    } else {
-      vm_wait<0>();
-    }
-    __syncthreads();
+    // item i + 1 landed (own pieces: all but the pieces of item i + 2 and
+    // the dQ atomics issued after item i + 1's pieces); the barrier publishes
+    // every wave's pieces (and dS image) and certifies slot i % 3 is no
+    // longer read
+    const int pieces = wave == 0 ? 5 : 4;
+    vm_wait_n((i + 2 < niter ? pieces : 0) + (i >= 1 ? NATOM : 0) + (i >= 2 ? NATOM : 0));
+    lds_barrier();
   };
   // unrolled by the ring depth: every slot offset is a compile-time immediate
   for (int i = 0; i < niter; i += NSLOT) {
@@ -370,6 +513,7 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     if (i + 1 < niter) step(i + 1, std::integral_constant<int, 1>{});
     if (i + 2 < niter) step(i + 2, std::integral_constant<int, 2>{});
   }
+  if constexpr (DQ != 0) dq_item(niter - 1);
   mfma_drain_acc(dva, dka);
 
   // ---- dK = scale * (dK^T)^T, dV: lane = key, registers r -> d = 32 db + crow(r, h)
@@ -427,5 +571,123 @@ MXK_API int mxk_attn_bwd_dkdv256(const void* q, const void* k, const void* v, co
     hipLaunchKernelGGL(mxk_attn_bwd_dkdv256_kernel<false>, dim3(nwg), dim3(256), 0, stream,
                        Q, K, V, dO, rowc, dK, dV, S, Hq, Hkv, q_tok, k_tok, v_tok, dk_tok, dv_tok,
                        scale);
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// ---------------------------------------------------------------------------
+// One-pass backward (variants 7 / 8): prep -> the 256-key kernel with DQ ->
+// (fp32: convert).
+//
+// prep: one 16-lane group per (b, q, head) row of 128 dims: delta = dO . O,
+// the row pair {-lse/scale, -delta}, and the row's dQ accumulator zeroed
+// (ZERO 1: fp32 dq_acc; 2: the bf16 dq the packed atomics add into).
+template <int ZERO>
+__global__ void __launch_bounds__(256)
+mxk_attn_bwd_prep_kernel(const uint16_t* __restrict__ o, const uint16_t* __restrict__ dout,
+                         const float* __restrict__ lse, float* __restrict__ rowc,
+                         void* __restrict__ dqz, int S, int Hq, long rows, float inv_scale) {
+  const long row = (static_cast<long>(blockIdx.x) * 256 + threadIdx.x) >> 4;
+  const int sub = threadIdx.x & 15;
+  if (row >= rows) return;
+  const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(o + row * D + sub * 8);
+  const bf16x8_t g = *reinterpret_cast<const bf16x8_t*>(dout + row * D + sub * 8);
+  float sum = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    sum += mxk::bf2f(static_cast<uint16_t>(a[e])) * mxk::bf2f(static_cast<uint16_t>(g[e]));
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 16);
+  if constexpr (ZERO == 1) {
+    float4* z = reinterpret_cast<float4*>(static_cast<float*>(dqz) + row * D) + 2 * sub;
+    z[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+    z[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+  } else if constexpr (ZERO == 2) {
+    reinterpret_cast<uint4*>(static_cast<uint16_t*>(dqz) + row * D)[sub] = make_uint4(0, 0, 0, 0);
+  }
+  if (sub == 0) {
+    const long bq = row / Hq;               // row = (b S + q) Hq + hq
+    const int hq = static_cast<int>(row - bq * Hq);
+    const long bb = bq / S, qi = bq - bb * S;
+    const long ri = (bb * Hq + hq) * S + qi;
+    *reinterpret_cast<float2*>(rowc + 2 * ri) = make_float2(-lse[ri] * inv_scale, -sum);
+  }
+}
+
+// dq = bf16(scale * dq_acc), 8 elements per thread
+__global__ void __launch_bounds__(256)
+mxk_attn_bwd_dq_convert_kernel(const float* __restrict__ acc, uint16_t* __restrict__ dq, long n8,
+                               float scale) {
+  const long i = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const float4 x = reinterpret_cast<const float4*>(acc)[2 * i];
+  const float4 y = reinterpret_cast<const float4*>(acc)[2 * i + 1];
+  uint4 o;
+  o.x = mxk::pack2bf(x.x * scale, x.y * scale);
+  o.y = mxk::pack2bf(x.z * scale, x.w * scale);
+  o.z = mxk::pack2bf(y.x * scale, y.y * scale);
+  o.w = mxk::pack2bf(y.z * scale, y.w * scale);
+  reinterpret_cast<uint4*>(dq)[i] = o;
+}
+
+// Workspace bytes of the one-pass backward: rowc (8 B per row) and, for the
+// fp32 atomics, dq_acc (512 B per row).
+MXK_API long mxk_attn_bwd_onepass_workspace(int B, int S, int Hq, int bf16_atomics) {
+  const long rows = static_cast<long>(B) * Hq * S;
+  return rows * 8 + (bf16_atomics ? 0 : rows * D * 4);
+}
+
+// One-pass backward: dq [B, S, Hq, 128] contiguous.  bf16_atomics 0: fp32
+// atomics into a zeroed dq_acc, then dq = bf16(scale dq_acc); 1: packed bf16
+// atomics straight into the zeroed dq (half the atomic bytes, each partial
+// sum rounded to bf16).  Results depend on the atomics' arrival order.
+MXK_API int mxk_attn_bwd_onepass(const void* q, const void* k, const void* v, const void* o,
+                                 const void* dout, const float* lse, void* dq, void* dk, void* dv,
+                                 void* workspace, int B, int S, int Hq, int Hkv, long q_tok,
+                                 long k_tok, long v_tok, long dk_tok, long dv_tok, float scale,
+                                 int causal, int bf16_atomics, hipStream_t stream) {
+  if (B < 1 || S < KBLK || S % KBLK || Hkv < 1 || Hq % Hkv || q_tok % 8 || k_tok % 8 ||
+      v_tok % 8 || dk_tok % 4 || dv_tok % 4 ||
+      static_cast<long>(S) * q_tok * 2 >= (1L << 32) ||
+      static_cast<long>(S) * k_tok * 2 >= (1L << 32) ||
+      static_cast<long>(S) * Hq * D * 2 >= (1L << 32) ||
+      (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
+       reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
+       reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
+       reinterpret_cast<uintptr_t>(workspace)) % 16 ||
+      (reinterpret_cast<uintptr_t>(dk) | reinterpret_cast<uintptr_t>(dv)) % 8)
+    return static_cast<int>(hipErrorInvalidValue);
+  const long rows = static_cast<long>(B) * Hq * S;
+  float* rowc = static_cast<float*>(workspace);
+  float* dq_acc = rowc + 2 * rows;
+  const auto* O = static_cast<const uint16_t*>(o);
+  const auto* dO = static_cast<const uint16_t*>(dout);
+  const unsigned pblocks = static_cast<unsigned>((rows * 16 + 255) / 256);
+  if (bf16_atomics)
+    hipLaunchKernelGGL(mxk_attn_bwd_prep_kernel<2>, dim3(pblocks), dim3(256), 0, stream, O, dO, lse,
+                       rowc, dq, S, Hq, rows, 1.f / scale);
+  else
+    hipLaunchKernelGGL(mxk_attn_bwd_prep_kernel<1>, dim3(pblocks), dim3(256), 0, stream, O, dO, lse,
+                       rowc, static_cast<void*>(dq_acc), S, Hq, rows, 1.f / scale);
+  const int nwg = B * Hkv * (S / KBLK);
+  const auto* Q = static_cast<const uint16_t*>(q);
+  const auto* K = static_cast<const uint16_t*>(k);
+  const auto* V = static_cast<const uint16_t*>(v);
+  auto* dK = static_cast<uint16_t*>(dk);
+  auto* dV = static_cast<uint16_t*>(dv);
+  void* dqo = bf16_atomics ? dq : static_cast<void*>(dq_acc);
+#define MXK_ONEPASS_LAUNCH(C, M)                                                                  \
+  hipLaunchKernelGGL((mxk_attn_bwd_dkdv256_kernel<C, M>), dim3(nwg), dim3(256), 0, stream, Q, K,   \
+                     V, dO, rowc, dK, dV, S, Hq, Hkv, q_tok, k_tok, v_tok, dk_tok, dv_tok, scale, \
+                     dqo)
+  if (causal && bf16_atomics) MXK_ONEPASS_LAUNCH(true, 2);
+  else if (causal) MXK_ONEPASS_LAUNCH(true, 1);
+  else if (bf16_atomics) MXK_ONEPASS_LAUNCH(false, 2);
+  else MXK_ONEPASS_LAUNCH(false, 1);
+#undef MXK_ONEPASS_LAUNCH
+  if (!bf16_atomics) {
+    const long n8 = rows * D / 8;
+    hipLaunchKernelGGL(mxk_attn_bwd_dq_convert_kernel, dim3(static_cast<unsigned>((n8 + 255) / 256)),
+                       dim3(256), 0, stream, dq_acc, static_cast<uint16_t*>(dq), n8, scale);
+  }
   MXK_RETURN_LAUNCH_STATUS();
 }

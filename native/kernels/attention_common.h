@@ -125,3 +125,9 @@ MXK_API int mxk_attn_bwd_dkdv256(const void* q, const void* k, const void* v, co
                                  const float* rowc, void* dk, void* dv, int B, int S, int Hq,
                                  int Hkv, long q_tok, long k_tok, long v_tok, long dk_tok,
                                  long dv_tok, float scale, int causal, hipStream_t stream);
+MXK_API long mxk_attn_bwd_onepass_workspace(int B, int S, int Hq, int bf16_atomics);
+MXK_API int mxk_attn_bwd_onepass(const void* q, const void* k, const void* v, const void* o,
+                                 const void* dout, const float* lse, void* dq, void* dk, void* dv,
+                                 void* workspace, int B, int S, int Hq, int Hkv, long q_tok,
+                                 long k_tok, long v_tok, long dk_tok, long dv_tok, float scale,
+                                 int causal, int bf16_atomics, hipStream_t stream);

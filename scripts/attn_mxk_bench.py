@@ -53,6 +53,8 @@ def main():
     res["mxk_bwd_v3"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=3))
     res["mxk_bwd_v5"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=5))
     res["mxk_bwd_v6"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=6))
+    res["mxk_bwd_v7"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=7))
+    res["mxk_bwd_v8"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=8))
     qg, kg, vg = (t.detach().transpose(1, 2).requires_grad_() for t in (q, k, v))
     dot = do.transpose(1, 2)
 

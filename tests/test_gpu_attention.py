@@ -74,7 +74,7 @@ def test_attn_bwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused):
         assert err < tol, (name, err, tol)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
     (1, 256, 8, 2, True),
     (2, 384, 4, 1, True),
@@ -146,3 +146,37 @@ def test_attn_bwd_dkdv256_v6(cuda_device, B, S, Hq, Hkv, causal):
     for a5, a6 in zip(v5[1:], (dk, dv)):       # same math, other summation order
         scale_ = max(1.0, a5.float().abs().max().item())
         assert (a5.float() - a6.float()).abs().max().item() <= 1e-2 * scale_
+
+
+@pytest.mark.parametrize("bf16_atomics", [False, True])
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
+    (1, 256, 4, 4, False),
+    (2, 512, 8, 2, True),
+    (1, 1024, 8, 1, True),
+    (1, 2048, 32, 8, True),
+])
+def test_attn_bwd_onepass_v7_v8(cuda_device, B, S, Hq, Hkv, causal, bf16_atomics):
+    """One-pass backward (variants 7 / 8): the 256-key workgroups also
+    compute dQ = dS K from an LDS image of their dS and add it with fp32
+    (7, into a zeroed fp32 accumulator, then a convert pass) or packed-bf16
+    (8, straight into the zeroed dq) atomics.  Every output vs the fp32
+    reference; dK / dV bit-identical to variant 6 (same kernel body); dQ
+    close to variant 6's deterministic dQ (fp32: summation order only)."""
+    variant = 8 if bf16_atomics else 7
+    q, k, v = _qkv(B, S, Hq, Hkv, cuda_device, seed=17, fused=True)
+    o, lse = A.attn_fwd(q, k, v, causal=causal)
+    g = torch.Generator(device=cuda_device).manual_seed(19)
+    dout = torch.randn(B, S, Hq, 128, device=cuda_device, generator=g).bfloat16()
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    A.attention_ref(qr, kr, vr, causal=causal).backward(dout.float())
+    dq, dk, dv = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, variant=variant)
+    for name, got, want in (("dq", dq, qr.grad), ("dk", dk, kr.grad), ("dv", dv, vr.grad)):
+        assert not torch.isnan(got).any(), name
+        err = (got.float() - want).abs().max().item()
+        tol = 3e-2 * max(1.0, want.abs().max().item())
+        assert err < tol, (name, err, tol)
+    d6 = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, variant=6)
+    assert torch.equal(d6[1], dk) and torch.equal(d6[2], dv)
+    scale_ = max(1.0, d6[0].float().abs().max().item())
+    lim = (2e-2 if bf16_atomics else 1e-2) * scale_
+    assert (d6[0].float() - dq.float()).abs().max().item() <= lim

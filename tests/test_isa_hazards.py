@@ -83,7 +83,9 @@ def close_vgpr_result_reads(asm: str, states: int = 12) -> dict[str, int]:
     instruction other than the next MFMA of its chain within ``states`` wait
     states (``s_nop N`` counts N + 1).  The 256-key attention backward keeps
     S / dP in VGPRs through inline-asm MFMAs, which hipcc does not pad: the
-    VALU softmax must not read them early (8-pass XDL -> VALU: 12 states)."""
+    VALU softmax must not read them early (8-pass XDL -> VALU: 12 states).
+    Linear scan of the listing: fall-through only (an unconditional branch
+    ends the tracking; jump targets are not followed)."""
     bad = {}
     for name in re.findall(r"^(_Z[^\s:]+):", asm, re.M):
         i = asm.find(name + ":")
@@ -108,6 +110,8 @@ def close_vgpr_result_reads(asm: str, states: int = 12) -> dict[str, int]:
             if any(pend.get(r, states) < states for r in _regs(rest)):
                 n += 1
             pend = {r: c + step for r, c in pend.items() if c + step < states}
+            if op in ("s_branch", "s_endpgm", "s_setpc_b64"):
+                pend = {}     # the next line is not reached by fall-through
         if n:
             bad[name] = n
     return bad
