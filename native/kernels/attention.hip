@@ -532,10 +532,18 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
                                  long k_tok, long v_tok, float scale, int causal, int variant,
                                  hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv ||
-      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 9 ||
+      q_tok % 8 || k_tok % 8 || v_tok % 8 || variant < 0 || variant > 10 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) % 16)
     return static_cast<int>(hipErrorInvalidValue);
+  if (variant == 10) {
+    // one wave per SIMD, two 32-row groups per wave (attention_fwd256.hip);
+    // shapes it does not take (S % 256, 32-bit offsets) run variant 4
+    const int st = mxk_attn_fwd256(q, k, v, o, lse, B, S, Hq, Hkv, q_tok, k_tok, v_tok, scale,
+                                   causal, stream);
+    if (st != static_cast<int>(hipErrorInvalidValue)) return st;
+    variant = 4;
+  }
   const int nwg = B * Hq * (S / BQ);
   const long span = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
   if (variant != 0 && span >= (1L << 32)) variant = 0;
@@ -596,6 +604,7 @@ MXK_API int mxk_attn_fwd_variant(const void* q, const void* k, const void* v, vo
 
 // 1 if forward variant v is in this build (5-9 only in the experiments library)
 MXK_API int mxk_attn_fwd_variant_built(int v) {
+  if (v == 10) return 1;
 #ifdef MXK_GEMM_EXPERIMENTS
   return v >= 0 && v <= 9;
 #else

@@ -131,3 +131,7 @@ MXK_API int mxk_attn_bwd_onepass(const void* q, const void* k, const void* v, co
                                  void* workspace, int B, int S, int Hq, int Hkv, long q_tok,
                                  long k_tok, long v_tok, long dk_tok, long dv_tok, float scale,
                                  int causal, int bf16_atomics, hipStream_t stream);
+// forward variant 10 (attention_fwd256.hip)
+MXK_API int mxk_attn_fwd256(const void* q, const void* k, const void* v, void* o, float* lse,
+                            int B, int S, int Hq, int Hkv, long q_tok, long k_tok, long v_tok,
+                            float scale, int causal, hipStream_t stream);

@@ -1,0 +1,410 @@
+// Flash attention forward, one wave per SIMD with two 32-row groups per wave
+// (gfx950; forward variant 10).
+//
+// The default forward (attention.hip variant 4: 4 waves x 32 rows, two
+// workgroups per CU) keeps the matrix cores 45 % busy: each wave runs its
+// QK^T MFMAs, then its softmax, then its PV MFMAs, and only the other wave
+// of the SIMD can fill the gaps (profiles/r4_attention/pmc_fwd4_bwd5.txt).
+// Here a workgroup is 4 waves = 256 query rows of one (batch, q-head), one
+// wave per SIMD, and each wave owns two independent 32-row groups g0 / g1
+// (/opt/skills/guides/cdna_hip_programming.md Appendix B, 'Fused attention
+// prefill', the 4-wave one-wave-per-SIMD structure).  Per 64-key K / V tile
+// j the wave runs four phases, each pairing one group's MFMAs with the other
+// group's softmax on the VALU:
+//
+//   1  S^T(g0, j) = K Q(g0)^T          beside  softmax(g1, j-1) part B
+//   2  O^T(g1) += V^T P^T(g1, j-1)     beside  softmax(g0, j)   part A
+//   -- barrier: tile j+1 landed, slot of tile j-1 free: DMA of tile j+3 --
+//   3  S^T(g1, j) = K Q(g1)^T          beside  softmax(g0, j)   part B
+//   4  O^T(g0) += V^T P^T(g0, j)       beside  softmax(g1, j)   part A
+//
+// part A: causal mask, row max (in-lane + one permlane32_swap), lazy
+// rescale decision (the row max only moves when it grew by more than 2^8),
+// first half of the exps; part B: second half, row sums, the bf16 P^T
+// operands and the (rare) O rescale.
+//
+// Registers: O^T of both groups (2 x 4 x 16) in AGPRs, pinned by inline-asm
+// MFMAs; S^T of both groups (2 x 2 x 16) in VGPRs, also asm MFMAs (the VALU
+// reads them), with explicit XDL-write -> VALU-read wait states; Q in VGPRs.
+// Swapped QK^T as in attention.hip: the query is the MFMA lane, so the row
+// statistics are per lane and P^T leaves the accumulator as the B operand of
+// O^T += V^T P^T with V^T by ds_read_b64_tr_b16 from the row-major V image.
+// K / V tiles by LDS-DMA into a 4-slot ring (two tiles of lead), one barrier
+// per tile.  Causal: every wave walks every tile of its block (a wave past
+// its diagonal sees only masked keys) - no divergent control flow.
+//
+// Layouts as attention.hip: q [B, S, Hq, 128] (token stride q_tok), k / v
+// [B, S, Hkv, 128] (k_tok / v_tok), o [B, S, Hq, 128] contiguous, lse
+// [B, Hq, S] fp32 (natural log).  S % 256 == 0.
+#include "attention_common.h"
+
+namespace {
+constexpr int QB = 256;                        // query rows per workgroup
+constexpr int KT = 64;                         // keys per tile
+constexpr int FSLOT = 2 * TILE_BYTES;          // K | V image of one tile (32 KiB)
+constexpr int FNSLOT = 4;
+constexpr int FLDS = FNSLOT * FSLOT;           // 128 KiB
+
+// MFMA with a VGPR accumulator (S^T): FENCE for the first of a chain whose
+// C / operands a VALU instruction may just have written
+template <bool FENCE = false>
+__device__ __forceinline__ void fmfma_v(f32x16_t& acc, const bf16x8_t& a, const bf16x8_t& b) {
+  if constexpr (FENCE)
+    asm volatile("s_nop 2\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+// S^T chain with the B operand (Q^T fragment) held in AGPRs: the 64
+// registers of both groups' Q live in the accumulator file for the whole
+// kernel, beside O^T, leaving the arch VGPRs to S^T, P^T and the operands
+template <bool FENCE = false>
+__device__ __forceinline__ void fmfma_vq(f32x16_t& acc, const bf16x8_t& a, bf16x8_t& bq) {
+  // "+a" on the Q fragment: the AGPR copy is the live value (an "a" input
+  // alone lets the allocator keep Q in VGPRs and copy it in per MFMA)
+  if constexpr (FENCE)
+    asm volatile("s_nop 2\n\tv_mfma_f32_32x32x16_bf16 %0, %2, %1, %0" : "+v"(acc), "+a"(bq) : "v"(a));
+  else
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %1, %0" : "+v"(acc), "+a"(bq) : "v"(a));
+}
+// MFMA with the accumulator pinned to AGPRs (O^T)
+__device__ __forceinline__ void fmfma_a(f32x16_t& acc, const bf16x8_t& a, const bf16x8_t& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+// 8-pass XDL write -> VALU read: 12 wait states, results redefined behind them
+__device__ __forceinline__ void ffence2(f32x16_t& x, f32x16_t& y) {
+  asm volatile("s_nop 7\n\ts_nop 4" : "+v"(x), "+v"(y));
+}
+// VALU-written MFMA operands (P^T) and accumulators (a rescaled O^T) ->
+// MFMA read: the wait states, with both named so nothing of either is
+// written behind the nops
+__device__ __forceinline__ void fops_ready(const bf16x8_t (&p)[4], f32x16_t (&acc)[4]) {
+  asm volatile("s_nop 2"
+               : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3])
+               : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]));
+}
+// acc *= a for a 16-register accumulator tile held in AGPRs, inside one asm
+// statement (read, multiply, write back through one VGPR): the allocator
+// then never materialises a VGPR copy of the O tiles for the (rare) rescale
+#define MXK_AS1(i) "v_accvgpr_read_b32 %16, %" #i "\n\tv_mul_f32 %16, %16, %17\n\tv_accvgpr_write_b32 %" #i ", %16\n\t"
+__device__ __forceinline__ void agpr_scale16(f32x16_t& x, float a) {
+  float t;
+  asm volatile(MXK_AS1(0) MXK_AS1(1) MXK_AS1(2) MXK_AS1(3) MXK_AS1(4) MXK_AS1(5) MXK_AS1(6)
+               MXK_AS1(7) MXK_AS1(8) MXK_AS1(9) MXK_AS1(10) MXK_AS1(11) MXK_AS1(12) MXK_AS1(13)
+               MXK_AS1(14) MXK_AS1(15) "s_nop 1"
+               : "+a"(x[0]), "+a"(x[1]), "+a"(x[2]), "+a"(x[3]), "+a"(x[4]), "+a"(x[5]),
+                 "+a"(x[6]), "+a"(x[7]), "+a"(x[8]), "+a"(x[9]), "+a"(x[10]), "+a"(x[11]),
+                 "+a"(x[12]), "+a"(x[13]), "+a"(x[14]), "+a"(x[15]), "=&v"(t)
+               : "v"(a));
+}
+#undef MXK_AS1
+__device__ __forceinline__ void vm_wait_n8() { __builtin_amdgcn_s_waitcnt(8 | (7 << 4) | (15 << 8)); }
+}  // namespace
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 1)
+mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                       const uint16_t* __restrict__ v, uint16_t* __restrict__ o,
+                       float* __restrict__ lse, int S, int Hq, int Hkv, long q_tok, long k_tok,
+                       long v_tok, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[FLDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  const int nqb = S / QB;
+  int bh, qb;
+  map_block_xcd(blockIdx.x, gridDim.x, nqb, Hq / Hkv, CAUSAL, &bh, &qb);
+  const int b = bh / Hq, hq = bh % Hq;
+  const int hkv = hq / (Hq / Hkv);
+  const int q0 = qb * QB;
+  const int qw0 = q0 + wave * 64;              // g0: qw0 + r32, g1: qw0 + 32 + r32
+
+  const uint16_t* qb_ptr = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
+  const uint16_t* kb_ptr = k + static_cast<long>(b) * S * k_tok + static_cast<long>(hkv) * D;
+  const uint16_t* vb_ptr = v + static_cast<long>(b) * S * v_tok + static_cast<long>(hkv) * D;
+
+  const int J = CAUSAL ? (q0 + QB) / KT : S / KT;   // tiles of this block
+
+  // ---- DMA: wave w moves pieces 4 w .. 4 w + 3 of K and of V (1 KiB, 4 rows
+  // each; lane i at row 4 g + (i >> 4), chunk (i & 15) ^ swizzle(row))
+  const mxk::u32x4 rk = mxk::make_rsrc(kb_ptr, static_cast<unsigned>(S * k_tok * 2));
+  const mxk::u32x4 rv = mxk::make_rsrc(vb_ptr, static_cast<unsigned>(S * v_tok * 2));
+  const int prow = lane >> 4, pslot = lane & 15;
+  uint32_t kvo[4], vvo[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int row = 4 * (4 * wave + p) + prow;
+    const int ch = pslot ^ ((prow << 2) | p);
+    kvo[p] = static_cast<uint32_t>(row * k_tok * 2 + ch * 16);
+    vvo[p] = static_cast<uint32_t>(row * v_tok * 2 + ch * 16);
+  }
+  const uint32_t k_step = static_cast<uint32_t>(KT * k_tok * 2);
+  const uint32_t v_step = static_cast<uint32_t>(KT * v_tok * 2);
+  const uint32_t sm32 = mxk::lds_addr32(smem);
+  auto issue = [&](int j) {
+    const uint32_t d0 = sm32 + (j % FNSLOT) * FSLOT + (4 * wave) * 1024;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      mxk::dma16m(rk, d0 + p * 1024, kvo[p], j * k_step);
+      mxk::dma16m(rv, d0 + TILE_BYTES + p * 1024, vvo[p], j * v_step);
+    }
+  };
+  issue(0);
+  if (J > 1) issue(1);
+  if (J > 2) issue(2);
+
+  // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[row][16 s + 8 h .. + 7]
+  bf16x8_t qf[2][8];
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      qf[g][s] = *reinterpret_cast<const bf16x8_t*>(
+          qb_ptr + static_cast<long>(qw0 + 32 * g + r32) * q_tok + 16 * s + 8 * h);
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[g][s]));
+  vm_wait0();      // Q and tiles 0..2
+  __syncthreads();
+
+  // LDS read offsets (loop invariants + slot immediates): K rows r32 (+32
+  // for key half 1 = +8 KiB), chunk 2 s + h; V^T transposed reads at keys
+  // tr_key (+8) of k-step ks (+4 KiB each), chunk 4 db + tr_ch
+  int koff[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) koff[s] = swz(r32, 2 * s + h);
+  const int G = lane >> 4, i16 = lane & 15;
+  const int tr_key = 4 * h + (i16 >> 2);
+  const int tr_ch = 2 * (G & 1) + ((i16 & 3) >> 1);
+  const int tr_byte = 8 * (i16 & 1);
+  int voff[4][2];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    voff[db][0] = TILE_BYTES + swz(tr_key, 4 * db + tr_ch) + tr_byte;
+    voff[db][1] = TILE_BYTES + swz(tr_key + 8, 4 * db + tr_ch) + tr_byte;
+  }
+
+  const float c = scale * 1.4426950408889634f;   // scores -> log2 domain
+  f32x16_t oacc[2][4];                           // O^T: rows d = 32 db + crow, lane = query
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[g][db][r] = 0.f;
+  f32x16_t sacc[2][2];                           // S^T: rows key = 32 kh + crow, lane = query
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f}, alpha[2] = {1.f, 1.f};
+  bf16x8_t pf[2][4];                             // P^T operands, k-step ks = keys 16 ks ..
+
+  // ---- the four phase bodies ----
+  auto qk = [&](int g, const char* kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sacc[g][0][r] = 0.f;
+      sacc[g][1][r] = 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const bf16x8_t a0 = lds_b128(kt + koff[s]);
+      const bf16x8_t a1 = lds_b128(kt + koff[s] + 32 * 256);
+      if (s == 0) {
+        fmfma_vq<true>(sacc[g][0], a0, qf[g][s]);
+        fmfma_vq<true>(sacc[g][1], a1, qf[g][s]);
+      } else {
+        fmfma_vq(sacc[g][0], a0, qf[g][s]);
+        fmfma_vq(sacc[g][1], a1, qf[g][s]);
+      }
+    }
+    ffence2(sacc[g][0], sacc[g][1]);
+  };
+  auto pv = [&](int g, const char* vt) {
+    fops_ready(pf[g], oacc[g]);
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8_t a = cat8(lds_tr_b64(vt + voff[db][0] + ks * 4096),
+                                lds_tr_b64(vt + voff[db][1] + ks * 4096));
+        fmfma_a(oacc[g][db], a, pf[g][ks]);
+      }
+  };
+  // part A: mask, row max, lazy rescale decision, exps of key half 0
+  auto sm_a = [&](int g, int j) {
+    const int myq = qw0 + 32 * g + r32;
+    const int key0 = j * KT;
+    if (CAUSAL && key0 + KT - 1 > qw0 + 32 * g) {   // wave-uniform: tiles at / past the diagonal
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (key0 + 32 * kh + crow(r, h) > myq) sacc[g][kh][r] = -INFINITY;
+    }
+    float mx = sacc[g][0][0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[g][0][r]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[g][1][r]);
+    mx = half_max(mx);
+    float m_new = fmaxf(m[g], mx);
+    // lazy rescale: keep the stale max unless the new one exceeds it by
+    // more than 2^8 (P stays <= 256, exact in bf16's exponent range)
+    const bool grow = (m_new - m[g]) * c > 8.f;
+    if (!grow) m_new = m[g];
+    alpha[g] = grow ? fexp2((m[g] - m_new) * c) : 1.f;
+    m[g] = m_new;
+    const float nmc = -m_new * c;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[g][0][r] = fexp2(fmaf(sacc[g][0][r], c, nmc));
+  };
+  // part B: exps of key half 1, row sum, O rescale, bf16 P^T operands
+  auto sm_b = [&](int g) {
+    const float nmc = -m[g] * c;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[g][1][r] = fexp2(fmaf(sacc[g][1][r], c, nmc));
+    float ls = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ls += sacc[g][0][r];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ls += sacc[g][1][r];
+    l[g] = l[g] * alpha[g] + ls;
+    // the bf16 packing below overwrites P in place: pin it behind the row
+    // sum, or the scheduler packs first and spills the fp32 P for the sum
+    asm volatile("" : "+v"(sacc[g][0]), "+v"(sacc[g][1]) : "v"(ls));
+    if (__builtin_amdgcn_ballot_w64(alpha[g] != 1.f)) {   // rare after the first tiles
+#pragma unroll
+      for (int db = 0; db < 4; ++db) agpr_scale16(oacc[g][db], alpha[g]);
+    }
+    pf[g][0] = pack8(sacc[g][0], 0);
+    pf[g][1] = pack8(sacc[g][0], 8);
+    pf[g][2] = pack8(sacc[g][1], 0);
+    pf[g][3] = pack8(sacc[g][1], 8);
+  };
+  // barrier B_j (between phases 2 and 3 of tile j): tile j+1 landed (own
+  // pieces; tile j+2's 8 may be in flight), every wave is past phase 2 of
+  // tile j (the last reader of tile j-1's slot), then tile j+3's DMA
+  auto barrier_j = [&](int j) {
+    if (j + 2 < J) vm_wait_n8();
+    else vm_wait0();
+    __builtin_amdgcn_s_barrier();
+    if (j + 3 < J) issue(j + 3);
+  };
+
+  // The tile body below always finishes the previous tile's g1 first.  For
+  // tile 0 that work is made a no-op: S^T(g1) = -inf (so P^T(g1) = 0, l(g1)
+  // stays 0, no rescale) against a zeroed V image in slot 3 (no NaN from
+  // uninitialised LDS), and m(g1) starts over at -inf after it.
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    sacc[1][0][r] = -INFINITY;
+    sacc[1][1][r] = -INFINITY;
+  }
+  m[1] = 0.f;
+  {
+    uint4* z = reinterpret_cast<uint4*>(smem + 3 * FSLOT + TILE_BYTES);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[tid + 256 * i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+  }
+  auto tile = [&](int j, auto slot_c) {
+    constexpr int SL = decltype(slot_c)::value;        // == j % 4
+    constexpr int PSL = (SL + FNSLOT - 1) % FNSLOT;    // tile j-1's slot
+    const char* tj = smem + SL * FSLOT;
+    const char* tp = smem + PSL * FSLOT;
+    // phase 1: S^T(g0, j) beside softmax(g1, j-1) part B
+    qk(0, tj);
+    sm_b(1);
+    if constexpr (SL == 0) m[1] = j == 0 ? -INFINITY : m[1];
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 2: O^T(g1) += V^T P^T(g1, j-1) beside softmax(g0, j) part A
+    pv(1, tp);
+    sm_a(0, j);
+    __builtin_amdgcn_sched_barrier(0);
+    barrier_j(j);
+    // phase 3: S^T(g1, j) beside softmax(g0, j) part B
+    qk(1, tj);
+    sm_b(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 4: O^T(g0) += V^T P^T(g0, j) beside softmax(g1, j) part A
+    pv(0, tj);
+    sm_a(1, j);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // J is a multiple of 4 (S % 256 == 0): one body of four tiles, the ring's
+  // slots as compile-time immediates
+  for (int j = 0; j < J; j += 4) {
+    tile(j, std::integral_constant<int, 0>{});
+    tile(j + 1, std::integral_constant<int, 1>{});
+    tile(j + 2, std::integral_constant<int, 2>{});
+    tile(j + 3, std::integral_constant<int, 3>{});
+  }
+  // tail: g1's last tile (J-1)
+  {
+    const char* tp = smem + 3 * FSLOT;   // tile J-1: J % 4 == 0
+    sm_b(1);
+    __builtin_amdgcn_sched_barrier(0);
+    pv(1, tp);
+  }
+  // O accumulators final: drain the asm MFMAs before reading them
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int db = 0; db < 4; ++db) asm volatile("" : "+a"(oacc[g][db]));
+
+  // ---- epilogue: O = O^T / l per lane (query), 16-B stores; lse
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int myq = qw0 + 32 * g + r32;
+    const float lt = half_sum(l[g]);
+    const float inv = 1.f / lt;
+    uint16_t* orow = o + (static_cast<long>(b) * S + myq) * Hq * D + static_cast<long>(hq) * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int g0 = 2 * kk, g1 = 2 * kk + 1;
+        const uint32_t x0 = mxk::pack2bf(oacc[g][db][4 * g0] * inv, oacc[g][db][4 * g0 + 1] * inv);
+        const uint32_t x1 = mxk::pack2bf(oacc[g][db][4 * g0 + 2] * inv, oacc[g][db][4 * g0 + 3] * inv);
+        const uint32_t y0 = mxk::pack2bf(oacc[g][db][4 * g1] * inv, oacc[g][db][4 * g1 + 1] * inv);
+        const uint32_t y1 = mxk::pack2bf(oacc[g][db][4 * g1 + 2] * inv, oacc[g][db][4 * g1 + 3] * inv);
+        const auto p0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+        const auto p1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+        uint4 ov;
+        ov.x = p0[0];
+        ov.y = p1[0];
+        ov.z = p0[1];
+        ov.w = p1[1];
+        *reinterpret_cast<uint4*>(orow + 32 * db + 16 * kk + 8 * h) = ov;
+      }
+    }
+    if (h == 0) lse[(static_cast<long>(b) * Hq + hq) * S + myq] = m[g] * scale + logf(lt);
+  }
+}
+
+// Forward variant 10.  Returns hipErrorInvalidValue for layouts it does not
+// take (S % 256, 32-bit buffer offsets); attention.hip then falls back.
+MXK_API int mxk_attn_fwd256(const void* q, const void* k, const void* v, void* o, float* lse,
+                            int B, int S, int Hq, int Hkv, long q_tok, long k_tok, long v_tok,
+                            float scale, int causal, hipStream_t stream) {
+  if (B < 1 || S < QB || S % QB || Hkv < 1 || Hq % Hkv || q_tok % 8 || k_tok % 8 || v_tok % 8 ||
+      static_cast<long>(S) * k_tok * 2 >= (1L << 32) ||
+      static_cast<long>(S) * v_tok * 2 >= (1L << 32) ||
+      (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
+       reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) % 16)
+    return static_cast<int>(hipErrorInvalidValue);
+  const int nwg = B * Hq * (S / QB);
+  const auto* Q = static_cast<const uint16_t*>(q);
+  const auto* K = static_cast<const uint16_t*>(k);
+  const auto* V = static_cast<const uint16_t*>(v);
+  auto* O = static_cast<uint16_t*>(o);
+  if (causal)
+    hipLaunchKernelGGL(mxk_attn_fwd256_kernel<true>, dim3(nwg), dim3(256), 0, stream, Q, K, V, O,
+                       lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  else
+    hipLaunchKernelGGL(mxk_attn_fwd256_kernel<false>, dim3(nwg), dim3(256), 0, stream, Q, K, V, O,
+                       lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  MXK_RETURN_LAUNCH_STATUS();
+}

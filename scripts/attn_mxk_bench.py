@@ -43,6 +43,7 @@ def main():
     res["mxk_fwd_v0"] = bench(lambda: A.attn_fwd(q, k, v, causal=True, variant=0))
     res["mxk_fwd_v2"] = bench(lambda: A.attn_fwd(q, k, v, causal=True, variant=2))
     res["mxk_fwd_v4"] = bench(lambda: A.attn_fwd(q, k, v, causal=True, variant=4))
+    res["mxk_fwd_v10"] = bench(lambda: A.attn_fwd(q, k, v, causal=True, variant=10))
     qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
     with torch.no_grad():
         res["sdpa_fwd"] = bench(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=True,

@@ -30,7 +30,7 @@ def _qkv(B, S, Hq, Hkv, dev, seed=0, fused=False):
     (1, 2048, 32, 8, True, True),     # the Llama-3-8B step's attention shape (B = 1)
     (1, 1024, 4, 2, False, False),    # 16 tiles: every K / V ring slot reused
 ])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 9, 10])
 def test_attn_fwd_matches_reference(cuda_device, B, S, Hq, Hkv, causal, fused, variant):
     from mxk8s.ops import _lib
     if not _lib.lib().mxk_attn_fwd_variant_built(variant):

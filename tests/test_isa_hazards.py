@@ -127,11 +127,13 @@ def test_detector_flags_a_close_vgpr_result_read():
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-def test_attention_bwd256_asm_mfma_hazards_and_spills(tmp_path):
-    """attention_bwd256.hip: dK^T / dV^T pinned to AGPRs and S / dP to VGPRs
-    by inline-asm MFMAs; no early read of either, and no spill (its Q / dO
+@pytest.mark.parametrize("src", ["attention_bwd256.hip", "attention_fwd256.hip"])
+def test_attention_bwd256_asm_mfma_hazards_and_spills(src, tmp_path):
+    """attention_bwd256.hip / attention_fwd256.hip: the accumulated tiles
+    (dK^T / dV^T; O^T) pinned to AGPRs and S / dP (S^T) to VGPRs by
+    inline-asm MFMAs; no early read of either, and no spill (their LDS-DMA
     ring waits are counted vmcnt waits)."""
-    asm = _asm("attention_bwd256.hip", str(tmp_path / "b256.s"))
+    asm = _asm(src, str(tmp_path / (src + ".s")))
     assert "v_mfma" in asm
     assert close_accumulator_reads(asm) == {}
     assert close_vgpr_result_reads(asm) == {}
