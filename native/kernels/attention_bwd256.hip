@@ -384,24 +384,30 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
   // softmax of one 32-key tile: P = exp2(c S'), dS = P dP' (causal mask on
   // the diagonal slices), converted to the bf16 B operands of the two
   // k-steps of 16 queries
-  auto softmax = [&](f32x16_t& sacc, f32x16_t& pacc, int kt, int qs0, bool diag,
-                     bf16x8_t (&pf)[2], bf16x8_t (&sf)[2]) {
+  // softmax of one 32-key tile, chunk cc (0..7) of 8: registers 2 cc and
+  // 2 cc + 1 of P = exp2(c S') (causal mask on the diagonal slices) and
+  // dS = P dP'; after chunks 3 and 7 the bf16 B operands of the k-step of
+  // 16 queries they complete.  The chunks are placed between the MFMA pairs
+  // of the neighbouring phase (one sched region each), so the VALU work
+  // issues in the MFMAs' shadow instead of as one block between them.
+  auto softmax_chunk = [&](f32x16_t& sacc, f32x16_t& pacc, int kt, int qs0, bool diag,
+                           bf16x8_t (&pf)[2], bf16x8_t (&sf)[2], int cc) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    for (int r = 2 * cc; r < 2 * cc + 2; ++r) {
       float p = fexp2(sacc[r] * c);
       if (diag && kw0 + 32 * kt + r32 > qs0 + crow(r, h)) p = 0.f;
       sacc[r] = p;
       pacc[r] = p * pacc[r];
     }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
+    if ((cc & 3) == 3) {
+      const int s2 = cc >> 2;
       pf[s2] = pack8(sacc, 8 * s2);
       sf[s2] = pack8(pacc, 8 * s2);
     }
   };
   // dV^T[., kt] += dO^T P, dK^T[., kt] += Q^T dS (A: transposed reads)
   auto dkdv = [&](const char* qt, const char* dt, int kt, const bf16x8_t (&pf)[2],
-                  const bf16x8_t (&sf)[2]) {
+                  const bf16x8_t (&sf)[2], auto&& beside) {
     mfma_operands_ready(pf, sf);
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
@@ -415,6 +421,8 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
                                  lds_tr_b64(qt + swz(row + 8, ch) + tr_byte));
         mfma_acc(dva[db][kt], ao, pf[s2]);
         mfma_acc(dka[db][kt], aq, sf[s2]);
+        beside(2 * db + s2);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   };
@@ -465,6 +473,7 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
       mfma_result_fence(s0, p0);
       __builtin_amdgcn_sched_barrier(0);
       // phase B: S' / dP' of key tile 1 beside the softmax of tile 0
+      bf16x8_t pf0[2], sf0[2], pf1[2], sf1[2];
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         const bf16x8_t qa = lds_b128(qt + roff[s]);
@@ -472,18 +481,16 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
         const bf16x8_t kf = lds_b128(smem + koff[s] + 32 * 256);
         mfma_v(s1, qa, kf);
         mfma_v(p1, da, vf[1][s]);
+        softmax_chunk(s0, p0, 0, qs0, diag, pf0, sf0, s);
+        __builtin_amdgcn_sched_barrier(0);
       }
       mfma_result_fence(s1, p1);
-      bf16x8_t pf0[2], sf0[2], pf1[2], sf1[2];
-      softmax(s0, p0, 0, qs0, diag, pf0, sf0);
       __builtin_amdgcn_sched_barrier(0);
       // phase C: dK / dV of tile 0 beside the softmax of tile 1
-      dkdv(qt, dt, 0, pf0, sf0);
-      softmax(s1, p1, 1, qs0, diag, pf1, sf1);
-      __builtin_amdgcn_sched_barrier(0);
+      dkdv(qt, dt, 0, pf0, sf0,
+           [&](int cc) { softmax_chunk(s1, p1, 1, qs0, diag, pf1, sf1, cc); });
       // phase D: dK / dV of tile 1
-      dkdv(qt, dt, 1, pf1, sf1);
-      __builtin_amdgcn_sched_barrier(0);
+      dkdv(qt, dt, 1, pf1, sf1, [](int) {});
       if constexpr (DQ != 0) {
         // dS into the image (buffer i & 1; its previous item's dQ reads
         // ended before the last barrier): element j of sf[kt][s2] is row

@@ -199,8 +199,12 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f}, alpha[2] = {1.f, 1.f};
   bf16x8_t pf[2][4];                             // P^T operands, k-step ks = keys 16 ks ..
 
-  // ---- the four phase bodies ----
-  auto qk = [&](int g, const char* kt) {
+  // ---- the four phase bodies.  Each MFMA loop calls beside(i) after its
+  // i-th MFMA group and closes a sched region there: the other group's
+  // softmax, cut into matching chunks, then issues in the MFMAs' shadow
+  // (left to itself the scheduler emits the softmax as one VALU block
+  // between MFMA runs, with the matrix core idle).
+  auto qk = [&](int g, const char* kt, auto&& beside) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       sacc[g][0][r] = 0.f;
@@ -217,10 +221,13 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
         fmfma_vq(sacc[g][0], a0, qf[g][s]);
         fmfma_vq(sacc[g][1], a1, qf[g][s]);
       }
+      beside(s);
+      __builtin_amdgcn_sched_barrier(0);
     }
     ffence2(sacc[g][0], sacc[g][1]);
+    __builtin_amdgcn_sched_barrier(0);
   };
-  auto pv = [&](int g, const char* vt) {
+  auto pv = [&](int g, const char* vt, auto&& beside) {
     fops_ready(pf[g], oacc[g]);
 #pragma unroll
     for (int db = 0; db < 4; ++db)
@@ -229,58 +236,67 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
         const bf16x8_t a = cat8(lds_tr_b64(vt + voff[db][0] + ks * 4096),
                                 lds_tr_b64(vt + voff[db][1] + ks * 4096));
         fmfma_a(oacc[g][db], a, pf[g][ks]);
+        beside(4 * db + ks);
+        __builtin_amdgcn_sched_barrier(0);
       }
   };
-  // part A: mask, row max, lazy rescale decision, exps of key half 0
-  auto sm_a = [&](int g, int j) {
-    const int myq = qw0 + 32 * g + r32;
-    const int key0 = j * KT;
-    if (CAUSAL && key0 + KT - 1 > qw0 + 32 * g) {   // wave-uniform: tiles at / past the diagonal
+  // part A, chunk cc of 16 (beside the 16 PV MFMAs): 0-7 causal mask and
+  // running row max over 4 scores each; 8 the max across the lane halves,
+  // the lazy rescale decision and alpha; 9-15 the exps of key half 0
+  float mx[2] = {-INFINITY, -INFINITY}, nmc[2] = {0.f, 0.f};
+  auto sm_a = [&](int g, int j, int cc) {
+    if (cc < 8) {
+      const int kh = cc >> 2, r0 = 4 * (cc & 3);
+      const int myq = qw0 + 32 * g + r32;
+      const int key0 = j * KT;
+      const bool diag = CAUSAL && key0 + KT - 1 > qw0 + 32 * g;   // wave-uniform
 #pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
+      for (int r = r0; r < r0 + 4; ++r) {
+        if (diag && key0 + 32 * kh + crow(r, h) > myq) sacc[g][kh][r] = -INFINITY;
+        mx[g] = cc == 0 && r == 0 ? sacc[g][0][0] : fmaxf(mx[g], sacc[g][kh][r]);
+      }
+    } else if (cc == 8) {
+      const float mm = half_max(mx[g]);
+      float m_new = fmaxf(m[g], mm);
+      // lazy rescale: keep the stale max unless the new one exceeds it by
+      // more than 2^8 (P stays <= 256, exact in bf16's exponent range)
+      const bool grow = (m_new - m[g]) * c > 8.f;
+      if (!grow) m_new = m[g];
+      alpha[g] = grow ? fexp2((m[g] - m_new) * c) : 1.f;
+      m[g] = m_new;
+      nmc[g] = -m_new * c;
+    } else {
+      const int r0 = cc == 15 ? 12 : 2 * (cc - 9), r1 = cc == 15 ? 16 : r0 + 2;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (key0 + 32 * kh + crow(r, h) > myq) sacc[g][kh][r] = -INFINITY;
+      for (int r = r0; r < r1; ++r) sacc[g][0][r] = fexp2(fmaf(sacc[g][0][r], c, nmc[g]));
     }
-    float mx = sacc[g][0][0];
-#pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[g][0][r]);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[g][1][r]);
-    mx = half_max(mx);
-    float m_new = fmaxf(m[g], mx);
-    // lazy rescale: keep the stale max unless the new one exceeds it by
-    // more than 2^8 (P stays <= 256, exact in bf16's exponent range)
-    const bool grow = (m_new - m[g]) * c > 8.f;
-    if (!grow) m_new = m[g];
-    alpha[g] = grow ? fexp2((m[g] - m_new) * c) : 1.f;
-    m[g] = m_new;
-    const float nmc = -m_new * c;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sacc[g][0][r] = fexp2(fmaf(sacc[g][0][r], c, nmc));
   };
-  // part B: exps of key half 1, row sum, O rescale, bf16 P^T operands
-  auto sm_b = [&](int g) {
-    const float nmc = -m[g] * c;
+  // part B, chunk cc of 8 (beside the 16 QK MFMAs, two per chunk): exps of
+  // key half 1 (registers 2 cc, 2 cc + 1), the row sum, the bf16 P^T operands
+  // (k-steps 0 / 2 after chunk 3, 1 / 3 after chunk 7), then l and the rare
+  // O rescale
+  float ls[2] = {0.f, 0.f};
+  auto sm_b = [&](int g, int cc) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sacc[g][1][r] = fexp2(fmaf(sacc[g][1][r], c, nmc));
-    float ls = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ls += sacc[g][0][r];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ls += sacc[g][1][r];
-    l[g] = l[g] * alpha[g] + ls;
-    // the bf16 packing below overwrites P in place: pin it behind the row
-    // sum, or the scheduler packs first and spills the fp32 P for the sum
-    asm volatile("" : "+v"(sacc[g][0]), "+v"(sacc[g][1]) : "v"(ls));
-    if (__builtin_amdgcn_ballot_w64(alpha[g] != 1.f)) {   // rare after the first tiles
-#pragma unroll
-      for (int db = 0; db < 4; ++db) agpr_scale16(oacc[g][db], alpha[g]);
+    for (int r = 2 * cc; r < 2 * cc + 2; ++r) {
+      sacc[g][1][r] = fexp2(fmaf(sacc[g][1][r], c, nmc[g]));
+      ls[g] = (cc == 0 && r == 0 ? 0.f : ls[g]) + sacc[g][0][r];
+      ls[g] += sacc[g][1][r];
     }
-    pf[g][0] = pack8(sacc[g][0], 0);
-    pf[g][1] = pack8(sacc[g][0], 8);
-    pf[g][2] = pack8(sacc[g][1], 0);
-    pf[g][3] = pack8(sacc[g][1], 8);
+    if ((cc & 3) == 3)   // pack behind the sums: in place, P's fp32 would be spilled for them
+      asm volatile("" : "+v"(sacc[g][0]), "+v"(sacc[g][1]) : "v"(ls[g]));
+    if (cc == 3) {
+      pf[g][0] = pack8(sacc[g][0], 0);
+      pf[g][2] = pack8(sacc[g][1], 0);
+    } else if (cc == 7) {
+      pf[g][1] = pack8(sacc[g][0], 8);
+      pf[g][3] = pack8(sacc[g][1], 8);
+      l[g] = l[g] * alpha[g] + ls[g];
+      if (__builtin_amdgcn_ballot_w64(alpha[g] != 1.f)) {   // rare after the first tiles
+#pragma unroll
+        for (int db = 0; db < 4; ++db) agpr_scale16(oacc[g][db], alpha[g]);
+      }
+    }
   };
   // barrier B_j (between phases 2 and 3 of tile j): tile j+1 landed (own
   // pieces; tile j+2's 8 may be in flight), every wave is past phase 2 of
@@ -314,23 +330,15 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     const char* tj = smem + SL * FSLOT;
     const char* tp = smem + PSL * FSLOT;
     // phase 1: S^T(g0, j) beside softmax(g1, j-1) part B
-    qk(0, tj);
-    sm_b(1);
+    qk(0, tj, [&](int cc) { sm_b(1, cc); });
     if constexpr (SL == 0) m[1] = j == 0 ? -INFINITY : m[1];
-    __builtin_amdgcn_sched_barrier(0);
     // phase 2: O^T(g1) += V^T P^T(g1, j-1) beside softmax(g0, j) part A
-    pv(1, tp);
-    sm_a(0, j);
-    __builtin_amdgcn_sched_barrier(0);
+    pv(1, tp, [&](int cc) { sm_a(0, j, cc); });
     barrier_j(j);
     // phase 3: S^T(g1, j) beside softmax(g0, j) part B
-    qk(1, tj);
-    sm_b(0);
-    __builtin_amdgcn_sched_barrier(0);
+    qk(1, tj, [&](int cc) { sm_b(0, cc); });
     // phase 4: O^T(g0) += V^T P^T(g0, j) beside softmax(g1, j) part A
-    pv(0, tj);
-    sm_a(1, j);
-    __builtin_amdgcn_sched_barrier(0);
+    pv(0, tj, [&](int cc) { sm_a(1, j, cc); });
   };
   // J is a multiple of 4 (S % 256 == 0): one body of four tiles, the ring's
   // slots as compile-time immediates
@@ -343,9 +351,10 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   // tail: g1's last tile (J-1)
   {
     const char* tp = smem + 3 * FSLOT;   // tile J-1: J % 4 == 0
-    sm_b(1);
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) sm_b(1, cc);
     __builtin_amdgcn_sched_barrier(0);
-    pv(1, tp);
+    pv(1, tp, [](int) {});
   }
   // O accumulators final: drain the asm MFMAs before reading them
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
