@@ -180,8 +180,10 @@ class Controller:
     def __init__(self, client: KubeClient, namespace: str = "amd-gpu",
                  release: str = "amd-gpu-stack", chart_dir: str = chart_render.CHART_DIR,
                  delete_wait_s: float = 5.0, injected: Sequence[str] = (),
-                 replace_backoff_s: float = 1.0, replace_backoff_max_s: float = 300.0):
+                 replace_backoff_s: float = 1.0, replace_backoff_max_s: float = 300.0,
+                 clock=time.monotonic):
         self.client = client
+        self.clock = clock            # replace backoff time source (tests inject one)
         # consecutive replaces of one object back off exponentially: a
         # mutating admission policy that re-adds an item after every replace
         # would otherwise make each reconcile replace it again, and the
@@ -244,7 +246,7 @@ class Controller:
         if obj["kind"] == "Job":    # pod template is immutable: re-create
             return self._recreate_job(path, name, obj, live, res)
         st = self._replaces.setdefault(path, [0, 0.0, None])
-        now = time.monotonic()
+        now = self.clock()
         if now < st[1]:
             res.pending.append(name)      # backing off: retried on a later pass
             return live

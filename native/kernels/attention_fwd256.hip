@@ -309,12 +309,13 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   };
 
   // The tile body below always finishes the previous tile's g1 first.  For
-  // tile 0 that work is made a no-op: S^T(g1) = -inf (so P^T(g1) = 0, l(g1)
+  // tile 0 that work is made a no-op: P^T(g1) = 0 (so l(g1)
   // stays 0, no rescale) against a zeroed V image in slot 3 (no NaN from
   // uninitialised LDS), and m(g1) starts over at -inf after it.
+  // (part B exps key half 1 only: half 0 arrives already exponentiated)
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    sacc[1][0][r] = -INFINITY;
+    sacc[1][0][r] = 0.f;
     sacc[1][1][r] = -INFINITY;
   }
   m[1] = 0.f;

@@ -342,7 +342,8 @@ def test_mutating_policy_replace_loop_backs_off_and_names_drift(api, caplog):
     drifted so the admin can pass --injected-name."""
     import logging
     _policy(api)
-    ctl = op.Controller(KubeClient(api.url), NS, replace_backoff_s=0.3)
+    now = [1000.0]                                   # injected clock: no timing flakiness
+    ctl = op.Controller(KubeClient(api.url), NS, replace_backoff_s=0.3, clock=lambda: now[0])
     ctl.reconcile_once()
     path = f"{DS}/amd-gpu-stack-device-plugin"
     name = "DaemonSet/amd-gpu-stack-device-plugin"
@@ -359,12 +360,15 @@ def test_mutating_policy_replace_loop_backs_off_and_names_drift(api, caplog):
     mutate()                                   # the webhook mutates the replaced object again
     r2 = ctl.reconcile_once()
     assert name not in r2.updated and name in r2.pending
-    time.sleep(0.35)
+    now[0] += 0.35
     r3 = ctl.reconcile_once()                  # backoff expired: replaced again
     assert name in r3.updated
     mutate()
-    r4 = ctl.reconcile_once()                  # second backoff is twice as long
+    now[0] += 0.35
+    r4 = ctl.reconcile_once()                  # second backoff is twice as long (0.6 s)
     assert name in r4.pending
+    now[0] += 0.3
+    assert name in ctl.reconcile_once().updated
     # with the name allow-listed there is no drift at all
     ctl2 = op.Controller(KubeClient(api.url), NS, injected=["KYVERNO_"])
     assert name not in ctl2.reconcile_once().updated
