@@ -105,12 +105,6 @@ __device__ __forceinline__ void mfma_v(f32x16_t& acc, const bf16x8_t& a, const b
 __device__ __forceinline__ void mfma_result_fence(f32x16_t& x, f32x16_t& y) {
   asm volatile("s_nop 7\n\ts_nop 4" : "+v"(x), "+v"(y));
 }
-// keep an inline-asm MFMA's VGPR operands allocated until after the VALU
-// work placed behind it (the VALU must not rewrite a register the MFMA is
-// still reading; hipcc cannot see the asm is an MFMA)
-__device__ __forceinline__ void keep_operands(const bf16x8_t& a, const bf16x8_t& b) {
-  asm volatile("" ::"v"(a), "v"(b));
-}
 __device__ __forceinline__ void mfma_result_fence1(f32x16_t& x) {
   asm volatile("s_nop 7\n\ts_nop 4" : "+v"(x));
 }
@@ -428,7 +422,6 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
         mfma_acc(dva[db][kt], ao, pf[s2]);
         mfma_acc(dka[db][kt], aq, sf[s2]);
         beside(2 * db + s2);
-        keep_operands(ao, aq);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -489,8 +482,6 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
         mfma_v(s1, qa, kf);
         mfma_v(p1, da, vf[1][s]);
         softmax_chunk(s0, p0, 0, qs0, diag, pf0, sf0, s);
-        keep_operands(qa, da);
-        keep_operands(kf, kf);
         __builtin_amdgcn_sched_barrier(0);
       }
       mfma_result_fence(s1, p1);

@@ -97,14 +97,6 @@ __device__ __forceinline__ void agpr_scale16(f32x16_t& x, float a) {
                : "v"(a));
 }
 #undef MXK_AS1
-// An inline-asm MFMA's VGPR operands must not be rewritten by the VALU
-// while the MFMA still reads them, and hipcc does not know the asm is an
-// MFMA: seen as wrong O columns when the softmax chunk placed behind a PV
-// MFMA reused its V^T operand register at once.  Naming the operands again
-// after the chunk keeps their registers out of the chunk's reach.
-__device__ __forceinline__ void keep_operands(const bf16x8_t& a, const bf16x8_t& b) {
-  asm volatile("" ::"v"(a), "v"(b));
-}
 __device__ __forceinline__ void vm_wait_n8() { __builtin_amdgcn_s_waitcnt(8 | (7 << 4) | (15 << 8)); }
 }  // namespace
 
@@ -230,7 +222,6 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
         fmfma_vq(sacc[g][1], a1, qf[g][s]);
       }
       beside(s);
-      keep_operands(a0, a1);
       __builtin_amdgcn_sched_barrier(0);
     }
     ffence2(sacc[g][0], sacc[g][1]);
@@ -246,7 +237,6 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
                                 lds_tr_b64(vt + voff[db][1] + ks * 4096));
         fmfma_a(oacc[g][db], a, pf[g][ks]);
         beside(4 * db + ks);
-        keep_operands(a, a);
         __builtin_amdgcn_sched_barrier(0);
       }
   };

@@ -113,7 +113,7 @@ __device__ __forceinline__ void dma16(const u32x4& rsrc, const char* lds, uint32
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds)));
   unsigned keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 4\n\t"
       "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
       : "s"(m), "v"(voff), "s"(rsrc), "s"(soff)
@@ -127,9 +127,17 @@ __device__ __forceinline__ void dma16(const u32x4& rsrc, const char* lds, uint32
 // write stays invisible to the compiler (inline asm), so it inserts no
 // conservative vmcnt(0) before transposed LDS reads, which the builtin
 // __builtin_amdgcn_raw_ptr_buffer_load_lds does.
+//
+// Opens with s_nop 4: a descriptor / offset SGPR that a VALU instruction has
+// just written (v_readlane of an SGPR spilled to VGPR lanes, v_readfirstlane)
+// needs 5 wait states before a vector-memory instruction reads it, and hipcc
+// pads that only for its own loads.  Seen in the causal 256-row forward: a
+// descriptor word restored right before the DMA was read stale (keys of whole
+// tiles missing from O, then a memory fault).  tests/test_isa_hazards.py
+// (valu_sgpr_to_vmem) audits the listings.
 __device__ __forceinline__ void dma16m(const u32x4& rsrc, uint32_t lds_addr, uint32_t voff,
                                        uint32_t soff) {
-  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
                :
                : "v"(voff), "s"(rsrc), "s"(soff), "{m0}"(lds_addr)
                : "memory");

@@ -126,6 +126,66 @@ def test_detector_flags_a_close_vgpr_result_read():
     assert close_vgpr_result_reads(safe) == {}
 
 
+
+def _sregs(text: str) -> set[int]:
+    out = set()
+    for m in re.finditer(r"\bs\[(\d+):(\d+)\]|\bs(\d+)\b", text):
+        lo = int(m.group(1) or m.group(3))
+        hi = int(m.group(2) or m.group(3))
+        out.update(range(lo, hi + 1))
+    return out
+
+
+def valu_sgpr_to_vmem(asm: str, states: int = 5) -> dict[str, int]:
+    """A VALU write of an SGPR (``v_readlane`` / ``v_readfirstlane`` / an
+    ``_e64`` compare into an SGPR pair) read by a vector-memory instruction as
+    descriptor, offset or base within ``states`` wait states.  hipcc pads this
+    for its own loads, not for an inline-asm ``buffer_load ... lds``: with the
+    causal forward's SGPRs spilled to VGPR lanes, a descriptor word restored by
+    ``v_readlane`` right before the DMA was read stale (keys lost from O: the
+    record count; a memory fault: the base)."""
+    bad = {}
+    for name in re.findall(r"^(_Z[^\s:]+):", asm, re.M):
+        i = asm.find(name + ":")
+        j = asm.find(".Lfunc_end", i)
+        body = [ln.split(";")[0].strip() for ln in asm[i:j].split("\n")]
+        body = [ln for ln in body if ln and not ln.startswith(".") and not ln.endswith(":")]
+        pend: dict[int, int] = {}
+        n = 0
+        for ln in body:
+            op, _, rest = ln.partition(" ")
+            m = re.match(r"s_nop (\d+)", ln)
+            step = int(m.group(1)) + 1 if m else 1
+            if op.startswith(("buffer_", "global_", "flat_", "scratch_")) and \
+                    any(r in pend for r in _sregs(rest)):
+                n += 1
+            pend = {r: c + step for r, c in pend.items() if c + step < states}
+            if op.startswith(("v_readlane", "v_readfirstlane")) or \
+                    (op.startswith("v_cmp") and op.endswith("_e64")):
+                for r in _sregs(rest.split(",")[0]):
+                    pend[r] = 0
+            if op in ("s_branch", "s_endpgm", "s_setpc_b64"):
+                pend = {}
+        if n:
+            bad[name] = n
+    return bad
+
+
+def test_detector_flags_a_stale_descriptor_word():
+    asm = ("_Zdma:\n\tv_readlane_b32 s27, v225, 18\n\ts_nop 0\n"
+           "\tbuffer_load_dwordx4 v137, s[24:27], s3 offen lds\n.Lfunc_end0:\n")
+    assert valu_sgpr_to_vmem(asm) == {"_Zdma": 1}
+    assert valu_sgpr_to_vmem(asm.replace("s_nop 0", "s_nop 4")) == {}
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src", ["attention.hip", "attention_bwd256.hip", "attention_fwd256.hip",
+                                 "gemm_bf16.hip", "gemm_bf16_layouts.hip"])
+def test_asm_dma_reads_no_fresh_valu_sgpr(src, tmp_path):
+    asm = _asm(src, str(tmp_path / (src + ".s")))
+    assert "buffer_load" in asm
+    assert valu_sgpr_to_vmem(asm) == {}
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src", ["attention_bwd256.hip", "attention_fwd256.hip"])
 def test_attention_bwd256_asm_mfma_hazards_and_spills(src, tmp_path):
