@@ -409,20 +409,30 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
   auto dkdv = [&](const char* qt, const char* dt, int kt, const bf16x8_t (&pf)[2],
                   const bf16x8_t (&sf)[2], auto&& beside) {
     mfma_operands_ready(pf, sf);
+    // transposed operands one MFMA pair ahead (as phase B)
+    auto tread = [&](const char* base, int i) {
+      const int row = 16 * (i & 1) + tr_row;
+      const int ch = 4 * (i >> 1) + tr_ch;
+      return cat8(lds_tr_b64(base + swz(row, ch) + tr_byte),
+                  lds_tr_b64(base + swz(row + 8, ch) + tr_byte));
+    };
+    bf16x8_t ao = tread(dt, 0), aq = tread(qt, 0);
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        const int row = 16 * s2 + tr_row;
-        const int ch = 4 * db + tr_ch;
-        const bf16x8_t ao = cat8(lds_tr_b64(dt + swz(row, ch) + tr_byte),
-                                 lds_tr_b64(dt + swz(row + 8, ch) + tr_byte));
-        const bf16x8_t aq = cat8(lds_tr_b64(qt + swz(row, ch) + tr_byte),
-                                 lds_tr_b64(qt + swz(row + 8, ch) + tr_byte));
+        const int i = 2 * db + s2;
+        bf16x8_t no = ao, nq = aq;
+        if (i < 7) {
+          no = tread(dt, i + 1);
+          nq = tread(qt, i + 1);
+        }
         mfma_acc(dva[db][kt], ao, pf[s2]);
         mfma_acc(dka[db][kt], aq, sf[s2]);
         beside(2 * db + s2);
         __builtin_amdgcn_sched_barrier(0);
+        ao = no;
+        aq = nq;
       }
     }
   };
@@ -474,15 +484,27 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
       __builtin_amdgcn_sched_barrier(0);
       // phase B: S' / dP' of key tile 1 beside the softmax of tile 0
       bf16x8_t pf0[2], sf0[2], pf1[2], sf1[2];
+      // operands one MFMA pair ahead: the reads for pair s + 1 issue at the
+      // top of region s, behind pair s and its softmax chunk (read in their
+      // own region, each pair waited out a whole LDS round trip)
+      bf16x8_t qa = lds_b128(qt + roff[0]);
+      bf16x8_t da = lds_b128(dt + roff[0]);
+      bf16x8_t kf = lds_b128(smem + koff[0] + 32 * 256);
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        const bf16x8_t qa = lds_b128(qt + roff[s]);
-        const bf16x8_t da = lds_b128(dt + roff[s]);
-        const bf16x8_t kf = lds_b128(smem + koff[s] + 32 * 256);
+        bf16x8_t nq = qa, nd = da, nk = kf;
+        if (s < 7) {
+          nq = lds_b128(qt + roff[s + 1]);
+          nd = lds_b128(dt + roff[s + 1]);
+          nk = lds_b128(smem + koff[s + 1] + 32 * 256);
+        }
         mfma_v(s1, qa, kf);
         mfma_v(p1, da, vf[1][s]);
         softmax_chunk(s0, p0, 0, qs0, diag, pf0, sf0, s);
         __builtin_amdgcn_sched_barrier(0);
+        qa = nq;
+        da = nd;
+        kf = nk;
       }
       mfma_result_fence(s1, p1);
       __builtin_amdgcn_sched_barrier(0);

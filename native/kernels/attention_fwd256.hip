@@ -66,6 +66,12 @@ __device__ __forceinline__ void fmfma_vq(f32x16_t& acc, const bf16x8_t& a, bf16x
   else
     asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %1, %0" : "+v"(acc), "+a"(bq) : "v"(a));
 }
+// first MFMA of an S^T chain: C = 0 as an inline constant (no VALU
+// zeroing, so no VALU-write -> MFMA wait either); early-clobber output, as
+// an MFMA's D must not overlap its A / B
+__device__ __forceinline__ void fmfma_vq0(f32x16_t& acc, const bf16x8_t& a, bf16x8_t& bq) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %1, 0" : "=&v"(acc), "+a"(bq) : "v"(a));
+}
 // MFMA with the accumulator pinned to AGPRs (O^T)
 __device__ __forceinline__ void fmfma_a(f32x16_t& acc, const bf16x8_t& a, const bf16x8_t& b) {
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
@@ -144,7 +150,10 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   const uint32_t v_step = static_cast<uint32_t>(KT * v_tok * 2);
   const uint32_t sm32 = mxk::lds_addr32(smem);
   auto issue = [&](int j) {
-    const uint32_t d0 = sm32 + (j % FNSLOT) * FSLOT + (4 * wave) * 1024;
+    uint32_t d0 = sm32 + (j % FNSLOT) * FSLOT + (4 * wave) * 1024;
+    // opaque base: the 8 piece addresses are one s_add each here, not 32
+    // loop-invariant SGPRs (4 slots x 8 pieces) hoisted and spilled
+    asm volatile("" : "+s"(d0));
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       mxk::dma16m(rk, d0 + p * 1024, kvo[p], j * k_step);
@@ -204,41 +213,50 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   // softmax, cut into matching chunks, then issues in the MFMAs' shadow
   // (left to itself the scheduler emits the softmax as one VALU block
   // between MFMA runs, with the matrix core idle).
+  // Operands are read one MFMA group ahead: the reads for group i + 1 issue
+  // at the top of region i, so their LDS latency hides behind group i's
+  // MFMAs and the softmax chunk beside them (read in the same region as
+  // their MFMA, each MFMA waited out a full LDS round trip).
   auto qk = [&](int g, const char* kt, auto&& beside) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sacc[g][0][r] = 0.f;
-      sacc[g][1][r] = 0.f;
-    }
+    bf16x8_t a0 = lds_b128(kt + koff[0]);
+    bf16x8_t a1 = lds_b128(kt + koff[0] + 32 * 256);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const bf16x8_t a0 = lds_b128(kt + koff[s]);
-      const bf16x8_t a1 = lds_b128(kt + koff[s] + 32 * 256);
-      if (s == 0) {
-        fmfma_vq<true>(sacc[g][0], a0, qf[g][s]);
-        fmfma_vq<true>(sacc[g][1], a1, qf[g][s]);
+      bf16x8_t n0 = a0, n1 = a1;
+      if (s < 7) {
+        n0 = lds_b128(kt + koff[s + 1]);
+        n1 = lds_b128(kt + koff[s + 1] + 32 * 256);
+      }
+      if (s == 0) {   // C = 0: no VALU zeroing of S^T
+        fmfma_vq0(sacc[g][0], a0, qf[g][s]);
+        fmfma_vq0(sacc[g][1], a1, qf[g][s]);
       } else {
         fmfma_vq(sacc[g][0], a0, qf[g][s]);
         fmfma_vq(sacc[g][1], a1, qf[g][s]);
       }
       beside(s);
       __builtin_amdgcn_sched_barrier(0);
+      a0 = n0;
+      a1 = n1;
     }
     ffence2(sacc[g][0], sacc[g][1]);
     __builtin_amdgcn_sched_barrier(0);
   };
+  auto vread = [&](const char* vt, int i) {
+    const int db = i >> 2, ks = i & 3;
+    return cat8(lds_tr_b64(vt + voff[db][0] + ks * 4096), lds_tr_b64(vt + voff[db][1] + ks * 4096));
+  };
   auto pv = [&](int g, const char* vt, auto&& beside) {
     fops_ready(pf[g], oacc[g]);
+    bf16x8_t a = vread(vt, 0);
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8_t a = cat8(lds_tr_b64(vt + voff[db][0] + ks * 4096),
-                                lds_tr_b64(vt + voff[db][1] + ks * 4096));
-        fmfma_a(oacc[g][db], a, pf[g][ks]);
-        beside(4 * db + ks);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+    for (int i = 0; i < 16; ++i) {
+      const bf16x8_t n = i < 15 ? vread(vt, i + 1) : a;
+      fmfma_a(oacc[g][i >> 2], a, pf[g][i & 3]);
+      beside(i);
+      __builtin_amdgcn_sched_barrier(0);
+      a = n;
+    }
   };
   // part A, chunk cc of 16 (beside the 16 PV MFMAs): 0-7 causal mask and
   // running row max over 4 scores each; 8 the max across the lane halves,
@@ -247,12 +265,16 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   auto sm_a = [&](int g, int j, int cc) {
     if (cc < 8) {
       const int kh = cc >> 2, r0 = 4 * (cc & 3);
-      const int myq = qw0 + 32 * g + r32;
-      const int key0 = j * KT;
-      const bool diag = CAUSAL && key0 + KT - 1 > qw0 + 32 * g;   // wave-uniform
+      // causal: key 32 kh + crow(r, h) of the tile is masked past the lane's
+      // query, i.e. when (r & 3) + 8 (r >> 2) > lim - one compare against a
+      // constant per score (VCC only: no SGPR mask pairs to spill)
+      int lim = 1 << 20;
+      if (CAUSAL) lim = qw0 + 32 * g + r32 - j * KT - 32 * kh - 4 * h;
 #pragma unroll
       for (int r = r0; r < r0 + 4; ++r) {
-        if (diag && key0 + 32 * kh + crow(r, h) > myq) sacc[g][kh][r] = -INFINITY;
+        // a scalar select written back: an `if (...) v[r] = x` on the
+        // 16-wide vector compiles to a select of the whole vector
+        if (CAUSAL) sacc[g][kh][r] = (r & 3) + 8 * (r >> 2) > lim ? -INFINITY : sacc[g][kh][r];
         mx[g] = cc == 0 && r == 0 ? sacc[g][0][0] : fmaxf(mx[g], sacc[g][kh][r]);
       }
     } else if (cc == 8) {
@@ -283,14 +305,21 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
       ls[g] = (cc == 0 && r == 0 ? 0.f : ls[g]) + sacc[g][0][r];
       ls[g] += sacc[g][1][r];
     }
-    if ((cc & 3) == 3)   // pack behind the sums: in place, P's fp32 would be spilled for them
-      asm volatile("" : "+v"(sacc[g][0]), "+v"(sacc[g][1]) : "v"(ls[g]));
+    // pack behind the sums (packed first, P's fp32 stays live for them and
+    // spills).  After the last chunk a schedule boundary: an asm naming the
+    // whole S^T tiles there made the allocator copy both into the tuples it
+    // merges at the rescale branch
+    if (cc == 3) asm volatile("" : "+v"(sacc[g][0]), "+v"(sacc[g][1]) : "v"(ls[g]));
+    if (cc == 7) __builtin_amdgcn_sched_barrier(0);
     if (cc == 3) {
       pf[g][0] = pack8(sacc[g][0], 0);
       pf[g][2] = pack8(sacc[g][1], 0);
     } else if (cc == 7) {
       pf[g][1] = pack8(sacc[g][0], 8);
       pf[g][3] = pack8(sacc[g][1], 8);
+      // packed here, ahead of the rescale branch (sunk below it, the fp32 P
+      // was copied whole into the registers of the branch merge)
+      asm volatile("" : "+v"(pf[g][1]), "+v"(pf[g][3]));
       l[g] = l[g] * alpha[g] + ls[g];
       if (__builtin_amdgcn_ballot_w64(alpha[g] != 1.f)) {   // rare after the first tiles
 #pragma unroll
@@ -348,6 +377,10 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     tile(j + 1, std::integral_constant<int, 1>{});
     tile(j + 2, std::integral_constant<int, 2>{});
     tile(j + 3, std::integral_constant<int, 3>{});
+    // 8-pass XDL -> accumulator read: the register allocator may copy O^T(g0)
+    // (just written by phase 4's MFMAs) on the loop's exit edge
+    asm volatile("s_nop 7\n\ts_nop 4"
+                 : "+a"(oacc[0][0]), "+a"(oacc[0][1]), "+a"(oacc[0][2]), "+a"(oacc[0][3]));
   }
   // tail: g1's last tile (J-1)
   {

@@ -16,8 +16,8 @@ qkv = torch.randn(B, S, (Hq + 2 * Hkv) * D, device=dev, generator=g).bfloat16()
 q, k, v = qkv.split([Hq * D, Hkv * D, Hkv * D], dim=-1)
 q, k, v = q.view(B, S, Hq, D), k.view(B, S, Hkv, D), v.view(B, S, Hkv, D)
 dout = torch.randn(B, S, Hq, D, device=dev, generator=g).bfloat16()
-fwd_variants = [int(x) for x in os.environ.get("FWD_VARIANTS", "4").split(",")]
-bwd_variants = [int(x) for x in os.environ.get("BWD_VARIANTS", "5").split(",")]
+fwd_variants = [int(x) for x in os.environ.get("FWD_VARIANTS", "4").split(",") if x]
+bwd_variants = [int(x) for x in os.environ.get("BWD_VARIANTS", "5").split(",") if x]
 for _ in range(int(os.environ.get("ITERS", 6))):
     for fv in fwd_variants:
         o, lse = A.attn_fwd(q, k, v, causal=True, variant=fv)
