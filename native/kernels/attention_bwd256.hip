@@ -51,18 +51,24 @@ namespace {
 constexpr int KW = 64;                        // keys per wave
 constexpr int KBLK = 256;                     // keys per workgroup
 constexpr int QS = 32;                        // query rows per item
-constexpr int NSLOT = 3;                      // Q / dO ring depth
 constexpr int QIMG = QS * 256;                // 8 KiB: one 32-row slice image
-constexpr int SLOT = 2 * QIMG + QS * 8;       // Q | dO | rowc (32 x float2)
 constexpr int KIMG = KBLK * 256;              // 64 KiB
-// ring first: every ring offset (< 49920) fits a ds_read's 16-bit immediate
-constexpr int KOFF = NSLOT * SLOT;             // K image after the ring
-constexpr int LDS_BYTES = KOFF + KIMG;
-// one-pass variants (DQ != 0): the workgroup's dS (32 queries x 256 keys,
-// bf16) is exchanged through a double-buffered LDS image for the dQ product
-constexpr int DSOFF = KOFF + KIMG;
 constexpr int DSIMG = QS * 512;               // 16 KiB: [32 q][256 key positions]
-constexpr int LDS_BYTES_DQ = DSOFF + 2 * DSIMG;
+// LDS layout: the ring's rowc blocks (32 x float2 per slot), the ring's
+// Q | dO slice images, the K image; the one-pass variants (DQ != 0) add a
+// double-buffered image of the workgroup's dS (32 queries x 256 keys, bf16)
+// for the dQ product.  Ring depth 4 (three items of DMA lead) without dQ, 3
+// with it (LDS: 132 / 145 KiB); every ring offset stays a ds_read immediate
+// (< 65536): rowc first, then the slices.
+template <int DQ>
+struct Lay {
+  static constexpr int NS = DQ ? 3 : 4;                 // Q / dO ring depth
+  static constexpr int RCB = NS * QS * 8;               // rowc blocks
+  static constexpr int KOFF = RCB + NS * 2 * QIMG;      // K image after the ring
+  static constexpr int DSOFF = KOFF + KIMG;
+  static constexpr int BYTES = DQ ? DSOFF + 2 * DSIMG : KOFF + KIMG;
+  static_assert(RCB + (NS - 1) * 2 * QIMG + QIMG < 65536, "ring immediates");
+};
 
 __device__ __forceinline__ void dma4m(const mxk::u32x4& rsrc, uint32_t lds_addr, uint32_t voff,
                                       uint32_t soff) {
@@ -130,6 +136,7 @@ __device__ __forceinline__ void vm_wait_n(int n) {
     case 4: vm_wait<4>(); break;
     case 5: vm_wait<5>(); break;
     case 8: vm_wait<8>(); break;
+    case 10: vm_wait<10>(); break;
     case 12: vm_wait<12>(); break;
     case 13: vm_wait<13>(); break;
     case 16: vm_wait<16>(); break;
@@ -180,7 +187,9 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
                             uint16_t* __restrict__ dv, int S, int Hq, int Hkv, long q_tok,
                             long k_tok, long v_tok, long dk_tok, long dv_tok, float scale,
                             void* __restrict__ dqo = nullptr) {
-  __shared__ __attribute__((aligned(16))) char smem[DQ ? LDS_BYTES_DQ : LDS_BYTES];
+  using L = Lay<DQ>;
+  constexpr int NSLOT = L::NS, KOFF = L::KOFF, DSOFF = L::DSOFF;
+  __shared__ __attribute__((aligned(16))) char smem[L::BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -248,16 +257,17 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
   auto issue = [&](int i) {
     const int gq = i / nsl;
     const int qs0 = q_begin + (i - gq * nsl) * QS;
-    const uint32_t slot = ring + (i % NSLOT) * SLOT;
+    const uint32_t slot = ring + L::RCB + (i % NSLOT) * 2 * QIMG;
     const uint32_t so = static_cast<uint32_t>((qs0 * tok + gq * D) * 2);
 #pragma unroll
     for (int j = 0; j < 4; ++j) mxk::dma16m(rsl, slot + sdst + j * 1024, svo[j], so);
     if (wave == 0)   // lanes 0-31: -lse/scale of rows 0..31, lanes 32-63: -delta
-      dma4m(rr, slot + 2 * QIMG, static_cast<uint32_t>(r32 * 8 + h * 4),
+      dma4m(rr, ring + (i % NSLOT) * QS * 8, static_cast<uint32_t>(r32 * 8 + h * 4),
             static_cast<uint32_t>((gq * S + qs0) * 8));
   };
-  issue(0);
-  if (niter > 1) issue(1);
+#pragma unroll
+  for (int i = 0; i < NSLOT - 1; ++i)
+    if (i < niter) issue(i);
 
   // V's B fragments (dP = dO V^T, key on the lane): lane holds
   // V[kw0 + 32 kt + r32][16 s + 8 h .. + 7]
@@ -439,17 +449,17 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
 
   auto step = [&](int i, auto slot_c) {
     constexpr int SL = decltype(slot_c)::value;   // == i % NSLOT
-    // slot (i + 2) % 3 was last read in item i - 1 (barrier-certified)
-    if (i + 2 < niter) issue(i + 2);
+    // slot (i + NSLOT - 1) % NSLOT was last read in item i - 1 (barrier-certified)
+    if (i + NSLOT - 1 < niter) issue(i + NSLOT - 1);
     if constexpr (DQ != 0) {
       if (i > 0) dq_item(i - 1);    // its dS image was completed before this item's barrier
     }
     const int gq = i / nsl;
     const int qs0 = q_begin + (i - gq * nsl) * QS;
     if (!CAUSAL || qs0 + QS - 1 >= kw0) {     // else every key of this wave is masked
-      const char* qt = smem + SL * SLOT;
+      const char* qt = smem + L::RCB + SL * 2 * QIMG;
       const char* dt = qt + QIMG;
-      const float* rc = reinterpret_cast<const float*>(qt + 2 * QIMG);
+      const float* rc = reinterpret_cast<const float*>(smem + SL * QS * 8);
       const bool diag = CAUSAL && qs0 < kw0 + KW - 1;
 
       // initial accumulators straight from LDS (no VALU write in front of
@@ -533,7 +543,8 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     // every wave's pieces (and dS image) and certifies slot i % 3 is no
     // longer read
     const int pieces = wave == 0 ? 5 : 4;
-    vm_wait_n((i + 2 < niter ? pieces : 0) + (i >= 1 ? NATOM : 0) + (i >= 2 ? NATOM : 0));
+    const int younger = min(NSLOT - 2, max(0, niter - 2 - i));   // items issued after i + 1
+    vm_wait_n(pieces * younger + (i >= 1 ? NATOM : 0) + (i >= 2 ? NATOM : 0));
     lds_barrier();
   };
   // unrolled by the ring depth: every slot offset is a compile-time immediate
@@ -541,6 +552,8 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     step(i, std::integral_constant<int, 0>{});
     if (i + 1 < niter) step(i + 1, std::integral_constant<int, 1>{});
     if (i + 2 < niter) step(i + 2, std::integral_constant<int, 2>{});
+    if constexpr (NSLOT > 3)
+      if (i + 3 < niter) step(i + 3, std::integral_constant<int, 3>{});
   }
   if constexpr (DQ != 0) dq_item(niter - 1);
   mfma_drain_acc(dva, dka);

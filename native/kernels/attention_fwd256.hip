@@ -262,19 +262,20 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   // running row max over 4 scores each; 8 the max across the lane halves,
   // the lazy rescale decision and alpha; 9-15 the exps of key half 0
   float mx[2] = {-INFINITY, -INFINITY}, nmc[2] = {0.f, 0.f};
-  auto sm_a = [&](int g, int j, int cc) {
+  auto sm_a = [&](int g, int j, int cc, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
     if (cc < 8) {
       const int kh = cc >> 2, r0 = 4 * (cc & 3);
       // causal: key 32 kh + crow(r, h) of the tile is masked past the lane's
       // query, i.e. when (r & 3) + 8 (r >> 2) > lim - one compare against a
       // constant per score (VCC only: no SGPR mask pairs to spill)
       int lim = 1 << 20;
-      if (CAUSAL) lim = qw0 + 32 * g + r32 - j * KT - 32 * kh - 4 * h;
+      if (MASK) lim = qw0 + 32 * g + r32 - j * KT - 32 * kh - 4 * h;
 #pragma unroll
       for (int r = r0; r < r0 + 4; ++r) {
         // a scalar select written back: an `if (...) v[r] = x` on the
         // 16-wide vector compiles to a select of the whole vector
-        if (CAUSAL) sacc[g][kh][r] = (r & 3) + 8 * (r >> 2) > lim ? -INFINITY : sacc[g][kh][r];
+        if (MASK) sacc[g][kh][r] = (r & 3) + 8 * (r >> 2) > lim ? -INFINITY : sacc[g][kh][r];
         mx[g] = cc == 0 && r == 0 ? sacc[g][0][0] : fmaxf(mx[g], sacc[g][kh][r]);
       }
     } else if (cc == 8) {
@@ -354,7 +355,7 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     for (int i = 0; i < 4; ++i) z[tid + 256 * i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
   }
-  auto tile = [&](int j, auto slot_c) {
+  auto tile = [&](int j, auto slot_c, auto mask_c) {
     constexpr int SL = decltype(slot_c)::value;        // == j % 4
     constexpr int PSL = (SL + FNSLOT - 1) % FNSLOT;    // tile j-1's slot
     const char* tj = smem + SL * FSLOT;
@@ -363,25 +364,38 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     qk(0, tj, [&](int cc) { sm_b(1, cc); });
     if constexpr (SL == 0) m[1] = j == 0 ? -INFINITY : m[1];
     // phase 2: O^T(g1) += V^T P^T(g1, j-1) beside softmax(g0, j) part A
-    pv(1, tp, [&](int cc) { sm_a(0, j, cc); });
+    pv(1, tp, [&](int cc) { sm_a(0, j, cc, mask_c); });
     barrier_j(j);
     // phase 3: S^T(g1, j) beside softmax(g0, j) part B
     qk(1, tj, [&](int cc) { sm_b(0, cc); });
     // phase 4: O^T(g0) += V^T P^T(g0, j) beside softmax(g1, j) part A
-    pv(0, tj, [&](int cc) { sm_a(1, j, cc); });
+    pv(0, tj, [&](int cc) { sm_a(1, j, cc, mask_c); });
   };
   // J is a multiple of 4 (S % 256 == 0): one body of four tiles, the ring's
-  // slots as compile-time immediates
-  for (int j = 0; j < J; j += 4) {
-    tile(j, std::integral_constant<int, 0>{});
-    tile(j + 1, std::integral_constant<int, 1>{});
-    tile(j + 2, std::integral_constant<int, 2>{});
-    tile(j + 3, std::integral_constant<int, 3>{});
-    // 8-pass XDL -> accumulator read: the register allocator may copy O^T(g0)
-    // (just written by phase 4's MFMAs) on the loop's exit edge
-    asm volatile("s_nop 7\n\ts_nop 4"
-                 : "+a"(oacc[0][0]), "+a"(oacc[0][1]), "+a"(oacc[0][2]), "+a"(oacc[0][3]));
+  // slots as compile-time immediates.  Causal: every diagonal tile of the
+  // block's four waves is one of its last four (wave w's first is J - 4 + w),
+  // so only the last body carries the mask
+  auto body = [&](int j, auto mask_c) {
+    tile(j, std::integral_constant<int, 0>{}, mask_c);
+    tile(j + 1, std::integral_constant<int, 1>{}, mask_c);
+    tile(j + 2, std::integral_constant<int, 2>{}, mask_c);
+    tile(j + 3, std::integral_constant<int, 3>{}, mask_c);
+  };
+  // 8-pass XDL -> accumulator read: the register allocator may copy O^T(g0)
+  // (just written by phase 4's MFMAs) on the loop's exit edge
+#define MXK_O0_FENCE                                                                   \
+  asm volatile("s_nop 7\n\ts_nop 4"                                                    \
+               : "+a"(oacc[0][0]), "+a"(oacc[0][1]), "+a"(oacc[0][2]), "+a"(oacc[0][3]))
+  const int Jm = CAUSAL ? J - 4 : J;
+  for (int j = 0; j < Jm; j += 4) {
+    body(j, std::false_type{});
+    MXK_O0_FENCE;
   }
+  if constexpr (CAUSAL) {
+    body(Jm, std::true_type{});
+    MXK_O0_FENCE;
+  }
+#undef MXK_O0_FENCE
   // tail: g1's last tile (J-1)
   {
     const char* tp = smem + 3 * FSLOT;   // tile J-1: J % 4 == 0
