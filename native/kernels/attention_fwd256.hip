@@ -137,15 +137,12 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   // each; lane i at row 4 g + (i >> 4), chunk (i & 15) ^ swizzle(row))
   const mxk::u32x4 rk = mxk::make_rsrc(kb_ptr, static_cast<unsigned>(S * k_tok * 2));
   const mxk::u32x4 rv = mxk::make_rsrc(vb_ptr, static_cast<unsigned>(S * v_tok * 2));
-  const int prow = lane >> 4, pslot = lane & 15;
-  uint32_t kvo[4], vvo[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int row = 4 * (4 * wave + p) + prow;
-    const int ch = pslot ^ ((prow << 2) | p);
-    kvo[p] = static_cast<uint32_t>(row * k_tok * 2 + ch * 16);
-    vvo[p] = static_cast<uint32_t>(row * v_tok * 2 + ch * 16);
-  }
+  // per piece p: row 4 (4 wave + p) + prow, chunk (pslot ^ (prow << 2)) ^ p,
+  // formed at issue time (2 VALU per piece) rather than held in 8 VGPRs
+  // through the loop (the arch VGPRs are S^T's double buffer's)
+  const int prow = lane >> 4, cbase = (lane & 15) ^ (prow << 2);
+  const uint32_t krow0 = static_cast<uint32_t>((16 * wave + prow) * k_tok * 2);
+  const uint32_t vrow0 = static_cast<uint32_t>((16 * wave + prow) * v_tok * 2);
   const uint32_t k_step = static_cast<uint32_t>(KT * k_tok * 2);
   const uint32_t v_step = static_cast<uint32_t>(KT * v_tok * 2);
   const uint32_t sm32 = mxk::lds_addr32(smem);
@@ -156,8 +153,11 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     asm volatile("" : "+s"(d0));
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      mxk::dma16m(rk, d0 + p * 1024, kvo[p], j * k_step);
-      mxk::dma16m(rv, d0 + TILE_BYTES + p * 1024, vvo[p], j * v_step);
+      const uint32_t ch16 = static_cast<uint32_t>((cbase ^ p) << 4);
+      mxk::dma16m(rk, d0 + p * 1024, krow0 + static_cast<uint32_t>(p * 4 * k_tok * 2) + ch16,
+                  j * k_step);
+      mxk::dma16m(rv, d0 + TILE_BYTES + p * 1024,
+                  vrow0 + static_cast<uint32_t>(p * 4 * v_tok * 2) + ch16, j * v_step);
     }
   };
   issue(0);
@@ -204,133 +204,160 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     for (int db = 0; db < 4; ++db)
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[g][db][r] = 0.f;
-  f32x16_t sacc[2][2];                           // S^T: rows key = 32 kh + crow, lane = query
+  // S^T of both groups, double-buffered by tile parity: buffer j & 1 takes
+  // S(j) in phase 1 of tile j while the other finishes P(j-1)
+  f32x16_t sacc[2][2][2];                        // [buf][g][kh]: rows key = 32 kh + crow, lane = query
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f}, alpha[2] = {1.f, 1.f};
-  bf16x8_t pf[2][4];                             // P^T operands, k-step ks = keys 16 ks ..
+  // P^T operands [buf][g][ks] (k-step ks = keys 16 ks ..), double-buffered
+  // by tile parity: tile j's key half 0 is packed in phase 2 of tile j while
+  // phase 2 reads tile j-1's
+  bf16x8_t pf[2][2][4];
 
-  // ---- the four phase bodies.  Each MFMA loop calls beside(i) after its
-  // i-th MFMA group and closes a sched region there: the other group's
-  // softmax, cut into matching chunks, then issues in the MFMAs' shadow
-  // (left to itself the scheduler emits the softmax as one VALU block
-  // between MFMA runs, with the matrix core idle).
-  // Operands are read one MFMA group ahead: the reads for group i + 1 issue
-  // at the top of region i, so their LDS latency hides behind group i's
-  // MFMAs and the softmax chunk beside them (read in the same region as
-  // their MFMA, each MFMA waited out a full LDS round trip).
-  auto qk = [&](int g, const char* kt, auto&& beside) {
-    bf16x8_t a0 = lds_b128(kt + koff[0]);
-    bf16x8_t a1 = lds_b128(kt + koff[0] + 32 * 256);
+  // ---- the two phase bodies.  Each MFMA loop calls beside(i) after its
+  // i-th MFMA group and closes a sched region there: the softmax, cut into
+  // matching chunks, then issues in the MFMAs' shadow (left to itself the
+  // scheduler emits the softmax as one VALU block between MFMA runs, with
+  // the matrix core idle).  Both groups share every K / V operand read:
+  // each fragment feeds one MFMA per group.  Operands are read one MFMA
+  // group ahead (the reads for group i + 1 issue at the top of region i).
+  //
+  // phase 1: S^T(g, j) = K Q(g)^T for both groups (8 x 4 MFMAs)
+  auto qk2 = [&](auto buf_c, const char* kt, auto&& beside) {
+    constexpr int B = decltype(buf_c)::value;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      bf16x8_t n0 = a0, n1 = a1;
-      if (s < 7) {
-        n0 = lds_b128(kt + koff[s + 1]);
-        n1 = lds_b128(kt + koff[s + 1] + 32 * 256);
-      }
-      if (s == 0) {   // C = 0: no VALU zeroing of S^T
-        fmfma_vq0(sacc[g][0], a0, qf[g][s]);
-        fmfma_vq0(sacc[g][1], a1, qf[g][s]);
-      } else {
-        fmfma_vq(sacc[g][0], a0, qf[g][s]);
-        fmfma_vq(sacc[g][1], a1, qf[g][s]);
+      const bf16x8_t a0 = lds_b128(kt + koff[s]);
+      const bf16x8_t a1 = lds_b128(kt + koff[s] + 32 * 256);
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        if (s == 0) {   // C = 0: no VALU zeroing of S^T
+          fmfma_vq0(sacc[B][g][0], a0, qf[g][s]);
+          fmfma_vq0(sacc[B][g][1], a1, qf[g][s]);
+        } else {
+          fmfma_vq(sacc[B][g][0], a0, qf[g][s]);
+          fmfma_vq(sacc[B][g][1], a1, qf[g][s]);
+        }
       }
       beside(s);
       __builtin_amdgcn_sched_barrier(0);
-      a0 = n0;
-      a1 = n1;
     }
-    ffence2(sacc[g][0], sacc[g][1]);
+    ffence2(sacc[B][0][0], sacc[B][0][1]);
+    ffence2(sacc[B][1][0], sacc[B][1][1]);
     __builtin_amdgcn_sched_barrier(0);
   };
   auto vread = [&](const char* vt, int i) {
     const int db = i >> 2, ks = i & 3;
     return cat8(lds_tr_b64(vt + voff[db][0] + ks * 4096), lds_tr_b64(vt + voff[db][1] + ks * 4096));
   };
-  auto pv = [&](int g, const char* vt, auto&& beside) {
-    fops_ready(pf[g], oacc[g]);
+  // phase 2: O^T(g) += V^T P^T(g, j-1) for both groups (16 x 2 MFMAs)
+  auto pv2 = [&](auto buf_c, const char* vt, auto&& beside) {
+    constexpr int B = decltype(buf_c)::value;
+    fops_ready(pf[B][0], oacc[0]);
+    fops_ready(pf[B][1], oacc[1]);
     bf16x8_t a = vread(vt, 0);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const bf16x8_t n = i < 15 ? vread(vt, i + 1) : a;
-      fmfma_a(oacc[g][i >> 2], a, pf[g][i & 3]);
+      fmfma_a(oacc[0][i >> 2], a, pf[B][0][i & 3]);
+      fmfma_a(oacc[1][i >> 2], a, pf[B][1][i & 3]);
       beside(i);
       __builtin_amdgcn_sched_barrier(0);
       a = n;
     }
   };
-  // part A, chunk cc of 16 (beside the 16 PV MFMAs): 0-7 causal mask and
-  // running row max over 4 scores each; 8 the max across the lane halves,
-  // the lazy rescale decision and alpha; 9-15 the exps of key half 0
+  // softmax start of tile j, chunk cc of 16 (beside phase 2's MFMA pairs):
+  // 0-3 causal mask and row max of (g, kh) = (cc >> 1, cc & 1); 4 the max
+  // across the lane halves, the lazy rescale decision and alpha of both
+  // groups; 5-15 the exps of key half 0 (3 per chunk, g0's then g1's)
   float mx[2] = {-INFINITY, -INFINITY}, nmc[2] = {0.f, 0.f};
-  auto sm_a = [&](int g, int j, int cc, auto mask_c) {
+  float ls[2] = {0.f, 0.f};
+  auto start = [&](auto buf_c, int j, int cc, auto mask_c) {
+    constexpr int B = decltype(buf_c)::value;
     constexpr bool MASK = decltype(mask_c)::value;
-    if (cc < 8) {
-      const int kh = cc >> 2, r0 = 4 * (cc & 3);
+    if (cc < 4) {
+      const int g = cc >> 1, kh = cc & 1;
       // causal: key 32 kh + crow(r, h) of the tile is masked past the lane's
       // query, i.e. when (r & 3) + 8 (r >> 2) > lim - one compare against a
       // constant per score (VCC only: no SGPR mask pairs to spill)
-      int lim = 1 << 20;
-      if (MASK) lim = qw0 + 32 * g + r32 - j * KT - 32 * kh - 4 * h;
+      if (MASK) {
+        const int lim = qw0 + 32 * g + r32 - j * KT - 32 * kh - 4 * h;
 #pragma unroll
-      for (int r = r0; r < r0 + 4; ++r) {
-        // a scalar select written back: an `if (...) v[r] = x` on the
-        // 16-wide vector compiles to a select of the whole vector
-        if (MASK) sacc[g][kh][r] = (r & 3) + 8 * (r >> 2) > lim ? -INFINITY : sacc[g][kh][r];
-        mx[g] = cc == 0 && r == 0 ? sacc[g][0][0] : fmaxf(mx[g], sacc[g][kh][r]);
+        for (int r = 0; r < 16; ++r)
+          // a scalar select written back: an `if (...) v[r] = x` on the
+          // 16-wide vector compiles to a select of the whole vector
+          sacc[B][g][kh][r] = (r & 3) + 8 * (r >> 2) > lim ? -INFINITY : sacc[B][g][kh][r];
       }
-    } else if (cc == 8) {
-      const float mm = half_max(mx[g]);
-      float m_new = fmaxf(m[g], mm);
-      // lazy rescale: keep the stale max unless the new one exceeds it by
-      // more than 2^8 (P stays <= 256, exact in bf16's exponent range)
-      const bool grow = (m_new - m[g]) * c > 8.f;
-      if (!grow) m_new = m[g];
-      alpha[g] = grow ? fexp2((m[g] - m_new) * c) : 1.f;
-      m[g] = m_new;
-      nmc[g] = -m_new * c;
+      float x = kh ? mx[g] : sacc[B][g][0][0];
+#pragma unroll
+      for (int r = kh ? 0 : 1; r < 16; ++r) x = fmaxf(x, sacc[B][g][kh][r]);
+      mx[g] = x;
+    } else if (cc == 4) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const float mm = half_max(mx[g]);
+        float m_new = fmaxf(m[g], mm);
+        // lazy rescale: keep the stale max unless the new one exceeds it by
+        // more than 2^8 (P stays <= 256, exact in bf16's exponent range)
+        const bool grow = (m_new - m[g]) * c > 8.f;
+        if (!grow) m_new = m[g];
+        alpha[g] = grow ? fexp2((m[g] - m_new) * c) : 1.f;
+        m[g] = m_new;
+        nmc[g] = -m_new * c;
+      }
     } else {
-      const int r0 = cc == 15 ? 12 : 2 * (cc - 9), r1 = cc == 15 ? 16 : r0 + 2;
+      // exps of key half 0 with the row sums; each group's bf16 P^T operands
+      // of k-steps 0 / 1 once their 8 registers are done (behind the sums)
+      const int e0 = 3 * (cc - 5), e1 = cc == 15 ? 32 : e0 + 3;
 #pragma unroll
-      for (int r = r0; r < r1; ++r) sacc[g][0][r] = fexp2(fmaf(sacc[g][0][r], c, nmc[g]));
-    }
-  };
-  // part B, chunk cc of 8 (beside the 16 QK MFMAs, two per chunk): exps of
-  // key half 1 (registers 2 cc, 2 cc + 1), the row sum, the bf16 P^T operands
-  // (k-steps 0 / 2 after chunk 3, 1 / 3 after chunk 7), then l and the rare
-  // O rescale
-  float ls[2] = {0.f, 0.f};
-  auto sm_b = [&](int g, int cc) {
-#pragma unroll
-    for (int r = 2 * cc; r < 2 * cc + 2; ++r) {
-      sacc[g][1][r] = fexp2(fmaf(sacc[g][1][r], c, nmc[g]));
-      ls[g] = (cc == 0 && r == 0 ? 0.f : ls[g]) + sacc[g][0][r];
-      ls[g] += sacc[g][1][r];
-    }
-    // pack behind the sums (packed first, P's fp32 stays live for them and
-    // spills).  After the last chunk a schedule boundary: an asm naming the
-    // whole S^T tiles there made the allocator copy both into the tuples it
-    // merges at the rescale branch
-    if (cc == 3) asm volatile("" : "+v"(sacc[g][0]), "+v"(sacc[g][1]) : "v"(ls[g]));
-    if (cc == 7) __builtin_amdgcn_sched_barrier(0);
-    if (cc == 3) {
-      pf[g][0] = pack8(sacc[g][0], 0);
-      pf[g][2] = pack8(sacc[g][1], 0);
-    } else if (cc == 7) {
-      pf[g][1] = pack8(sacc[g][0], 8);
-      pf[g][3] = pack8(sacc[g][1], 8);
-      // packed here, ahead of the rescale branch (sunk below it, the fp32 P
-      // was copied whole into the registers of the branch merge)
-      asm volatile("" : "+v"(pf[g][1]), "+v"(pf[g][3]));
-      l[g] = l[g] * alpha[g] + ls[g];
-      if (__builtin_amdgcn_ballot_w64(alpha[g] != 1.f)) {   // rare after the first tiles
-#pragma unroll
-        for (int db = 0; db < 4; ++db) agpr_scale16(oacc[g][db], alpha[g]);
+      for (int e = e0; e < e1; ++e) {
+        const int g = e >> 4, r = e & 15;
+        sacc[B][g][0][r] = fexp2(fmaf(sacc[B][g][0][r], c, nmc[g]));
+        ls[g] = (r == 0 ? 0.f : ls[g]) + sacc[B][g][0][r];
+      }
+      if (cc == 7 || cc == 10 || cc == 12 || cc == 15) {
+        const int g = cc >= 12 ? 1 : 0, hf = cc == 10 || cc == 15 ? 1 : 0;
+        asm volatile("" : "+v"(sacc[B][g][0]) : "v"(ls[g]));
+        pf[B][g][hf] = pack8(sacc[B][g][0], 8 * hf);
       }
     }
   };
-  // barrier B_j (between phases 2 and 3 of tile j): tile j+1 landed (own
-  // pieces; tile j+2's 8 may be in flight), every wave is past phase 2 of
-  // tile j (the last reader of tile j-1's slot), then tile j+3's DMA
+  // softmax finish of tile j-1, chunk cc of 8 (beside phase 1's groups of
+  // four MFMAs): exps of key half 1 (registers 2 cc, 2 cc + 1 of both
+  // groups), the row sums, the bf16 P^T operands of k-steps 2 / 3 (after
+  // chunks 3 / 7), then l and the rare O rescale
+  auto finish = [&](auto buf_c, int cc) {
+    constexpr int B = decltype(buf_c)::value;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int r = 2 * cc; r < 2 * cc + 2; ++r) {
+        sacc[B][g][1][r] = fexp2(fmaf(sacc[B][g][1][r], c, nmc[g]));
+        ls[g] += sacc[B][g][1][r];
+      }
+    // pack behind the sums (packed first, P's fp32 stays live for them)
+    if (cc == 3)
+      asm volatile("" : "+v"(sacc[B][0][1]), "+v"(sacc[B][1][1]) : "v"(ls[0]), "v"(ls[1]));
+    if (cc == 7) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if (cc == 3) {
+        pf[B][g][2] = pack8(sacc[B][g][1], 0);
+      } else if (cc == 7) {
+        pf[B][g][3] = pack8(sacc[B][g][1], 8);
+        // packed here, ahead of the rescale branch (sunk below it, the fp32
+        // P was copied whole into the registers of the branch merge)
+        asm volatile("" : "+v"(pf[B][g][3]));
+        l[g] = l[g] * alpha[g] + ls[g];
+        if (__builtin_amdgcn_ballot_w64(alpha[g] != 1.f)) {   // rare after the first tiles
+#pragma unroll
+          for (int db = 0; db < 4; ++db) agpr_scale16(oacc[g][db], alpha[g]);
+        }
+      }
+    }
+  };
+  // barrier B_j (after phase 2 of tile j): tile j+1 landed (own pieces;
+  // tile j+2's 8 may be in flight), every wave is past phase 2 of tile j
+  // (the last reader of tile j-1's slot, its V), then tile j+3's DMA
   auto barrier_j = [&](int j) {
     if (j + 2 < J) vm_wait_n8();
     else vm_wait0();
@@ -338,17 +365,17 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     if (j + 3 < J) issue(j + 3);
   };
 
-  // The tile body below always finishes the previous tile's g1 first.  For
-  // tile 0 that work is made a no-op: P^T(g1) = 0 (so l(g1)
-  // stays 0, no rescale) against a zeroed V image in slot 3 (no NaN from
-  // uninitialised LDS), and m(g1) starts over at -inf after it.
-  // (part B exps key half 1 only: half 0 arrives already exponentiated)
+  // Tile 0's phase 1 finishes a tile -1 and its phase 2 adds it to O: made
+  // a no-op by P(-1) = 0 (key half 0's operands packed as 0; half 1 at -inf
+  // with nmc = 0: exp 0, ls stays 0), so l stays 0 and alpha 1, against a
+  // zeroed V image in slot 3 (no NaN from uninitialised LDS)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    sacc[1][0][r] = 0.f;
-    sacc[1][1][r] = -INFINITY;
+  for (int g = 0; g < 2; ++g) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[1][g][1][r] = -INFINITY;
+    pf[1][g][0] = bf16x8_t{};
+    pf[1][g][1] = bf16x8_t{};
   }
-  m[1] = 0.f;
   {
     uint4* z = reinterpret_cast<uint4*>(smem + 3 * FSLOT + TILE_BYTES);
 #pragma unroll
@@ -360,16 +387,13 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     constexpr int PSL = (SL + FNSLOT - 1) % FNSLOT;    // tile j-1's slot
     const char* tj = smem + SL * FSLOT;
     const char* tp = smem + PSL * FSLOT;
-    // phase 1: S^T(g0, j) beside softmax(g1, j-1) part B
-    qk(0, tj, [&](int cc) { sm_b(1, cc); });
-    if constexpr (SL == 0) m[1] = j == 0 ? -INFINITY : m[1];
-    // phase 2: O^T(g1) += V^T P^T(g1, j-1) beside softmax(g0, j) part A
-    pv(1, tp, [&](int cc) { sm_a(0, j, cc, mask_c); });
+    using cur = std::integral_constant<int, SL & 1>;
+    using prv = std::integral_constant<int, (SL & 1) ^ 1>;
+    // phase 1: S^T(j) beside the finish of softmax(j-1)
+    qk2(cur{}, tj, [&](int cc) { finish(prv{}, cc); });
+    // phase 2: O^T += V^T P^T(j-1) beside the start of softmax(j)
+    pv2(prv{}, tp, [&](int cc) { start(cur{}, j, cc, mask_c); });
     barrier_j(j);
-    // phase 3: S^T(g1, j) beside softmax(g0, j) part B
-    qk(1, tj, [&](int cc) { sm_b(0, cc); });
-    // phase 4: O^T(g0) += V^T P^T(g0, j) beside softmax(g1, j) part A
-    pv(0, tj, [&](int cc) { sm_a(1, j, cc, mask_c); });
   };
   // J is a multiple of 4 (S % 256 == 0): one body of four tiles, the ring's
   // slots as compile-time immediates.  Causal: every diagonal tile of the
@@ -381,29 +405,27 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     tile(j + 2, std::integral_constant<int, 2>{}, mask_c);
     tile(j + 3, std::integral_constant<int, 3>{}, mask_c);
   };
-  // 8-pass XDL -> accumulator read: the register allocator may copy O^T(g0)
-  // (just written by phase 4's MFMAs) on the loop's exit edge
-#define MXK_O0_FENCE                                                                   \
+  // 8-pass XDL -> accumulator read: the register allocator may copy O^T
+  // (just written by phase 2's MFMAs) on the loop's exit edge
+#define MXK_O_FENCE                                                                    \
   asm volatile("s_nop 7\n\ts_nop 4"                                                    \
-               : "+a"(oacc[0][0]), "+a"(oacc[0][1]), "+a"(oacc[0][2]), "+a"(oacc[0][3]))
+               : "+a"(oacc[0][0]), "+a"(oacc[0][1]), "+a"(oacc[0][2]), "+a"(oacc[0][3]), \
+                 "+a"(oacc[1][0]), "+a"(oacc[1][1]), "+a"(oacc[1][2]), "+a"(oacc[1][3]))
   const int Jm = CAUSAL ? J - 4 : J;
   for (int j = 0; j < Jm; j += 4) {
     body(j, std::false_type{});
-    MXK_O0_FENCE;
+    MXK_O_FENCE;
   }
   if constexpr (CAUSAL) {
     body(Jm, std::true_type{});
-    MXK_O0_FENCE;
+    MXK_O_FENCE;
   }
-#undef MXK_O0_FENCE
-  // tail: g1's last tile (J-1)
-  {
-    const char* tp = smem + 3 * FSLOT;   // tile J-1: J % 4 == 0
+#undef MXK_O_FENCE
+  // tail: finish the last tile (J-1, slot 3, buffer 1) and add it
 #pragma unroll
-    for (int cc = 0; cc < 8; ++cc) sm_b(1, cc);
-    __builtin_amdgcn_sched_barrier(0);
-    pv(1, tp, [](int) {});
-  }
+  for (int cc = 0; cc < 8; ++cc) finish(std::integral_constant<int, 1>{}, cc);
+  __builtin_amdgcn_sched_barrier(0);
+  pv2(std::integral_constant<int, 1>{}, smem + 3 * FSLOT, [](int) {});
   // O accumulators final: drain the asm MFMAs before reading them
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
