@@ -106,13 +106,18 @@ __device__ __forceinline__ void agpr_scale16(f32x16_t& x, float a) {
 __device__ __forceinline__ void vm_wait_n8() { __builtin_amdgcn_s_waitcnt(8 | (7 << 4) | (15 << 8)); }
 }  // namespace
 
-template <bool CAUSAL>
+// STAMP (diagnostic build, mxk_attn_fwd256_stamps): each wave adds up the
+// shader cycles of its phase 1, phase 2 and barrier segments and writes
+// them with its total to stamps[wave id][4]; the production instance has none
+template <bool CAUSAL, bool STAMP = false>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                        const uint16_t* __restrict__ v, uint16_t* __restrict__ o,
                        float* __restrict__ lse, int S, int Hq, int Hkv, long q_tok, long k_tok,
-                       long v_tok, float scale) {
+                       long v_tok, float scale, unsigned long long* __restrict__ stamps = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[FLDS];
+  unsigned long long st_p1 = 0, st_p2 = 0, st_bar = 0, st_0 = 0;
+  if constexpr (STAMP) st_0 = __builtin_readcyclecounter();
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -316,7 +321,9 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
       }
       if (cc == 7 || cc == 10 || cc == 12 || cc == 15) {
         const int g = cc >= 12 ? 1 : 0, hf = cc == 10 || cc == 15 ? 1 : 0;
-        asm volatile("" : "+v"(sacc[B][g][0]) : "v"(ls[g]));
+        // a schedule boundary, not an asm naming the tile: that made the
+        // allocator copy the whole 16-register tuple for the asm
+        __builtin_amdgcn_sched_barrier(0);
         pf[B][g][hf] = pack8(sacc[B][g][0], 8 * hf);
       }
     }
@@ -390,10 +397,21 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     using cur = std::integral_constant<int, SL & 1>;
     using prv = std::integral_constant<int, (SL & 1) ^ 1>;
     // phase 1: S^T(j) beside the finish of softmax(j-1)
+    unsigned long long ta = 0, tb = 0;
+    if constexpr (STAMP) ta = __builtin_readcyclecounter();
     qk2(cur{}, tj, [&](int cc) { finish(prv{}, cc); });
+    if constexpr (STAMP) {
+      tb = __builtin_readcyclecounter();
+      st_p1 += tb - ta;
+    }
     // phase 2: O^T += V^T P^T(j-1) beside the start of softmax(j)
     pv2(prv{}, tp, [&](int cc) { start(cur{}, j, cc, mask_c); });
+    if constexpr (STAMP) {
+      ta = __builtin_readcyclecounter();
+      st_p2 += ta - tb;
+    }
     barrier_j(j);
+    if constexpr (STAMP) st_bar += __builtin_readcyclecounter() - ta;
   };
   // J is a multiple of 4 (S % 256 == 0): one body of four tiles, the ring's
   // slots as compile-time immediates.  Causal: every diagonal tile of the
@@ -461,6 +479,15 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     }
     if (h == 0) lse[(static_cast<long>(b) * Hq + hq) * S + myq] = m[g] * scale + logf(lt);
   }
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 4;
+      w[0] = __builtin_readcyclecounter() - st_0;
+      w[1] = st_p1;
+      w[2] = st_p2;
+      w[3] = st_bar;
+    }
+  }
 }
 
 // Forward variant 10.  Returns hipErrorInvalidValue for layouts it does not
@@ -485,5 +512,29 @@ MXK_API int mxk_attn_fwd256(const void* q, const void* k, const void* v, void* o
   else
     hipLaunchKernelGGL(mxk_attn_fwd256_kernel<false>, dim3(nwg), dim3(256), 0, stream, Q, K, V, O,
                        lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// Diagnostic: forward variant 10 with per-wave segment cycle counts
+// (stamps: [B * Hq * S / 256 workgroups][4 waves][total, phase 1, phase 2,
+// barrier]); same arguments as mxk_attn_fwd256 otherwise.
+MXK_API int mxk_attn_fwd256_stamps(const void* q, const void* k, const void* v, void* o,
+                                   float* lse, int B, int S, int Hq, int Hkv, long q_tok,
+                                   long k_tok, long v_tok, float scale, int causal,
+                                   unsigned long long* stamps, hipStream_t stream) {
+  if (B < 1 || S < QB || S % QB || Hkv < 1 || Hq % Hkv || q_tok % 8 || k_tok % 8 || v_tok % 8 ||
+      !stamps)
+    return static_cast<int>(hipErrorInvalidValue);
+  const int nwg = B * Hq * (S / QB);
+  const auto* Q = static_cast<const uint16_t*>(q);
+  const auto* K = static_cast<const uint16_t*>(k);
+  const auto* V = static_cast<const uint16_t*>(v);
+  auto* O = static_cast<uint16_t*>(o);
+  if (causal)
+    hipLaunchKernelGGL((mxk_attn_fwd256_kernel<true, true>), dim3(nwg), dim3(256), 0, stream, Q, K,
+                       V, O, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps);
+  else
+    hipLaunchKernelGGL((mxk_attn_fwd256_kernel<false, true>), dim3(nwg), dim3(256), 0, stream, Q,
+                       K, V, O, lse, S, Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps);
   MXK_RETURN_LAUNCH_STATUS();
 }
