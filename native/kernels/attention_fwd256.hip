@@ -108,7 +108,9 @@ __device__ __forceinline__ void vm_wait_n8() { __builtin_amdgcn_s_waitcnt(8 | (7
 
 // STAMP (diagnostic build, mxk_attn_fwd256_stamps): each wave adds up the
 // shader cycles of its phase 1, phase 2 and barrier segments and writes
-// them with its total to stamps[wave id][4]; the production instance has none
+// them with its total, its prologue and its time to the tail's end to
+// stamps[wave id][6]; the
+// production instance has none
 template <bool CAUSAL, bool STAMP = false>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
@@ -116,7 +118,7 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
                        float* __restrict__ lse, int S, int Hq, int Hkv, long q_tok, long k_tok,
                        long v_tok, float scale, unsigned long long* __restrict__ stamps = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[FLDS];
-  unsigned long long st_p1 = 0, st_p2 = 0, st_bar = 0, st_0 = 0;
+  unsigned long long st_p1 = 0, st_p2 = 0, st_bar = 0, st_0 = 0, st_pro = 0, st_tail = 0;
   if constexpr (STAMP) st_0 = __builtin_readcyclecounter();
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -151,37 +153,45 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   const uint32_t k_step = static_cast<uint32_t>(KT * k_tok * 2);
   const uint32_t v_step = static_cast<uint32_t>(KT * v_tok * 2);
   const uint32_t sm32 = mxk::lds_addr32(smem);
-  auto issue = [&](int j) {
-    uint32_t d0 = sm32 + (j % FNSLOT) * FSLOT + (4 * wave) * 1024;
-    // opaque base: the 8 piece addresses are one s_add each here, not 32
+  // piece p (0..3) of tile j: one K and one V LDS-DMA instruction
+  auto issue_piece = [&](int j, int p) {
+    uint32_t d0 = sm32 + (j % FNSLOT) * FSLOT + (4 * wave + p) * 1024;
+    // opaque base: the piece addresses are one s_add each here, not 32
     // loop-invariant SGPRs (4 slots x 8 pieces) hoisted and spilled
     asm volatile("" : "+s"(d0));
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const uint32_t ch16 = static_cast<uint32_t>((cbase ^ p) << 4);
-      mxk::dma16m(rk, d0 + p * 1024, krow0 + static_cast<uint32_t>(p * 4 * k_tok * 2) + ch16,
-                  j * k_step);
-      mxk::dma16m(rv, d0 + TILE_BYTES + p * 1024,
-                  vrow0 + static_cast<uint32_t>(p * 4 * v_tok * 2) + ch16, j * v_step);
-    }
+    const uint32_t ch16 = static_cast<uint32_t>((cbase ^ p) << 4);
+    mxk::dma16m(rk, d0, krow0 + static_cast<uint32_t>(p * 4 * k_tok * 2) + ch16, j * k_step);
+    mxk::dma16m(rv, d0 + TILE_BYTES, vrow0 + static_cast<uint32_t>(p * 4 * v_tok * 2) + ch16,
+                j * v_step);
   };
+  auto issue = [&](int j) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) issue_piece(j, p);
+  };
+  // Prologue: tile 0's DMA, Q (asm loads: a compiler-visible load's first
+  // use would carry a vmcnt(0) that also waits for tiles 1 and 2), then
+  // tiles 1 and 2; the loop starts once Q and tile 0 are in (vmcnt 16: the
+  // 16 pieces of tiles 1 and 2 may still fly; barrier B_0 waits for tile 1)
   issue(0);
-  if (J > 1) issue(1);
-  if (J > 2) issue(2);
-
   // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[row][16 s + 8 h .. + 7]
   bf16x8_t qf[2][8];
 #pragma unroll
   for (int g = 0; g < 2; ++g)
 #pragma unroll
     for (int s = 0; s < 8; ++s)
-      qf[g][s] = *reinterpret_cast<const bf16x8_t*>(
-          qb_ptr + static_cast<long>(qw0 + 32 * g + r32) * q_tok + 16 * s + 8 * h);
-#pragma unroll
-  for (int g = 0; g < 2; ++g)
-#pragma unroll
-    for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[g][s]));
-  vm_wait0();      // Q and tiles 0..2
+      asm volatile("global_load_dwordx4 %0, %1, off"
+                   : "=v"(qf[g][s])
+                   : "v"(qb_ptr + static_cast<long>(qw0 + 32 * g + r32) * q_tok + 16 * s + 8 * h)
+                   : "memory");
+  // J >= 4 always (S % 256 == 0): no branch here, whose merge would copy
+  // the Q registers before their loads land
+  issue(1);
+  issue(2);
+  asm volatile("s_waitcnt vmcnt(16)"
+               : "+v"(qf[0][0]), "+v"(qf[0][1]), "+v"(qf[0][2]), "+v"(qf[0][3]), "+v"(qf[0][4]),
+                 "+v"(qf[0][5]), "+v"(qf[0][6]), "+v"(qf[0][7]), "+v"(qf[1][0]), "+v"(qf[1][1]),
+                 "+v"(qf[1][2]), "+v"(qf[1][3]), "+v"(qf[1][4]), "+v"(qf[1][5]), "+v"(qf[1][6]),
+                 "+v"(qf[1][7]));
   __syncthreads();
 
   // LDS read offsets (loop invariants + slot immediates): K rows r32 (+32
@@ -218,33 +228,38 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
   // phase 2 reads tile j-1's
   bf16x8_t pf[2][2][4];
 
-  // ---- the two phase bodies.  Each MFMA loop calls beside(i) after its
-  // i-th MFMA group and closes a sched region there: the softmax, cut into
-  // matching chunks, then issues in the MFMAs' shadow (left to itself the
-  // scheduler emits the softmax as one VALU block between MFMA runs, with
-  // the matrix core idle).  Both groups share every K / V operand read:
-  // each fragment feeds one MFMA per group.  Operands are read one MFMA
-  // group ahead (the reads for group i + 1 issue at the top of region i).
+  // ---- the two phase bodies, each 32 MFMAs.  Each MFMA is followed by
+  // beside(u) and a sched region boundary: one unit of the softmax (about
+  // one exp and three other VALU ops) then issues in that MFMA's shadow.
+  // (Coarser regions - a unit beside four MFMAs - let the scheduler emit
+  // the VALU block first and the MFMAs back to back behind it: measured
+  // 2281 cycles for phase 1's 1024 MFMA cycles.)  Both groups share every
+  // K / V fragment read: each feeds one MFMA per group.  Operands are read
+  // one k-step ahead.
   //
-  // phase 1: S^T(g, j) = K Q(g)^T for both groups (8 x 4 MFMAs)
+  // phase 1: S^T(g, j) = K Q(g)^T for both groups
   auto qk2 = [&](auto buf_c, const char* kt, auto&& beside) {
     constexpr int B = decltype(buf_c)::value;
+    bf16x8_t a[2] = {lds_b128(kt + koff[0]), lds_b128(kt + koff[0] + 32 * 256)};
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const bf16x8_t a0 = lds_b128(kt + koff[s]);
-      const bf16x8_t a1 = lds_b128(kt + koff[s] + 32 * 256);
-#pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        if (s == 0) {   // C = 0: no VALU zeroing of S^T
-          fmfma_vq0(sacc[B][g][0], a0, qf[g][s]);
-          fmfma_vq0(sacc[B][g][1], a1, qf[g][s]);
-        } else {
-          fmfma_vq(sacc[B][g][0], a0, qf[g][s]);
-          fmfma_vq(sacc[B][g][1], a1, qf[g][s]);
-        }
+      bf16x8_t n[2] = {a[0], a[1]};
+      if (s < 7) {
+        n[0] = lds_b128(kt + koff[s + 1]);
+        n[1] = lds_b128(kt + koff[s + 1] + 32 * 256);
       }
-      beside(s);
-      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int g = u >> 1, kh = u & 1;
+        if (s == 0)   // C = 0: no VALU zeroing of S^T
+          fmfma_vq0(sacc[B][g][kh], a[kh], qf[g][s]);
+        else
+          fmfma_vq(sacc[B][g][kh], a[kh], qf[g][s]);
+        beside(4 * s + u);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      a[0] = n[0];
+      a[1] = n[1];
     }
     ffence2(sacc[B][0][0], sacc[B][0][1]);
     ffence2(sacc[B][1][0], sacc[B][1][1]);
@@ -254,7 +269,7 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     const int db = i >> 2, ks = i & 3;
     return cat8(lds_tr_b64(vt + voff[db][0] + ks * 4096), lds_tr_b64(vt + voff[db][1] + ks * 4096));
   };
-  // phase 2: O^T(g) += V^T P^T(g, j-1) for both groups (16 x 2 MFMAs)
+  // phase 2: O^T(g) += V^T P^T(g, j-1) for both groups
   auto pv2 = [&](auto buf_c, const char* vt, auto&& beside) {
     constexpr int B = decltype(buf_c)::value;
     fops_ready(pf[B][0], oacc[0]);
@@ -263,108 +278,104 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const bf16x8_t n = i < 15 ? vread(vt, i + 1) : a;
-      fmfma_a(oacc[0][i >> 2], a, pf[B][0][i & 3]);
-      fmfma_a(oacc[1][i >> 2], a, pf[B][1][i & 3]);
-      beside(i);
-      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        fmfma_a(oacc[g][i >> 2], a, pf[B][g][i & 3]);
+        beside(2 * i + g);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       a = n;
     }
   };
-  // softmax start of tile j, chunk cc of 16 (beside phase 2's MFMA pairs):
-  // 0-3 causal mask and row max of (g, kh) = (cc >> 1, cc & 1); 4 the max
-  // across the lane halves, the lazy rescale decision and alpha of both
-  // groups; 5-15 the exps of key half 0 (3 per chunk, g0's then g1's)
+  // softmax start of tile j, unit u of 32 (beside phase 2's MFMAs):
+  // 0-7 causal mask and row max over 8 scores each ((g, kh) = (u >> 2,
+  // (u >> 1) & 1), registers 8 (u & 1) ..); 8 / 9 the max across the lane
+  // halves, the lazy rescale decision and alpha of g0 / g1; 10-31 the exps
+  // of key half 0 (2 per unit in 10-19, then 1) with the row sums, each
+  // group's bf16 P^T operands of k-steps 0 / 1 once their 8 registers are done
   float mx[2] = {-INFINITY, -INFINITY}, nmc[2] = {0.f, 0.f};
   float ls[2] = {0.f, 0.f};
-  auto start = [&](auto buf_c, int j, int cc, auto mask_c) {
+  auto start = [&](auto buf_c, int j, int u, auto mask_c) {
     constexpr int B = decltype(buf_c)::value;
     constexpr bool MASK = decltype(mask_c)::value;
-    if (cc < 4) {
-      const int g = cc >> 1, kh = cc & 1;
+    if (u < 8) {
+      const int g = u >> 2, kh = (u >> 1) & 1, r0 = 8 * (u & 1);
       // causal: key 32 kh + crow(r, h) of the tile is masked past the lane's
       // query, i.e. when (r & 3) + 8 (r >> 2) > lim - one compare against a
       // constant per score (VCC only: no SGPR mask pairs to spill)
       if (MASK) {
         const int lim = qw0 + 32 * g + r32 - j * KT - 32 * kh - 4 * h;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
+        for (int r = r0; r < r0 + 8; ++r)
           // a scalar select written back: an `if (...) v[r] = x` on the
           // 16-wide vector compiles to a select of the whole vector
           sacc[B][g][kh][r] = (r & 3) + 8 * (r >> 2) > lim ? -INFINITY : sacc[B][g][kh][r];
       }
-      float x = kh ? mx[g] : sacc[B][g][0][0];
+      const bool first = (u & 3) == 0;
+      float x = first ? sacc[B][g][kh][r0] : mx[g];
 #pragma unroll
-      for (int r = kh ? 0 : 1; r < 16; ++r) x = fmaxf(x, sacc[B][g][kh][r]);
+      for (int r = first ? r0 + 1 : r0; r < r0 + 8; ++r) x = fmaxf(x, sacc[B][g][kh][r]);
       mx[g] = x;
-    } else if (cc == 4) {
-#pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        const float mm = half_max(mx[g]);
-        float m_new = fmaxf(m[g], mm);
-        // lazy rescale: keep the stale max unless the new one exceeds it by
-        // more than 2^8 (P stays <= 256, exact in bf16's exponent range)
-        const bool grow = (m_new - m[g]) * c > 8.f;
-        if (!grow) m_new = m[g];
-        alpha[g] = grow ? fexp2((m[g] - m_new) * c) : 1.f;
-        m[g] = m_new;
-        nmc[g] = -m_new * c;
-      }
+    } else if (u < 10) {
+      const int g = u - 8;
+      const float mm = half_max(mx[g]);
+      float m_new = fmaxf(m[g], mm);
+      // lazy rescale: keep the stale max unless the new one exceeds it by
+      // more than 2^8 (P stays <= 256, exact in bf16's exponent range)
+      const bool grow = (m_new - m[g]) * c > 8.f;
+      if (!grow) m_new = m[g];
+      alpha[g] = grow ? fexp2((m[g] - m_new) * c) : 1.f;
+      m[g] = m_new;
+      nmc[g] = -m_new * c;
     } else {
-      // exps of key half 0 with the row sums; each group's bf16 P^T operands
-      // of k-steps 0 / 1 once their 8 registers are done (behind the sums)
-      const int e0 = 3 * (cc - 5), e1 = cc == 15 ? 32 : e0 + 3;
+      const int e0 = u < 20 ? 2 * (u - 10) : u, e1 = u < 20 ? e0 + 2 : u + 1;
 #pragma unroll
       for (int e = e0; e < e1; ++e) {
         const int g = e >> 4, r = e & 15;
         sacc[B][g][0][r] = fexp2(fmaf(sacc[B][g][0][r], c, nmc[g]));
         ls[g] = (r == 0 ? 0.f : ls[g]) + sacc[B][g][0][r];
-      }
-      if (cc == 7 || cc == 10 || cc == 12 || cc == 15) {
-        const int g = cc >= 12 ? 1 : 0, hf = cc == 10 || cc == 15 ? 1 : 0;
-        // a schedule boundary, not an asm naming the tile: that made the
-        // allocator copy the whole 16-register tuple for the asm
-        __builtin_amdgcn_sched_barrier(0);
-        pf[B][g][hf] = pack8(sacc[B][g][0], 8 * hf);
+        if ((r & 7) == 7) pf[B][g][r >> 3] = pack8(sacc[B][g][0], r & 8);
       }
     }
   };
-  // softmax finish of tile j-1, chunk cc of 8 (beside phase 1's groups of
-  // four MFMAs): exps of key half 1 (registers 2 cc, 2 cc + 1 of both
-  // groups), the row sums, the bf16 P^T operands of k-steps 2 / 3 (after
-  // chunks 3 / 7), then l and the rare O rescale
-  auto finish = [&](auto buf_c, int cc) {
+  // softmax finish of tile j-1, unit u of 32 (beside phase 1's MFMAs): the
+  // exp of key half 1's register u >> 1 of group u & 1 and its row sum;
+  // the bf16 P^T operands of k-steps 2 / 3 once their 8 registers are done;
+  // after the last, l and the rare O rescale of both groups
+  auto finish = [&](auto buf_c, int u) {
     constexpr int B = decltype(buf_c)::value;
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-      for (int r = 2 * cc; r < 2 * cc + 2; ++r) {
-        sacc[B][g][1][r] = fexp2(fmaf(sacc[B][g][1][r], c, nmc[g]));
-        ls[g] += sacc[B][g][1][r];
-      }
-    // pack behind the sums (packed first, P's fp32 stays live for them)
-    if (cc == 3)
+    const int g = u & 1, r = u >> 1;
+    sacc[B][g][1][r] = fexp2(fmaf(sacc[B][g][1][r], c, nmc[g]));
+    ls[g] += sacc[B][g][1][r];
+    if (u == 15) {
+      // pack behind the sums (packed first, P's fp32 stays live for them
+      // and spills)
       asm volatile("" : "+v"(sacc[B][0][1]), "+v"(sacc[B][1][1]) : "v"(ls[0]), "v"(ls[1]));
-    if (cc == 7) __builtin_amdgcn_sched_barrier(0);
+      pf[B][0][2] = pack8(sacc[B][0][1], 0);
+      pf[B][1][2] = pack8(sacc[B][1][1], 0);
+    }
+    if (r == 15) {
+      pf[B][g][3] = pack8(sacc[B][g][1], 8);
+      // packed here, ahead of the rescale branch (sunk below it, the fp32
+      // P was copied whole into the registers of the branch merge)
+      asm volatile("" : "+v"(pf[B][g][3]));
+    }
+    if (u == 31) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      if (cc == 3) {
-        pf[B][g][2] = pack8(sacc[B][g][1], 0);
-      } else if (cc == 7) {
-        pf[B][g][3] = pack8(sacc[B][g][1], 8);
-        // packed here, ahead of the rescale branch (sunk below it, the fp32
-        // P was copied whole into the registers of the branch merge)
-        asm volatile("" : "+v"(pf[B][g][3]));
-        l[g] = l[g] * alpha[g] + ls[g];
-        if (__builtin_amdgcn_ballot_w64(alpha[g] != 1.f)) {   // rare after the first tiles
+      for (int gg = 0; gg < 2; ++gg) {
+        l[gg] = l[gg] * alpha[gg] + ls[gg];
+        if (__builtin_amdgcn_ballot_w64(alpha[gg] != 1.f)) {   // rare after the first tiles
 #pragma unroll
-          for (int db = 0; db < 4; ++db) agpr_scale16(oacc[g][db], alpha[g]);
+          for (int db = 0; db < 4; ++db) agpr_scale16(oacc[gg][db], alpha[gg]);
         }
       }
     }
   };
   // barrier B_j (after phase 2 of tile j): tile j+1 landed (own pieces;
   // tile j+2's 8 may be in flight), every wave is past phase 2 of tile j
-  // (the last reader of tile j-1's slot, its V), then tile j+3's DMA
+  // (the last reader of tile j-1's slot, its V), then tile j+3's DMA.
+  // (Spreading the 8 DMA instructions over phase 1 instead, one per 4
+  // MFMAs, measured +1030 cycles in phase 1 against -430 here.)
   auto barrier_j = [&](int j) {
     if (j + 2 < J) vm_wait_n8();
     else vm_wait0();
@@ -399,7 +410,7 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
     // phase 1: S^T(j) beside the finish of softmax(j-1)
     unsigned long long ta = 0, tb = 0;
     if constexpr (STAMP) ta = __builtin_readcyclecounter();
-    qk2(cur{}, tj, [&](int cc) { finish(prv{}, cc); });
+    qk2(cur{}, tj, [&](int u) { finish(prv{}, u); });
     if constexpr (STAMP) {
       tb = __builtin_readcyclecounter();
       st_p1 += tb - ta;
@@ -430,6 +441,7 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
                : "+a"(oacc[0][0]), "+a"(oacc[0][1]), "+a"(oacc[0][2]), "+a"(oacc[0][3]), \
                  "+a"(oacc[1][0]), "+a"(oacc[1][1]), "+a"(oacc[1][2]), "+a"(oacc[1][3]))
   const int Jm = CAUSAL ? J - 4 : J;
+  if constexpr (STAMP) st_pro = __builtin_readcyclecounter() - st_0;
   for (int j = 0; j < Jm; j += 4) {
     body(j, std::false_type{});
     MXK_O_FENCE;
@@ -441,9 +453,10 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
 #undef MXK_O_FENCE
   // tail: finish the last tile (J-1, slot 3, buffer 1) and add it
 #pragma unroll
-  for (int cc = 0; cc < 8; ++cc) finish(std::integral_constant<int, 1>{}, cc);
+  for (int u = 0; u < 32; ++u) finish(std::integral_constant<int, 1>{}, u);
   __builtin_amdgcn_sched_barrier(0);
   pv2(std::integral_constant<int, 1>{}, smem + 3 * FSLOT, [](int) {});
+  if constexpr (STAMP) st_tail = __builtin_readcyclecounter() - st_0;
   // O accumulators final: drain the asm MFMAs before reading them
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
@@ -451,13 +464,18 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
 #pragma unroll
     for (int db = 0; db < 4; ++db) asm volatile("" : "+a"(oacc[g][db]));
 
-  // ---- epilogue: O = O^T / l per lane (query), 16-B stores; lse
+  // ---- epilogue: O = O^T / l, staged through LDS so every global store
+  // instruction writes 4 whole 256-B rows (8 full lines) - stored straight
+  // from the lanes, each instruction touched 32 rows with 32 B each; lse.
+  // The wave's 64 x 256 B image goes to slots 0-1 (its 16 KiB at 16 KiB x
+  // wave), free since the last barrier (the tail reads slot 3 only); the
+  // 16-B chunk index is XORed with the row's low 4 bits (conflict-free).
+  char* img = smem + wave * 16384;
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    const int myq = qw0 + 32 * g + r32;
+    const int row = 32 * g + r32;
     const float lt = half_sum(l[g]);
     const float inv = 1.f / lt;
-    uint16_t* orow = o + (static_cast<long>(b) * S + myq) * Hq * D + static_cast<long>(hq) * D;
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
 #pragma unroll
@@ -474,18 +492,31 @@ mxk_attn_fwd256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restric
         ov.y = p1[0];
         ov.z = p0[1];
         ov.w = p1[1];
-        *reinterpret_cast<uint4*>(orow + 32 * db + 16 * kk + 8 * h) = ov;
+        const int ch = 4 * db + 2 * kk + h;   // 16-B chunk: d = 8 ch ..
+        *reinterpret_cast<uint4*>(img + row * 256 + ((ch ^ (row & 15)) << 4)) = ov;
       }
     }
-    if (h == 0) lse[(static_cast<long>(b) * Hq + hq) * S + myq] = m[g] * scale + logf(lt);
+    if (h == 0) lse[(static_cast<long>(b) * Hq + hq) * S + qw0 + row] = m[g] * scale + logf(lt);
+  }
+  {
+    const int ch = lane & 15;
+    uint16_t* obase = o + (static_cast<long>(b) * S + qw0) * Hq * D + static_cast<long>(hq) * D + 8 * ch;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int row = 4 * t + (lane >> 4);
+      const uint4 ov = *reinterpret_cast<const uint4*>(img + row * 256 + ((ch ^ (row & 15)) << 4));
+      *reinterpret_cast<uint4*>(obase + static_cast<long>(row) * Hq * D) = ov;
+    }
   }
   if constexpr (STAMP) {
     if (lane == 0) {
-      unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 4;
+      unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 6;
       w[0] = __builtin_readcyclecounter() - st_0;
       w[1] = st_p1;
       w[2] = st_p2;
       w[3] = st_bar;
+      w[4] = st_pro;
+      w[5] = st_tail;
     }
   }
 }
@@ -517,7 +548,8 @@ MXK_API int mxk_attn_fwd256(const void* q, const void* k, const void* v, void* o
 
 // Diagnostic: forward variant 10 with per-wave segment cycle counts
 // (stamps: [B * Hq * S / 256 workgroups][4 waves][total, phase 1, phase 2,
-// barrier]); same arguments as mxk_attn_fwd256 otherwise.
+// barrier, prologue, start -> end of the tail]); same arguments as
+// mxk_attn_fwd256 otherwise.
 MXK_API int mxk_attn_fwd256_stamps(const void* q, const void* k, const void* v, void* o,
                                    float* lse, int B, int S, int Hq, int Hkv, long q_tok,
                                    long k_tok, long v_tok, float scale, int causal,

@@ -23,7 +23,7 @@ v = torch.randn(B, S, Hkv, D, device=dev, generator=g).bfloat16()
 o = torch.empty_like(q)
 lse = torch.empty(B, Hq, S, device=dev)
 nwg = B * Hq * (S // 256)
-st = torch.zeros(nwg * 4 * 4, dtype=torch.int64, device=dev)
+st = torch.zeros(nwg * 4 * 6, dtype=torch.int64, device=dev)
 L = _lib.lib()
 f = L.mxk_attn_fwd256_stamps
 vp, i_, l_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
@@ -35,12 +35,13 @@ for causal in (1, 0):
                Hq * D, Hkv * D, Hkv * D, D ** -0.5, causal, st.data_ptr(), _lib.stream_ptr(dev))
         assert rc == 0, rc
     torch.cuda.synchronize()
-    s = st.view(nwg, 4, 4).float().cpu()
+    s = st.view(nwg, 4, 6).float().cpu()
     qb = torch.arange(nwg) % (S // 256)        # block -> q block (not exact under the XCD map)
     tiles = 4 * (S // 256) if not causal else None
-    tot, p1, p2, bar = (s[:, :, i] for i in range(4))
+    tot, p1, p2, bar, pro, tail = (s[:, :, i] for i in range(6))
     print(f"causal={causal} median per wave: total {tot.median():.0f} cyc, phase1 {p1.median():.0f}, "
-          f"phase2 {p2.median():.0f}, barrier {bar.median():.0f}, other {(tot - p1 - p2 - bar).median():.0f}")
+          f"phase2 {p2.median():.0f}, barrier {bar.median():.0f}, prologue {pro.median():.0f}, "
+          f"tail {(tail - p1 - p2 - bar - pro).median():.0f}, epilogue {(tot - tail).median():.0f}")
     # per tile: the total tile count of a wave is J (causal: 4 (qb + 1))
     J = (p1 + p2 + bar).sum(1)
     print(f"   sum over waves: phase1 {p1.sum() / tot.sum():.3f}, phase2 {p2.sum() / tot.sum():.3f}, "

@@ -186,6 +186,48 @@ def test_asm_dma_reads_no_fresh_valu_sgpr(src, tmp_path):
     assert "buffer_load" in asm
     assert valu_sgpr_to_vmem(asm) == {}
 
+
+def asm_load_dests_touched(asm: str, kernel_re: str, wait: str) -> list[str]:
+    """Instructions that read or write the destination registers of the
+    inline-asm ``global_load`` run of a kernel's prologue before ``wait``
+    (the asm ``s_waitcnt`` that covers them).  hipcc counts an asm load's
+    destination as written at ``;;#ASMEND`` and may copy or reuse it before
+    the data lands (seen: a branch merge copied all 16 Q registers)."""
+    bad = []
+    for name in re.findall(r"^(_Z[^\s:]+):", asm, re.M):
+        if not re.search(kernel_re, name):
+            continue
+        i = asm.find(name + ":")
+        j = asm.find(".Lfunc_end", i)
+        body = [ln.split(";")[0].strip() for ln in asm[i:j].split("\n")]
+        body = [ln for ln in body if ln and not ln.startswith(".") and not ln.endswith(":")]
+        k0 = next(k for k, ln in enumerate(body) if ln.startswith("global_load"))
+        dst: set[int] = set()
+        for ln in body[k0:]:
+            if ln.startswith(wait):
+                break
+            op, _, rest = ln.partition(" ")
+            if op.startswith("global_load"):
+                d, _, srcs = rest.partition(",")
+                if _regs(srcs) & dst:
+                    bad.append(ln)
+                dst |= _regs(d)
+            elif _regs(rest) & dst:
+                bad.append(ln)
+    return bad
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_fwd256_prologue_q_loads_untouched_before_their_wait(tmp_path):
+    asm = _asm("attention_fwd256.hip", str(tmp_path / "f.s"))
+    assert asm_load_dests_touched(asm, "mxk_attn_fwd256_kernel", "s_waitcnt vmcnt(16)") == []
+
+
+def test_detector_flags_a_copy_of_an_inflight_load():
+    asm = ("_Zq:\n\tglobal_load_dwordx4 v[2:5], v[30:31], off\n\tv_mov_b64_e32 v[70:71], v[2:3]\n"
+           "\ts_waitcnt vmcnt(16)\n.Lfunc_end0:\n")
+    assert asm_load_dests_touched(asm, "_Zq", "s_waitcnt vmcnt(16)") == ["v_mov_b64_e32 v[70:71], v[2:3]"]
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src", ["attention_bwd256.hip", "attention_fwd256.hip"])
 def test_attention_bwd256_asm_mfma_hazards_and_spills(src, tmp_path):
