@@ -179,14 +179,27 @@ __device__ __forceinline__ void zero16(f32x16_t& x) {
 // (transposed reads of the resident K image) and adds the 32 x 32 result to
 // global memory: DQ 1 fp32 atomics into dq_acc [B, S, Hq, 128] (then a
 // convert pass), DQ 2 packed-bf16 atomics straight into dq (scaled here).
-template <bool CAUSAL, int DQ = 0>
+// STAMP (diagnostic build, mxk_attn_bwd_dkdv256_stamps): each wave adds up
+// the shader cycles of the step's phases A-D and its end-of-step wait +
+// barrier, and writes them with its total to stamps[wave id][6]
+template <bool CAUSAL, int DQ = 0, bool STAMP = false>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                             const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
                             const float* __restrict__ rowc, uint16_t* __restrict__ dk,
                             uint16_t* __restrict__ dv, int S, int Hq, int Hkv, long q_tok,
                             long k_tok, long v_tok, long dk_tok, long dv_tok, float scale,
-                            void* __restrict__ dqo = nullptr) {
+                            void* __restrict__ dqo = nullptr,
+                            unsigned long long* __restrict__ stamps = nullptr) {
+  unsigned long long st_t0 = 0, st_ph[5] = {0, 0, 0, 0, 0}, st_c = 0;
+  if constexpr (STAMP) st_t0 = __builtin_readcyclecounter();
+  auto stamp = [&](int ph) {
+    if constexpr (STAMP) {
+      const unsigned long long t = __builtin_readcyclecounter();
+      if (ph >= 0) st_ph[ph] += t - st_c;
+      st_c = t;
+    }
+  };
   using L = Lay<DQ>;
   constexpr int NSLOT = L::NS, KOFF = L::KOFF, DSOFF = L::DSOFF;
   __shared__ __attribute__((aligned(16))) char smem[L::BYTES];
@@ -481,6 +494,7 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
         p1[4 * g + 0] = d4.x; p1[4 * g + 1] = d4.y; p1[4 * g + 2] = d4.z; p1[4 * g + 3] = d4.w;
       }
       __builtin_amdgcn_sched_barrier(0);
+      stamp(-1);
       // phase A: S' / dP' of key tile 0
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
@@ -492,6 +506,7 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
       }
       mfma_result_fence(s0, p0);
       __builtin_amdgcn_sched_barrier(0);
+      stamp(0);
       // phase B: S' / dP' of key tile 1 beside the softmax of tile 0
       bf16x8_t pf0[2], sf0[2], pf1[2], sf1[2];
       // operands one MFMA pair ahead: the reads for pair s + 1 issue at the
@@ -518,11 +533,14 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
       }
       mfma_result_fence(s1, p1);
       __builtin_amdgcn_sched_barrier(0);
+      stamp(1);
       // phase C: dK / dV of tile 0 beside the softmax of tile 1
       dkdv(qt, dt, 0, pf0, sf0,
            [&](int cc) { softmax_chunk(s1, p1, 1, qs0, diag, pf1, sf1, cc); });
+      stamp(2);
       // phase D: dK / dV of tile 1
       dkdv(qt, dt, 1, pf1, sf1, [](int) {});
+      stamp(3);
       if constexpr (DQ != 0) {
         // dS into the image (buffer i & 1; its previous item's dQ reads
         // ended before the last barrier): element j of sf[kt][s2] is row
@@ -544,8 +562,13 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     // longer read
     const int pieces = wave == 0 ? 5 : 4;
     const int younger = min(NSLOT - 2, max(0, niter - 2 - i));   // items issued after i + 1
+    if constexpr (STAMP) {
+      if (st_c == 0) st_c = __builtin_readcyclecounter();   // a skipped (masked) item
+    }
     vm_wait_n(pieces * younger + (i >= 1 ? NATOM : 0) + (i >= 2 ? NATOM : 0));
     lds_barrier();
+    stamp(4);
+    if constexpr (STAMP) st_c = 0;
   };
   // unrolled by the ring depth: every slot offset is a compile-time immediate
   for (int i = 0; i < niter; i += NSLOT) {
@@ -577,6 +600,14 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
         pk.y = mxk::pack2bf(dva[db][kt][4 * g + 2], dva[db][kt][4 * g + 3]);
         *reinterpret_cast<uint2*>(dvr + d) = pk;
       }
+    }
+  }
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 6;
+      w[0] = __builtin_readcyclecounter() - st_t0;
+#pragma unroll
+      for (int e = 0; e < 5; ++e) w[1 + e] = st_ph[e];
     }
   }
 }
@@ -731,5 +762,33 @@ MXK_API int mxk_attn_bwd_onepass(const void* q, const void* k, const void* v, co
     hipLaunchKernelGGL(mxk_attn_bwd_dq_convert_kernel, dim3(static_cast<unsigned>((n8 + 255) / 256)),
                        dim3(256), 0, stream, dq_acc, static_cast<uint16_t*>(dq), n8, scale);
   }
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// Diagnostic: the dK / dV kernel with per-wave segment cycle counts
+// (stamps: [B * Hkv * S / 256 workgroups][4 waves][total, A, B, C, D,
+// end-of-step wait + barrier]); arguments as mxk_attn_bwd_dkdv256.
+MXK_API int mxk_attn_bwd_dkdv256_stamps(const void* q, const void* k, const void* v,
+                                        const void* dout, const float* rowc, void* dk, void* dv,
+                                        int B, int S, int Hq, int Hkv, long q_tok, long k_tok,
+                                        long v_tok, long dk_tok, long dv_tok, float scale,
+                                        int causal, unsigned long long* stamps, hipStream_t stream) {
+  if (B < 1 || S < KBLK || S % KBLK || Hkv < 1 || Hq % Hkv || !stamps)
+    return static_cast<int>(hipErrorInvalidValue);
+  const int nwg = B * Hkv * (S / KBLK);
+  const auto* Q = static_cast<const uint16_t*>(q);
+  const auto* K = static_cast<const uint16_t*>(k);
+  const auto* V = static_cast<const uint16_t*>(v);
+  const auto* dO = static_cast<const uint16_t*>(dout);
+  auto* dK = static_cast<uint16_t*>(dk);
+  auto* dV = static_cast<uint16_t*>(dv);
+  if (causal)
+    hipLaunchKernelGGL((mxk_attn_bwd_dkdv256_kernel<true, 0, true>), dim3(nwg), dim3(256), 0,
+                       stream, Q, K, V, dO, rowc, dK, dV, S, Hq, Hkv, q_tok, k_tok, v_tok, dk_tok,
+                       dv_tok, scale, nullptr, stamps);
+  else
+    hipLaunchKernelGGL((mxk_attn_bwd_dkdv256_kernel<false, 0, true>), dim3(nwg), dim3(256), 0,
+                       stream, Q, K, V, dO, rowc, dK, dV, S, Hq, Hkv, q_tok, k_tok, v_tok, dk_tok,
+                       dv_tok, scale, nullptr, stamps);
   MXK_RETURN_LAUNCH_STATUS();
 }
