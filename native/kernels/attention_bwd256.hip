@@ -180,8 +180,9 @@ __device__ __forceinline__ void zero16(f32x16_t& x) {
 // global memory: DQ 1 fp32 atomics into dq_acc [B, S, Hq, 128] (then a
 // convert pass), DQ 2 packed-bf16 atomics straight into dq (scaled here).
 // STAMP (diagnostic build, mxk_attn_bwd_dkdv256_stamps): each wave adds up
-// the shader cycles of the step's phases A-D and its end-of-step wait +
-// barrier, and writes them with its total to stamps[wave id][6]
+// the shader cycles of the step's phases (AB, softmax 0, C, D) and its
+// end-of-step wait + barrier, and writes them with its total to
+// stamps[wave id][6]
 template <bool CAUSAL, int DQ = 0, bool STAMP = false>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
@@ -432,7 +433,7 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
   auto dkdv = [&](const char* qt, const char* dt, int kt, const bf16x8_t (&pf)[2],
                   const bf16x8_t (&sf)[2], auto&& beside) {
     mfma_operands_ready(pf, sf);
-    // transposed operands one MFMA pair ahead (as phase B)
+    // transposed operands one MFMA pair ahead (as phase AB)
     auto tread = [&](const char* base, int i) {
       const int row = 16 * (i & 1) + tr_row;
       const int ch = 4 * (i >> 1) + tr_ch;
@@ -495,43 +496,51 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
       }
       __builtin_amdgcn_sched_barrier(0);
       stamp(-1);
-      // phase A: S' / dP' of key tile 0
+      // phase AB: S' / dP' of both key tiles, each Q / dO fragment read once
+      // for both (split into a tile-0 and a tile-1 phase, the fragments were
+      // read twice: 48 b128 reads a step instead of 32), operands one k-step
+      // ahead.  Measured before: phase A 954 and phase B 1132 cycles a step
+      // for 16 MFMAs each (512 at the MFMA roof).
+      bf16x8_t pf0[2], sf0[2], pf1[2], sf1[2];
+      {
+        bf16x8_t qa = lds_b128(qt + roff[0]);
+        bf16x8_t da = lds_b128(dt + roff[0]);
+        bf16x8_t k0 = lds_b128(smem + koff[0]);
+        bf16x8_t k1 = lds_b128(smem + koff[0] + 32 * 256);
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const bf16x8_t qa = lds_b128(qt + roff[s]);
-        const bf16x8_t da = lds_b128(dt + roff[s]);
-        const bf16x8_t kf = lds_b128(smem + koff[s]);
-        mfma_v(s0, qa, kf);
-        mfma_v(p0, da, vf[0][s]);
+        for (int s = 0; s < 8; ++s) {
+          bf16x8_t nq = qa, nd = da, n0 = k0, n1 = k1;
+          if (s < 7) {
+            nq = lds_b128(qt + roff[s + 1]);
+            nd = lds_b128(dt + roff[s + 1]);
+            n0 = lds_b128(smem + koff[s + 1]);
+            n1 = lds_b128(smem + koff[s + 1] + 32 * 256);
+          }
+          if (s == 0) {   // each chain's C may be a VALU copy made just before it
+            mfma_v<true>(s0, qa, k0);
+            mfma_v<true>(p0, da, vf[0][s]);
+            mfma_v<true>(s1, qa, k1);
+            mfma_v<true>(p1, da, vf[1][s]);
+          } else {
+            mfma_v(s0, qa, k0);
+            mfma_v(p0, da, vf[0][s]);
+            mfma_v(s1, qa, k1);
+            mfma_v(p1, da, vf[1][s]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          qa = nq;
+          da = nd;
+          k0 = n0;
+          k1 = n1;
+        }
       }
       mfma_result_fence(s0, p0);
+      mfma_result_fence(s1, p1);
       __builtin_amdgcn_sched_barrier(0);
       stamp(0);
-      // phase B: S' / dP' of key tile 1 beside the softmax of tile 0
-      bf16x8_t pf0[2], sf0[2], pf1[2], sf1[2];
-      // operands one MFMA pair ahead: the reads for pair s + 1 issue at the
-      // top of region s, behind pair s and its softmax chunk (read in their
-      // own region, each pair waited out a whole LDS round trip)
-      bf16x8_t qa = lds_b128(qt + roff[0]);
-      bf16x8_t da = lds_b128(dt + roff[0]);
-      bf16x8_t kf = lds_b128(smem + koff[0] + 32 * 256);
+      // softmax of tile 0 (no MFMA beside it)
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        bf16x8_t nq = qa, nd = da, nk = kf;
-        if (s < 7) {
-          nq = lds_b128(qt + roff[s + 1]);
-          nd = lds_b128(dt + roff[s + 1]);
-          nk = lds_b128(smem + koff[s + 1] + 32 * 256);
-        }
-        mfma_v(s1, qa, kf);
-        mfma_v(p1, da, vf[1][s]);
-        softmax_chunk(s0, p0, 0, qs0, diag, pf0, sf0, s);
-        __builtin_amdgcn_sched_barrier(0);
-        qa = nq;
-        da = nd;
-        kf = nk;
-      }
-      mfma_result_fence(s1, p1);
+      for (int cc = 0; cc < 8; ++cc) softmax_chunk(s0, p0, 0, qs0, diag, pf0, sf0, cc);
       __builtin_amdgcn_sched_barrier(0);
       stamp(1);
       // phase C: dK / dV of tile 0 beside the softmax of tile 1

@@ -43,7 +43,7 @@ for _ in range(3):
 torch.cuda.synchronize()
 s = st.view(nwg, 4, 6).double().cpu()
 tot = s[:, :, 0]
-names = ["A", "B", "C", "D", "wait+barrier"]
+names = ["AB", "softmax0", "C", "D", "wait+barrier"]
 share = {n: (s[:, :, 1 + e].sum() / tot.sum()).item() for e, n in enumerate(names)}
 other = 1 - sum(share.values())
 # steps: a key block kb of the (b, hkv) pair sweeps 4 heads x (S - 256 kb) / 32 slices
@@ -52,6 +52,6 @@ steps = (4 * (S - 256 * kb) // 32).double()
 per_step = {n: (s[:, :, 1 + e].sum(1) / 4 / steps).median().item() for e, n in enumerate(names)}
 print("share of wave cycles: " + ", ".join(f"{n} {v:.3f}" for n, v in share.items()) +
       f", other {other:.3f}")
-print("median cycles per step (64 MFMAs = 2048 at the roof; A/B/C/D 16 each = 512): " +
+print("median cycles per step (64 MFMAs = 2048 at the roof; AB 32 = 1024, C / D 16 = 512): " +
       ", ".join(f"{n} {v:.0f}" for n, v in per_step.items()))
 print("done", flush=True)

@@ -228,6 +228,50 @@ def test_detector_flags_a_copy_of_an_inflight_load():
            "\ts_waitcnt vmcnt(16)\n.Lfunc_end0:\n")
     assert asm_load_dests_touched(asm, "_Zq", "s_waitcnt vmcnt(16)") == ["v_mov_b64_e32 v[70:71], v[2:3]"]
 
+
+def valu_write_then_mfma_read(asm: str, states: int = 2) -> dict[str, int]:
+    """An inline-asm MFMA reading (as A, B or C) a VGPR that a VALU
+    instruction wrote fewer than ``states`` wait states before (hipcc pads
+    this only for its own MFMAs).  Seen: merging the 256-key backward's two
+    S / dP phases put the VALU copies of the initial accumulators right in
+    front of the tile-1 chains (dK off by 9.6)."""
+    bad = {}
+    for name in re.findall(r"^(_Z[^\s:]+):", asm, re.M):
+        i = asm.find(name + ":")
+        j = asm.find(".Lfunc_end", i)
+        body = [ln.split(";")[0].strip() for ln in asm[i:j].split("\n")]
+        body = [ln for ln in body if ln and not ln.startswith(".") and not ln.endswith(":")]
+        pend: dict[int, int] = {}
+        n = 0
+        for ln in body:
+            op, _, rest = ln.partition(" ")
+            m = re.match(r"s_nop (\d+)", ln)
+            step = int(m.group(1)) + 1 if m else 1
+            if op.startswith("v_mfma"):
+                srcs = rest.partition(",")[2]
+                if any(pend.get(r, states) < states for r in _regs(srcs)):
+                    n += 1
+                pend = {r: c + step for r, c in pend.items() if c + step < states}
+                continue
+            pend = {r: c + step for r, c in pend.items() if c + step < states}
+            if op.startswith("v_") and not op.startswith(("v_accvgpr_write", "v_readlane",
+                                                          "v_readfirstlane", "v_cmp")):
+                dst = rest.partition(",")[0]
+                for r in _regs(dst):
+                    pend[r] = 0
+            if op in ("s_branch", "s_endpgm", "s_setpc_b64"):
+                pend = {}
+        if n:
+            bad[name] = n
+    return bad
+
+
+def test_detector_flags_a_fresh_mfma_operand():
+    asm = ("_Zc:\n\tv_mov_b64_e32 v[32:33], v[16:17]\n"
+           "\tv_mfma_f32_32x32x16_bf16 v[32:47], v[0:3], v[4:7], v[32:47]\n.Lfunc_end0:\n")
+    assert valu_write_then_mfma_read(asm) == {"_Zc": 1}
+    assert valu_write_then_mfma_read(asm.replace("\tv_mfma", "\ts_nop 1\n\tv_mfma")) == {}
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src", ["attention_bwd256.hip", "attention_fwd256.hip"])
 def test_attention_bwd256_asm_mfma_hazards_and_spills(src, tmp_path):
@@ -239,6 +283,7 @@ def test_attention_bwd256_asm_mfma_hazards_and_spills(src, tmp_path):
     assert "v_mfma" in asm
     assert close_accumulator_reads(asm) == {}
     assert close_vgpr_result_reads(asm) == {}
+    assert valu_write_then_mfma_read(asm) == {}
     counts = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s+(\d+)", asm)]
     assert counts and not any(counts)
 
