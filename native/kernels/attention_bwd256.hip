@@ -111,6 +111,22 @@ __device__ __forceinline__ void mfma_v(f32x16_t& acc, const bf16x8_t& a, const b
 __device__ __forceinline__ void mfma_result_fence(f32x16_t& x, f32x16_t& y) {
   asm volatile("s_nop 7\n\ts_nop 4" : "+v"(x), "+v"(y));
 }
+// S' / dP' of both key tiles for one k-step, then 12 wait states, in one
+// statement
+__device__ __forceinline__ void mfma4_fenced(f32x16_t& s0, f32x16_t& p0, f32x16_t& s1,
+                                             f32x16_t& p1, const bf16x8_t& qa,
+                                             const bf16x8_t& da, const bf16x8_t& k0,
+                                             const bf16x8_t& k1, const bf16x8_t& v0,
+                                             const bf16x8_t& v1) {
+  asm volatile(
+      "v_mfma_f32_32x32x16_bf16 %0, %4, %6, %0\n\t"
+      "v_mfma_f32_32x32x16_bf16 %1, %5, %8, %1\n\t"
+      "v_mfma_f32_32x32x16_bf16 %2, %4, %7, %2\n\t"
+      "v_mfma_f32_32x32x16_bf16 %3, %5, %9, %3\n\t"
+      "s_nop 7\n\ts_nop 4"
+      : "+v"(s0), "+v"(p0), "+v"(s1), "+v"(p1)
+      : "v"(qa), "v"(da), "v"(k0), "v"(k1), "v"(v0), "v"(v1));
+}
 __device__ __forceinline__ void mfma_result_fence1(f32x16_t& x) {
   asm volatile("s_nop 7\n\ts_nop 4" : "+v"(x));
 }
@@ -279,8 +295,12 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
       dma4m(rr, ring + (i % NSLOT) * QS * 8, static_cast<uint32_t>(r32 * 8 + h * 4),
             static_cast<uint32_t>((gq * S + qs0) * 8));
   };
+  // items of DMA lead: DQ == 0 keeps an item's slices one step longer (its
+  // key tile 1 is finished in the next step, see the step body), so the
+  // ring of 4 holds the pending item, the current one and two ahead
+  constexpr int LEAD = DQ ? NSLOT - 1 : NSLOT - 2;
 #pragma unroll
-  for (int i = 0; i < NSLOT - 1; ++i)
+  for (int i = 0; i < LEAD; ++i)
     if (i < niter) issue(i);
 
   // V's B fragments (dP = dO V^T, key on the lane): lane holds
@@ -296,6 +316,13 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
     for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(vf[kt][s]));
+  if constexpr (DQ == 0) {
+    // the slices the first step's no-op pending tile reads (slot NSLOT - 1,
+    // not filled before step 1): zeros, not uninitialised LDS
+    uint4* z = reinterpret_cast<uint4*>(smem + L::RCB + (NSLOT - 1) * 2 * QIMG);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z[tid + 256 * e] = make_uint4(0, 0, 0, 0);
+  }
   vm_wait<0>();
   __syncthreads();
 
@@ -416,10 +443,14 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
   // issues in the MFMAs' shadow instead of as one block between them.
   auto softmax_chunk = [&](f32x16_t& sacc, f32x16_t& pacc, int kt, int qs0, bool diag,
                            bf16x8_t (&pf)[2], bf16x8_t (&sf)[2], int cc) {
+    // key kw0 + 32 kt + r32 is past query qs0 + crow(r, h) when lim >
+    // (r & 3) + 8 (r >> 2): one compare against a constant per score (off
+    // the diagonal lim is below every constant)
+    const int lim = diag ? kw0 + 32 * kt + r32 - qs0 - 4 * h : -1;
 #pragma unroll
     for (int r = 2 * cc; r < 2 * cc + 2; ++r) {
       float p = fexp2(sacc[r] * c);
-      if (diag && kw0 + 32 * kt + r32 > qs0 + crow(r, h)) p = 0.f;
+      if (lim > (r & 3) + 8 * (r >> 2)) p = 0.f;
       sacc[r] = p;
       pacc[r] = p * pacc[r];
     }
@@ -461,16 +492,32 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     }
   };
 
+  // DQ == 0: the pending item's key tile 1 (S' / dP' accumulators, the
+  // first query row of its slice, its diagonal flag).  Before the first
+  // item a no-op tile: P = exp2(-inf) = 0 and dP' = 0, so dS = 0 (its dK /
+  // dV MFMAs add zeros; the slices they read are the zeroed slot NSLOT - 1).
+  f32x16_t ps1, pp1;
+  int p_qs0 = 0;
+  bool p_diag = false;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    ps1[r] = -INFINITY;
+    pp1[r] = 0.f;
+  }
   auto step = [&](int i, auto slot_c) {
     constexpr int SL = decltype(slot_c)::value;   // == i % NSLOT
-    // slot (i + NSLOT - 1) % NSLOT was last read in item i - 1 (barrier-certified)
-    if (i + NSLOT - 1 < niter) issue(i + NSLOT - 1);
+    // slot (i + LEAD) % NSLOT was last read in step i - 1 (barrier-certified)
+    if (i + LEAD < niter) issue(i + LEAD);
     if constexpr (DQ != 0) {
       if (i > 0) dq_item(i - 1);    // its dS image was completed before this item's barrier
     }
     const int gq = i / nsl;
     const int qs0 = q_begin + (i - gq * nsl) * QS;
-    if (!CAUSAL || qs0 + QS - 1 >= kw0) {     // else every key of this wave is masked
+    // DQ != 0: a wave whose keys are all masked skips the item.  DQ == 0
+    // runs it anyway (the mask zeroes P and dS): the barrier makes the step
+    // as long as its busiest wave either way, and a skip branch made the
+    // allocator spill the pending tile across its merge
+    if (DQ == 0 || !CAUSAL || qs0 + QS - 1 >= kw0) {
       const char* qt = smem + L::RCB + SL * 2 * QIMG;
       const char* dt = qt + QIMG;
       const float* rc = reinterpret_cast<const float*>(smem + SL * QS * 8);
@@ -501,55 +548,83 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
       // read twice: 48 b128 reads a step instead of 32), operands one k-step
       // ahead.  Measured before: phase A 954 and phase B 1132 cycles a step
       // for 16 MFMAs each (512 at the MFMA roof).
+      //
+      // DQ == 0 pipelines across steps: beside phase AB the softmax of the
+      // PREVIOUS item's key tile 1, then its dK / dV beside this item's tile-0
+      // softmax, then this item's tile-0 dK / dV; tile 1 stays pending (its
+      // S' / dP' in ps1 / pp1) until the next step.  Every MFMA phase then has
+      // VALU work beside it but the last (run alone, the tile-0 softmax
+      // measured 721 cycles a step).  DQ != 0: the item's softmax of tile 0
+      // alone, dK / dV of tile 0 beside the softmax of tile 1, then tile 1.
       bf16x8_t pf0[2], sf0[2], pf1[2], sf1[2];
       {
         bf16x8_t qa = lds_b128(qt + roff[0]);
         bf16x8_t da = lds_b128(dt + roff[0]);
         bf16x8_t k0 = lds_b128(smem + koff[0]);
-        bf16x8_t k1 = lds_b128(smem + koff[0] + 32 * 256);
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-          bf16x8_t nq = qa, nd = da, n0 = k0, n1 = k1;
+          // K of tile 1 read in its own k-step (its MFMA is the third): one
+          // operand fewer held ahead (VGPRs)
+          const bf16x8_t k1 = lds_b128(smem + koff[s] + 32 * 256);
+          bf16x8_t nq = qa, nd = da, n0 = k0;
           if (s < 7) {
             nq = lds_b128(qt + roff[s + 1]);
             nd = lds_b128(dt + roff[s + 1]);
             n0 = lds_b128(smem + koff[s + 1]);
-            n1 = lds_b128(smem + koff[s + 1] + 32 * 256);
           }
           if (s == 0) {   // each chain's C may be a VALU copy made just before it
             mfma_v<true>(s0, qa, k0);
             mfma_v<true>(p0, da, vf[0][s]);
             mfma_v<true>(s1, qa, k1);
             mfma_v<true>(p1, da, vf[1][s]);
-          } else {
+          } else if (s < 7) {
             mfma_v(s0, qa, k0);
             mfma_v(p0, da, vf[0][s]);
             mfma_v(s1, qa, k1);
             mfma_v(p1, da, vf[1][s]);
+          } else {
+            // the last four with the XDL-write -> VALU wait states inside the
+            // same statement: with a separate fence statement the allocator
+            // moved the results into the fence's registers ahead of it (the
+            // pending tile's copies), reading them 10 states after the MFMA
+            mfma4_fenced(s0, p0, s1, p1, qa, da, k0, k1, vf[0][s], vf[1][s]);
           }
+          if constexpr (DQ == 0) softmax_chunk(ps1, pp1, 1, p_qs0, p_diag, pf1, sf1, s);
           __builtin_amdgcn_sched_barrier(0);
           qa = nq;
           da = nd;
           k0 = n0;
-          k1 = n1;
         }
       }
-      mfma_result_fence(s0, p0);
-      mfma_result_fence(s1, p1);
-      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);   // (k-step 7's statement carried the wait states)
       stamp(0);
-      // softmax of tile 0 (no MFMA beside it)
+      if constexpr (DQ == 0) {
+        constexpr int PSL = (SL + NSLOT - 1) % NSLOT;   // the pending item's slot
+        const char* pq = smem + L::RCB + PSL * 2 * QIMG;
+        dkdv(pq, pq + QIMG, 1, pf1, sf1,
+             [&](int cc) { softmax_chunk(s0, p0, 0, qs0, diag, pf0, sf0, cc); });
+        stamp(1);
+        dkdv(qt, dt, 0, pf0, sf0, [](int) {});
+        stamp(2);
+        ps1 = s1;
+        pp1 = p1;
+        p_qs0 = qs0;
+        p_diag = diag;
+        stamp(3);
+      } else {
+        // softmax of tile 0 (no MFMA beside it)
 #pragma unroll
-      for (int cc = 0; cc < 8; ++cc) softmax_chunk(s0, p0, 0, qs0, diag, pf0, sf0, cc);
-      __builtin_amdgcn_sched_barrier(0);
-      stamp(1);
-      // phase C: dK / dV of tile 0 beside the softmax of tile 1
-      dkdv(qt, dt, 0, pf0, sf0,
-           [&](int cc) { softmax_chunk(s1, p1, 1, qs0, diag, pf1, sf1, cc); });
-      stamp(2);
-      // phase D: dK / dV of tile 1
-      dkdv(qt, dt, 1, pf1, sf1, [](int) {});
-      stamp(3);
+        for (int cc = 0; cc < 8; ++cc) softmax_chunk(s0, p0, 0, qs0, diag, pf0, sf0, cc);
+        __builtin_amdgcn_sched_barrier(0);
+        stamp(1);
+        // phase C: dK / dV of tile 0 beside the softmax of tile 1
+        dkdv(qt, dt, 0, pf0, sf0,
+             [&](int cc) { softmax_chunk(s1, p1, 1, qs0, diag, pf1, sf1, cc); });
+        stamp(2);
+        // phase D: dK / dV of tile 1
+        dkdv(qt, dt, 1, pf1, sf1, [](int) {});
+        stamp(3);
+      }
       if constexpr (DQ != 0) {
         // dS into the image (buffer i & 1; its previous item's dQ reads
         // ended before the last barrier): element j of sf[kt][s2] is row
@@ -570,7 +645,7 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     // every wave's pieces (and dS image) and certifies slot i % 3 is no
     // longer read
     const int pieces = wave == 0 ? 5 : 4;
-    const int younger = min(NSLOT - 2, max(0, niter - 2 - i));   // items issued after i + 1
+    const int younger = min(LEAD - 1, max(0, niter - 2 - i));   // items issued after i + 1
     if constexpr (STAMP) {
       if (st_c == 0) st_c = __builtin_readcyclecounter();   // a skipped (masked) item
     }
@@ -588,6 +663,14 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
       if (i + 3 < niter) step(i + 3, std::integral_constant<int, 3>{});
   }
   if constexpr (DQ != 0) dq_item(niter - 1);
+  if constexpr (DQ == 0) {   // the last pending tile 1
+    const char* pq = smem + L::RCB + ((niter - 1) % NSLOT) * 2 * QIMG;
+    bf16x8_t pf1[2], sf1[2];
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) softmax_chunk(ps1, pp1, 1, p_qs0, p_diag, pf1, sf1, cc);
+    __builtin_amdgcn_sched_barrier(0);
+    dkdv(pq, pq + QIMG, 1, pf1, sf1, [](int) {});
+  }
   mfma_drain_acc(dva, dka);
 
   // ---- dK = scale * (dK^T)^T, dV: lane = key, registers r -> d = 32 db + crow(r, h)
