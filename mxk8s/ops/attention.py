@@ -76,7 +76,7 @@ def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None, variant: 
     return o, lse
 
 
-_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "5"))
+_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "6"))
 
 
 def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = None,
@@ -85,7 +85,16 @@ def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = N
 
     ``dk``/``dv`` may be preallocated views (e.g. slices of a fused dQKV
     buffer) with a token stride; by default they are fresh contiguous tensors.
-    ``variant`` 5 (default): variant 3 with the delta pass (dO . O per query
+    ``variant`` 6 (default; S % 256 == 0, else 5): variant 5's dQ kernel (it
+    also writes the row constants -lse/scale and -delta), then dK / dV by the
+    256-key workgroups of attention_bwd256.hip (one wave per SIMD, dK^T / dV^T
+    in accumulators, S / dP of both key tiles from one read of each Q / dO
+    fragment, a key tile's softmax and dK / dV pipelined into the next step):
+    1.018 vs 1.044 ms for variant 5 per Llama-3-8B layer at B 8, deterministic
+    (profiles/r5_attention/).  8: one pass, dQ added by packed-bf16 atomics
+    from the 256-key workgroups (0.983 ms; dQ summed in bf16 in a
+    nondeterministic order); 7: the same with fp32 atomics and a convert pass
+    (1.139 ms).  5: variant 3 with the delta pass (dO . O per query
     row) folded into the dQ kernel, which then runs before dK/dV: no separate
     delta kernel, 1.042 vs 1.064 ms per Llama-3-8B layer at B 8
     (profiles/r4_final/attention_b8.log).  3: variant 2 with explicitly software-pipelined

@@ -561,16 +561,15 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
         bf16x8_t qa = lds_b128(qt + roff[0]);
         bf16x8_t da = lds_b128(dt + roff[0]);
         bf16x8_t k0 = lds_b128(smem + koff[0]);
+        bf16x8_t k1 = lds_b128(smem + koff[0] + 32 * 256);
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-          // K of tile 1 read in its own k-step (its MFMA is the third): one
-          // operand fewer held ahead (VGPRs)
-          const bf16x8_t k1 = lds_b128(smem + koff[s] + 32 * 256);
-          bf16x8_t nq = qa, nd = da, n0 = k0;
+          bf16x8_t nq = qa, nd = da, n0 = k0, n1 = k1;
           if (s < 7) {
             nq = lds_b128(qt + roff[s + 1]);
             nd = lds_b128(dt + roff[s + 1]);
             n0 = lds_b128(smem + koff[s + 1]);
+            n1 = lds_b128(smem + koff[s + 1] + 32 * 256);
           }
           if (s == 0) {   // each chain's C may be a VALU copy made just before it
             mfma_v<true>(s0, qa, k0);
@@ -594,6 +593,7 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
           qa = nq;
           da = nd;
           k0 = n0;
+          k1 = n1;
         }
       }
       __builtin_amdgcn_sched_barrier(0);   // (k-step 7's statement carried the wait states)

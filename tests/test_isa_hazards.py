@@ -284,8 +284,13 @@ def test_attention_bwd256_asm_mfma_hazards_and_spills(src, tmp_path):
     assert close_accumulator_reads(asm) == {}
     assert close_vgpr_result_reads(asm) == {}
     assert valu_write_then_mfma_read(asm) == {}
+    # production instances (the cycle-stamp diagnostic ones, last template
+    # argument STAMP = true, are exempt)
+    names = re.findall(r"^\s+\.name:\s+(_Z\S+)", asm, re.M)
     counts = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s+(\d+)", asm)]
-    assert counts and not any(counts)
+    assert len(names) == len(counts) and names
+    prod = {n: c for n, c in zip(names, counts) if "Lb1EEv" not in n}
+    assert prod and not any(prod.values()), prod
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
