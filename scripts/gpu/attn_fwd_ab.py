@@ -13,7 +13,7 @@ from mxk8s.ops import attention as A  # noqa: E402
 
 
 def main():
-    B, S, Hq, Hkv, D = int(os.environ.get("B", 8)), 2048, 32, 8, 128
+    B, S, Hq, Hkv, D = int(os.environ.get("B", 8)), int(os.environ.get("S", 2048)), 32, 8, 128
     variants = [int(x) for x in os.environ.get("VARIANTS", "0,2").split(",")]
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
