@@ -168,8 +168,7 @@ mxk_gemm_bf16_w13_swiglu_k(const uint16_t* __restrict__ X, const uint16_t* __res
   // tile rows 128..255 of the B panel are the up rows F + g0 ..: pieces 4..7
   dma_b.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(W13 + static_cast<size_t>(g0) * ldw),
                                                  0, (F + 128) * ldw * 2, 0x00020000);
-#pragma unroll
-  for (int p = 4; p < 8; ++p) dma_b.voff[p] += static_cast<uint32_t>((F - 128) * ldw * 2);
+  dma_b.hi = static_cast<uint32_t>((F - 128) * ldw * 2);
 
   const int frow = lane & 15;
   const int fch = (lane >> 4) ^ (frow >> 1);
@@ -382,7 +381,7 @@ MXK_API void mxk_gemm_stagger_part_xcd(int b, int T, int cx, int* out) {
 }
 
 namespace {
-constexpr int kNumVariants = 58;
+constexpr int kNumVariants = 59;
 constexpr int kDefaultVariant = 52;
 constexpr int kNarrowCVariant = 1;
 constexpr const char* kVariantNames[kNumVariants] = {
@@ -394,7 +393,8 @@ constexpr const char* kVariantNames[kNumVariants] = {
     "w4j_ldsst_swz6", "w4j_ldsst_swz5", "w4j_ldsst_map4x8", "w4j_ldsst_map2x16",
     "w4j_ldsst_map16x2", "w4j_ldsst_rot_xcd", "diag_stamps", "w4i_ldsst_full_template",
     "w4k_1bar_a3_ldsst", "diag_w4k_nodma", "diag_w4k_noreads", "diag_w4k_nowait",
-    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore", "w4j_stagger", "w4j_stagger_cached", "w4j_l2pf", "w4j_stagger_xcd"};
+    "diag_w4k_mfma_only", "w4k_border", "diag_w4k_nostore", "w4j_stagger", "w4j_stagger_cached", "w4j_l2pf", "w4j_stagger_xcd",
+    "w4p_persistent"};
 
 }  // namespace
 #ifdef MXK_GEMM_EXPERIMENTS
@@ -424,6 +424,15 @@ void launch_256(int v, int nwg, hipStream_t stream, const void* A, const void* B
                          static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
                          static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
       break;
+    case 58: {
+      // persistent: one workgroup per available CU (at most one per tile)
+      const int cus = mxk_gemm_available_cus();
+      const int grid = cus > 0 && cus < nwg ? cus : nwg;
+      MXK_LAUNCH_GEMM((mxk_gemm_bf16_tn_w4p<1, 1>), dim3(grid), dim3(W4_THREADS), stream,
+                         static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
+                         static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc);
+      break;
+    }
     case 1: launch_w4j<0>(nwg, stream, A, Bt, C, M, N, K, lda, ldb, ldc); break;
     case 6: launch_w4j<2>(nwg, stream, A, Bt, C, M, N, K, lda, ldb, ldc); break;
     case 9:
@@ -448,7 +457,7 @@ bool variant_built(int v) {
 #ifdef MXK_GEMM_EXPERIMENTS
   return v >= 0 && v < kNumVariants;
 #else
-  return v == 1 || v == 6 || v == 9 || v == 26 || v == 47 || v == 52;
+  return v == 1 || v == 6 || v == 9 || v == 26 || v == 47 || v == 52 || v == 58;
 #endif
 }
 

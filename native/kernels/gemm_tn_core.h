@@ -49,10 +49,20 @@ using mxk::stagger_part_xcd;
 
 struct DmaK {
   __amdgpu_buffer_rsrc_t rsrc;   // 256-row panel, whole K
-  uint32_t voff[8];              // piece p: row-in-piece * ld * 2 + swizzled chunk + (4p + wave) * 8 rows
+  // piece p's lane offset = voff (this lane's row-in-piece * ld * 2 + its
+  // swizzled chunk + the wave's 8 rows) in one VGPR; the piece's 32-row
+  // step p * pstride (+ hi for pieces 4..7) goes into the scalar offset,
+  // beside the K-tile's byte offset: 1 VGPR per operand instead of 8 (the
+  // persistent schedule's loop state did not fit beside the K loop's
+  // fragments otherwise)
+  uint32_t voff;
+  uint32_t pstride;   // 32 rows, bytes (wave-uniform)
+  uint32_t hi = 0;    // extra offset of pieces 4..7 (the w13 up rows)
   __device__ __forceinline__ void issue(char* lds_op, int p, int k_bytes, int wave_s) const {
+    const uint32_t so = static_cast<uint32_t>(k_bytes) + static_cast<uint32_t>(p) * pstride +
+                        (p >= 4 ? hi : 0u);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_op + (p * 4 + wave_s) * 1024),
-                                             16, voff[p], k_bytes, 0, 0);
+                                             16, voff, static_cast<int>(so), 0, 0);
   }
 };
 
@@ -66,10 +76,8 @@ __device__ __forceinline__ DmaK make_dmak(const uint16_t* src, int ld, int row0,
   // swm 7: the full XOR swizzle; 4: only the 64-B halves swap (each 4-lane
   // group keeps an ascending 64-B source run); 0: linear (A/B variants 37/38)
   const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & swm);
-  const uint32_t lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
-#pragma unroll
-  for (int p = 0; p < 8; ++p)
-    d.voff[p] = lane_off + static_cast<uint32_t>((p * 4 + wave) * 8 * ld * 2);
+  d.voff = static_cast<uint32_t>(r * ld * 2 + c * 16) + static_cast<uint32_t>(wave * 8 * ld * 2);
+  d.pstride = static_cast<uint32_t>(32 * ld * 2);
   return d;
 }
 
@@ -557,10 +565,14 @@ __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
 // of stages 0 and 1, the K-tiles unrolled by the 6-K-tile slot cycle, the two
 // DMA-free tail K-tiles, the MFMA drain.  smem: A3_LDS bytes; b_base relative
 // to a B slot.
+// pre (the persistent kernel's second and later tiles): stage 0 was issued
+// before the previous tile's epilogue, whose 32 C stores per wave are still
+// counted in vmcnt; stage 1 goes out after a barrier (its slots held the
+// epilogue's LDS slices).
 template <int ABL = 0, int ORDER = 0, bool SPLITA = false>
 __device__ __forceinline__ void w4k_mainloop(f32x4_t (&acc)[8][8], char* smem, const DmaK& dma_a,
                                              const DmaK& dma_b, int a_base, int a_hi, int b_base,
-                                             int ns, int lane, int wave_s) {
+                                             int ns, int lane, int wave_s, bool pre = false) {
   const int frow = lane & 15;
   const int fch = (lane >> 4) ^ ((frow >> 1) & 7);
   const int off_k0 = frow * 128 + fch * 16;
@@ -568,22 +580,33 @@ __device__ __forceinline__ void w4k_mainloop(f32x4_t (&acc)[8][8], char* smem, c
   constexpr int SUB = 2048;
   auto aoff = [&](int r) { return SPLITA && r >= 4 ? a_hi + (r - 4) * SUB : a_base + r * SUB; };
 
+  // an opaque zero: a constant zero is hoisted out of the persistent tile
+  // loop, held in VGPRs across the K loop and spilled (its reload carried a
+  // vmcnt(0) that drained the next tile's prefetched stage)
+  float z = 0.f;
+  asm volatile("" : "+v"(z));
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{z, z, z, z};
 
   // stages 0 and 1: A slots 0, 1 and B slots 0, 1
+  if (!pre) {
 #pragma unroll
-  for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+    for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
 #pragma unroll
-  for (int p = 0; p < 8; ++p) dma_b.issue(smem + A3_B0, p, 0, wave_s);
+    for (int p = 0; p < 8; ++p) dma_b.issue(smem + A3_B0, p, 0, wave_s);
+  } else {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+  }
   if (ns > 1) {
 #pragma unroll
     for (int p = 0; p < 8; ++p) dma_a.issue(smem + A3_SLOT, p, BK * 2, wave_s);
 #pragma unroll
     for (int p = 0; p < 8; ++p) dma_b.issue(smem + A3_B0 + A3_SLOT, p, BK * 2, wave_s);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    if (pre) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");   // + the 32 stores
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -658,4 +681,71 @@ mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict_
                                smem + wave_s * mxk::kStoreLdsWave);
   } else if constexpr (EPI == 2) store_block_wide<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
+}
+
+// Persistent form of the default schedule (52): one workgroup per CU walks
+// tiles t = blockIdx.x, + gridDim.x, ... of the same MAP (with 256
+// workgroups a workgroup keeps its XCD and super-block position, the rounds
+// advance as in the one-shot launch).  After a tile's K loop the next tile's
+// stage 0 (A slot 0, B slot 0) is issued BEFORE the epilogue, so its fetch
+// latency hides behind the C stores instead of opening the next K loop; the
+// epilogue's LDS slices move to A slots 1-2 (waves 0-2) and B slot 1 (wave
+// 3), which stage 1 refills only after a barrier.
+template <int MAP, int ORDER = 1>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_tn_w4p(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+  static_assert(3 * mxk::kStoreLdsWave <= 2 * A3_SLOT && mxk::kStoreLdsWave <= A3_SLOT,
+                "epilogue slices in A slots 1-2 and B slot 1");
+  __shared__ __attribute__((aligned(16))) char smem[A3_LDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;
+  const int ntiles = (M / BM) * (N / BN);
+  constexpr int SUB = 2048;
+  char* slice = wave_s < 3 ? smem + A3_SLOT + wave_s * mxk::kStoreLdsWave : smem + A3_B0 + A3_SLOT;
+  int t = blockIdx.x;
+  int m0, n0;
+  w4b_tile<MAP>(t, ntiles, M / BM, N / BN, &m0, &n0);
+  DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
+  DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
+  bool pre = false;
+  for (;;) {
+    f32x4_t acc[8][8];
+    int lane_k = lane;   // opaque per tile (see lane_e below)
+    asm volatile("" : "+v"(lane_k));
+    w4k_mainloop<0, ORDER>(acc, smem, dma_a, dma_b, wm * 8 * SUB, 0, wn * 8 * SUB, K / BK, lane_k,
+                           wave_s, pre);
+    // every wave's last fragment reads retired: all slots free
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    const int tn = t + static_cast<int>(gridDim.x);
+    int m1 = 0, n1 = 0;
+    if (tn < ntiles) {
+      // opaque tile counts: the map's divisions by them are redone here,
+      // not hoisted out of the loop as VGPR reciprocals that then spill
+      int tiles_m = M / BM, tiles_n = N / BN;
+      asm volatile("" : "+s"(tiles_m), "+s"(tiles_n));
+      w4b_tile<MAP>(tn, ntiles, tiles_m, tiles_n, &m1, &n1);
+      dma_a = make_dmak(A, lda, m1, lane, wave_s);
+      dma_b = make_dmak(Bt, ldb, n1, lane, wave_s);
+#pragma unroll
+      for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+#pragma unroll
+      for (int p = 0; p < 8; ++p) dma_b.issue(smem + A3_B0, p, 0, wave_s);
+    }
+    // an opaque lane id: the epilogue's lane-derived addresses are formed
+    // here, not hoisted out of the tile loop (live across the K loop they
+    // made the allocator spill)
+    int lane_e = lane;
+    asm volatile("" : "+v"(lane_e));
+    mxk::store_block_lds<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane_e, slice);
+    if (tn >= ntiles) break;
+    t = tn;
+    m0 = m1;
+    n0 = n1;
+    pre = true;
+  }
 }
