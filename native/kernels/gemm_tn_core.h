@@ -49,20 +49,10 @@ using mxk::stagger_part_xcd;
 
 struct DmaK {
   __amdgpu_buffer_rsrc_t rsrc;   // 256-row panel, whole K
-  // piece p's lane offset = voff (this lane's row-in-piece * ld * 2 + its
-  // swizzled chunk + the wave's 8 rows) in one VGPR; the piece's 32-row
-  // step p * pstride (+ hi for pieces 4..7) goes into the scalar offset,
-  // beside the K-tile's byte offset: 1 VGPR per operand instead of 8 (the
-  // persistent schedule's loop state did not fit beside the K loop's
-  // fragments otherwise)
-  uint32_t voff;
-  uint32_t pstride;   // 32 rows, bytes (wave-uniform)
-  uint32_t hi = 0;    // extra offset of pieces 4..7 (the w13 up rows)
+  uint32_t voff[8];              // piece p: row-in-piece * ld * 2 + swizzled chunk + (4p + wave) * 8 rows
   __device__ __forceinline__ void issue(char* lds_op, int p, int k_bytes, int wave_s) const {
-    const uint32_t so = static_cast<uint32_t>(k_bytes) + static_cast<uint32_t>(p) * pstride +
-                        (p >= 4 ? hi : 0u);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_op + (p * 4 + wave_s) * 1024),
-                                             16, voff, static_cast<int>(so), 0, 0);
+                                             16, voff[p], k_bytes, 0, 0);
   }
 };
 
@@ -76,8 +66,10 @@ __device__ __forceinline__ DmaK make_dmak(const uint16_t* src, int ld, int row0,
   // swm 7: the full XOR swizzle; 4: only the 64-B halves swap (each 4-lane
   // group keeps an ascending 64-B source run); 0: linear (A/B variants 37/38)
   const int c = (lane & 7) ^ ((4 * (wave & 1) + (r >> 1)) & swm);
-  d.voff = static_cast<uint32_t>(r * ld * 2 + c * 16) + static_cast<uint32_t>(wave * 8 * ld * 2);
-  d.pstride = static_cast<uint32_t>(32 * ld * 2);
+  const uint32_t lane_off = static_cast<uint32_t>(r * ld * 2 + c * 16);
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+    d.voff[p] = lane_off + static_cast<uint32_t>((p * 4 + wave) * 8 * ld * 2);
   return d;
 }
 
@@ -709,13 +701,15 @@ mxk_gemm_bf16_tn_w4p(const uint16_t* __restrict__ A, const uint16_t* __restrict_
   int t = blockIdx.x;
   int m0, n0;
   w4b_tile<MAP>(t, ntiles, M / BM, N / BN, &m0, &n0);
-  DmaK dma_a = make_dmak(A, lda, m0, lane, wave_s);
-  DmaK dma_b = make_dmak(Bt, ldb, n0, lane, wave_s);
   bool pre = false;
   for (;;) {
     f32x4_t acc[8][8];
     int lane_k = lane;   // opaque per tile (see lane_e below)
     asm volatile("" : "+v"(lane_k));
+    // the DMA descriptors are rebuilt per tile (only m0 / n0 cross the
+    // loop): carried, their 16 offset VGPRs pushed the K loop into spills
+    const DmaK dma_a = make_dmak(A, lda, m0, lane_k, wave_s);
+    const DmaK dma_b = make_dmak(Bt, ldb, n0, lane_k, wave_s);
     w4k_mainloop<0, ORDER>(acc, smem, dma_a, dma_b, wm * 8 * SUB, 0, wn * 8 * SUB, K / BK, lane_k,
                            wave_s, pre);
     // every wave's last fragment reads retired: all slots free
@@ -729,12 +723,12 @@ mxk_gemm_bf16_tn_w4p(const uint16_t* __restrict__ A, const uint16_t* __restrict_
       int tiles_m = M / BM, tiles_n = N / BN;
       asm volatile("" : "+s"(tiles_m), "+s"(tiles_n));
       w4b_tile<MAP>(tn, ntiles, tiles_m, tiles_n, &m1, &n1);
-      dma_a = make_dmak(A, lda, m1, lane, wave_s);
-      dma_b = make_dmak(Bt, ldb, n1, lane, wave_s);
+      const DmaK na = make_dmak(A, lda, m1, lane_k, wave_s);
+      const DmaK nb = make_dmak(Bt, ldb, n1, lane_k, wave_s);
 #pragma unroll
-      for (int p = 0; p < 8; ++p) dma_a.issue(smem, p, 0, wave_s);
+      for (int p = 0; p < 8; ++p) na.issue(smem, p, 0, wave_s);
 #pragma unroll
-      for (int p = 0; p < 8; ++p) dma_b.issue(smem + A3_B0, p, 0, wave_s);
+      for (int p = 0; p < 8; ++p) nb.issue(smem + A3_B0, p, 0, wave_s);
     }
     // an opaque lane id: the epilogue's lane-derived addresses are formed
     // here, not hoisted out of the tile loop (live across the K loop they
