@@ -272,6 +272,37 @@ def test_detector_flags_a_fresh_mfma_operand():
     assert valu_write_then_mfma_read(asm) == {"_Zc": 1}
     assert valu_write_then_mfma_read(asm.replace("\tv_mfma", "\ts_nop 1\n\tv_mfma")) == {}
 
+
+def scratch_in_loops(asm: str) -> dict[str, int]:
+    """Scratch (spill) instructions between a loop header label and the last
+    branch back to it, per kernel (linear layout: LLVM keeps a loop's blocks
+    contiguous)."""
+    bad = {}
+    for name in re.findall(r"^(_Z[^\s:]+):", asm, re.M):
+        i = asm.find(name + ":")
+        j = asm.find(".Lfunc_end", i)
+        lines = asm[i:j].split("\n")
+        n = 0
+        for k, ln in enumerate(lines):
+            m = re.match(r"^(\.LBB\d+_\d+):.*Loop Header", ln)
+            if not m:
+                continue
+            lab = m.group(1)
+            ends = [e for e in range(k + 1, len(lines))
+                    if re.match(r"\s*s_c?branch\S*\s+" + re.escape(lab) + r"\b", lines[e])]
+            if ends:
+                n += sum(1 for e in range(k, ends[-1]) if "scratch_" in lines[e].split(";")[0])
+        if n:
+            bad[name] = n
+    return bad
+
+
+def test_detector_flags_a_reload_in_a_loop():
+    asm = ("_Zl:\n.LBB0_1:  ; =>This Inner Loop Header: Depth=1\n"
+           "\tscratch_load_dword v1, off, off\n\ts_cbranch_scc1 .LBB0_1\n"
+           "\tscratch_load_dword v2, off, off\n.Lfunc_end0:\n")
+    assert scratch_in_loops(asm) == {"_Zl": 1}
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src", ["attention_bwd256.hip", "attention_fwd256.hip"])
 def test_attention_bwd256_asm_mfma_hazards_and_spills(src, tmp_path):
@@ -284,13 +315,10 @@ def test_attention_bwd256_asm_mfma_hazards_and_spills(src, tmp_path):
     assert close_accumulator_reads(asm) == {}
     assert close_vgpr_result_reads(asm) == {}
     assert valu_write_then_mfma_read(asm) == {}
-    # production instances (the cycle-stamp diagnostic ones, last template
-    # argument STAMP = true, are exempt)
-    names = re.findall(r"^\s+\.name:\s+(_Z\S+)", asm, re.M)
-    counts = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s+(\d+)", asm)]
-    assert len(names) == len(counts) and names
-    prod = {n: c for n, c in zip(names, counts) if "Lb1EEv" not in n}
-    assert prod and not any(prod.values()), prod
+    # no scratch access inside a loop (a reload there is a vector-memory op
+    # the counted vmcnt waits of the LDS-DMA rings do not expect); a spill
+    # stored before the loop and reloaded after it is harmless
+    assert scratch_in_loops(asm) == {}
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
