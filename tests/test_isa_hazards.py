@@ -223,6 +223,42 @@ def test_fwd256_prologue_q_loads_untouched_before_their_wait(tmp_path):
     assert asm_load_dests_touched(asm, "mxk_attn_fwd256_kernel", "s_waitcnt vmcnt(16)") == []
 
 
+_TRANS = ("v_exp_f32", "v_log_f32", "v_rcp_f32", "v_rsq_f32", "v_sqrt_f32", "v_sin_f32", "v_cos_f32")
+
+
+def trans_result_read_next(asm: str) -> list[str]:
+    """An instruction reading the result of the transcendental right before
+    it (gfx950 needs one wait state there; hipcc pads its own instructions
+    but not an inline-asm reader).  Seen: the 256-row forward's asm row-sum
+    adds behind the v_exp_f32 of their score - wrong sums in the lanes the
+    transcendental unit had not finished."""
+    bad = []
+    body = [ln.split(";")[0].strip() for ln in asm.split("\n")]
+    body = [ln for ln in body if ln and not ln.startswith(".") and not ln.endswith(":")]
+    for k, ln in enumerate(body[:-1]):
+        op, _, rest = ln.partition(" ")
+        if not op.startswith(_TRANS):
+            continue
+        nxt = body[k + 1]
+        if nxt.startswith("s_nop") or "," not in nxt:
+            continue
+        if _regs(nxt.split(",", 1)[1]) & _regs(rest.split(",")[0]):
+            bad.append(ln + " | " + nxt)
+    return bad
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src", ["attention.hip", "attention_bwd256.hip", "attention_fwd256.hip"])
+def test_no_asm_read_of_a_fresh_transcendental(src, tmp_path):
+    asm = _asm(src, str(tmp_path / "t.s"))
+    assert trans_result_read_next(asm) == []
+
+
+def test_detector_flags_a_fresh_transcendental_read():
+    asm = "\tv_exp_f32_e32 v26, v26\n\tv_add_f32_e32 v4, v4, v26\n\tv_exp_f32_e32 v2, v2\n\ts_nop 0\n\tv_add_f32_e32 v4, v4, v2\n"
+    assert trans_result_read_next(asm) == ["v_exp_f32_e32 v26, v26 | v_add_f32_e32 v4, v4, v26"]
+
+
 def test_detector_flags_a_copy_of_an_inflight_load():
     asm = ("_Zq:\n\tglobal_load_dwordx4 v[2:5], v[30:31], off\n\tv_mov_b64_e32 v[70:71], v[2:3]\n"
            "\ts_waitcnt vmcnt(16)\n.Lfunc_end0:\n")
