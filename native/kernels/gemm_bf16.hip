@@ -278,6 +278,121 @@ mxk_gemm_bf16_w13_swiglu_k(const uint16_t* __restrict__ X, const uint16_t* __res
                                      m0 + wm * 128 + (wn ? 64 : 0), g0, lane);
 }
 
+#ifdef MXK_GEMM_EXPERIMENTS
+// Persistent form of the fused up-projection (A/B record, MXK_W13_SCHED=3):
+// one workgroup per CU walks tiles t = blockIdx.x, + gridDim.x, ... with the
+// one-barrier K loop (TN schedule 52's, A fragments split gate / up).  After
+// a tile's K loop the NEXT tile's stage 0 (A slot 0, B slot 0) is issued
+// before this tile's epilogue, so the gu / h stores drain while the next K
+// loop starts instead of ahead of a fresh workgroup's prologue.  The
+// epilogue works in the LDS that stage 0 leaves free: gu staged through A
+// slots 1-2 (waves 0-2) and B slot 1 (wave 3), then the gate / up hand-off
+// in two rounds of 16 KiB per wave through A slots 1-2 (the one-shot kernel
+// hands over 32 KiB per wave in one round, 128 KiB, more than is free).
+__device__ __forceinline__ DmaK make_dmak_w13(const uint16_t* W13, int ldw, int g0, int F, int lane,
+                                              int wave_s) {
+  DmaK d = make_dmak(W13, ldw, g0, lane, wave_s);
+  // tile rows 128..255 of the B panel are the up rows F + g0 ..: pieces 4..7
+  d.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(W13 + static_cast<size_t>(g0) * ldw), 0,
+                                             (F + 128) * ldw * 2, 0x00020000);
+#pragma unroll
+  for (int p = 4; p < 8; ++p) d.voff[p] += static_cast<uint32_t>((F - 128) * ldw * 2);
+  return d;
+}
+
+__global__ void __launch_bounds__(W4_THREADS, 1)
+mxk_gemm_bf16_w13_swiglu_p(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W13,
+                           uint16_t* __restrict__ GU, uint16_t* __restrict__ H, int M, int F, int K,
+                           int ldx, int ldw, int ldgu, int ldh) {
+  static_assert(3 * mxk::kStoreLdsWave <= 2 * A3_SLOT && mxk::kStoreLdsWave <= A3_SLOT,
+                "gu slices in A slots 1-2 and B slot 1");
+  __shared__ __attribute__((aligned(16))) char smem[A3_LDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave_s >> 1;
+  const int wn = wave_s & 1;               // 0: gate columns, 1: up columns
+  const int ntiles = (M / BM) * (F / 128);
+  constexpr int SUB = 2048;
+  const int a_lo = (wm * 8 + (wn ? 4 : 0)) * SUB;
+  const int a_hi = (wm * 8 + (wn ? 0 : 4)) * SUB;
+  char* slice = wave_s < 3 ? smem + A3_SLOT + wave_s * mxk::kStoreLdsWave : smem + A3_B0 + A3_SLOT;
+  int t = blockIdx.x;
+  int m0, n0v;
+  w4b_tile<1>(t, ntiles, M / BM, F / 128, &m0, &n0v);
+  bool pre = false;
+  for (;;) {
+    f32x4_t acc[8][8];
+    int lane_k = lane;   // opaque per tile (gemm_tn_core.h w4p)
+    asm volatile("" : "+v"(lane_k));
+    const int g0 = n0v >> 1;
+    const DmaK dma_a = make_dmak(X, ldx, m0, lane_k, wave_s);
+    const DmaK dma_b = make_dmak_w13(W13, ldw, g0, F, lane_k, wave_s);
+    // stage 0 issued before the previous epilogue's 32 gu + 16 h stores:
+    // vmcnt 63 (stage 1's 16 pieces + 47 of the stores) waits for it
+    w4k_mainloop<0, 1, true, 63>(acc, smem, dma_a, dma_b, a_lo, a_hi, wn * 8 * SUB, K / BK, lane_k,
+                                 wave_s, pre);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    const int tn = t + static_cast<int>(gridDim.x);
+    int m1 = 0, n1v = 0;
+    if (tn < ntiles) {
+      int tiles_m = M / BM, tiles_n = F / 128;
+      asm volatile("" : "+s"(tiles_m), "+s"(tiles_n));
+      w4b_tile<1>(tn, ntiles, tiles_m, tiles_n, &m1, &n1v);
+      const DmaK na = make_dmak(X, ldx, m1, lane_k, wave_s);
+      const DmaK nb = make_dmak_w13(W13, ldw, n1v >> 1, F, lane_k, wave_s);
+#pragma unroll
+      for (int p = 0; p < 8; ++p) na.issue(smem, p, 0, wave_s);
+#pragma unroll
+      for (int p = 0; p < 8; ++p) nb.issue(smem + A3_B0, p, 0, wave_s);
+    }
+    int lane_e = lane;
+    asm volatile("" : "+v"(lane_e));
+    // 1. gu: each wave its half, the two 64-row passes swapped back for the
+    //    rotated up waves
+    mxk::store_block_lds<false>(acc, GU, ldgu, m0 + wm * 128, (wn ? F : 0) + g0, lane_e, slice, wn);
+    const bool up = wn != 0;
+    // 2. the gate / up hand-off of acc[4..7] in two rounds of two row blocks
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();         // slices (round 0) / round 0's reads (round 1) done
+      char* mine_out = smem + A3_SLOT + (wm * 2 + wn) * 16384 + lane_e * 16;
+      const char* theirs = smem + A3_SLOT + (wm * 2 + (wn ^ 1)) * 16384 + lane_e * 16;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          *reinterpret_cast<f32x4_t*>(mine_out + (ii * 8 + j) * 1024) = acc[4 + 2 * r + ii][j];
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const f32x4_t o = *reinterpret_cast<const f32x4_t*>(theirs + (ii * 8 + j) * 1024);
+          f32x4_t hv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float g = up ? o[e] : acc[2 * r + ii][j][e], u = up ? acc[2 * r + ii][j][e] : o[e];
+            hv[e] = g * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(g * -1.44269504f)) * u;
+          }
+          acc[2 * r + ii][j] = hv;
+        }
+    }
+    // 3. h of the kept 64 rows
+    mxk::store_block_wide<false, 4, 8>(reinterpret_cast<const f32x4_t(&)[4][8]>(acc[0]), H, ldh,
+                                       m0 + wm * 128 + (wn ? 64 : 0), g0, lane_e);
+    if (tn >= ntiles) break;
+    t = tn;
+    m0 = m1;
+    n0v = n1v;
+    pre = true;
+  }
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // Generic bounds-checked MFMA GEMM (any M, N, K; K-contiguous operands).
 // 64x64 tile, 256 threads (2x2 waves of 32x32), register-staged through LDS.
@@ -540,9 +655,9 @@ int w13_sched() {
 }  // namespace
 
 // K loop of the fused up-projection: 0 three-barrier w4j (default), 1 the
-// one-barrier loop of TN schedule 52, 2 = 0 with non-temporal gu stores
-// (env MXK_W13_SCHED)
-MXK_API void mxk_gemm_w13_set_sched(int v) { g_w13_sched.store(v == 1 || v == 2 ? v : 0); }
+// one-barrier loop of TN schedule 52, 2 = 0 with non-temporal gu stores,
+// 3 the persistent form (experiments library; env MXK_W13_SCHED)
+MXK_API void mxk_gemm_w13_set_sched(int v) { g_w13_sched.store(v >= 1 && v <= 3 ? v : 0); }
 
 MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, void* h, int M,
                                      int F, int K, int ldx, int ldw, int ldgu, int ldh,
@@ -556,7 +671,13 @@ MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, v
 #ifdef MXK_GEMM_EXPERIMENTS
   // A/B records (experiments library): 1 = one-barrier K loop, 2 = non-temporal
   // gu stores; both step-neutral (profiles/r4_step/)
-  if (w13_sched() == 2)
+  if (w13_sched() == 3) {
+    const int cus = mxk_gemm_available_cus();
+    const int grid = cus > 0 && cus < nwg ? cus : nwg;
+    MXK_LAUNCH_GEMM(mxk_gemm_bf16_w13_swiglu_p, dim3(grid), dim3(W4_THREADS), stream,
+                    static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
+                    static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu, ldh);
+  } else if (w13_sched() == 2)
     MXK_LAUNCH_GEMM((mxk_gemm_bf16_w13_swiglu_k<false, true>), dim3(nwg), dim3(W4_THREADS), stream,
                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w13),
                     static_cast<uint16_t*>(gu), static_cast<uint16_t*>(h), M, F, K, ldx, ldw, ldgu, ldh);

@@ -561,7 +561,10 @@ __device__ __forceinline__ void w4k_ktile(f32x4_t (&acc)[8][8], bf16x8_t (&f0a)[
 // before the previous tile's epilogue, whose 32 C stores per wave are still
 // counted in vmcnt; stage 1 goes out after a barrier (its slots held the
 // epilogue's LDS slices).
-template <int ABL = 0, int ORDER = 0, bool SPLITA = false>
+// PRE_VM: the vmcnt that, in a pre call, leaves stage 1's 16 DMA pieces and
+// the previous epilogue's stores in flight but waits for stage 0 (32 plain
+// C stores: 48; at most 63)
+template <int ABL = 0, int ORDER = 0, bool SPLITA = false, int PRE_VM = 48>
 __device__ __forceinline__ void w4k_mainloop(f32x4_t (&acc)[8][8], char* smem, const DmaK& dma_a,
                                              const DmaK& dma_b, int a_base, int a_hi, int b_base,
                                              int ns, int lane, int wave_s, bool pre = false) {
@@ -597,7 +600,7 @@ __device__ __forceinline__ void w4k_mainloop(f32x4_t (&acc)[8][8], char* smem, c
     for (int p = 0; p < 8; ++p) dma_a.issue(smem + A3_SLOT, p, BK * 2, wave_s);
 #pragma unroll
     for (int p = 0; p < 8; ++p) dma_b.issue(smem + A3_B0 + A3_SLOT, p, BK * 2, wave_s);
-    if (pre) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");   // + the 32 stores
+    if (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PRE_VM) : "memory");   // + the stores
     else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

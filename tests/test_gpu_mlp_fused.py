@@ -13,13 +13,15 @@ def dev():
     return torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("sched", [0, 1, 2])
+@pytest.mark.parametrize("sched", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,F,K", [(256, 128, 64), (512, 384, 256), (2048, 1792, 1024),
                                    (512, 256, 448), (16384, 14336, 4096)])
 def test_w13_swiglu_vs_fp32(dev, M, F, K, sched):
     """The production K loop (0: three-barrier w4j) and the experiments
     library's A/B records (1: the one-barrier loop of TN schedule 52, whose
-    6-K-tile slot cycle K = 448 leaves at a remainder; 2: non-temporal gu)."""
+    6-K-tile slot cycle K = 448 leaves at a remainder; 2: non-temporal gu;
+    3: the persistent form, several tiles per workgroup at the larger
+    shapes)."""
     from mxk8s.ops import _lib
     from mxk8s.ops.linear import w13_swiglu
     if sched and not _lib.lib().mxk_gemm_bf16_tn_variant_built(54):
