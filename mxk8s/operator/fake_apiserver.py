@@ -111,6 +111,7 @@ class FakeApiServer:
         self._httpd = None
         self.normalize = normalize
         self.job_orphan_linger = job_orphan_linger
+        self._lingering: list[tuple[threading.Timer, object]] = []
 
     # ------------------------------------------------------------ storage
     def _bump(self, obj: dict) -> None:
@@ -139,7 +140,20 @@ class FakeApiServer:
                     del self.objects[path]
                     self._bump({})
                     self._event("DELETED", path, cur)
-        threading.Timer(self.job_orphan_linger, release).start()
+        t = threading.Timer(self.job_orphan_linger, release)
+        t.daemon = True
+        self._lingering.append((t, release))
+        t.start()
+
+    def release_lingering(self) -> None:
+        """The garbage collector's release of every lingering Job, now (tests
+        drive it instead of sleeping past ``job_orphan_linger``, which a
+        loaded machine can overshoot before the assertion that needs the Job
+        still there)."""
+        pending, self._lingering = self._lingering, []
+        for t, release in pending:
+            t.cancel()
+            release()
 
     def handle(self, method: str, raw_path: str, body: dict | None) -> tuple[int, dict]:
         url = urllib.parse.urlparse(raw_path)
@@ -297,6 +311,9 @@ class FakeApiServer:
         return f"http://127.0.0.1:{self._httpd.server_address[1]}"
 
     def stop(self) -> None:
+        for t, _ in self._lingering:
+            t.cancel()
+        self._lingering = []
         if self._httpd:
             self._httpd.shutdown()
             self._httpd.server_close()

@@ -256,7 +256,9 @@ def test_owner_references_and_transition_times(api):
 def test_job_recreate_uses_background_propagation_and_tolerates_lingering():
     """a plain DELETE of a Job orphans its pod and the Job lingers
     behind the orphan finalizer, so an immediate POST gets 409."""
-    srv = FakeApiServer(job_orphan_linger=0.6).start()
+    # a linger far beyond the test's run, released by the test itself: with
+    # 0.6 s a loaded machine could let it pass before the pending assertion
+    srv = FakeApiServer(job_orphan_linger=60.0).start()
     job = f"/apis/batch/v1/namespaces/{NS}/jobs/amd-gpu-stack-validator"
     try:
         _policy(srv)
@@ -274,7 +276,7 @@ def test_job_recreate_uses_background_propagation_and_tolerates_lingering():
         srv.objects[job]["spec"]["template"]["spec"]["containers"][0]["args"].append("--y")
         r = ctl.reconcile_once()
         assert r.pending == ["Job/amd-gpu-stack-validator"] and r.state == "notReady"
-        time.sleep(0.8)                   # the garbage collector releases it
+        srv.release_lingering()           # the garbage collector releases it
         r = ctl.reconcile_once()
         assert "Job/amd-gpu-stack-validator" in r.created and not r.pending
     finally:
