@@ -72,7 +72,7 @@ def gemm_validator() -> dict:
             "spec": {"restartPolicy": "OnFailure", "tolerations": TOLERATIONS,
                      "containers": [_gpu_container(
                          "gemm", ["python3", "-m", "mxk8s.validate", "--tests=rocminfo,gemm",
-                                  "--gpus=1", "--gemm-sizes=4096,8192,16384"], 1)],
+                                  "--gpus=1", "--gemm-sizes=4096,8192,16384", "--profile"], 1)],
                      "volumes": [_dshm("8Gi")]}}
 
 

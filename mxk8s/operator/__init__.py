@@ -29,6 +29,8 @@ labels, this single-node stack uses the chart's node selector and tolerations.
 from __future__ import annotations
 
 import copy
+import hashlib
+import json
 import dataclasses
 import logging
 import re
@@ -174,6 +176,7 @@ class ReconcileResult:
     deleted: list = dataclasses.field(default_factory=list)
     operands: list = dataclasses.field(default_factory=list)
     pending: list = dataclasses.field(default_factory=list)   # retried next pass
+    backoff: list = dataclasses.field(default_factory=list)   # replace held by the backoff
 
 
 class Controller:
@@ -190,7 +193,9 @@ class Controller:
         # MODIFIED event wake the loop again (a hot loop)
         self.replace_backoff_s = replace_backoff_s
         self.replace_backoff_max_s = replace_backoff_max_s
-        self._replaces: dict = {}     # path -> [consecutive replaces, next allowed, names logged]
+        # path -> [consecutive replaces, next allowed, names logged, desired hash];
+        # a new desired object (a policy edit) starts a fresh backoff
+        self._replaces: dict = {}
         self.injected = tuple(INJECTED_NAME_PREFIXES) + tuple(injected)
         self.namespace = namespace
         self.release = release
@@ -245,10 +250,13 @@ class Controller:
             return live
         if obj["kind"] == "Job":    # pod template is immutable: re-create
             return self._recreate_job(path, name, obj, live, res)
-        st = self._replaces.setdefault(path, [0, 0.0, None])
+        want = hashlib.sha256(json.dumps(obj, sort_keys=True, default=str).encode()).hexdigest()
+        st = self._replaces.get(path)
+        if st is None or st[3] != want:
+            st = self._replaces[path] = [0, 0.0, None, want]
         now = self.clock()
         if now < st[1]:
-            res.pending.append(name)      # backing off: retried on a later pass
+            res.backoff.append(name)      # backing off: retried when the backoff ends
             return live
         names = drift_names(obj, live, self.injected)
         if names and names != st[2]:
@@ -366,10 +374,11 @@ class Controller:
                 if not r:
                     not_ready.append(obj["metadata"]["name"])
         self.garbage_collect(name, keep, res)
-        if not_ready or res.pending:
+        if not_ready or res.pending or res.backoff:
             res.state = "notReady"
-            res.message = "waiting for " + ", ".join(not_ready + [f"{p} (re-creating)"
-                                                                  for p in res.pending])
+            res.message = "waiting for " + ", ".join(
+                not_ready + [f"{p} (re-creating)" for p in res.pending]
+                + [f"{p} (drifted; replace backing off)" for p in res.backoff])
         else:
             res.message = f"{len(keep)} operand objects in sync"
         self._status(pol, res)
@@ -458,20 +467,28 @@ class Controller:
         self.wakeups.append(result)
         return result
 
+    def next_wait(self, interval: float) -> float:
+        """The wait before the next pass: ``interval``, or less when a held
+        replace's backoff ends sooner (nothing else would wake the loop)."""
+        now = self.clock()
+        ends = [st[1] - now for st in self._replaces.values() if st[1] > now]
+        return min([interval] + [max(0.05, e) for e in ends])
+
     def run(self, interval: float = 300.0, stop=None) -> None:
         """Level-triggered loop: reconcile, then sleep until something this
-        controller owns (or its policy) changes, at most ``interval`` s."""
+        controller owns (or its policy) changes, at most ``interval`` s or
+        until the earliest replace backoff ends."""
         while stop is None or not stop():
             try:
                 r = self.reconcile_once()
-                if r.created or r.updated or r.deleted or r.pending:
-                    log.info("reconciled: %s (created %d, updated %d, deleted %d, pending %d)",
-                             r.state, len(r.created), len(r.updated), len(r.deleted),
-                             len(r.pending))
+                if r.created or r.updated or r.deleted or r.pending or r.backoff:
+                    log.info("reconciled: %s (created %d, updated %d, deleted %d, pending %d, "
+                             "backing off %d)", r.state, len(r.created), len(r.updated),
+                             len(r.deleted), len(r.pending), len(r.backoff))
             except Exception as e:   # API server blip: retry after the next wake-up
                 log.error("reconcile failed: %s", e)
             try:
-                self.wait_for_change(interval, stop)
+                self.wait_for_change(self.next_wait(interval), stop)
             except Exception as e:
                 log.error("watch setup failed: %s", e)
                 time.sleep(min(interval, 5.0))

@@ -100,23 +100,28 @@ def _read_meta(ckpt_dir: str) -> Optional[dict]:
         return None
 
 
-def _complete_dirs(ckpt_dir: str) -> list[str]:
-    """Step directories that hold a complete-looking shard set (params plus
-    at least one optimizer shard), oldest first (zero-padded step names)."""
+def _complete_dirs(ckpt_dir: str, shards: Optional[int] = None) -> list[str]:
+    """Step directories that hold a complete shard set, oldest first
+    (zero-padded step names): params plus every optimizer shard
+    ``optim-rank0 .. optim-rank<shards-1>`` (``shards``: the current save's
+    shard count, 1 when the optimizer is replicated).  An interrupted
+    sharded save - rank 0's files on disk, a later rank's missing - is not
+    complete and never takes a retention slot.  ``shards=None`` (no current
+    save to compare with) only asks for params plus ``optim-rank0``."""
     out = []
+    want = [f"optim-rank{r}.safetensors" for r in range(shards or 1)]
     for d in sorted(os.listdir(ckpt_dir)):
         full = os.path.join(ckpt_dir, d)
         if not (d.startswith("step-") and os.path.isdir(full)):
             continue
-        names = os.listdir(full)
-        if "params.safetensors" in names and any(n.startswith("optim-rank") and
-                                                  n.endswith(".safetensors") for n in names):
+        names = set(os.listdir(full))
+        if "params.safetensors" in names and all(w in names for w in want):
             out.append(d)
     return out
 
 
 def _history(prev: Optional[dict], current: str, keep: int,
-             ckpt_dir: Optional[str] = None) -> list[str]:
+             ckpt_dir: Optional[str] = None, shards: Optional[int] = None) -> list[str]:
     """Committed step directories, oldest first, ending with ``current``:
     the previous commit record's history (or its single ``path`` for records
     written before the history existed), truncated to the ``keep`` newest.
@@ -131,7 +136,7 @@ def _history(prev: Optional[dict], current: str, keep: int,
         if prev and prev.get("format") == FORMAT and prev.get("path"):
             hist = [prev["path"]]
         if ckpt_dir is not None:
-            hist = sorted(set(hist) | set(_complete_dirs(ckpt_dir)))
+            hist = sorted(set(hist) | set(_complete_dirs(ckpt_dir, shards)))
     hist = [h for h in hist if h != current] + [current]
     return hist[-max(1, keep):]
 
@@ -176,7 +181,8 @@ def save(ckpt_dir: str, ddp, opt, step: int, keep: int = 2) -> None:
     # every shard is on disk before the commit record names this step
     mxdist.barrier()
     if rank == 0:
-        history = _history(_read_meta(ckpt_dir), sub, keep, ckpt_dir)
+        history = _history(_read_meta(ckpt_dir), sub, keep, ckpt_dir,
+                           shards=world if sharded else 1)
         _write_meta(ckpt_dir, {"step": step, "optimizer_step": opt.step_count, "world_size": world,
                                "sharded": sharded, "layout": fp, "numel": ddp.space.numel,
                                "format": FORMAT, "path": sub, "history": history})

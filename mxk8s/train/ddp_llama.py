@@ -119,9 +119,15 @@ def train_step(model, ddp, opt, tokens) -> torch.Tensor:
 def run_ddp_bench(args) -> dict:
     world, rank, local = mxdist.world_info()
     if torch.cuda.is_available():
+        # MXK_BENCH_BACKEND=gloo rehearses the multi-rank step (ZeRO-1
+        # reduce-scatter / all-gather, side-stream events) with more ranks
+        # than GPUs: ranks share GPUs round-robin, which RCCL refuses.  The
+        # measured configuration is always RCCL with one rank per GPU.
+        backend = os.environ.get("MXK_BENCH_BACKEND", "nccl")
+        if backend != "nccl":
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-        backend = "nccl"
     else:
         dev = torch.device("cpu")
         backend = "gloo"
@@ -205,6 +211,7 @@ def run_ddp_bench(args) -> dict:
         "peak_mem_gib": round(peak_mem / 2 ** 30, 2),
         "mean_loss": final_loss,
         "bucket_mb": bucket_mb,
+        "backend": backend if world > 1 else None,
         "grad_reduce_dtype": reduce_dtype,
         "param_gather": ("overlapped with the next forward" if getattr(opt, "_module_buckets", None)
                          else "in step()") if ddp.sharded else None,

@@ -109,7 +109,7 @@ def format_text(summary: dict) -> str:
     return "\n".join(lines) + "\n"
 
 
-def profile_gemm(sizes: str, out_dir: str, variants: str = "", timeout: int = 600,
+def profile_gemm(sizes: str, out_dir: str, variants: str = "", timeout: int = 240,
                  filt: str = "") -> dict:
     """Run the GEMM validator under rocprofv3 once per counter group."""
     rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"

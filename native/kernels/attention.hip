@@ -1764,7 +1764,13 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
   auto* dV = static_cast<uint16_t*>(dv);
   const int nwg = B * Hq * (S / BQ);
   const long span0 = static_cast<long>(S) * (k_tok > v_tok ? k_tok : v_tok) * 2;
-  if ((variant == 7 || variant == 8) && S % 256 == 0) {
+  // the one-pass kernel's own layout limits (32-bit buffer ranges of the Q,
+  // K and dQ panels): outside them variants 7 / 8 degrade to variant 5, as
+  // variant 6 does, instead of failing
+  const bool onepass_ok = S % 256 == 0 && static_cast<long>(S) * q_tok * 2 < (1L << 32) &&
+                          static_cast<long>(S) * k_tok * 2 < (1L << 32) &&
+                          static_cast<long>(S) * Hq * D * 2 < (1L << 32);
+  if ((variant == 7 || variant == 8) && onepass_ok) {
     // one pass (attention_bwd256.hip): dQ by fp32 (7) or packed-bf16 (8)
     // atomics from the 256-key workgroups; not bit-reproducible
     return mxk_attn_bwd_onepass(q, k, v, o, dout, lse, dq, dk, dv, workspace, B, S, Hq, Hkv, q_tok,

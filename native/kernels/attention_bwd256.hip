@@ -72,7 +72,7 @@ struct Lay {
 
 __device__ __forceinline__ void dma4m(const mxk::u32x4& rsrc, uint32_t lds_addr, uint32_t voff,
                                       uint32_t soff) {
-  asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
+  asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, %2 offen lds"
                :
                : "v"(voff), "s"(rsrc), "s"(soff), "{m0}"(lds_addr)
                : "memory");

@@ -1,11 +1,18 @@
 #!/usr/bin/env python3
 """Time the hand-written flash attention (fwd, and fwd+bwd once available)
 against torch SDPA on the Llama-3-8B shape: B=1, Hq=32, Hkv=8, S=2048,
-D=128, causal, bf16, random data.  Prints one RESULT json line per kernel."""
+D=128, causal, bf16, random data.  Prints one RESULT json line per kernel.
+
+Timing follows bench.py: the chip is warmed for >= WARM_S (2 s) of
+back-to-back launches before the first entry and >= 0.3 s per entry, then
+each entry is the median over 7 blocks of back-to-back launches bracketed by
+one event pair (per-launch events let the host fall behind the GPU and put
+an event packet between every two kernels)."""
 import json
 import os
 import statistics
 import sys
+import time
 
 import torch
 import torch.nn.functional as F
@@ -14,19 +21,35 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mxk8s.ops import attention as A  # noqa: E402
 
 
-def bench(fn, iters=30):
-    for _ in range(5):
-        fn()
-    torch.cuda.synchronize()
+WARM_S = float(os.environ.get("WARM_S", 2.0))
+_warm = {"done": False}
+
+
+def _spin(fn, seconds):
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        if time.perf_counter() - t0 >= seconds:
+            return
+
+
+def bench(fn, blocks=7, reps=20):
+    if not _warm["done"]:          # the first entry must not time a cold chip
+        _spin(fn, WARM_S)
+        _warm["done"] = True
+    _spin(fn, 0.3)
     ts = []
-    for _ in range(iters):
+    for _ in range(blocks):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
-        fn()
+        for _ in range(reps):
+            fn()
         e.record()
         e.synchronize()
-        ts.append(s.elapsed_time(e))
+        ts.append(s.elapsed_time(e) / reps)
     return statistics.median(ts)
 
 
@@ -63,7 +86,10 @@ def main():
         out = F.scaled_dot_product_attention(qg, kg, vg, is_causal=True, enable_gqa=True)
         out.backward(dot)
     res["sdpa_fwd_bwd"] = bench(sdpa_fb)
-    res["mxk_fwd_bwd"] = res["mxk_fwd"] + res["mxk_bwd"]
+    def mxk_fb():
+        o_, l_ = A.attn_fwd(q, k, v, causal=True)
+        A.attn_bwd(q, k, v, o_, l_, do, causal=True)
+    res["mxk_fwd_bwd"] = bench(mxk_fb)
     # useful FLOPs: fwd 2 products, bwd 5 products (causal halves all)
     def mult(name):
         return 3.5 if name.endswith("fwd_bwd") else 2.5 if "_bwd" in name else 1.0

@@ -17,6 +17,9 @@
 #   prof_ddp      kernel trace + roctx breakdown of the DDP step [STEPS]
 #   pmc_gemm      PMC counters of the TN GEMM              [VARIANTS, SIZES, COUNTERS]
 #   contention    DDP step beside a CU-pinned HBM streamer  [CONT_CUS, CONT_PLACE]
+#   ddp_gloo2     the multi-rank DDP step (ZeRO-1) rehearsed: 2 gloo ranks on one GPU,
+#                 2 Llama-3-8B layers (NOT the headline config)
+#   validator_gloo2  bench.py validator mode, 2 gloo ranks on one GPU
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 R=$PWD
@@ -82,6 +85,12 @@ for step in "$@"; do
         --variants "${VARIANTS:-26}" --iters 6 --rounds 2 --warmup-s 0.5 ;;
     contention)
       run contention 900 python3 -u scripts/contention_bench.py --cus "${CONT_CUS:-16,32,64}" --placement "${CONT_PLACE:-spread}" --gbps "${CONT_GBPS:-5,700}" ;;
+    ddp_gloo2)
+      run ddp_gloo2 600 env MXK_BENCH_BACKEND=gloo python3 -u bench.py --mode ddp --gpus 2 \
+        --layers 2 --steps "${DDP_STEPS:-3}" --warmup 1 ${DDP_ARGS:-} ;;
+    validator_gloo2)
+      run validator_gloo2 400 env MXK_BENCH_BACKEND=gloo python3 -u bench.py --gpus 2 --steps 10 \
+        --warmup 2 --allreduce-sizes 1,16,256 --ab-sizes "" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -53,3 +53,21 @@ def test_pruning_many_complete_dirs_is_logged(tmp_path, capsys):
         _mkstep(root, s)
     ck._prune(root, ["step-000000004"])
     assert "pruning 3 complete step directories" in capsys.readouterr().err
+
+
+def test_interrupted_sharded_save_is_not_complete(tmp_path):
+    """a sharded save interrupted after rank 0's shards were written
+    (rank 1's missing) must not take a retention slot and push a real commit
+    into the prune."""
+    root = str(tmp_path)
+    for s in (1, 2):
+        d = _mkstep(root, s)
+        open(os.path.join(root, d, "optim-rank1.safetensors"), "w").close()
+    _mkstep(root, 3)                          # rank 0 wrote, rank 1 did not
+    cur = _mkstep(root, 4)
+    open(os.path.join(root, cur, "optim-rank1.safetensors"), "w").close()
+    assert ck._complete_dirs(root, shards=2) == ["step-000000001", "step-000000002", cur]
+    hist = ck._history(None, cur, 3, root, shards=2)
+    assert hist == ["step-000000001", "step-000000002", cur]
+    ck._prune(root, hist)
+    assert sorted(d for d in os.listdir(root) if d.startswith("step-")) == hist

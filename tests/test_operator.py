@@ -361,16 +361,25 @@ def test_mutating_policy_replace_loop_backs_off_and_names_drift(api, caplog):
     assert any("KYVERNO_INJECTED" in rec.getMessage() for rec in caplog.records)
     mutate()                                   # the webhook mutates the replaced object again
     r2 = ctl.reconcile_once()
-    assert name not in r2.updated and name in r2.pending
+    assert name not in r2.updated and name in r2.backoff and not r2.pending
+    assert "replace backing off" in r2.message and "re-creating" not in r2.message
+    # nothing else would wake the loop when the backoff ends: run() waits at most that long
+    assert 0.05 <= ctl.next_wait(300.0) <= 0.3
     now[0] += 0.35
     r3 = ctl.reconcile_once()                  # backoff expired: replaced again
     assert name in r3.updated
     mutate()
     now[0] += 0.35
     r4 = ctl.reconcile_once()                  # second backoff is twice as long (0.6 s)
-    assert name in r4.pending
+    assert name in r4.backoff
     now[0] += 0.3
     assert name in ctl.reconcile_once().updated
+    # a real policy change (new desired object) is not held by the old backoff
+    mutate()
+    assert name in ctl.reconcile_once().backoff
+    _policy(api, {"devicePlugin": {"healthInterval": 7}})
+    assert name in ctl.reconcile_once().updated
+    assert ctl.next_wait(300.0) <= 0.3        # a fresh backoff: 1st step again
     # with the name allow-listed there is no drift at all
     ctl2 = op.Controller(KubeClient(api.url), NS, injected=["KYVERNO_"])
     assert name not in ctl2.reconcile_once().updated
