@@ -27,7 +27,7 @@ CXXFLAGS  := -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -Inative/l
 LDLIBS_NODE := -ldl -lpthread
 
 KERNEL_SRCS := native/kernels/gemm_bf16.hip native/kernels/vector_add.hip \
-               native/kernels/fused_ops.hip native/kernels/optim.hip native/kernels/attention.hip native/kernels/attention_bwd256.hip native/kernels/attention_fwd256.hip \
+               native/kernels/fused_ops.hip native/kernels/optim.hip native/kernels/attention.hip native/kernels/attention_bwd256.hip native/kernels/attention_fwd256.hip native/kernels/attention_dq256.hip \
                native/kernels/gemm_bf16_layouts.hip native/kernels/xent.hip native/kernels/contention.hip
 KERNEL_OBJS := $(patsubst native/kernels/%.hip,$(BUILD)/kernels/%.o,$(KERNEL_SRCS))
 EXP_SRCS    := $(KERNEL_SRCS) $(wildcard native/kernels/experiments/*.hip)

@@ -1723,7 +1723,7 @@ mxk_attn_bwd_gqa_reduce_kernel(const float* __restrict__ dk_p, const float* __re
 // variant 0, the per-query-head dK/dV kernel).
 MXK_API long mxk_attn_bwd_workspace_variant(int B, int S, int Hq, int variant) {
   const long rows = static_cast<long>(B) * Hq * S;
-  if (variant == 6) return rows * 8;   // {-lse/scale, -delta} row pairs
+  if (variant == 6 || variant == 9) return rows * 8;   // {-lse/scale, -delta} row pairs
   if (variant == 7 || variant == 8) return mxk_attn_bwd_onepass_workspace(B, S, Hq, variant == 8);
   return rows * 4 + (variant == 0 ? 2 * rows * D * 4 : 0);
 }
@@ -1745,7 +1745,7 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
                                  long q_tok, long k_tok, long v_tok, long dk_tok, long dv_tok,
                                  float scale, int causal, int variant, hipStream_t stream) {
   if (head_dim != D || B < 1 || S < BQ || S % BQ || Hkv < 1 || Hq % Hkv || q_tok % 8 ||
-      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 8 ||
+      k_tok % 8 || v_tok % 8 || dk_tok % 4 || dv_tok % 4 || variant < 0 || variant > 9 ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
        reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
@@ -1777,6 +1777,22 @@ MXK_API int mxk_attn_bwd_variant(const void* q, const void* k, const void* v, co
                                 k_tok, v_tok, dk_tok, dv_tok, scale, causal, variant == 8, stream);
   }
   if (variant == 7 || variant == 8) variant = 5;
+  if (variant == 9) {
+    // dQ by 4-head x 64-row workgroups, one wave per SIMD (attention_dq256.hip,
+    // rowc pairs folded in), then the 256-key dK / dV; a layout either kernel
+    // does not take (Hq / Hkv not a multiple of 4, S % 256, 32-bit buffer
+    // ranges) runs variant 6
+    const long qspan9 = static_cast<long>(S) * (q_tok > static_cast<long>(Hq) * D ? q_tok : Hq * D) * 2;
+    if (S % 256 == 0 && (Hq / Hkv) % 4 == 0 && span0 < (1L << 32) && qspan9 < (1L << 32)) {
+      float* rowc = static_cast<float*>(workspace);
+      const int st = mxk_attn_bwd_dq256(q, k, v, o, dout, lse, dq, rowc, B, S, Hq, Hkv, q_tok, k_tok,
+                                        v_tok, scale, causal, stream);
+      if (st) return st;
+      return mxk_attn_bwd_dkdv256(q, k, v, dout, rowc, dk, dv, B, S, Hq, Hkv, q_tok, k_tok, v_tok,
+                                  dk_tok, dv_tok, scale, causal, stream);
+    }
+    variant = 6;
+  }
   if (variant == 6) {
     // dQ with the delta pass folded in, writing {-lse/scale, -delta} rows,
     // then dK / dV with 256 keys per workgroup (attention_bwd256.hip)

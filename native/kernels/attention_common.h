@@ -131,6 +131,12 @@ MXK_API int mxk_attn_bwd_onepass(const void* q, const void* k, const void* v, co
                                  void* workspace, int B, int S, int Hq, int Hkv, long q_tok,
                                  long k_tok, long v_tok, long dk_tok, long dv_tok, float scale,
                                  int causal, int bf16_atomics, hipStream_t stream);
+// dQ of backward variant 9 (attention_dq256.hip): 4 query heads x 64 rows per
+// workgroup, one wave per SIMD; writes the rowc pairs for mxk_attn_bwd_dkdv256
+MXK_API int mxk_attn_bwd_dq256(const void* q, const void* k, const void* v, const void* o,
+                               const void* dout, const float* lse, void* dq, float* rowc, int B,
+                               int S, int Hq, int Hkv, long q_tok, long k_tok, long v_tok,
+                               float scale, int causal, hipStream_t stream);
 // forward variant 10 (attention_fwd256.hip)
 MXK_API int mxk_attn_fwd256(const void* q, const void* k, const void* v, void* o, float* lse,
                             int B, int S, int Hq, int Hkv, long q_tok, long k_tok, long v_tok,

@@ -1,0 +1,414 @@
+// Flash attention backward, dQ with one wave per SIMD (gfx950; backward
+// variant 9).
+//
+// The dQ kernel of variants 5 / 6 (attention.hip, mxk_attn_bwd_dq_kernel:
+// 4 waves x 32 query rows, two workgroups per CU) takes 459.5 us of the
+// 1.018 ms Llama-3-8B layer backward at 44.8 % MFMA busy and 81.9 % L2 hit
+// (profiles/r5_attention/pmc_default_fwd4_bwd6_and_v8.txt): every K / V
+// fragment it reads from LDS feeds ONE MFMA, and every 128 query rows
+// re-stream the head's keys.  Here (the one-wave-per-SIMD structure of the
+// 256-key dK / dV kernel, attention_bwd256.hip, applied to the query side):
+//
+//   * one workgroup = 4 waves = the 4 query heads of one GQA quad x the same
+//     64 query rows: the waves share every K / V tile (one LDS-DMA stream per
+//     quad instead of one per head) and, being on the same rows, the same
+//     causal key range - no wave idles past its diagonal;
+//   * a wave owns its 64 rows as two 32-row tiles g0 / g1: every K / V / K^T
+//     fragment read from LDS feeds one MFMA per tile (two per read);
+//   * Q and dO of the 64 rows are resident for the whole sweep as MFMA B
+//     operands in the accumulator file (2 x 64 AGPRs), beside dQ^T (128
+//     AGPRs), so the arch VGPRs hold only S^T / dP^T and operands;
+//   * key on the register, query on the lane (S^T = K Q^T, dP^T = V dO^T):
+//     the row constants -lse and -delta are per lane, and dS^T converted to
+//     bf16 IS the B operand of dQ^T += K^T dS^T (K^T by ds_read_b64_tr_b16
+//     from the row-major K image), no LDS round trip;
+//   * per 32-key step j two phases, each with VALU work beside its MFMAs:
+//       A(j)    S^T, dP^T of step j (32 MFMAs)   beside softmax(j-1) of g1
+//       B(j-1)  dQ^T += K^T dS^T(j-1) (16)       beside softmax(j)   of g0
+//     (softmax: P = exp2(c S - lse log2 e), the causal mask on the two
+//     diagonal steps, dS = P (dP - delta), bf16 pairs);
+//   * K / V tiles of 64 keys by LDS-DMA into a 4-slot ring (two tiles of
+//     lead), one barrier per tile (two steps).
+//
+// The delta pass is folded in (delta = dO . O from the row's own dO
+// fragments and O), and the kernel writes the {-lse/scale, -delta} row pairs
+// that the 256-key dK / dV kernel streams, so variant 9 is this kernel then
+// mxk_attn_bwd_dkdv256 - deterministic, no atomics.
+//
+// Layouts as attention.hip: q [B, S, Hq, 128] (token stride q_tok), k / v
+// [B, S, Hkv, 128] (k_tok / v_tok), o / dout / dq [B, S, Hq, 128] contiguous,
+// lse [B, Hq, S] fp32 (natural log), rowc [B, Hq, S] x float2.  Hq / Hkv a
+// multiple of 4, S % 64 == 0, K / V panels within a 32-bit buffer range.
+#include "attention_common.h"
+
+namespace {
+constexpr int QW = 64;                     // query rows per wave (and workgroup)
+constexpr int KT = 64;                     // keys per DMA tile (two steps of 32)
+constexpr int QSLOT = 2 * TILE_BYTES;      // K | V image of one tile (32 KiB)
+constexpr int QNSLOT = 4;
+constexpr int QLDS = QNSLOT * QSLOT;       // 128 KiB
+
+// S^T / dP^T chains: accumulator in VGPRs (the VALU reads it), B operand (a
+// Q / dO fragment) pinned in AGPRs ("+a": the AGPR copy is the live value).
+// First of a chain: C = 0 as an inline constant (no VALU zeroing, so no
+// VALU-write -> MFMA-read wait); early-clobber, D must not overlap A / B.
+__device__ __forceinline__ void mq0(f32x16_t& acc, const bf16x8_t& a, bf16x8_t& bq) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %1, 0" : "=&v"(acc), "+a"(bq) : "v"(a));
+}
+__device__ __forceinline__ void mq(f32x16_t& acc, const bf16x8_t& a, bf16x8_t& bq) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %1, %0" : "+v"(acc), "+a"(bq) : "v"(a));
+}
+// the last k-step of phase A: four MFMAs and the XDL-write -> VALU-read wait
+// states (8-pass 32x32x16: 12) in ONE statement, so the allocator cannot
+// copy a result between the MFMA and the nops
+__device__ __forceinline__ void mq4_fenced(f32x16_t& s0, f32x16_t& s1, f32x16_t& p0, f32x16_t& p1,
+                                           bf16x8_t& q0, bf16x8_t& q1, bf16x8_t& d0, bf16x8_t& d1,
+                                           const bf16x8_t& ka, const bf16x8_t& va) {
+  asm volatile(
+      "v_mfma_f32_32x32x16_bf16 %0, %8, %4, %0\n\t"
+      "v_mfma_f32_32x32x16_bf16 %1, %8, %5, %1\n\t"
+      "v_mfma_f32_32x32x16_bf16 %2, %9, %6, %2\n\t"
+      "v_mfma_f32_32x32x16_bf16 %3, %9, %7, %3\n\t"
+      "s_nop 7\n\ts_nop 4"
+      : "+v"(s0), "+v"(s1), "+v"(p0), "+v"(p1), "+a"(q0), "+a"(q1), "+a"(d0), "+a"(d1)
+      : "v"(ka), "v"(va));
+}
+// dQ^T accumulation, accumulator pinned to AGPRs
+__device__ __forceinline__ void ma(f32x16_t& acc, const bf16x8_t& a, const bf16x8_t& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+// VALU-written dS^T operands -> MFMA read: the wait states, with the operands
+// named so none of them is written behind the nops
+__device__ __forceinline__ void ds_ready(const bf16x8_t (&x)[2][2]) {
+  asm volatile("s_nop 2" ::"v"(x[0][0]), "v"(x[0][1]), "v"(x[1][0]), "v"(x[1][1]));
+}
+template <int N>
+__device__ __forceinline__ void vmw() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+__device__ __forceinline__ uint32_t pk2(float lo, float hi) { return mxk::pack2bf(lo, hi); }
+}  // namespace
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 1)
+mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                          const uint16_t* __restrict__ v, const uint16_t* __restrict__ o,
+                          const uint16_t* __restrict__ dout, const float* __restrict__ lse,
+                          uint16_t* __restrict__ dq, float* __restrict__ rowc, int S, int Hq,
+                          int Hkv, long q_tok, long k_tok, long v_tok, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[QLDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  // workgroup -> (batch, quad of query heads, 64-row block): the quads of one
+  // KV head and all their blocks are consecutive logical ids of one XCD,
+  // heaviest block first (map_block_xcd), so a KV head's K / V stays in its L2
+  const int grp = Hq / Hkv;
+  const int nq4 = Hq / 4;
+  const int nqb = S / QW;
+  int bq4, qb;
+  map_block_xcd(blockIdx.x, gridDim.x, nqb, grp / 4, CAUSAL, &bq4, &qb);
+  const int b = bq4 / nq4;
+  const int hq = (bq4 - b * nq4) * 4 + wave;
+  const int hkv = hq / grp;                    // the same for the 4 waves
+  const int q0 = qb * QW;
+
+  const uint16_t* qh = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
+  const long tokd = static_cast<long>(Hq) * D;
+  const uint16_t* doh = dout + static_cast<long>(b) * S * tokd + static_cast<long>(hq) * D;
+  const uint16_t* oh = o + static_cast<long>(b) * S * tokd + static_cast<long>(hq) * D;
+  const uint16_t* kb_ptr = k + static_cast<long>(b) * S * k_tok + static_cast<long>(hkv) * D;
+  const uint16_t* vb_ptr = v + static_cast<long>(b) * S * v_tok + static_cast<long>(hkv) * D;
+  const long lrow0 = (static_cast<long>(b) * Hq + hq) * S + q0;
+
+  const int T = CAUSAL ? qb + 1 : S / KT;      // 64-key tiles (keys 0 .. q0 + 63 when causal)
+
+  // ---- DMA: wave w moves pieces 4 w .. 4 w + 3 of K and of V (1 KiB, 4 rows
+  // each; lane i at row 4 g + (i >> 4), chunk (i & 15) ^ swizzle(row))
+  const mxk::u32x4 rk = mxk::make_rsrc(kb_ptr, static_cast<unsigned>(S * k_tok * 2));
+  const mxk::u32x4 rv = mxk::make_rsrc(vb_ptr, static_cast<unsigned>(S * v_tok * 2));
+  const int prow = lane >> 4, cbase = (lane & 15) ^ (prow << 2);
+  const uint32_t krow0 = static_cast<uint32_t>((16 * wave + prow) * k_tok * 2);
+  const uint32_t vrow0 = static_cast<uint32_t>((16 * wave + prow) * v_tok * 2);
+  const uint32_t k_step = static_cast<uint32_t>(KT * k_tok * 2);
+  const uint32_t v_step = static_cast<uint32_t>(KT * v_tok * 2);
+  const uint32_t sm32 = mxk::lds_addr32(smem);
+  auto issue = [&](int t) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      uint32_t d0 = sm32 + (t % QNSLOT) * QSLOT + (4 * wave + p) * 1024;
+      asm volatile("" : "+s"(d0));
+      const uint32_t ch16 = static_cast<uint32_t>((cbase ^ p) << 4);
+      mxk::dma16m(rk, d0, krow0 + static_cast<uint32_t>(p * 4 * k_tok * 2) + ch16, t * k_step);
+      mxk::dma16m(rv, d0 + TILE_BYTES, vrow0 + static_cast<uint32_t>(p * 4 * v_tok * 2) + ch16,
+                  t * v_step);
+    }
+  };
+  issue(0);
+  if (T > 1) issue(1);
+
+  // ---- Q / dO B fragments (lane: row q0 + 32 g + r32, dims 16 s + 8 h .. + 7),
+  // delta = dO . O of the row (the two lane halves hold 64 dims each), lse
+  bf16x8_t qf[2][8], df[2][8];
+  float nl[2], dl[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const long row = q0 + 32 * g + r32;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      qf[g][s] = *reinterpret_cast<const bf16x8_t*>(qh + row * q_tok + 16 * s + 8 * h);
+      df[g][s] = *reinterpret_cast<const bf16x8_t*>(doh + row * tokd + 16 * s + 8 * h);
+      const bf16x8_t of = *reinterpret_cast<const bf16x8_t*>(oh + row * tokd + 16 * s + 8 * h);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        part += mxk::bf2f(static_cast<uint16_t>(df[g][s][e])) * mxk::bf2f(static_cast<uint16_t>(of[e]));
+    }
+    const float delta = half_sum(part);
+    const float l = lse[lrow0 + 32 * g + r32];
+    nl[g] = -l * 1.4426950408889634f;
+    dl[g] = delta;
+    if (h == 0)
+      *reinterpret_cast<float2*>(rowc + 2 * (lrow0 + 32 * g + r32)) = make_float2(-l / scale, -delta);
+  }
+  // consume every per-row load here: the compiler's vmcnt waits for them then
+  // sit before tile 2's DMA (it cannot see the DMA; a wait placed after it
+  // would also wait for tile 2)
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[g][s]), "v"(df[g][s]) : "memory");
+  if (T > 2) {
+    issue(2);
+    vmw<16>();       // the rowc store and tile 0 (tiles 1 and 2 may fly)
+  } else if (T > 1) {
+    vmw<8>();
+  } else {
+    vmw<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+
+  // ---- LDS read offsets: K / V rows r32 (+ 8 KiB for the step's key half),
+  // chunk 2 s + h; K^T transposed reads at keys tr_key (+8) of k-step kk
+  // (+ 4 KiB), chunk 4 db + tr_ch
+  int koff[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) koff[s] = swz(r32, 2 * s + h);
+  const int G = lane >> 4, i16 = lane & 15;
+  const int tr_key = 4 * h + (i16 >> 2);
+  const int tr_ch = 2 * (G & 1) + ((i16 & 3) >> 1);
+  const int tr_byte = 8 * (i16 & 1);
+  int ktr[4][2];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    ktr[db][0] = swz(tr_key, 4 * db + tr_ch) + tr_byte;
+    ktr[db][1] = swz(tr_key + 8, 4 * db + tr_ch) + tr_byte;
+  }
+
+  const float c = scale * 1.4426950408889634f;
+  f32x16_t dqa[2][4];                 // dQ^T: rows d = 32 db + crow, lane = query (AGPRs)
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dqa[g][db][r] = 0.f;
+  f32x16_t sacc[2][2], pacc[2][2];    // [step parity][g]: rows key = crow, lane = query
+  bf16x8_t dsf[2][2][2];              // dS^T operands [step parity][g][k-step of 16 keys]
+  // step -1 (a no-op): its g1 softmax sees S = -inf (P = 0, dS = 0) and its
+  // g0 operands are zero, so B(-1) adds K^T . 0 (tile 0's finite keys)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    sacc[1][1][r] = -INFINITY;
+    pacc[1][1][r] = 0.f;
+  }
+  dsf[1][0][0] = bf16x8_t{};
+  dsf[1][0][1] = bf16x8_t{};
+
+  // softmax unit of step j's tile g (8 units: registers 2 u, 2 u + 1 and
+  // their bf16 pair; the k-step operand is complete after units 3 / 7).
+  // MASK (the two diagonal steps): key kv0 + crow(r, h) past query
+  // q0 + 32 g + r32, i.e. (r & 3) + 8 (r >> 2) > lim, one compare a score.
+  uint32_t dsw[2][2][2][4];           // the operands as bf16 pairs, [parity][g][kk][word]
+  auto smx = [&](auto par_c, int g, int u, int lim, auto mask_c) {
+    constexpr int P = decltype(par_c)::value;
+    constexpr bool MASK = decltype(mask_c)::value;
+    float x[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int r = 2 * u + e;
+      float p = fexp2(fmaf(sacc[P][g][r], c, nl[g]));
+      if (MASK) p = (r & 3) + 8 * (r >> 2) > lim ? 0.f : p;
+      x[e] = p * (pacc[P][g][r] - dl[g]);
+    }
+    dsw[P][g][u >> 2][u & 3] = pk2(x[0], x[1]);
+    if ((u & 3) == 3) {
+      const uint32_t* w = dsw[P][g][u >> 2];
+      dsf[P][g][u >> 2] = __builtin_bit_cast(bf16x8_t, u32x4_t{w[0], w[1], w[2], w[3]});
+    }
+  };
+  auto lim_of = [&](int j, int g) { return q0 + 32 * g + r32 - 32 * j - 4 * h; };
+
+  // phase A(j): S^T, dP^T of step j (parity PA) from the K / V rows at kt;
+  // beside: unit u of softmax(j-1) of g1 (parity PA ^ 1) every 4 MFMAs
+  auto phaseA = [&](auto par_c, const char* kt, int j, auto mask_c) {
+    constexpr int PA = decltype(par_c)::value;
+    using prv = std::integral_constant<int, PA ^ 1>;
+    const int lim = lim_of(j - 1, 1);
+    bf16x8_t ka = lds_b128(kt + koff[0]), va = lds_b128(kt + TILE_BYTES + koff[0]);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      bf16x8_t nk = ka, nv = va;
+      if (s < 7) {
+        nk = lds_b128(kt + koff[s + 1]);
+        nv = lds_b128(kt + TILE_BYTES + koff[s + 1]);
+      }
+      if (s == 0) {
+        mq0(sacc[PA][0], ka, qf[0][0]);
+        __builtin_amdgcn_sched_barrier(0);
+        mq0(sacc[PA][1], ka, qf[1][0]);
+        smx(prv{}, 1, 0, lim, mask_c);
+        __builtin_amdgcn_sched_barrier(0);
+        mq0(pacc[PA][0], va, df[0][0]);
+        __builtin_amdgcn_sched_barrier(0);
+        mq0(pacc[PA][1], va, df[1][0]);
+      } else if (s < 7) {
+        mq(sacc[PA][0], ka, qf[0][s]);
+        __builtin_amdgcn_sched_barrier(0);
+        mq(sacc[PA][1], ka, qf[1][s]);
+        smx(prv{}, 1, s, lim, mask_c);
+        __builtin_amdgcn_sched_barrier(0);
+        mq(pacc[PA][0], va, df[0][s]);
+        __builtin_amdgcn_sched_barrier(0);
+        mq(pacc[PA][1], va, df[1][s]);
+      } else {
+        smx(prv{}, 1, 7, lim, mask_c);
+        __builtin_amdgcn_sched_barrier(0);
+        mq4_fenced(sacc[PA][0], sacc[PA][1], pacc[PA][0], pacc[PA][1], qf[0][7], qf[1][7],
+                   df[0][7], df[1][7], ka, va);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      ka = nk;
+      va = nv;
+    }
+  };
+  // phase B(j-1): dQ^T += K^T dS^T of step j-1 (parity PB) with K^T from the
+  // K image at kt; beside: unit u of softmax(j) of g0 (parity PB ^ 1) every 2
+  // MFMAs (SOFT false: nothing beside, the tail)
+  auto kread = [&](const char* kt, int i) {
+    const int db = i >> 1, kk = i & 1;
+    return cat8(lds_tr_b64(kt + ktr[db][0] + kk * 4096), lds_tr_b64(kt + ktr[db][1] + kk * 4096));
+  };
+  auto phaseB = [&](auto par_c, const char* kt, int j, auto mask_c, auto soft_c) {
+    constexpr int PB = decltype(par_c)::value;
+    constexpr bool SOFT = decltype(soft_c)::value;
+    using cur = std::integral_constant<int, PB ^ 1>;
+    const int lim = lim_of(j, 0);
+    ds_ready(dsf[PB]);
+    bf16x8_t a = kread(kt, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bf16x8_t n = i < 7 ? kread(kt, i + 1) : a;
+      ma(dqa[0][i >> 1], a, dsf[PB][0][i & 1]);
+      if (SOFT) smx(cur{}, 0, i, lim, mask_c);
+      __builtin_amdgcn_sched_barrier(0);
+      ma(dqa[1][i >> 1], a, dsf[PB][1][i & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      a = n;
+    }
+  };
+
+  // tile t = steps 2 t (parity 0) and 2 t + 1 (parity 1).  MASK: the
+  // causal block's last tile (its two steps are the diagonal ones).
+  auto tile = [&](int t, auto mask_c) {
+    using F = std::false_type;
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    const char* cur = smem + (t & 3) * QSLOT;
+    const char* prv = t ? smem + ((t + 3) & 3) * QSLOT : cur;
+    // step 2t: A(2t) beside softmax(2t-1, g1) (never diagonal); B(2t-1)
+    // beside softmax(2t, g0)
+    phaseA(P0{}, cur, 2 * t, F{});
+    phaseB(P1{}, prv + 32 * 256, 2 * t, mask_c, std::true_type{});
+    // step 2t+1: A(2t+1) beside softmax(2t, g1); B(2t) beside softmax(2t+1, g0)
+    phaseA(P1{}, cur + 32 * 256, 2 * t + 1, mask_c);
+    phaseB(P0{}, cur, 2 * t + 1, mask_c, std::true_type{});
+    // barrier: tile t+1 landed (own pieces; tile t+2's 8 may fly), every
+    // wave past B(2t-1) - the last reader of tile t-1's slot - then tile
+    // t+3's DMA into that slot
+    if (t + 2 < T) vmw<8>();
+    else vmw<0>();
+    __builtin_amdgcn_s_barrier();
+    if (t + 3 < T) issue(t + 3);
+  };
+  const int Tm = CAUSAL ? T - 1 : T;
+  for (int t = 0; t < Tm; ++t) tile(t, std::false_type{});
+  if constexpr (CAUSAL) tile(T - 1, std::true_type{});
+  // tail: softmax(J-1) of g1, then B(J-1)
+  {
+    const int j = 2 * T - 1;
+    const int lim = lim_of(j, 1);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      smx(std::integral_constant<int, 1>{}, 1, u, lim, std::integral_constant<bool, CAUSAL>{});
+    __builtin_amdgcn_sched_barrier(0);
+    phaseB(std::integral_constant<int, 1>{}, smem + ((T - 1) & 3) * QSLOT + 32 * 256, j + 1,
+           std::false_type{}, std::false_type{});
+  }
+  // dQ^T final: drain the asm MFMAs before the accumulators are read
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int db = 0; db < 4; ++db) asm volatile("" : "+a"(dqa[g][db]));
+
+  // ---- dQ = scale (dQ^T)^T: lane = query row, registers 4 rg .. 4 rg + 3 ->
+  // dims 32 db + 8 rg + 4 h .. + 3 (one 8-B store each)
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    uint16_t* dr = dq + (static_cast<long>(b) * S + q0 + 32 * g + r32) * tokd + static_cast<long>(hq) * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        uint2 pk;
+        pk.x = pk2(dqa[g][db][4 * rg] * scale, dqa[g][db][4 * rg + 1] * scale);
+        pk.y = pk2(dqa[g][db][4 * rg + 2] * scale, dqa[g][db][4 * rg + 3] * scale);
+        *reinterpret_cast<uint2*>(dr + 32 * db + 8 * rg + 4 * h) = pk;
+      }
+  }
+}
+
+// dQ of backward variant 9 (+ the rowc pairs for mxk_attn_bwd_dkdv256).
+// Returns a HIP status; hipErrorInvalidValue for a layout it does not take.
+MXK_API int mxk_attn_bwd_dq256(const void* q, const void* k, const void* v, const void* o,
+                               const void* dout, const float* lse, void* dq, float* rowc, int B,
+                               int S, int Hq, int Hkv, long q_tok, long k_tok, long v_tok,
+                               float scale, int causal, hipStream_t stream) {
+  if (B < 1 || S < QW || S % QW || Hkv < 1 || Hq % Hkv || (Hq / Hkv) % 4 || q_tok % 8 ||
+      k_tok % 8 || v_tok % 8 || static_cast<long>(S) * k_tok * 2 >= (1L << 32) ||
+      static_cast<long>(S) * v_tok * 2 >= (1L << 32) ||
+      (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
+       reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
+       reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
+       reinterpret_cast<uintptr_t>(rowc)) % 16)
+    return static_cast<int>(hipErrorInvalidValue);
+  const int nwg = B * (Hq / 4) * (S / QW);
+  const auto* Q = static_cast<const uint16_t*>(q);
+  const auto* K = static_cast<const uint16_t*>(k);
+  const auto* V = static_cast<const uint16_t*>(v);
+  const auto* O = static_cast<const uint16_t*>(o);
+  const auto* dO = static_cast<const uint16_t*>(dout);
+  auto* dQ = static_cast<uint16_t*>(dq);
+  if (causal)
+    hipLaunchKernelGGL(mxk_attn_bwd_dq256_kernel<true>, dim3(nwg), dim3(256), 0, stream, Q, K, V, O,
+                       dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  else
+    hipLaunchKernelGGL(mxk_attn_bwd_dq256_kernel<false>, dim3(nwg), dim3(256), 0, stream, Q, K, V,
+                       O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  MXK_RETURN_LAUNCH_STATUS();
+}

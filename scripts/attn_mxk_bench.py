@@ -79,6 +79,7 @@ def main():
     res["mxk_bwd_v6"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=6))
     res["mxk_bwd_v7"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=7))
     res["mxk_bwd_v8"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=8))
+    res["mxk_bwd_v9"] = bench(lambda: A.attn_bwd(q, k, v, o, lse, do, causal=True, variant=9))
     qg, kg, vg = (t.detach().transpose(1, 2).requires_grad_() for t in (q, k, v))
     dot = do.transpose(1, 2)
 

@@ -20,6 +20,7 @@
 #   ddp_gloo2     the multi-rank DDP step (ZeRO-1) rehearsed: 2 gloo ranks on one GPU,
 #                 2 Llama-3-8B layers (NOT the headline config)
 #   validator_gloo2  bench.py validator mode, 2 gloo ranks on one GPU
+#   ddp_l2        the same 2-layer step on one rank (the reference for ddp_gloo2)
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 R=$PWD
@@ -88,6 +89,8 @@ for step in "$@"; do
     ddp_gloo2)
       run ddp_gloo2 600 env MXK_BENCH_BACKEND=gloo python3 -u bench.py --mode ddp --gpus 2 \
         --layers 2 --steps "${DDP_STEPS:-3}" --warmup 1 ${DDP_ARGS:-} ;;
+    ddp_l2)
+      run ddp_l2 300 python3 -u bench.py --mode ddp --layers 2 --steps "${DDP_STEPS:-3}" --warmup 1 ${DDP_ARGS:-} ;;
     validator_gloo2)
       run validator_gloo2 400 env MXK_BENCH_BACKEND=gloo python3 -u bench.py --gpus 2 --steps 10 \
         --warmup 2 --allreduce-sizes 1,16,256 --ab-sizes "" ;;

@@ -184,3 +184,45 @@ def test_attn_bwd_onepass_v7_v8(cuda_device, B, S, Hq, Hkv, causal, bf16_atomics
     scale_ = max(1.0, d6[0].float().abs().max().item())
     lim = (2e-2 if bf16_atomics else 1e-2) * scale_
     assert (d6[0].float() - dq.float()).abs().max().item() <= lim
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal,fused", [
+    (1, 256, 4, 1, False, False),    # one quad, one row block per tile ring slot
+    (2, 512, 8, 2, True, True),      # two quads, diagonal steps, strided q / dk / dv
+    (1, 1024, 8, 1, True, False),    # MQA: two quads of one KV head
+    (1, 768, 8, 2, False, True),     # three 256-key blocks, full attention
+    (1, 2048, 32, 8, True, True),    # the Llama-3-8B shape (B = 1)
+    (1, 512, 4, 2, True, False),     # group of 2: not a quad -> variant 6 runs
+])
+def test_attn_bwd_dq256_v9(cuda_device, B, S, Hq, Hkv, causal, fused):
+    """Backward variant 9: dQ by workgroups of the 4 query heads of a GQA quad
+    x 64 rows, one wave per SIMD (attention_dq256.hip: Q / dO resident as MFMA
+    operands in the accumulator file beside dQ^T, K / V by LDS-DMA shared by
+    the 4 heads, the delta pass folded in), then the 256-key dK / dV.  Every
+    output vs the fp32 reference into strided slices of a fused buffer;
+    bit-identical across two runs (no atomics); close to variant 6 (same
+    math, other summation order of dQ)."""
+    q, k, v = _qkv(B, S, Hq, Hkv, cuda_device, seed=23, fused=fused)
+    o, lse = A.attn_fwd(q, k, v, causal=causal)
+    g = torch.Generator(device=cuda_device).manual_seed(29)
+    dout = torch.randn(B, S, Hq, 128, device=cuda_device, generator=g).bfloat16()
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    A.attention_ref(qr, kr, vr, causal=causal).backward(dout.float())
+    buf = torch.full((B, S, (Hq + 2 * Hkv) * 128), float("nan"), device=cuda_device,
+                     dtype=torch.bfloat16)
+    dk = buf[..., Hq * 128:(Hq + Hkv) * 128].view(B, S, Hkv, 128)
+    dv = buf[..., (Hq + Hkv) * 128:].view(B, S, Hkv, 128)
+    dq, _, _ = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, dk=dk, dv=dv, variant=9)
+    for name, got, want in (("dq", dq, qr.grad), ("dk", dk, kr.grad), ("dv", dv, vr.grad)):
+        assert not torch.isnan(got).any(), name
+        err = (got.float() - want).abs().max().item()
+        tol = 3e-2 * max(1.0, want.abs().max().item())
+        assert err < tol, (name, err, tol)
+    again = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, variant=9)
+    assert torch.equal(again[0], dq) and torch.equal(again[1], dk) and torch.equal(again[2], dv)
+    d6 = A.attn_bwd(q, k, v, o, lse, dout, causal=causal, variant=6)
+    for name, a6, got in (("dq", d6[0], dq), ("dk", d6[1], dk), ("dv", d6[2], dv)):
+        err = (a6.float() - got.float()).abs().max().item()
+        assert err <= 1e-2 * max(1.0, a6.float().abs().max().item()), (name, err)
+    if (Hq // Hkv) % 4:
+        assert torch.equal(d6[0], dq)     # the fallback is variant 6 itself
