@@ -85,6 +85,8 @@ _SIGNATURES = {
                                   _vp]),
     "mxk_attn_bwd_workspace": (_l, [_i, _i, _i]),
     "mxk_attn_bwd_workspace_variant": (_l, [_i, _i, _i, _i]),
+    "mxk_attn_bwd_dq256": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _l, _l, _l,
+                                _f, _i, _vp]),
     "mxk_attn_bwd_variant": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i,
                                   _i, _l, _l, _l, _l, _l, _f, _i, _i, _vp]),
     "mxk_attn_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i,
