@@ -87,6 +87,8 @@ _SIGNATURES = {
     "mxk_attn_bwd_workspace_variant": (_l, [_i, _i, _i, _i]),
     "mxk_attn_bwd_dq256": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _l, _l, _l,
                                 _f, _i, _vp]),
+    "mxk_attn_bwd_dq256_dbg": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _l, _l,
+                                    _l, _f, _i, _vp]),
     "mxk_attn_bwd_variant": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i,
                                   _i, _l, _l, _l, _l, _l, _f, _i, _i, _vp]),
     "mxk_attn_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i,

@@ -90,7 +90,10 @@ __device__ __forceinline__ void vmw() {
 __device__ __forceinline__ uint32_t pk2(float lo, float hi) { return mxk::pack2bf(lo, hi); }
 }  // namespace
 
-template <bool CAUSAL>
+// DBG (diagnostic instances, mxk_attn_bwd_dq256_dbg): the dS^T operand
+// replaced by 1 (1), by S (2) or by dP (3) wherever P > 0, so a wrong dQ
+// can be pinned on phase B, on the S or on the dP product
+template <bool CAUSAL, int DBG = 0>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                           const uint16_t* __restrict__ v, const uint16_t* __restrict__ o,
@@ -244,6 +247,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
       float p = fexp2(fmaf(sacc[P][g][r], c, nl[g]));
       if (MASK) p = (r & 3) + 8 * (r >> 2) > lim ? 0.f : p;
       x[e] = p * (pacc[P][g][r] - dl[g]);
+      if constexpr (DBG == 1) x[e] = p > 0.f ? 1.f : 0.f;
+      if constexpr (DBG == 2) x[e] = p > 0.f ? sacc[P][g][r] : 0.f;
+      if constexpr (DBG == 3) x[e] = p > 0.f ? pacc[P][g][r] : 0.f;
     }
     dsw[P][g][u >> 2][u & 3] = pk2(x[0], x[1]);
     if ((u & 3) == 3) {
@@ -337,6 +343,14 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     // step 2t+1: A(2t+1) beside softmax(2t, g1); B(2t) beside softmax(2t+1, g0)
     phaseA(P1{}, cur + 32 * 256, 2 * t + 1, mask_c);
     phaseB(P0{}, cur, 2 * t + 1, mask_c, std::true_type{});
+    // 8-pass XDL write -> accumulator read: the allocator may copy dQ^T (just
+    // written by phase B's MFMAs) on the loop's exit edge - seen: register 0
+    // of the last tile read one instruction behind its MFMA, stale in every
+    // non-causal block; the nops cover the latency and the accumulators are
+    // redefined behind them
+    asm volatile("s_nop 7\n\ts_nop 4"
+                 : "+a"(dqa[0][0]), "+a"(dqa[0][1]), "+a"(dqa[0][2]), "+a"(dqa[0][3]),
+                   "+a"(dqa[1][0]), "+a"(dqa[1][1]), "+a"(dqa[1][2]), "+a"(dqa[1][3]));
     // barrier: tile t+1 landed (own pieces; tile t+2's 8 may fly), every
     // wave past B(2t-1) - the last reader of tile t-1's slot - then tile
     // t+3's DMA into that slot
@@ -410,5 +424,30 @@ MXK_API int mxk_attn_bwd_dq256(const void* q, const void* k, const void* v, cons
   else
     hipLaunchKernelGGL(mxk_attn_bwd_dq256_kernel<false>, dim3(nwg), dim3(256), 0, stream, Q, K, V,
                        O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// Diagnostic: mxk_attn_bwd_dq256 with the dS^T operand replaced (dbg 1: 1,
+// 2: S, 3: dP wherever P > 0); non-causal only.
+MXK_API int mxk_attn_bwd_dq256_dbg(const void* q, const void* k, const void* v, const void* o,
+                                   const void* dout, const float* lse, void* dq, float* rowc, int B,
+                                   int S, int Hq, int Hkv, long q_tok, long k_tok, long v_tok,
+                                   float scale, int dbg, hipStream_t stream) {
+  if (B < 1 || S < QW || S % QW || Hkv < 1 || Hq % Hkv || (Hq / Hkv) % 4 || dbg < 1 || dbg > 3)
+    return static_cast<int>(hipErrorInvalidValue);
+  const int nwg = B * (Hq / 4) * (S / QW);
+  const auto* Q = static_cast<const uint16_t*>(q);
+  const auto* K = static_cast<const uint16_t*>(k);
+  const auto* V = static_cast<const uint16_t*>(v);
+  const auto* O = static_cast<const uint16_t*>(o);
+  const auto* dO = static_cast<const uint16_t*>(dout);
+  auto* dQ = static_cast<uint16_t*>(dq);
+#define MXK_DQ256_DBG(N)                                                                         \
+  hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<false, N>), dim3(nwg), dim3(256), 0, stream, Q, K, \
+                     V, O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale)
+  if (dbg == 1) MXK_DQ256_DBG(1);
+  else if (dbg == 2) MXK_DQ256_DBG(2);
+  else MXK_DQ256_DBG(3);
+#undef MXK_DQ256_DBG
   MXK_RETURN_LAUNCH_STATUS();
 }

@@ -180,7 +180,7 @@ def test_detector_flags_a_stale_descriptor_word():
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src", ["attention.hip", "attention_bwd256.hip", "attention_fwd256.hip",
-                                 "gemm_bf16.hip", "gemm_bf16_layouts.hip"])
+                                 "attention_dq256.hip", "gemm_bf16.hip", "gemm_bf16_layouts.hip"])
 def test_asm_dma_reads_no_fresh_valu_sgpr(src, tmp_path):
     asm = _asm(src, str(tmp_path / (src + ".s")))
     assert "buffer_load" in asm
@@ -248,7 +248,8 @@ def trans_result_read_next(asm: str) -> list[str]:
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("src", ["attention.hip", "attention_bwd256.hip", "attention_fwd256.hip"])
+@pytest.mark.parametrize("src", ["attention.hip", "attention_bwd256.hip", "attention_fwd256.hip",
+                                 "attention_dq256.hip"])
 def test_no_asm_read_of_a_fresh_transcendental(src, tmp_path):
     asm = _asm(src, str(tmp_path / "t.s"))
     assert trans_result_read_next(asm) == []
@@ -340,10 +341,11 @@ def test_detector_flags_a_reload_in_a_loop():
     assert scratch_in_loops(asm) == {"_Zl": 1}
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("src", ["attention_bwd256.hip", "attention_fwd256.hip"])
+@pytest.mark.parametrize("src", ["attention_bwd256.hip", "attention_fwd256.hip",
+                                 "attention_dq256.hip"])
 def test_attention_bwd256_asm_mfma_hazards_and_spills(src, tmp_path):
-    """attention_bwd256.hip / attention_fwd256.hip: the accumulated tiles
-    (dK^T / dV^T; O^T) pinned to AGPRs and S / dP (S^T) to VGPRs by
+    """attention_bwd256.hip / attention_fwd256.hip / attention_dq256.hip: the
+    accumulated tiles (dK^T / dV^T; O^T; dQ^T) pinned to AGPRs and S / dP (S^T) to VGPRs by
     inline-asm MFMAs; no early read of either, and no spill (their LDS-DMA
     ring waits are counted vmcnt waits)."""
     asm = _asm(src, str(tmp_path / (src + ".s")))
