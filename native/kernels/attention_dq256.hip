@@ -78,9 +78,30 @@ __device__ __forceinline__ void ma(f32x16_t& acc, const bf16x8_t& a, const bf16x
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 // VALU-written dS^T operands -> MFMA read: the wait states, with the operands
-// named so none of them is written behind the nops
-__device__ __forceinline__ void ds_ready(const bf16x8_t (&x)[2][2]) {
-  asm volatile("s_nop 2" ::"v"(x[0][0]), "v"(x[0][1]), "v"(x[1][0]), "v"(x[1][1]));
+// named so none of them is written behind the nops.  The dQ^T tiles are named
+// too ("+a"): the allocator shuffles them between the loop and the tail's
+// MFMA instance with v_accvgpr_write / _mov, which an inline-asm MFMA right
+// behind would read stale (register 0 of a tile, seen); a copy it needs now
+// sits in front of these nops
+__device__ __forceinline__ void ds_ready(const bf16x8_t (&x)[2][2], f32x16_t (&acc)[2][4]) {
+  asm volatile("s_nop 2"
+               : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]),
+                 "+a"(acc[1][0]), "+a"(acc[1][1]), "+a"(acc[1][2]), "+a"(acc[1][3])
+               : "v"(x[0][0]), "v"(x[0][1]), "v"(x[1][0]), "v"(x[1][1]));
+}
+// the same for the Q / dO fragments (MFMA B operands in AGPRs) in front of a
+// phase A: any allocator copy of them lands before the nops
+__device__ __forceinline__ void qd_ready(bf16x8_t (&qf)[2][8], bf16x8_t (&df)[2][8]) {
+  asm volatile(""
+               : "+a"(qf[0][0]), "+a"(qf[0][1]), "+a"(qf[0][2]), "+a"(qf[0][3]), "+a"(qf[0][4]),
+                 "+a"(qf[0][5]), "+a"(qf[0][6]), "+a"(qf[0][7]), "+a"(qf[1][0]), "+a"(qf[1][1]),
+                 "+a"(qf[1][2]), "+a"(qf[1][3]), "+a"(qf[1][4]), "+a"(qf[1][5]), "+a"(qf[1][6]),
+                 "+a"(qf[1][7]));
+  asm volatile("s_nop 1"
+               : "+a"(df[0][0]), "+a"(df[0][1]), "+a"(df[0][2]), "+a"(df[0][3]), "+a"(df[0][4]),
+                 "+a"(df[0][5]), "+a"(df[0][6]), "+a"(df[0][7]), "+a"(df[1][0]), "+a"(df[1][1]),
+                 "+a"(df[1][2]), "+a"(df[1][3]), "+a"(df[1][4]), "+a"(df[1][5]), "+a"(df[1][6]),
+                 "+a"(df[1][7]));
 }
 template <int N>
 __device__ __forceinline__ void vmw() {
@@ -265,6 +286,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     constexpr int PA = decltype(par_c)::value;
     using prv = std::integral_constant<int, PA ^ 1>;
     const int lim = lim_of(j - 1, 1);
+    qd_ready(qf, df);
     bf16x8_t ka = lds_b128(kt + koff[0]), va = lds_b128(kt + TILE_BYTES + koff[0]);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -314,7 +336,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     constexpr bool SOFT = decltype(soft_c)::value;
     using cur = std::integral_constant<int, PB ^ 1>;
     const int lim = lim_of(j, 0);
-    ds_ready(dsf[PB]);
+    ds_ready(dsf[PB], dqa);
     bf16x8_t a = kread(kt, 0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {

@@ -4,6 +4,7 @@
 import os
 import statistics
 import sys
+import time
 
 import torch
 
@@ -27,10 +28,12 @@ def main():
     for vv in variants[1:]:
         same = all(torch.equal(x, y) for x, y in zip(outs[variants[0]], outs[vv]))
         print(f"RESULT variant={vv} bit-identical to variant={variants[0]}: {same}", flush=True)
-    for _ in range(3):
+    # time-floored warm-up (the clock ramps over ~1 s; bench.py's protocol)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < float(os.environ.get("WARM_S", 2.0)):
         for vv in variants:
             A.attn_bwd(q, k, v, o, lse, dout, variant=vv)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     for _ in range(10):
         for vv in variants:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

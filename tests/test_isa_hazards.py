@@ -303,6 +303,58 @@ def valu_write_then_mfma_read(asm: str, states: int = 2) -> dict[str, int]:
     return bad
 
 
+def _aregs(text: str) -> set[int]:
+    out = set()
+    for m in re.finditer(r"\ba\[(\d+):(\d+)\]|\ba(\d+)\b", text):
+        lo = int(m.group(1) or m.group(3))
+        hi = int(m.group(2) or m.group(3))
+        out.update(range(lo, hi + 1))
+    return out
+
+
+def agpr_write_then_mfma_read(asm: str, states: int = 2) -> dict[str, int]:
+    """An inline-asm MFMA reading (as A, B or C) an AGPR that a
+    v_accvgpr_write / v_accvgpr_mov wrote fewer than ``states`` wait states
+    before.  Seen: the register allocator shuffling the dQ^T tiles between the
+    loop and the tail's own MFMA instance (attention_dq256.hip) wrote a48 -
+    register 0 of a tile - right in front of the MFMA accumulating into
+    a[48:63]: that register alone missed its earlier sum in every block."""
+    bad = {}
+    for name in re.findall(r"^(_Z[^\s:]+):", asm, re.M):
+        i = asm.find(name + ":")
+        j = asm.find(".Lfunc_end", i)
+        body = [ln.split(";")[0].strip() for ln in asm[i:j].split("\n")]
+        body = [ln for ln in body if ln and not ln.startswith(".") and not ln.endswith(":")]
+        pend: dict[int, int] = {}
+        n = 0
+        for ln in body:
+            op, _, rest = ln.partition(" ")
+            m = re.match(r"s_nop (\d+)", ln)
+            step = int(m.group(1)) + 1 if m else 1
+            if op.startswith("v_mfma"):
+                srcs = rest.partition(",")[2]
+                if any(pend.get(r, states) < states for r in _aregs(srcs)):
+                    n += 1
+                pend = {r: c + step for r, c in pend.items() if c + step < states}
+                continue
+            pend = {r: c + step for r, c in pend.items() if c + step < states}
+            if op.startswith(("v_accvgpr_write", "v_accvgpr_mov")):
+                for r in _aregs(rest.partition(",")[0]):
+                    pend[r] = 0
+            if op in ("s_branch", "s_endpgm", "s_setpc_b64"):
+                pend = {}
+        if n:
+            bad[name] = n
+    return bad
+
+
+def test_detector_flags_a_fresh_accumulator_copy():
+    asm = ("_Zd:\n\tv_accvgpr_write_b32 a48, v32\n"
+           "\tv_mfma_f32_32x32x16_bf16 a[48:63], v[4:7], v[0:3], a[48:63]\n.Lfunc_end0:\n")
+    assert agpr_write_then_mfma_read(asm) == {"_Zd": 1}
+    assert agpr_write_then_mfma_read(asm.replace("\tv_mfma", "\ts_nop 1\n\tv_mfma")) == {}
+
+
 def test_detector_flags_a_fresh_mfma_operand():
     asm = ("_Zc:\n\tv_mov_b64_e32 v[32:33], v[16:17]\n"
            "\tv_mfma_f32_32x32x16_bf16 v[32:47], v[0:3], v[4:7], v[32:47]\n.Lfunc_end0:\n")
@@ -353,6 +405,7 @@ def test_attention_bwd256_asm_mfma_hazards_and_spills(src, tmp_path):
     assert close_accumulator_reads(asm) == {}
     assert close_vgpr_result_reads(asm) == {}
     assert valu_write_then_mfma_read(asm) == {}
+    assert agpr_write_then_mfma_read(asm) == {}
     # no scratch access inside a loop (a reload there is a vector-memory op
     # the counted vmcnt waits of the LDS-DMA rings do not expect); a spill
     # stored before the loop and reloaded after it is harmless
