@@ -43,6 +43,11 @@ all: kernels node tools fake-amdsmi
 
 kernels: $(OUT_LIB)/libmxkernels.so
 
+# the 256-row dQ kernel's softmax beside MFMAs: no SLP-packed v_pk_*_f32
+# (an anti-lever beside MFMAs at one wave per SIMD; -1.5 % on the backward)
+$(BUILD)/kernels/attention_dq256.o: HIPFLAGS += -fno-slp-vectorize
+$(BUILD)/exp/attention_dq256.o: HIPFLAGS += -fno-slp-vectorize
+
 $(BUILD)/kernels/%.o: native/kernels/%.hip $(KERNEL_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

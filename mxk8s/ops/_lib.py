@@ -89,6 +89,8 @@ _SIGNATURES = {
                                 _f, _i, _vp]),
     "mxk_attn_bwd_dq256_dbg": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _l, _l,
                                     _l, _f, _i, _vp]),
+    "mxk_attn_bwd_dq256_stamps": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _l, _l,
+                                       _l, _f, _vp, _vp]),
     "mxk_attn_bwd_variant": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i,
                                   _i, _l, _l, _l, _l, _l, _f, _i, _i, _vp]),
     "mxk_attn_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i,

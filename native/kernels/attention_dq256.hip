@@ -113,15 +113,29 @@ __device__ __forceinline__ uint32_t pk2(float lo, float hi) { return mxk::pack2b
 
 // DBG (diagnostic instances, mxk_attn_bwd_dq256_dbg): the dS^T operand
 // replaced by 1 (1), by S (2) or by dP (3) wherever P > 0, so a wrong dQ
-// can be pinned on phase B, on the S or on the dP product
-template <bool CAUSAL, int DBG = 0>
+// can be pinned on phase B, on the S or on the dP product.  STAMP
+// (mxk_attn_bwd_dq256_stamps): each wave adds up the shader cycles of its
+// prologue, phases A, phases B, barrier segments and tail, and writes them
+// with its total to stamps[wave id][6]
+template <bool CAUSAL, int DBG = 0, bool STAMP = false>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                           const uint16_t* __restrict__ v, const uint16_t* __restrict__ o,
                           const uint16_t* __restrict__ dout, const float* __restrict__ lse,
                           uint16_t* __restrict__ dq, float* __restrict__ rowc, int S, int Hq,
-                          int Hkv, long q_tok, long k_tok, long v_tok, float scale) {
+                          int Hkv, long q_tok, long k_tok, long v_tok, float scale,
+                          unsigned long long* __restrict__ stamps = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[QLDS];
+  unsigned long long st_0 = 0, st_c = 0, st_seg[5] = {0, 0, 0, 0, 0};
+  if constexpr (STAMP) st_0 = st_c = __builtin_readcyclecounter();
+  // segment e (0 prologue, 1 phase A, 2 phase B, 3 barrier, 4 tail) ends here
+  auto stamp = [&](int e) {
+    if constexpr (STAMP) {
+      const unsigned long long t = __builtin_readcyclecounter();
+      st_seg[e] += t - st_c;
+      st_c = t;
+    }
+  };
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -337,16 +351,19 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     using cur = std::integral_constant<int, PB ^ 1>;
     const int lim = lim_of(j, 0);
     ds_ready(dsf[PB], dqa);
-    bf16x8_t a = kread(kt, 0);
+    // K^T operands two MFMA pairs ahead (one pair ahead exposed the
+    // transposed reads' latency: one wave per SIMD, nothing else hides it)
+    bf16x8_t a = kread(kt, 0), a1 = kread(kt, 1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const bf16x8_t n = i < 7 ? kread(kt, i + 1) : a;
+      const bf16x8_t n = i < 6 ? kread(kt, i + 2) : a;
       ma(dqa[0][i >> 1], a, dsf[PB][0][i & 1]);
       if (SOFT) smx(cur{}, 0, i, lim, mask_c);
       __builtin_amdgcn_sched_barrier(0);
       ma(dqa[1][i >> 1], a, dsf[PB][1][i & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      a = n;
+      a = a1;
+      a1 = n;
     }
   };
 
@@ -361,10 +378,14 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     // step 2t: A(2t) beside softmax(2t-1, g1) (never diagonal); B(2t-1)
     // beside softmax(2t, g0)
     phaseA(P0{}, cur, 2 * t, F{});
+    stamp(1);
     phaseB(P1{}, prv + 32 * 256, 2 * t, mask_c, std::true_type{});
+    stamp(2);
     // step 2t+1: A(2t+1) beside softmax(2t, g1); B(2t) beside softmax(2t+1, g0)
     phaseA(P1{}, cur + 32 * 256, 2 * t + 1, mask_c);
+    stamp(1);
     phaseB(P0{}, cur, 2 * t + 1, mask_c, std::true_type{});
+    stamp(2);
     // 8-pass XDL write -> accumulator read: the allocator may copy dQ^T (just
     // written by phase B's MFMAs) on the loop's exit edge - seen: register 0
     // of the last tile read one instruction behind its MFMA, stale in every
@@ -380,7 +401,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     else vmw<0>();
     __builtin_amdgcn_s_barrier();
     if (t + 3 < T) issue(t + 3);
+    stamp(3);
   };
+  stamp(0);
   const int Tm = CAUSAL ? T - 1 : T;
   for (int t = 0; t < Tm; ++t) tile(t, std::false_type{});
   if constexpr (CAUSAL) tile(T - 1, std::true_type{});
@@ -416,6 +439,15 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
         pk.y = pk2(dqa[g][db][4 * rg + 2] * scale, dqa[g][db][4 * rg + 3] * scale);
         *reinterpret_cast<uint2*>(dr + 32 * db + 8 * rg + 4 * h) = pk;
       }
+  }
+  if constexpr (STAMP) {
+    stamp(4);
+    if (lane == 0) {
+      unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 6;
+      w[0] = __builtin_readcyclecounter() - st_0;
+#pragma unroll
+      for (int e = 0; e < 5; ++e) w[1 + e] = st_seg[e];
+    }
   }
 }
 
@@ -471,5 +503,24 @@ MXK_API int mxk_attn_bwd_dq256_dbg(const void* q, const void* k, const void* v, 
   else if (dbg == 2) MXK_DQ256_DBG(2);
   else MXK_DQ256_DBG(3);
 #undef MXK_DQ256_DBG
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// Diagnostic: mxk_attn_bwd_dq256 (causal) with per-wave segment cycle counts,
+// stamps: [B * Hq / 4 * S / 64 workgroups][4 waves][total, prologue, A, B,
+// barrier, tail]
+MXK_API int mxk_attn_bwd_dq256_stamps(const void* q, const void* k, const void* v, const void* o,
+                                      const void* dout, const float* lse, void* dq, float* rowc,
+                                      int B, int S, int Hq, int Hkv, long q_tok, long k_tok,
+                                      long v_tok, float scale, unsigned long long* stamps,
+                                      hipStream_t stream) {
+  if (B < 1 || S < QW || S % QW || Hkv < 1 || Hq % Hkv || (Hq / Hkv) % 4 || !stamps)
+    return static_cast<int>(hipErrorInvalidValue);
+  const int nwg = B * (Hq / 4) * (S / QW);
+  hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<true, 0, true>), dim3(nwg), dim3(256), 0, stream,
+                     static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k),
+                     static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o),
+                     static_cast<const uint16_t*>(dout), lse, static_cast<uint16_t*>(dq), rowc, S,
+                     Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps);
   MXK_RETURN_LAUNCH_STATUS();
 }
