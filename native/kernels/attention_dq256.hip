@@ -267,69 +267,102 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   dsf[1][0][0] = bf16x8_t{};
   dsf[1][0][1] = bf16x8_t{};
 
-  // softmax unit of step j's tile g (8 units: registers 2 u, 2 u + 1 and
-  // their bf16 pair; the k-step operand is complete after units 3 / 7).
-  // MASK (the two diagonal steps): key kv0 + crow(r, h) past query
-  // q0 + 32 g + r32, i.e. (r & 3) + 8 (r >> 2) > lim, one compare a score.
+  // softmax of step j's tile g as 24 items (unit u = 0..7: item 3 u element
+  // 2 u, 3 u + 1 element 2 u + 1, 3 u + 2 their bf16 pair; the k-step operand
+  // is complete after units 3 / 7), placed one or two per MFMA gap: an item
+  // costs <= 20 issue cycles (fma, exp, sub, mul; the guide's one-wave
+  // budget is ~24 per 32-cycle gap with at most one 8-cycle exp), where whole
+  // units (two exps) made the gaps they sat in ~50 cycles.  MASK (the two
+  // diagonal steps): key kv0 + crow(r, h) past query q0 + 32 g + r32, i.e.
+  // (r & 3) + 8 (r >> 2) > lim, one compare a score.
   uint32_t dsw[2][2][2][4];           // the operands as bf16 pairs, [parity][g][kk][word]
-  auto smx = [&](auto par_c, int g, int u, int lim, auto mask_c) {
+  float xe[2];                        // the unit's two elements between their items
+  auto smi = [&](auto par_c, int g, int n, int lim, auto mask_c) {
     constexpr int P = decltype(par_c)::value;
     constexpr bool MASK = decltype(mask_c)::value;
-    float x[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int r = 2 * u + e;
+    const int u = n / 3, kind = n - 3 * u;
+    if (kind < 2) {
+      const int r = 2 * u + kind;
       float p = fexp2(fmaf(sacc[P][g][r], c, nl[g]));
       if (MASK) p = (r & 3) + 8 * (r >> 2) > lim ? 0.f : p;
-      x[e] = p * (pacc[P][g][r] - dl[g]);
-      if constexpr (DBG == 1) x[e] = p > 0.f ? 1.f : 0.f;
-      if constexpr (DBG == 2) x[e] = p > 0.f ? sacc[P][g][r] : 0.f;
-      if constexpr (DBG == 3) x[e] = p > 0.f ? pacc[P][g][r] : 0.f;
-    }
-    dsw[P][g][u >> 2][u & 3] = pk2(x[0], x[1]);
-    if ((u & 3) == 3) {
-      const uint32_t* w = dsw[P][g][u >> 2];
-      dsf[P][g][u >> 2] = __builtin_bit_cast(bf16x8_t, u32x4_t{w[0], w[1], w[2], w[3]});
+      float x = p * (pacc[P][g][r] - dl[g]);
+      if constexpr (DBG == 1) x = p > 0.f ? 1.f : 0.f;
+      if constexpr (DBG == 2) x = p > 0.f ? sacc[P][g][r] : 0.f;
+      if constexpr (DBG == 3) x = p > 0.f ? pacc[P][g][r] : 0.f;
+      xe[kind] = x;
+    } else {
+      dsw[P][g][u >> 2][u & 3] = pk2(xe[0], xe[1]);
+      if ((u & 3) == 3) {
+        const uint32_t* w = dsw[P][g][u >> 2];
+        dsf[P][g][u >> 2] = __builtin_bit_cast(bf16x8_t, u32x4_t{w[0], w[1], w[2], w[3]});
+      }
     }
   };
   auto lim_of = [&](int j, int g) { return q0 + 32 * g + r32 - 32 * j - 4 * h; };
 
+  // operands carried across phases: phase A's first K / V rows (read during
+  // the preceding phase B when both read the same tile) and phase B's first
+  // two K^T operands (read during the preceding phase A), so no phase opens
+  // with an exposed LDS latency
+  bf16x8_t pre_k, pre_v, pre_b0, pre_b1;
+  auto kread = [&](const char* kt, int i) {
+    const int db = i >> 1, kk = i & 1;
+    return cat8(lds_tr_b64(kt + ktr[db][0] + kk * 4096), lds_tr_b64(kt + ktr[db][1] + kk * 4096));
+  };
+
   // phase A(j): S^T, dP^T of step j (parity PA) from the K / V rows at kt;
-  // beside: unit u of softmax(j-1) of g1 (parity PA ^ 1) every 4 MFMAs
-  auto phaseA = [&](auto par_c, const char* kt, int j, auto mask_c) {
+  // beside: softmax(j-1) of g1 (parity PA ^ 1), items 0..23 after MFMAs
+  // 0..23.  PRE: the s = 0 operands are in pre_k / pre_v.  NEXTB (non-null):
+  // read the first two operands of the phase B that follows from there.
+  auto phaseA = [&](auto par_c, const char* kt, int j, auto mask_c, auto pre_c,
+                    const char* nextb) {
     constexpr int PA = decltype(par_c)::value;
+    constexpr bool PRE = decltype(pre_c)::value;
     using prv = std::integral_constant<int, PA ^ 1>;
     const int lim = lim_of(j - 1, 1);
     qd_ready(qf, df);
-    bf16x8_t ka = lds_b128(kt + koff[0]), va = lds_b128(kt + TILE_BYTES + koff[0]);
+    bf16x8_t ka = PRE ? pre_k : lds_b128(kt + koff[0]);
+    bf16x8_t va = PRE ? pre_v : lds_b128(kt + TILE_BYTES + koff[0]);
+    int item = 0;
+    auto beside = [&]() {
+      if (item < 24) smi(prv{}, 1, item, lim, mask_c);
+      ++item;
+    };
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       bf16x8_t nk = ka, nv = va;
       if (s < 7) {
         nk = lds_b128(kt + koff[s + 1]);
         nv = lds_b128(kt + TILE_BYTES + koff[s + 1]);
+      } else {
+        pre_b0 = kread(nextb, 0);
+        pre_b1 = kread(nextb, 1);
       }
       if (s == 0) {
         mq0(sacc[PA][0], ka, qf[0][0]);
+        beside();
         __builtin_amdgcn_sched_barrier(0);
         mq0(sacc[PA][1], ka, qf[1][0]);
-        smx(prv{}, 1, 0, lim, mask_c);
+        beside();
         __builtin_amdgcn_sched_barrier(0);
         mq0(pacc[PA][0], va, df[0][0]);
+        beside();
         __builtin_amdgcn_sched_barrier(0);
         mq0(pacc[PA][1], va, df[1][0]);
+        beside();
       } else if (s < 7) {
         mq(sacc[PA][0], ka, qf[0][s]);
+        beside();
         __builtin_amdgcn_sched_barrier(0);
         mq(sacc[PA][1], ka, qf[1][s]);
-        smx(prv{}, 1, s, lim, mask_c);
+        beside();
         __builtin_amdgcn_sched_barrier(0);
         mq(pacc[PA][0], va, df[0][s]);
+        beside();
         __builtin_amdgcn_sched_barrier(0);
         mq(pacc[PA][1], va, df[1][s]);
+        beside();
       } else {
-        smx(prv{}, 1, 7, lim, mask_c);
-        __builtin_amdgcn_sched_barrier(0);
         mq4_fenced(sacc[PA][0], sacc[PA][1], pacc[PA][0], pacc[PA][1], qf[0][7], qf[1][7],
                    df[0][7], df[1][7], ka, va);
       }
@@ -339,13 +372,13 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     }
   };
   // phase B(j-1): dQ^T += K^T dS^T of step j-1 (parity PB) with K^T from the
-  // K image at kt; beside: unit u of softmax(j) of g0 (parity PB ^ 1) every 2
-  // MFMAs (SOFT false: nothing beside, the tail)
-  auto kread = [&](const char* kt, int i) {
-    const int db = i >> 1, kk = i & 1;
-    return cat8(lds_tr_b64(kt + ktr[db][0] + kk * 4096), lds_tr_b64(kt + ktr[db][1] + kk * 4096));
-  };
-  auto phaseB = [&](auto par_c, const char* kt, int j, auto mask_c, auto soft_c) {
+  // K image at kt (its first two operands in pre_b0 / pre_b1); beside:
+  // softmax(j) of g0 (parity PB ^ 1), items 3 u / 3 u + 1 after MFMAs 2 u /
+  // 2 u + 1 and 3 u + 2 beside the latter.  SOFT false: nothing beside (the
+  // tail).  NEXTA (non-null): read the next phase A's s = 0 operands from
+  // there during the last MFMA pair.
+  auto phaseB = [&](auto par_c, const char* kt, int j, auto mask_c, auto soft_c,
+                    const char* nexta) {
     constexpr int PB = decltype(par_c)::value;
     constexpr bool SOFT = decltype(soft_c)::value;
     using cur = std::integral_constant<int, PB ^ 1>;
@@ -353,14 +386,24 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     ds_ready(dsf[PB], dqa);
     // K^T operands two MFMA pairs ahead (one pair ahead exposed the
     // transposed reads' latency: one wave per SIMD, nothing else hides it)
-    bf16x8_t a = kread(kt, 0), a1 = kread(kt, 1);
+    bf16x8_t a = pre_b0, a1 = pre_b1;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const bf16x8_t n = i < 6 ? kread(kt, i + 2) : a;
+      bf16x8_t n = a;
+      if (i < 6) {
+        n = kread(kt, i + 2);
+      } else if (i == 6 && nexta != nullptr) {
+        pre_k = lds_b128(nexta + koff[0]);
+        pre_v = lds_b128(nexta + TILE_BYTES + koff[0]);
+      }
       ma(dqa[0][i >> 1], a, dsf[PB][0][i & 1]);
-      if (SOFT) smx(cur{}, 0, i, lim, mask_c);
+      if (SOFT) smi(cur{}, 0, 3 * i, lim, mask_c);
       __builtin_amdgcn_sched_barrier(0);
       ma(dqa[1][i >> 1], a, dsf[PB][1][i & 1]);
+      if (SOFT) {
+        smi(cur{}, 0, 3 * i + 1, lim, mask_c);
+        smi(cur{}, 0, 3 * i + 2, lim, mask_c);
+      }
       __builtin_amdgcn_sched_barrier(0);
       a = a1;
       a1 = n;
@@ -377,14 +420,15 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     const char* prv = t ? smem + ((t + 3) & 3) * QSLOT : cur;
     // step 2t: A(2t) beside softmax(2t-1, g1) (never diagonal); B(2t-1)
     // beside softmax(2t, g0)
-    phaseA(P0{}, cur, 2 * t, F{});
+    using T_ = std::true_type;
+    phaseA(P0{}, cur, 2 * t, F{}, F{}, prv + 32 * 256);
     stamp(1);
-    phaseB(P1{}, prv + 32 * 256, 2 * t, mask_c, std::true_type{});
+    phaseB(P1{}, prv + 32 * 256, 2 * t, mask_c, T_{}, cur + 32 * 256);
     stamp(2);
     // step 2t+1: A(2t+1) beside softmax(2t, g1); B(2t) beside softmax(2t+1, g0)
-    phaseA(P1{}, cur + 32 * 256, 2 * t + 1, mask_c);
+    phaseA(P1{}, cur + 32 * 256, 2 * t + 1, mask_c, T_{}, cur);
     stamp(1);
-    phaseB(P0{}, cur, 2 * t + 1, mask_c, std::true_type{});
+    phaseB(P0{}, cur, 2 * t + 1, mask_c, T_{}, nullptr);
     stamp(2);
     // 8-pass XDL write -> accumulator read: the allocator may copy dQ^T (just
     // written by phase B's MFMAs) on the loop's exit edge - seen: register 0
@@ -411,12 +455,15 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   {
     const int j = 2 * T - 1;
     const int lim = lim_of(j, 1);
+    const char* kt = smem + ((T - 1) & 3) * QSLOT + 32 * 256;
+    pre_b0 = kread(kt, 0);
+    pre_b1 = kread(kt, 1);
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      smx(std::integral_constant<int, 1>{}, 1, u, lim, std::integral_constant<bool, CAUSAL>{});
+    for (int n = 0; n < 24; ++n)
+      smi(std::integral_constant<int, 1>{}, 1, n, lim, std::integral_constant<bool, CAUSAL>{});
     __builtin_amdgcn_sched_barrier(0);
-    phaseB(std::integral_constant<int, 1>{}, smem + ((T - 1) & 3) * QSLOT + 32 * 256, j + 1,
-           std::false_type{}, std::false_type{});
+    phaseB(std::integral_constant<int, 1>{}, kt, j + 1, std::false_type{}, std::false_type{},
+           nullptr);
   }
   // dQ^T final: drain the asm MFMAs before the accumulators are read
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
