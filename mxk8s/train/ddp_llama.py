@@ -173,8 +173,12 @@ def run_ddp_bench(args) -> dict:
     # "bench.timed" bounds the steady-state steps on a rocprofv3 marker trace:
     # scripts/kernel_breakdown.py --trace keeps only the kernels inside it
     with roctx.range("bench.timed"):
+        # continue the batch rotation after the warm-up: restarting at batch 0
+        # re-fed the warm-up's batch, whose loss Adam's first (sign-sized)
+        # update had just collapsed (0.87 at 2 layers: a memorised batch, not
+        # a training signal)
         for i in range(args.steps):
-            losses.append(train_step(model, ddp, opt, batches[i % nbatches]))
+            losses.append(train_step(model, ddp, opt, batches[(args.warmup + i) % nbatches]))
         sync()
     mxdist.barrier()
     sync()
