@@ -186,48 +186,86 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
                   t * v_step);
     }
   };
-  issue(0);
-  if (T > 1) issue(1);
-
-  // ---- Q / dO B fragments (lane: row q0 + 32 g + r32, dims 16 s + 8 h .. + 7),
-  // delta = dO . O of the row (the two lane halves hold 64 dims each), lse
-  bf16x8_t qf[2][8], df[2][8];
-  float nl[2], dl[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const long row = q0 + 32 * g + r32;
-    float part = 0.f;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      qf[g][s] = *reinterpret_cast<const bf16x8_t*>(qh + row * q_tok + 16 * s + 8 * h);
-      df[g][s] = *reinterpret_cast<const bf16x8_t*>(doh + row * tokd + 16 * s + 8 * h);
-      const bf16x8_t of = *reinterpret_cast<const bf16x8_t*>(oh + row * tokd + 16 * s + 8 * h);
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        part += mxk::bf2f(static_cast<uint16_t>(df[g][s][e])) * mxk::bf2f(static_cast<uint16_t>(of[e]));
-    }
-    const float delta = half_sum(part);
-    const float l = lse[lrow0 + 32 * g + r32];
-    nl[g] = -l * 1.4426950408889634f;
-    dl[g] = delta;
-    if (h == 0)
-      *reinterpret_cast<float2*>(rowc + 2 * (lrow0 + 32 * g + r32)) = make_float2(-l / scale, -delta);
-  }
-  // consume every per-row load here: the compiler's vmcnt waits for them then
-  // sit before tile 2's DMA (it cannot see the DMA; a wait placed after it
-  // would also wait for tile 2)
+  // ---- per-row operands (lane: row q0 + 32 g + r32, dims 16 s + 8 h .. + 7),
+  // every load in flight at once: asm loads, dO and Q straight into AGPRs
+  // (their home as MFMA B operands), O and lse into VGPRs, then K / V tiles
+  // 0-2.  Compiler-visible loads came out in four dependent batches under
+  // the VGPR pressure of the 192 registers they fill: four memory round
+  // trips, 24 % of the kernel's cycles (profiles/r6_dq256/).  Tiles 1 and 2
+  // are issued whatever T is (a block with fewer tiles never reads them;
+  // past S a buffer load returns zeros), so every count below is constant.
+  bf16x8_t qf[2][8], df[2][8], of[2][8];
+  float lv[2];
 #pragma unroll
   for (int g = 0; g < 2; ++g)
 #pragma unroll
-    for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[g][s]), "v"(df[g][s]) : "memory");
-  if (T > 2) {
-    issue(2);
-    vmw<16>();       // the rowc store and tile 0 (tiles 1 and 2 may fly)
-  } else if (T > 1) {
-    vmw<8>();
-  } else {
-    vmw<0>();
+    for (int s = 0; s < 8; ++s)
+      asm volatile("global_load_dwordx4 %0, %1, off"
+                   : "=a"(df[g][s])
+                   : "v"(doh + static_cast<long>(q0 + 32 * g + r32) * tokd + 16 * s + 8 * h)
+                   : "memory");
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      asm volatile("global_load_dwordx4 %0, %1, off"
+                   : "=v"(of[g][s])
+                   : "v"(oh + static_cast<long>(q0 + 32 * g + r32) * tokd + 16 * s + 8 * h)
+                   : "memory");
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+    asm volatile("global_load_dword %0, %1, off"
+                 : "=v"(lv[g])
+                 : "v"(lse + lrow0 + 32 * g + r32)
+                 : "memory");
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      asm volatile("global_load_dwordx4 %0, %1, off"
+                   : "=a"(qf[g][s])
+                   : "v"(qh + static_cast<long>(q0 + 32 * g + r32) * q_tok + 16 * s + 8 * h)
+                   : "memory");
+  issue(0);
+  issue(1);
+  issue(2);
+  // dO, O, lse landed (Q's 16 and the 24 DMA pieces may fly); the operands
+  // are redefined behind the wait so no use moves above it
+  asm volatile("s_waitcnt vmcnt(40)"
+               : "+a"(df[0][0]), "+a"(df[0][1]), "+a"(df[0][2]), "+a"(df[0][3]), "+a"(df[0][4]),
+                 "+a"(df[0][5]), "+a"(df[0][6]), "+a"(df[0][7]), "+a"(df[1][0]), "+a"(df[1][1]),
+                 "+a"(df[1][2]), "+a"(df[1][3]), "+a"(df[1][4]), "+a"(df[1][5]), "+a"(df[1][6]),
+                 "+a"(df[1][7]), "+v"(lv[0]), "+v"(lv[1]));
+  asm volatile(""
+               : "+v"(of[0][0]), "+v"(of[0][1]), "+v"(of[0][2]), "+v"(of[0][3]), "+v"(of[0][4]),
+                 "+v"(of[0][5]), "+v"(of[0][6]), "+v"(of[0][7]), "+v"(of[1][0]), "+v"(of[1][1]),
+                 "+v"(of[1][2]), "+v"(of[1][3]), "+v"(of[1][4]), "+v"(of[1][5]), "+v"(of[1][6]),
+                 "+v"(of[1][7]));
+  // delta = dO . O of the row (the two lane halves hold 64 dims each)
+  float nl[2], dl[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        part += mxk::bf2f(static_cast<uint16_t>(df[g][s][e])) * mxk::bf2f(static_cast<uint16_t>(of[g][s][e]));
+    const float delta = half_sum(part);
+    nl[g] = -lv[g] * 1.4426950408889634f;
+    dl[g] = delta;
+    if (h == 0)
+      *reinterpret_cast<float2*>(rowc + 2 * (lrow0 + 32 * g + r32)) =
+          make_float2(-lv[g] / scale, -delta);
   }
+  // Q and tile 0 landed (tiles 1 and 2 and the two rowc stores may fly)
+  asm volatile("s_waitcnt vmcnt(18)"
+               : "+a"(qf[0][0]), "+a"(qf[0][1]), "+a"(qf[0][2]), "+a"(qf[0][3]), "+a"(qf[0][4]),
+                 "+a"(qf[0][5]), "+a"(qf[0][6]), "+a"(qf[0][7]), "+a"(qf[1][0]), "+a"(qf[1][1]),
+                 "+a"(qf[1][2]), "+a"(qf[1][3]), "+a"(qf[1][4]), "+a"(qf[1][5]), "+a"(qf[1][6]),
+                 "+a"(qf[1][7])
+               :
+               : "memory");
   __builtin_amdgcn_s_barrier();
 
   // ---- LDS read offsets: K / V rows r32 (+ 8 KiB for the step's key half),
