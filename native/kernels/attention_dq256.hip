@@ -175,25 +175,41 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   const uint32_t k_step = static_cast<uint32_t>(KT * k_tok * 2);
   const uint32_t v_step = static_cast<uint32_t>(KT * v_tok * 2);
   const uint32_t sm32 = mxk::lds_addr32(smem);
+  // piece i (0..7) of tile t: K (i even) or V (i odd) rows 4 (4 wave + i / 2)
+  // .. + 3.  No s_nop in front (mxk::dma16m opens with one for VALU-written
+  // descriptor / offset SGPRs; here every one is SALU-made, which
+  // tests/test_isa_hazards.py's valu_sgpr_to_vmem audits)
+  auto issue_piece = [&](int t, int i) {
+    const int p = i >> 1;
+    uint32_t d0 = sm32 + (t % QNSLOT) * QSLOT + (4 * wave + p) * 1024 + (i & 1) * TILE_BYTES;
+    asm volatile("" : "+s"(d0));
+    const uint32_t ch16 = static_cast<uint32_t>((cbase ^ p) << 4);
+    const uint32_t voff = (i & 1) ? vrow0 + static_cast<uint32_t>(p * 4 * v_tok * 2) + ch16
+                                  : krow0 + static_cast<uint32_t>(p * 4 * k_tok * 2) + ch16;
+    const uint32_t soff = (i & 1) ? t * v_step : t * k_step;
+    if (i & 1)
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
+                   :
+                   : "v"(voff), "s"(rv), "s"(soff), "{m0}"(d0)
+                   : "memory");
+    else
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
+                   :
+                   : "v"(voff), "s"(rk), "s"(soff), "{m0}"(d0)
+                   : "memory");
+  };
   auto issue = [&](int t) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      uint32_t d0 = sm32 + (t % QNSLOT) * QSLOT + (4 * wave + p) * 1024;
-      asm volatile("" : "+s"(d0));
-      const uint32_t ch16 = static_cast<uint32_t>((cbase ^ p) << 4);
-      mxk::dma16m(rk, d0, krow0 + static_cast<uint32_t>(p * 4 * k_tok * 2) + ch16, t * k_step);
-      mxk::dma16m(rv, d0 + TILE_BYTES, vrow0 + static_cast<uint32_t>(p * 4 * v_tok * 2) + ch16,
-                  t * v_step);
-    }
+    for (int i = 0; i < 8; ++i) issue_piece(t, i);
   };
   // ---- per-row operands (lane: row q0 + 32 g + r32, dims 16 s + 8 h .. + 7),
   // every load in flight at once: asm loads, dO and Q straight into AGPRs
   // (their home as MFMA B operands), O and lse into VGPRs, then K / V tiles
-  // 0-2.  Compiler-visible loads came out in four dependent batches under
-  // the VGPR pressure of the 192 registers they fill: four memory round
-  // trips, 24 % of the kernel's cycles (profiles/r6_dq256/).  Tiles 1 and 2
-  // are issued whatever T is (a block with fewer tiles never reads them;
-  // past S a buffer load returns zeros), so every count below is constant.
+  // 0 and 1.  Compiler-visible loads came out in four dependent batches
+  // under the VGPR pressure of the 192 registers they fill: four memory round
+  // trips, 24 % of the kernel's cycles (profiles/r6_dq256/).  Tile t + 2 is
+  // issued during tile t whatever T is (a block with fewer tiles never reads
+  // it; past S a buffer load returns zeros), so every count is constant.
   bf16x8_t qf[2][8], df[2][8], of[2][8];
   float lv[2];
 #pragma unroll
@@ -228,10 +244,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
                    : "memory");
   issue(0);
   issue(1);
-  issue(2);
-  // dO, O, lse landed (Q's 16 and the 24 DMA pieces may fly); the operands
+  // dO, O, lse landed (Q's 16 and the 16 DMA pieces may fly); the operands
   // are redefined behind the wait so no use moves above it
-  asm volatile("s_waitcnt vmcnt(40)"
+  asm volatile("s_waitcnt vmcnt(32)"
                : "+a"(df[0][0]), "+a"(df[0][1]), "+a"(df[0][2]), "+a"(df[0][3]), "+a"(df[0][4]),
                  "+a"(df[0][5]), "+a"(df[0][6]), "+a"(df[0][7]), "+a"(df[1][0]), "+a"(df[1][1]),
                  "+a"(df[1][2]), "+a"(df[1][3]), "+a"(df[1][4]), "+a"(df[1][5]), "+a"(df[1][6]),
@@ -258,8 +273,8 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
       *reinterpret_cast<float2*>(rowc + 2 * (lrow0 + 32 * g + r32)) =
           make_float2(-lv[g] / scale, -delta);
   }
-  // Q and tile 0 landed (tiles 1 and 2 and the two rowc stores may fly)
-  asm volatile("s_waitcnt vmcnt(18)"
+  // Q and tile 0 landed (tile 1 and the two rowc stores may fly)
+  asm volatile("s_waitcnt vmcnt(10)"
                : "+a"(qf[0][0]), "+a"(qf[0][1]), "+a"(qf[0][2]), "+a"(qf[0][3]), "+a"(qf[0][4]),
                  "+a"(qf[0][5]), "+a"(qf[0][6]), "+a"(qf[0][7]), "+a"(qf[1][0]), "+a"(qf[1][1]),
                  "+a"(qf[1][2]), "+a"(qf[1][3]), "+a"(qf[1][4]), "+a"(qf[1][5]), "+a"(qf[1][6]),
@@ -353,7 +368,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   // 0..23.  PRE: the s = 0 operands are in pre_k / pre_v.  NEXTB (non-null):
   // read the first two operands of the phase B that follows from there.
   auto phaseA = [&](auto par_c, const char* kt, int j, auto mask_c, auto pre_c,
-                    const char* nextb) {
+                    const char* nextb, int dma_t) {
     constexpr int PA = decltype(par_c)::value;
     constexpr bool PRE = decltype(pre_c)::value;
     using prv = std::integral_constant<int, PA ^ 1>;
@@ -369,6 +384,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       bf16x8_t nk = ka, nv = va;
+      // DMA_T >= 0: one piece of that tile per k-step (8 pieces): spread
+      // over the phase instead of a burst behind the tile's barrier
+      if (dma_t >= 0) issue_piece(dma_t, s);
       if (s < 7) {
         nk = lds_b128(kt + koff[s + 1]);
         nv = lds_b128(kt + TILE_BYTES + koff[s + 1]);
@@ -459,12 +477,16 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     // step 2t: A(2t) beside softmax(2t-1, g1) (never diagonal); B(2t-1)
     // beside softmax(2t, g0)
     using T_ = std::true_type;
-    phaseA(P0{}, cur, 2 * t, F{}, F{}, prv + 32 * 256);
+    // tile t + 2's DMA during phase A(2t): its slot's tile t - 2 was last
+    // read in step 2t - 2, before the barrier that ended tile t - 1
+    // (the causal block's last tile has no next tile to move: none, which
+    // also keeps hipcc from computing the DMA's SGPR operands in VGPRs there)
+    phaseA(P0{}, cur, 2 * t, F{}, F{}, prv + 32 * 256, decltype(mask_c)::value ? -1 : t + 2);
     stamp(1);
     phaseB(P1{}, prv + 32 * 256, 2 * t, mask_c, T_{}, cur + 32 * 256);
     stamp(2);
     // step 2t+1: A(2t+1) beside softmax(2t, g1); B(2t) beside softmax(2t+1, g0)
-    phaseA(P1{}, cur + 32 * 256, 2 * t + 1, mask_c, T_{}, cur);
+    phaseA(P1{}, cur + 32 * 256, 2 * t + 1, mask_c, T_{}, cur, -1);
     stamp(1);
     phaseB(P0{}, cur, 2 * t + 1, mask_c, T_{}, nullptr);
     stamp(2);
@@ -476,13 +498,10 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     asm volatile("s_nop 7\n\ts_nop 4"
                  : "+a"(dqa[0][0]), "+a"(dqa[0][1]), "+a"(dqa[0][2]), "+a"(dqa[0][3]),
                    "+a"(dqa[1][0]), "+a"(dqa[1][1]), "+a"(dqa[1][2]), "+a"(dqa[1][3]));
-    // barrier: tile t+1 landed (own pieces; tile t+2's 8 may fly), every
-    // wave past B(2t-1) - the last reader of tile t-1's slot - then tile
-    // t+3's DMA into that slot
-    if (t + 2 < T) vmw<8>();
-    else vmw<0>();
+    // barrier: tile t+1 landed (own pieces; tile t+2's 8 may fly) and
+    // every wave past B(2t-1), the last reader of tile t-1's slot
+    vmw<8>();
     __builtin_amdgcn_s_barrier();
-    if (t + 3 < T) issue(t + 3);
     stamp(3);
   };
   stamp(0);
@@ -503,6 +522,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     phaseB(std::integral_constant<int, 1>{}, kt, j + 1, std::false_type{}, std::false_type{},
            nullptr);
   }
+  // the DMA of tiles past the block (T and T + 1) must land before the
+  // workgroup ends and its LDS goes to another one
+  vmw<0>();
   // dQ^T final: drain the asm MFMAs before the accumulators are read
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll

@@ -223,7 +223,7 @@ def test_dq256_prologue_loads_untouched_before_their_wait(tmp_path):
     in flight at once); nothing may read or copy their destinations before
     the counted wait."""
     asm = _asm("attention_dq256.hip", str(tmp_path / "d.s"), ("-fno-slp-vectorize",))
-    assert asm_load_dests_touched(asm, "mxk_attn_bwd_dq256_kernel", "s_waitcnt vmcnt(40)") == []
+    assert asm_load_dests_touched(asm, "mxk_attn_bwd_dq256_kernel", "s_waitcnt vmcnt(32)") == []
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
