@@ -117,15 +117,24 @@ __device__ __forceinline__ uint32_t pk2(float lo, float hi) { return mxk::pack2b
 // (mxk_attn_bwd_dq256_stamps): each wave adds up the shader cycles of its
 // prologue, phases A, phases B, barrier segments and tail, and writes them
 // with its total to stamps[wave id][6]
-template <bool CAUSAL, int DBG = 0, bool STAMP = false>
+//
+// PERSIST: one workgroup per CU loops over the (quad, row block) items in a
+// static schedule (dq256_item: on each XCD, round n hands its 32 workgroups
+// the 32 row blocks of one KV group, heaviest-first on even rounds and
+// lightest-first on odd ones, so every workgroup's causal work sums to the
+// same), and three tiles before the end of an item it pulls the next item's
+// Q / dO / O rows into L2 (one dword per 128-B line, LDS-DMA into a sink):
+// the item prologue then reads L2 instead of waiting on HBM with four waves
+// of memory parallelism (24 % of the non-persistent kernel's cycles).
+template <bool CAUSAL, int DBG = 0, bool STAMP = false, bool PERSIST = false>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                           const uint16_t* __restrict__ v, const uint16_t* __restrict__ o,
                           const uint16_t* __restrict__ dout, const float* __restrict__ lse,
                           uint16_t* __restrict__ dq, float* __restrict__ rowc, int S, int Hq,
                           int Hkv, long q_tok, long k_tok, long v_tok, float scale,
-                          unsigned long long* __restrict__ stamps = nullptr) {
-  __shared__ __attribute__((aligned(16))) char smem[QLDS];
+                          unsigned long long* __restrict__ stamps = nullptr, int nitems = 0) {
+  __shared__ __attribute__((aligned(16))) char smem[QLDS + 4 * 256];   // ring | prefetch sinks
   unsigned long long st_0 = 0, st_c = 0, st_seg[5] = {0, 0, 0, 0, 0};
   if constexpr (STAMP) st_0 = st_c = __builtin_readcyclecounter();
   // segment e (0 prologue, 1 phase A, 2 phase B, 3 barrier, 4 tail) ends here
@@ -148,15 +157,41 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   const int grp = Hq / Hkv;
   const int nq4 = Hq / 4;
   const int nqb = S / QW;
-  int bq4, qb;
-  map_block_xcd(blockIdx.x, gridDim.x, nqb, grp / 4, CAUSAL, &bq4, &qb);
+  const long tokd = static_cast<long>(Hq) * D;
+  const uint32_t sm32 = mxk::lds_addr32(smem);
+  const int prow = lane >> 4, cbase = (lane & 15) ^ (prow << 2);
+  // logical item id (XCD-contiguous, as map_block_xcd's) -> (bq4, qb)
+  auto decode = [&](int L, int* bq4_, int* qb_) {
+    const int g4 = grp / 4, per = g4 * nqb;
+    const int gg = L / per, r = L - gg * per;
+    const int j = r / g4;
+    *bq4_ = gg * g4 + (r - j * g4);
+    *qb_ = CAUSAL ? nqb - 1 - j : j;
+  };
+  // item n of this (persistent) workgroup; false when it has no more
+  auto item_of = [&](int n, int* bq4_, int* qb_) -> bool {
+    const int Gd = gridDim.x, w = blockIdx.x;
+    if (Gd % 8 == 0 && nitems % Gd == 0) {
+      const int C = Gd / 8, M = nitems / 8, c = w >> 3;
+      const int L = C * n + ((n & 1) ? C - 1 - c : c);
+      if (L >= M) return false;
+      decode((w & 7) * M + L, bq4_, qb_);
+      return true;
+    }
+    const int id = w + Gd * n;
+    if (id >= nitems) return false;
+    decode(mxk::xcd_remap(id, nitems), bq4_, qb_);
+    return true;
+  };
+
+  // one (quad, row block) item; (nbq4, nqb_) the workgroup's next one (-1: none)
+  auto run_item = [&](int bq4, int qb, int nbq4, int nqb_) {
   const int b = bq4 / nq4;
   const int hq = (bq4 - b * nq4) * 4 + wave;
   const int hkv = hq / grp;                    // the same for the 4 waves
   const int q0 = qb * QW;
 
   const uint16_t* qh = q + static_cast<long>(b) * S * q_tok + static_cast<long>(hq) * D;
-  const long tokd = static_cast<long>(Hq) * D;
   const uint16_t* doh = dout + static_cast<long>(b) * S * tokd + static_cast<long>(hq) * D;
   const uint16_t* oh = o + static_cast<long>(b) * S * tokd + static_cast<long>(hq) * D;
   const uint16_t* kb_ptr = k + static_cast<long>(b) * S * k_tok + static_cast<long>(hkv) * D;
@@ -169,12 +204,10 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   // each; lane i at row 4 g + (i >> 4), chunk (i & 15) ^ swizzle(row))
   const mxk::u32x4 rk = mxk::make_rsrc(kb_ptr, static_cast<unsigned>(S * k_tok * 2));
   const mxk::u32x4 rv = mxk::make_rsrc(vb_ptr, static_cast<unsigned>(S * v_tok * 2));
-  const int prow = lane >> 4, cbase = (lane & 15) ^ (prow << 2);
   const uint32_t krow0 = static_cast<uint32_t>((16 * wave + prow) * k_tok * 2);
   const uint32_t vrow0 = static_cast<uint32_t>((16 * wave + prow) * v_tok * 2);
   const uint32_t k_step = static_cast<uint32_t>(KT * k_tok * 2);
   const uint32_t v_step = static_cast<uint32_t>(KT * v_tok * 2);
-  const uint32_t sm32 = mxk::lds_addr32(smem);
   // piece i (0..7) of tile t: K (i even) or V (i odd) rows 4 (4 wave + i / 2)
   // .. + 3.  No s_nop in front (mxk::dma16m opens with one for VALU-written
   // descriptor / offset SGPRs; here every one is SALU-made, which
@@ -202,6 +235,30 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
 #pragma unroll
     for (int i = 0; i < 8; ++i) issue_piece(t, i);
   };
+  // the next item's Q / dO / O rows of this wave's head into L2: 3 x 64
+  // rows x 2 lines of 128 B, one dword each, 6 LDS-DMA loads into the wave's
+  // 256-B sink (never read)
+  auto prefetch_next = [&]() {
+    if (!PERSIST || nbq4 < 0) return;
+    const int nb = nbq4 / nq4, nh = (nbq4 - nb * nq4) * 4 + wave, nr0 = nqb_ * QW;
+    const uint16_t* bases[3] = {q + (static_cast<long>(nb) * S + nr0) * q_tok + static_cast<long>(nh) * D,
+                                dout + (static_cast<long>(nb) * S + nr0) * tokd + static_cast<long>(nh) * D,
+                                o + (static_cast<long>(nb) * S + nr0) * tokd + static_cast<long>(nh) * D};
+    const long strides[3] = {q_tok, tokd, tokd};
+    uint32_t sink = sm32 + QLDS + wave * 256;
+    asm volatile("" : "+s"(sink));
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+      const int tsr = m >> 1;
+      const int line = (m & 1) * 64 + lane;           // 0..127: row line >> 1, half line & 1
+      const mxk::u32x4 rs = mxk::make_rsrc(bases[tsr], static_cast<unsigned>(QW * strides[tsr] * 2));
+      const uint32_t voff = static_cast<uint32_t>((line >> 1) * strides[tsr] * 2 + (line & 1) * 128);
+      asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, 0 offen lds"
+                   :
+                   : "v"(voff), "s"(rs), "{m0}"(sink)
+                   : "memory");
+    }
+  };
   // ---- per-row operands (lane: row q0 + 32 g + r32, dims 16 s + 8 h .. + 7),
   // every load in flight at once: asm loads, dO and Q straight into AGPRs
   // (their home as MFMA B operands), O and lse into VGPRs, then K / V tiles
@@ -210,6 +267,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   // trips, 24 % of the kernel's cycles (profiles/r6_dq256/).  Tile t + 2 is
   // issued during tile t whatever T is (a block with fewer tiles never reads
   // it; past S a buffer load returns zeros), so every count is constant.
+  // a previous item's tail may still read its last tile's slot in another
+  // wave: every wave past it before this item's tiles 0 / 1 land
+  if (PERSIST) __builtin_amdgcn_s_barrier();
   bf16x8_t qf[2][8], df[2][8], of[2][8];
   float lv[2];
 #pragma unroll
@@ -368,11 +428,14 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   // 0..23.  PRE: the s = 0 operands are in pre_k / pre_v.  NEXTB (non-null):
   // read the first two operands of the phase B that follows from there.
   auto phaseA = [&](auto par_c, const char* kt, int j, auto mask_c, auto pre_c,
-                    const char* nextb, int dma_t) {
+                    const char* nextb, int dma_t, bool pf = false) {
     constexpr int PA = decltype(par_c)::value;
     constexpr bool PRE = decltype(pre_c)::value;
     using prv = std::integral_constant<int, PA ^ 1>;
     const int lim = lim_of(j - 1, 1);
+    // the L2 prefetch goes out ahead of this phase's DMA pieces: the tile's
+    // barrier (vmcnt 8: the pieces may fly) then also covers it
+    if (pf) prefetch_next();
     qd_ready(qf, df);
     bf16x8_t ka = PRE ? pre_k : lds_b128(kt + koff[0]);
     bf16x8_t va = PRE ? pre_v : lds_b128(kt + TILE_BYTES + koff[0]);
@@ -481,7 +544,8 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     // read in step 2t - 2, before the barrier that ended tile t - 1
     // (the causal block's last tile has no next tile to move: none, which
     // also keeps hipcc from computing the DMA's SGPR operands in VGPRs there)
-    phaseA(P0{}, cur, 2 * t, F{}, F{}, prv + 32 * 256, decltype(mask_c)::value ? -1 : t + 2);
+    phaseA(P0{}, cur, 2 * t, F{}, F{}, prv + 32 * 256, decltype(mask_c)::value ? -1 : t + 2,
+           t == (T > 3 ? T - 3 : 0));
     stamp(1);
     phaseB(P1{}, prv + 32 * 256, 2 * t, mask_c, T_{}, cur + 32 * 256);
     stamp(2);
@@ -547,6 +611,23 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
         *reinterpret_cast<uint2*>(dr + 32 * db + 8 * rg + 4 * h) = pk;
       }
   }
+  };   // run_item
+
+  if constexpr (PERSIST) {
+    int bq4, qb, nbq4 = -1, nqb_ = -1;
+    bool have = item_of(0, &bq4, &qb);
+    for (int n = 0; have; ++n) {
+      const bool more = item_of(n + 1, &nbq4, &nqb_);
+      run_item(bq4, qb, more ? nbq4 : -1, more ? nqb_ : -1);
+      bq4 = nbq4;
+      qb = nqb_;
+      have = more;
+    }
+  } else {
+    int bq4, qb;
+    map_block_xcd(blockIdx.x, gridDim.x, nqb, grp / 4, CAUSAL, &bq4, &qb);
+    run_item(bq4, qb, -1, -1);
+  }
   if constexpr (STAMP) {
     stamp(4);
     if (lane == 0) {
@@ -557,6 +638,41 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     }
   }
 }
+
+#include <atomic>
+#include <cstdlib>
+
+namespace {
+// MXK_DQ256_PERSIST: 1 (default) one persistent workgroup per CU, 0 one
+// workgroup per item (A/B)
+std::atomic<int> g_dq256_persist{-1};
+int dq256_persist() {
+  int v = g_dq256_persist.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("MXK_DQ256_PERSIST");
+    v = e ? std::atoi(e) : 1;
+    g_dq256_persist.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+// grid of the persistent launch (one workgroup per CU, never more than the
+// items), 0 for the one-workgroup-per-item launch
+int dq256_persistent_grid(int nitems) {
+  if (!dq256_persist()) return 0;
+  static std::atomic<int> cus{0};
+  int n = cus.load(std::memory_order_relaxed);
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus.store(n, std::memory_order_relaxed);
+  }
+  return nitems < n ? nitems : n;
+}
+}  // namespace
+
+MXK_API void mxk_attn_dq256_set_persist(int v) { g_dq256_persist.store(v); }
 
 // dQ of backward variant 9 (+ the rowc pairs for mxk_attn_bwd_dkdv256).
 // Returns a HIP status; hipErrorInvalidValue for a layout it does not take.
@@ -579,6 +695,18 @@ MXK_API int mxk_attn_bwd_dq256(const void* q, const void* k, const void* v, cons
   const auto* O = static_cast<const uint16_t*>(o);
   const auto* dO = static_cast<const uint16_t*>(dout);
   auto* dQ = static_cast<uint16_t*>(dq);
+  const int pg = dq256_persistent_grid(nwg);
+  if (pg > 0) {
+    if (causal)
+      hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<true, 0, false, true>), dim3(pg), dim3(256), 0,
+                         stream, Q, K, V, O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale,
+                         nullptr, nwg);
+    else
+      hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<false, 0, false, true>), dim3(pg), dim3(256), 0,
+                         stream, Q, K, V, O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale,
+                         nullptr, nwg);
+    MXK_RETURN_LAUNCH_STATUS();
+  }
   if (causal)
     hipLaunchKernelGGL(mxk_attn_bwd_dq256_kernel<true>, dim3(nwg), dim3(256), 0, stream, Q, K, V, O,
                        dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
@@ -624,10 +752,18 @@ MXK_API int mxk_attn_bwd_dq256_stamps(const void* q, const void* k, const void* 
   if (B < 1 || S < QW || S % QW || Hkv < 1 || Hq % Hkv || (Hq / Hkv) % 4 || !stamps)
     return static_cast<int>(hipErrorInvalidValue);
   const int nwg = B * (Hq / 4) * (S / QW);
-  hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<true, 0, true>), dim3(nwg), dim3(256), 0, stream,
-                     static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k),
-                     static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o),
-                     static_cast<const uint16_t*>(dout), lse, static_cast<uint16_t*>(dq), rowc, S,
-                     Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps);
+  const int pg = dq256_persistent_grid(nwg);
+  if (pg > 0)
+    hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<true, 0, true, true>), dim3(pg), dim3(256), 0,
+                       stream, static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k),
+                       static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o),
+                       static_cast<const uint16_t*>(dout), lse, static_cast<uint16_t*>(dq), rowc, S,
+                       Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps, nwg);
+  else
+    hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<true, 0, true>), dim3(nwg), dim3(256), 0, stream,
+                       static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k),
+                       static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o),
+                       static_cast<const uint16_t*>(dout), lse, static_cast<uint16_t*>(dq), rowc, S,
+                       Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps);
   MXK_RETURN_LAUNCH_STATUS();
 }
