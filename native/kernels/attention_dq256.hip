@@ -135,9 +135,11 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
                           int Hkv, long q_tok, long k_tok, long v_tok, float scale,
                           unsigned long long* __restrict__ stamps = nullptr, int nitems = 0) {
   __shared__ __attribute__((aligned(16))) char smem[QLDS + 4 * 256];   // ring | prefetch sinks
-  unsigned long long st_0 = 0, st_c = 0, st_seg[5] = {0, 0, 0, 0, 0};
+  unsigned long long st_0 = 0, st_c = 0, st_seg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if constexpr (STAMP) st_0 = st_c = __builtin_readcyclecounter();
-  // segment e (0 prologue, 1 phase A, 2 phase B, 3 barrier, 4 tail) ends here
+  // segment e ends here: 0 prologue (offsets, zeroing), 1 phase A, 2 phase
+  // B, 3 barrier, 4 tail + dQ store, 5 prologue load issue, 6 wait for dO /
+  // O, 7 delta + rowc + wait for Q / tile 0 + barrier
   auto stamp = [&](int e) {
     if constexpr (STAMP) {
       const unsigned long long t = __builtin_readcyclecounter();
@@ -304,6 +306,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
                    : "memory");
   issue(0);
   issue(1);
+  stamp(5);
   // dO, O, lse landed (Q's 16 and the 16 DMA pieces may fly); the operands
   // are redefined behind the wait so no use moves above it
   asm volatile("s_waitcnt vmcnt(32)"
@@ -316,6 +319,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
                  "+v"(of[0][5]), "+v"(of[0][6]), "+v"(of[0][7]), "+v"(of[1][0]), "+v"(of[1][1]),
                  "+v"(of[1][2]), "+v"(of[1][3]), "+v"(of[1][4]), "+v"(of[1][5]), "+v"(of[1][6]),
                  "+v"(of[1][7]));
+  stamp(6);
   // delta = dO . O of the row (the two lane halves hold 64 dims each)
   float nl[2], dl[2];
 #pragma unroll
@@ -342,6 +346,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
                :
                : "memory");
   __builtin_amdgcn_s_barrier();
+  stamp(7);
 
   // ---- LDS read offsets: K / V rows r32 (+ 8 KiB for the step's key half),
   // chunk 2 s + h; K^T transposed reads at keys tr_key (+8) of k-step kk
@@ -611,6 +616,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
         *reinterpret_cast<uint2*>(dr + 32 * db + 8 * rg + 4 * h) = pk;
       }
   }
+  stamp(4);
   };   // run_item
 
   if constexpr (PERSIST) {
@@ -629,12 +635,11 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     run_item(bq4, qb, -1, -1);
   }
   if constexpr (STAMP) {
-    stamp(4);
     if (lane == 0) {
-      unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 6;
+      unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 9;
       w[0] = __builtin_readcyclecounter() - st_0;
 #pragma unroll
-      for (int e = 0; e < 5; ++e) w[1 + e] = st_seg[e];
+      for (int e = 0; e < 8; ++e) w[1 + e] = st_seg[e];
     }
   }
 }
@@ -742,8 +747,8 @@ MXK_API int mxk_attn_bwd_dq256_dbg(const void* q, const void* k, const void* v, 
 }
 
 // Diagnostic: mxk_attn_bwd_dq256 (causal) with per-wave segment cycle counts,
-// stamps: [B * Hq / 4 * S / 64 workgroups][4 waves][total, prologue, A, B,
-// barrier, tail]
+// stamps: [workgroups of the launch][4 waves][total, the 8 segments of the
+// kernel's stamp()]
 MXK_API int mxk_attn_bwd_dq256_stamps(const void* q, const void* k, const void* v, const void* o,
                                       const void* dout, const float* lse, void* dq, float* rowc,
                                       int B, int S, int Hq, int Hkv, long q_tok, long k_tok,

@@ -27,7 +27,7 @@ scale = 1 / math.sqrt(D)
 dq = torch.empty_like(q)
 rowc = torch.empty(B, Hq, S, 2, device=dev)
 nwg = B * (Hq // 4) * (S // 64)
-st = torch.zeros(nwg * 4 * 6, dtype=torch.int64, device=dev)
+st = torch.zeros(nwg * 4 * 9, dtype=torch.int64, device=dev)
 L = _lib.lib()
 for _ in range(3):
     rc = L.mxk_attn_bwd_dq256_stamps(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
@@ -36,14 +36,16 @@ for _ in range(3):
                                      st.data_ptr(), _lib.stream_ptr(dev))
     assert rc == 0, rc
 torch.cuda.synchronize()
-x = st.view(nwg, 4, 6).double().cpu()
+x = st.view(nwg, 4, 9).double().cpu()
+x = x[x[:, 0, 0] > 0]          # the persistent launch fills one row per CU
 # steps per workgroup: the work order is XCD-remapped, so derive it from the
 # stamps' own phase-A count is not possible; sum over the grid instead
 steps = B * (Hq // 4) * sum(2 * (qb + 1) for qb in range(S // 64))
 tot = x.sum(dim=(0, 1))
-names = ["total", "prologue", "phase A", "phase B", "barrier+dma", "tail"]
+names = ["total", "prologue rest", "phase A", "phase B", "barrier", "tail+store",
+         "load issue", "wait dO/O", "delta+wait Q"]
 print(f"workgroups {nwg}, 32-key steps {steps} (x4 waves)")
-for i, n in enumerate(names):
+for i, n in enumerate(names[:9]):
     print(f"  {n:12s} {tot[i].item() / (4 * steps):9.1f} cycles per step per wave   "
           f"({100 * tot[i].item() / tot[0].item():5.1f} %)")
 wt = x[:, :, 0]
