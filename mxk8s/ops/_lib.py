@@ -89,7 +89,6 @@ _SIGNATURES = {
                                 _f, _i, _vp]),
     "mxk_attn_bwd_dq256_dbg": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _l, _l,
                                     _l, _f, _i, _vp]),
-    "mxk_attn_dq256_set_persist": (None, [_i]),
     "mxk_attn_bwd_dq256_stamps": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _l, _l,
                                        _l, _f, _vp, _vp]),
     "mxk_attn_bwd_variant": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i,

@@ -118,23 +118,20 @@ __device__ __forceinline__ uint32_t pk2(float lo, float hi) { return mxk::pack2b
 // prologue, phases A, phases B, barrier segments and tail, and writes them
 // with its total to stamps[wave id][6]
 //
-// PERSIST: one workgroup per CU loops over the (quad, row block) items in a
-// static schedule (dq256_item: on each XCD, round n hands its 32 workgroups
-// the 32 row blocks of one KV group, heaviest-first on even rounds and
-// lightest-first on odd ones, so every workgroup's causal work sums to the
-// same), and three tiles before the end of an item it pulls the next item's
-// Q / dO / O rows into L2 (one dword per 128-B line, LDS-DMA into a sink):
-// the item prologue then reads L2 instead of waiting on HBM with four waves
-// of memory parallelism (24 % of the non-persistent kernel's cycles).
-template <bool CAUSAL, int DBG = 0, bool STAMP = false, bool PERSIST = false>
+// (A persistent form - one workgroup per CU looping over heavy / light
+// paired row blocks, with an L2 prefetch of the next block's Q / dO / O -
+// measured within 0.2 % of this launch, 1.0275 vs 1.0293 ms per layer
+// backward, and spilled once the prologue staged through LDS; not kept,
+// profiles/r6_dq256/.)
+template <bool CAUSAL, int DBG = 0, bool STAMP = false>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                           const uint16_t* __restrict__ v, const uint16_t* __restrict__ o,
                           const uint16_t* __restrict__ dout, const float* __restrict__ lse,
                           uint16_t* __restrict__ dq, float* __restrict__ rowc, int S, int Hq,
                           int Hkv, long q_tok, long k_tok, long v_tok, float scale,
-                          unsigned long long* __restrict__ stamps = nullptr, int nitems = 0) {
-  __shared__ __attribute__((aligned(16))) char smem[QLDS + 4 * 256];   // ring | prefetch sinks
+                          unsigned long long* __restrict__ stamps = nullptr) {
+  __shared__ __attribute__((aligned(16))) char smem[QLDS];
   unsigned long long st_0 = 0, st_c = 0, st_seg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if constexpr (STAMP) st_0 = st_c = __builtin_readcyclecounter();
   // segment e ends here: 0 prologue (offsets, zeroing), 1 phase A, 2 phase
@@ -162,32 +159,8 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   const long tokd = static_cast<long>(Hq) * D;
   const uint32_t sm32 = mxk::lds_addr32(smem);
   const int prow = lane >> 4, cbase = (lane & 15) ^ (prow << 2);
-  // logical item id (XCD-contiguous, as map_block_xcd's) -> (bq4, qb)
-  auto decode = [&](int L, int* bq4_, int* qb_) {
-    const int g4 = grp / 4, per = g4 * nqb;
-    const int gg = L / per, r = L - gg * per;
-    const int j = r / g4;
-    *bq4_ = gg * g4 + (r - j * g4);
-    *qb_ = CAUSAL ? nqb - 1 - j : j;
-  };
-  // item n of this (persistent) workgroup; false when it has no more
-  auto item_of = [&](int n, int* bq4_, int* qb_) -> bool {
-    const int Gd = gridDim.x, w = blockIdx.x;
-    if (Gd % 8 == 0 && nitems % Gd == 0) {
-      const int C = Gd / 8, M = nitems / 8, c = w >> 3;
-      const int L = C * n + ((n & 1) ? C - 1 - c : c);
-      if (L >= M) return false;
-      decode((w & 7) * M + L, bq4_, qb_);
-      return true;
-    }
-    const int id = w + Gd * n;
-    if (id >= nitems) return false;
-    decode(mxk::xcd_remap(id, nitems), bq4_, qb_);
-    return true;
-  };
-
-  // one (quad, row block) item; (nbq4, nqb_) the workgroup's next one (-1: none)
-  auto run_item = [&](int bq4, int qb, int nbq4, int nqb_) {
+  // one (quad, row block) item
+  auto run_item = [&](int bq4, int qb) {
   const int b = bq4 / nq4;
   const int hq = (bq4 - b * nq4) * 4 + wave;
   const int hkv = hq / grp;                    // the same for the 4 waves
@@ -216,7 +189,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   // tests/test_isa_hazards.py's valu_sgpr_to_vmem audits)
   auto issue_piece = [&](int t, int i) {
     const int p = i >> 1;
-    uint32_t d0 = sm32 + (t % QNSLOT) * QSLOT + (4 * wave + p) * 1024 + (i & 1) * TILE_BYTES;
+    uint32_t d0 = sm32 + ((t + 2) & 3) * QSLOT + (4 * wave + p) * 1024 + (i & 1) * TILE_BYTES;
     asm volatile("" : "+s"(d0));
     const uint32_t ch16 = static_cast<uint32_t>((cbase ^ p) << 4);
     const uint32_t voff = (i & 1) ? vrow0 + static_cast<uint32_t>(p * 4 * v_tok * 2) + ch16
@@ -237,123 +210,100 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
 #pragma unroll
     for (int i = 0; i < 8; ++i) issue_piece(t, i);
   };
-  // the next item's Q / dO / O rows of this wave's head into L2: 3 x 64
-  // rows x 2 lines of 128 B, one dword each, 6 LDS-DMA loads into the wave's
-  // 256-B sink (never read)
-  auto prefetch_next = [&]() {
-    if (!PERSIST || nbq4 < 0) return;
-    const int nb = nbq4 / nq4, nh = (nbq4 - nb * nq4) * 4 + wave, nr0 = nqb_ * QW;
-    const uint16_t* bases[3] = {q + (static_cast<long>(nb) * S + nr0) * q_tok + static_cast<long>(nh) * D,
-                                dout + (static_cast<long>(nb) * S + nr0) * tokd + static_cast<long>(nh) * D,
-                                o + (static_cast<long>(nb) * S + nr0) * tokd + static_cast<long>(nh) * D};
-    const long strides[3] = {q_tok, tokd, tokd};
-    uint32_t sink = sm32 + QLDS + wave * 256;
-    asm volatile("" : "+s"(sink));
+  // ---- per-row operands, staged through LDS by full-row LDS-DMA (the
+  // K-tile piece mapping, swizzled images): as direct loads in the MFMA
+  // fragment layout every load instruction touched 32 B of 32 rows, and
+  // just issuing the 50 loads took 21 % of the kernel's cycles - the
+  // vector-memory path, not HBM, was the limit (an L2 prefetch of the next
+  // item changed nothing; profiles/r6_dq256/).  Each wave moves its own
+  // head's 64 rows (16 KiB a tensor) into its own region, so only the K / V
+  // tiles need the barrier:
+  //   1. dO -> region A_w (slots 0-1 area), O -> region B_w (slots 2-3 area)
+  //   2. dO fragments -> AGPRs, O fragments -> VGPRs; Q -> region A_w
+  //   3. delta, rowc; barrier (every wave done with its B region) ->
+  //      K / V tiles 0, 1 into slots 2, 3 (tile t lives in slot (t + 2) & 3)
+  //   4. Q fragments -> AGPRs; tile 0 landed; barrier
+  const uint32_t regA = sm32 + wave * 16384, regB = sm32 + 65536 + wave * 16384;
+  auto stage = [&](const uint16_t* base, long tok, uint32_t reg) {
+    const mxk::u32x4 rs = mxk::make_rsrc(base, static_cast<unsigned>(QW * tok * 2));
 #pragma unroll
-    for (int m = 0; m < 6; ++m) {
-      const int tsr = m >> 1;
-      const int line = (m & 1) * 64 + lane;           // 0..127: row line >> 1, half line & 1
-      const mxk::u32x4 rs = mxk::make_rsrc(bases[tsr], static_cast<unsigned>(QW * strides[tsr] * 2));
-      const uint32_t voff = static_cast<uint32_t>((line >> 1) * strides[tsr] * 2 + (line & 1) * 128);
-      asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, 0 offen lds"
+    for (int pc = 0; pc < 16; ++pc) {
+      uint32_t d0 = reg + pc * 1024;
+      asm volatile("" : "+s"(d0));
+      const uint32_t voff = static_cast<uint32_t>((4 * pc + prow) * tok * 2 + ((cbase ^ (pc & 3)) << 4));
+      asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
                    :
-                   : "v"(voff), "s"(rs), "{m0}"(sink)
+                   : "v"(voff), "s"(rs), "{m0}"(d0)
                    : "memory");
     }
   };
-  // ---- per-row operands (lane: row q0 + 32 g + r32, dims 16 s + 8 h .. + 7),
-  // every load in flight at once: asm loads, dO and Q straight into AGPRs
-  // (their home as MFMA B operands), O and lse into VGPRs, then K / V tiles
-  // 0 and 1.  Compiler-visible loads came out in four dependent batches
-  // under the VGPR pressure of the 192 registers they fill: four memory round
-  // trips, 24 % of the kernel's cycles (profiles/r6_dq256/).  Tile t + 2 is
-  // issued during tile t whatever T is (a block with fewer tiles never reads
-  // it; past S a buffer load returns zeros), so every count is constant.
-  // a previous item's tail may still read its last tile's slot in another
-  // wave: every wave past it before this item's tiles 0 / 1 land
-  if (PERSIST) __builtin_amdgcn_s_barrier();
-  bf16x8_t qf[2][8], df[2][8], of[2][8];
+  const uint16_t* qrow = qh + static_cast<long>(q0) * q_tok;
+  const uint16_t* dorow = doh + static_cast<long>(q0) * tokd;
+  const uint16_t* orow = oh + static_cast<long>(q0) * tokd;
   float lv[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g)
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-      asm volatile("global_load_dwordx4 %0, %1, off"
-                   : "=a"(df[g][s])
-                   : "v"(doh + static_cast<long>(q0 + 32 * g + r32) * tokd + 16 * s + 8 * h)
-                   : "memory");
-#pragma unroll
-  for (int g = 0; g < 2; ++g)
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-      asm volatile("global_load_dwordx4 %0, %1, off"
-                   : "=v"(of[g][s])
-                   : "v"(oh + static_cast<long>(q0 + 32 * g + r32) * tokd + 16 * s + 8 * h)
-                   : "memory");
 #pragma unroll
   for (int g = 0; g < 2; ++g)
     asm volatile("global_load_dword %0, %1, off"
                  : "=v"(lv[g])
                  : "v"(lse + lrow0 + 32 * g + r32)
                  : "memory");
+  stage(dorow, tokd, regA);
+  stage(orow, tokd, regB);
+  stamp(5);
+  vmw<0>();                          // own pieces (no other wave reads them)
+  asm volatile("" : "+v"(lv[0]), "+v"(lv[1]) :: "memory");
+  int koff[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) koff[s] = swz(r32, 2 * s + h);
+  const char* imA = smem + wave * 16384;
+  const char* imB = smem + 65536 + wave * 16384;
+  bf16x8_t qf[2][8], df[2][8];
+  float part[2] = {0.f, 0.f};
 #pragma unroll
   for (int g = 0; g < 2; ++g)
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
-      asm volatile("global_load_dwordx4 %0, %1, off"
-                   : "=a"(qf[g][s])
-                   : "v"(qh + static_cast<long>(q0 + 32 * g + r32) * q_tok + 16 * s + 8 * h)
-                   : "memory");
-  issue(0);
-  issue(1);
-  stamp(5);
-  // dO, O, lse landed (Q's 16 and the 16 DMA pieces may fly); the operands
-  // are redefined behind the wait so no use moves above it
-  asm volatile("s_waitcnt vmcnt(32)"
-               : "+a"(df[0][0]), "+a"(df[0][1]), "+a"(df[0][2]), "+a"(df[0][3]), "+a"(df[0][4]),
-                 "+a"(df[0][5]), "+a"(df[0][6]), "+a"(df[0][7]), "+a"(df[1][0]), "+a"(df[1][1]),
-                 "+a"(df[1][2]), "+a"(df[1][3]), "+a"(df[1][4]), "+a"(df[1][5]), "+a"(df[1][6]),
-                 "+a"(df[1][7]), "+v"(lv[0]), "+v"(lv[1]));
-  asm volatile(""
-               : "+v"(of[0][0]), "+v"(of[0][1]), "+v"(of[0][2]), "+v"(of[0][3]), "+v"(of[0][4]),
-                 "+v"(of[0][5]), "+v"(of[0][6]), "+v"(of[0][7]), "+v"(of[1][0]), "+v"(of[1][1]),
-                 "+v"(of[1][2]), "+v"(of[1][3]), "+v"(of[1][4]), "+v"(of[1][5]), "+v"(of[1][6]),
-                 "+v"(of[1][7]));
+    for (int s = 0; s < 8; ++s) {
+      df[g][s] = lds_b128(imA + koff[s] + g * 8192);
+      const bf16x8_t of = lds_b128(imB + koff[s] + g * 8192);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        part[g] += mxk::bf2f(static_cast<uint16_t>(df[g][s][e])) * mxk::bf2f(static_cast<uint16_t>(of[e]));
+    }
+  // region A_w is read: Q goes there (LDS traffic retired first)
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  stage(qrow, q_tok, regA);
   stamp(6);
   // delta = dO . O of the row (the two lane halves hold 64 dims each)
   float nl[2], dl[2];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    float part = 0.f;
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        part += mxk::bf2f(static_cast<uint16_t>(df[g][s][e])) * mxk::bf2f(static_cast<uint16_t>(of[g][s][e]));
-    const float delta = half_sum(part);
+    const float delta = half_sum(part[g]);
     nl[g] = -lv[g] * 1.4426950408889634f;
     dl[g] = delta;
     if (h == 0)
       *reinterpret_cast<float2*>(rowc + 2 * (lrow0 + 32 * g + r32)) =
           make_float2(-lv[g] / scale, -delta);
   }
-  // Q and tile 0 landed (tile 1 and the two rowc stores may fly)
-  asm volatile("s_waitcnt vmcnt(10)"
-               : "+a"(qf[0][0]), "+a"(qf[0][1]), "+a"(qf[0][2]), "+a"(qf[0][3]), "+a"(qf[0][4]),
-                 "+a"(qf[0][5]), "+a"(qf[0][6]), "+a"(qf[0][7]), "+a"(qf[1][0]), "+a"(qf[1][1]),
-                 "+a"(qf[1][2]), "+a"(qf[1][3]), "+a"(qf[1][4]), "+a"(qf[1][5]), "+a"(qf[1][6]),
-                 "+a"(qf[1][7])
-               :
-               : "memory");
+  // every wave done with its O region (slots 2-3): tiles 0 and 1 go there
+  __builtin_amdgcn_s_barrier();
+  issue(0);
+  issue(1);
+  // Q (own) landed: 16 pieces of tiles 0 / 1 and the two rowc stores may fly
+  vmw<18>();
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[g][s] = lds_b128(imA + koff[s] + g * 8192);
+  // Q read (tile 2 goes into slot 0 during tile 0) and tile 0 landed
+  // (tile 1's 8 may fly; the rowc stores are older than tile 0)
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  vmw<8>();
   __builtin_amdgcn_s_barrier();
   stamp(7);
 
   // ---- LDS read offsets: K / V rows r32 (+ 8 KiB for the step's key half),
   // chunk 2 s + h; K^T transposed reads at keys tr_key (+8) of k-step kk
   // (+ 4 KiB), chunk 4 db + tr_ch
-  int koff[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) koff[s] = swz(r32, 2 * s + h);
   const int G = lane >> 4, i16 = lane & 15;
   const int tr_key = 4 * h + (i16 >> 2);
   const int tr_ch = 2 * (G & 1) + ((i16 & 3) >> 1);
@@ -433,14 +383,11 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   // 0..23.  PRE: the s = 0 operands are in pre_k / pre_v.  NEXTB (non-null):
   // read the first two operands of the phase B that follows from there.
   auto phaseA = [&](auto par_c, const char* kt, int j, auto mask_c, auto pre_c,
-                    const char* nextb, int dma_t, bool pf = false) {
+                    const char* nextb, int dma_t) {
     constexpr int PA = decltype(par_c)::value;
     constexpr bool PRE = decltype(pre_c)::value;
     using prv = std::integral_constant<int, PA ^ 1>;
     const int lim = lim_of(j - 1, 1);
-    // the L2 prefetch goes out ahead of this phase's DMA pieces: the tile's
-    // barrier (vmcnt 8: the pieces may fly) then also covers it
-    if (pf) prefetch_next();
     qd_ready(qf, df);
     bf16x8_t ka = PRE ? pre_k : lds_b128(kt + koff[0]);
     bf16x8_t va = PRE ? pre_v : lds_b128(kt + TILE_BYTES + koff[0]);
@@ -540,8 +487,8 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     using F = std::false_type;
     using P0 = std::integral_constant<int, 0>;
     using P1 = std::integral_constant<int, 1>;
-    const char* cur = smem + (t & 3) * QSLOT;
-    const char* prv = t ? smem + ((t + 3) & 3) * QSLOT : cur;
+    const char* cur = smem + ((t + 2) & 3) * QSLOT;
+    const char* prv = t ? smem + ((t + 1) & 3) * QSLOT : cur;
     // step 2t: A(2t) beside softmax(2t-1, g1) (never diagonal); B(2t-1)
     // beside softmax(2t, g0)
     using T_ = std::true_type;
@@ -549,8 +496,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     // read in step 2t - 2, before the barrier that ended tile t - 1
     // (the causal block's last tile has no next tile to move: none, which
     // also keeps hipcc from computing the DMA's SGPR operands in VGPRs there)
-    phaseA(P0{}, cur, 2 * t, F{}, F{}, prv + 32 * 256, decltype(mask_c)::value ? -1 : t + 2,
-           t == (T > 3 ? T - 3 : 0));
+    phaseA(P0{}, cur, 2 * t, F{}, F{}, prv + 32 * 256, decltype(mask_c)::value ? -1 : t + 2);
     stamp(1);
     phaseB(P1{}, prv + 32 * 256, 2 * t, mask_c, T_{}, cur + 32 * 256);
     stamp(2);
@@ -581,7 +527,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   {
     const int j = 2 * T - 1;
     const int lim = lim_of(j, 1);
-    const char* kt = smem + ((T - 1) & 3) * QSLOT + 32 * 256;
+    const char* kt = smem + ((T + 1) & 3) * QSLOT + 32 * 256;
     pre_b0 = kread(kt, 0);
     pre_b1 = kread(kt, 1);
 #pragma unroll
@@ -619,21 +565,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   stamp(4);
   };   // run_item
 
-  if constexpr (PERSIST) {
-    int bq4, qb, nbq4 = -1, nqb_ = -1;
-    bool have = item_of(0, &bq4, &qb);
-    for (int n = 0; have; ++n) {
-      const bool more = item_of(n + 1, &nbq4, &nqb_);
-      run_item(bq4, qb, more ? nbq4 : -1, more ? nqb_ : -1);
-      bq4 = nbq4;
-      qb = nqb_;
-      have = more;
-    }
-  } else {
-    int bq4, qb;
-    map_block_xcd(blockIdx.x, gridDim.x, nqb, grp / 4, CAUSAL, &bq4, &qb);
-    run_item(bq4, qb, -1, -1);
-  }
+  int bq4, qb;
+  map_block_xcd(blockIdx.x, gridDim.x, nqb, grp / 4, CAUSAL, &bq4, &qb);
+  run_item(bq4, qb);
   if constexpr (STAMP) {
     if (lane == 0) {
       unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 9;
@@ -643,41 +577,6 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     }
   }
 }
-
-#include <atomic>
-#include <cstdlib>
-
-namespace {
-// MXK_DQ256_PERSIST: 1 (default) one persistent workgroup per CU, 0 one
-// workgroup per item (A/B)
-std::atomic<int> g_dq256_persist{-1};
-int dq256_persist() {
-  int v = g_dq256_persist.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = std::getenv("MXK_DQ256_PERSIST");
-    v = e ? std::atoi(e) : 1;
-    g_dq256_persist.store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
-// grid of the persistent launch (one workgroup per CU, never more than the
-// items), 0 for the one-workgroup-per-item launch
-int dq256_persistent_grid(int nitems) {
-  if (!dq256_persist()) return 0;
-  static std::atomic<int> cus{0};
-  int n = cus.load(std::memory_order_relaxed);
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    cus.store(n, std::memory_order_relaxed);
-  }
-  return nitems < n ? nitems : n;
-}
-}  // namespace
-
-MXK_API void mxk_attn_dq256_set_persist(int v) { g_dq256_persist.store(v); }
 
 // dQ of backward variant 9 (+ the rowc pairs for mxk_attn_bwd_dkdv256).
 // Returns a HIP status; hipErrorInvalidValue for a layout it does not take.
@@ -700,18 +599,6 @@ MXK_API int mxk_attn_bwd_dq256(const void* q, const void* k, const void* v, cons
   const auto* O = static_cast<const uint16_t*>(o);
   const auto* dO = static_cast<const uint16_t*>(dout);
   auto* dQ = static_cast<uint16_t*>(dq);
-  const int pg = dq256_persistent_grid(nwg);
-  if (pg > 0) {
-    if (causal)
-      hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<true, 0, false, true>), dim3(pg), dim3(256), 0,
-                         stream, Q, K, V, O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale,
-                         nullptr, nwg);
-    else
-      hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<false, 0, false, true>), dim3(pg), dim3(256), 0,
-                         stream, Q, K, V, O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale,
-                         nullptr, nwg);
-    MXK_RETURN_LAUNCH_STATUS();
-  }
   if (causal)
     hipLaunchKernelGGL(mxk_attn_bwd_dq256_kernel<true>, dim3(nwg), dim3(256), 0, stream, Q, K, V, O,
                        dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
@@ -757,18 +644,10 @@ MXK_API int mxk_attn_bwd_dq256_stamps(const void* q, const void* k, const void* 
   if (B < 1 || S < QW || S % QW || Hkv < 1 || Hq % Hkv || (Hq / Hkv) % 4 || !stamps)
     return static_cast<int>(hipErrorInvalidValue);
   const int nwg = B * (Hq / 4) * (S / QW);
-  const int pg = dq256_persistent_grid(nwg);
-  if (pg > 0)
-    hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<true, 0, true, true>), dim3(pg), dim3(256), 0,
-                       stream, static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k),
-                       static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o),
-                       static_cast<const uint16_t*>(dout), lse, static_cast<uint16_t*>(dq), rowc, S,
-                       Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps, nwg);
-  else
-    hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<true, 0, true>), dim3(nwg), dim3(256), 0, stream,
-                       static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k),
-                       static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o),
-                       static_cast<const uint16_t*>(dout), lse, static_cast<uint16_t*>(dq), rowc, S,
-                       Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps);
+  hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<true, 0, true>), dim3(nwg), dim3(256), 0, stream,
+                     static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k),
+                     static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o),
+                     static_cast<const uint16_t*>(dout), lse, static_cast<uint16_t*>(dq), rowc, S,
+                     Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps);
   MXK_RETURN_LAUNCH_STATUS();
 }
