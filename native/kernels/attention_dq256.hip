@@ -130,8 +130,8 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
                           const uint16_t* __restrict__ dout, const float* __restrict__ lse,
                           uint16_t* __restrict__ dq, float* __restrict__ rowc, int S, int Hq,
                           int Hkv, long q_tok, long k_tok, long v_tok, float scale,
-                          unsigned long long* __restrict__ stamps = nullptr) {
-  __shared__ __attribute__((aligned(16))) char smem[QLDS];
+                          unsigned long long* __restrict__ stamps = nullptr, int succ = 0) {
+  __shared__ __attribute__((aligned(16))) char smem[QLDS + 4 * 256];   // ring | prefetch sinks
   unsigned long long st_0 = 0, st_c = 0, st_seg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if constexpr (STAMP) st_0 = st_c = __builtin_readcyclecounter();
   // segment e ends here: 0 prologue (offsets, zeroing), 1 phase A, 2 phase
@@ -159,8 +159,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   const long tokd = static_cast<long>(Hq) * D;
   const uint32_t sm32 = mxk::lds_addr32(smem);
   const int prow = lane >> 4, cbase = (lane & 15) ^ (prow << 2);
-  // one (quad, row block) item
-  auto run_item = [&](int bq4, int qb) {
+  // one (quad, row block) item; (nbq4, nqb_): the item of the workgroup
+  // `succ` ids later (-1: none), which this one prefetches
+  auto run_item = [&](int bq4, int qb, int nbq4, int nqb_) {
   const int b = bq4 / nq4;
   const int hq = (bq4 - b * nq4) * 4 + wave;
   const int hkv = hq / grp;                    // the same for the 4 waves
@@ -209,6 +210,33 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   auto issue = [&](int t) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) issue_piece(t, i);
+  };
+  // the successor's Q / dO / O rows of this wave's head into L2 / MALL: 3 x
+  // 64 rows x 2 lines of 128 B, one dword each, 6 LDS-DMA loads into the
+  // wave's 256-B sink (never read).  The successor - the workgroup `succ`
+  // (= CU count) ids later - runs on this XCD (8 | succ), about when this
+  // one ends; its prologue then streams from cache what it would have
+  // fetched from HBM with nothing else to do
+  auto prefetch_next = [&]() {
+    if (nbq4 < 0) return;
+    const int nb = nbq4 / nq4, nh = (nbq4 - nb * nq4) * 4 + wave, nr0 = nqb_ * QW;
+    const uint16_t* bases[3] = {q + (static_cast<long>(nb) * S + nr0) * q_tok + static_cast<long>(nh) * D,
+                                dout + (static_cast<long>(nb) * S + nr0) * tokd + static_cast<long>(nh) * D,
+                                o + (static_cast<long>(nb) * S + nr0) * tokd + static_cast<long>(nh) * D};
+    const long strides[3] = {q_tok, tokd, tokd};
+    uint32_t sink = sm32 + QLDS + wave * 256;
+    asm volatile("" : "+s"(sink));
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+      const int tsr = m >> 1;
+      const int line = (m & 1) * 64 + lane;          // row line >> 1, 128-B half line & 1
+      const mxk::u32x4 rs = mxk::make_rsrc(bases[tsr], static_cast<unsigned>(QW * strides[tsr] * 2));
+      const uint32_t voff = static_cast<uint32_t>((line >> 1) * strides[tsr] * 2 + (line & 1) * 128);
+      asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, 0 offen lds"
+                   :
+                   : "v"(voff), "s"(rs), "{m0}"(sink)
+                   : "memory");
+    }
   };
   // ---- per-row operands, staged through LDS by full-row LDS-DMA (the
   // K-tile piece mapping, swizzled images): as direct loads in the MFMA
@@ -383,11 +411,14 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   // 0..23.  PRE: the s = 0 operands are in pre_k / pre_v.  NEXTB (non-null):
   // read the first two operands of the phase B that follows from there.
   auto phaseA = [&](auto par_c, const char* kt, int j, auto mask_c, auto pre_c,
-                    const char* nextb, int dma_t) {
+                    const char* nextb, int dma_t, bool pf = false) {
     constexpr int PA = decltype(par_c)::value;
     constexpr bool PRE = decltype(pre_c)::value;
     using prv = std::integral_constant<int, PA ^ 1>;
     const int lim = lim_of(j - 1, 1);
+    // the successor prefetch goes out ahead of this phase's DMA pieces: the
+    // tile's barrier (vmcnt 8: only the pieces may fly) then covers it
+    if (pf) prefetch_next();
     qd_ready(qf, df);
     bf16x8_t ka = PRE ? pre_k : lds_b128(kt + koff[0]);
     bf16x8_t va = PRE ? pre_v : lds_b128(kt + TILE_BYTES + koff[0]);
@@ -496,7 +527,8 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     // read in step 2t - 2, before the barrier that ended tile t - 1
     // (the causal block's last tile has no next tile to move: none, which
     // also keeps hipcc from computing the DMA's SGPR operands in VGPRs there)
-    phaseA(P0{}, cur, 2 * t, F{}, F{}, prv + 32 * 256, decltype(mask_c)::value ? -1 : t + 2);
+    phaseA(P0{}, cur, 2 * t, F{}, F{}, prv + 32 * 256, decltype(mask_c)::value ? -1 : t + 2,
+           t == (T > 4 ? T - 4 : 0));
     stamp(1);
     phaseB(P1{}, prv + 32 * 256, 2 * t, mask_c, T_{}, cur + 32 * 256);
     stamp(2);
@@ -565,9 +597,11 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   stamp(4);
   };   // run_item
 
-  int bq4, qb;
+  int bq4, qb, nbq4 = -1, nqb_ = -1;
   map_block_xcd(blockIdx.x, gridDim.x, nqb, grp / 4, CAUSAL, &bq4, &qb);
-  run_item(bq4, qb);
+  if (succ > 0 && static_cast<int>(blockIdx.x) + succ < static_cast<int>(gridDim.x))
+    map_block_xcd(blockIdx.x + succ, gridDim.x, nqb, grp / 4, CAUSAL, &nbq4, &nqb_);
+  run_item(bq4, qb, nbq4, nqb_);
   if constexpr (STAMP) {
     if (lane == 0) {
       unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 9;
@@ -577,6 +611,32 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     }
   }
 }
+
+#include <atomic>
+#include <cstdlib>
+
+namespace {
+// the successor distance of the prefetch: the CU count (workgroups of one
+// XCD are ids congruent mod 8, so the id `CUs` later runs on the same XCD
+// about when this one ends); MXK_DQ256_PREFETCH=0 turns the prefetch off (A/B)
+int dq256_succ() {
+  static std::atomic<int> v{-1};
+  int n = v.load(std::memory_order_relaxed);
+  if (n < 0) {
+    const char* e = std::getenv("MXK_DQ256_PREFETCH");
+    n = 0;
+    if (!(e && e[0] == '0')) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+      n -= n % 8;
+    }
+    v.store(n, std::memory_order_relaxed);
+  }
+  return n;
+}
+}  // namespace
 
 // dQ of backward variant 9 (+ the rowc pairs for mxk_attn_bwd_dkdv256).
 // Returns a HIP status; hipErrorInvalidValue for a layout it does not take.
@@ -599,12 +659,13 @@ MXK_API int mxk_attn_bwd_dq256(const void* q, const void* k, const void* v, cons
   const auto* O = static_cast<const uint16_t*>(o);
   const auto* dO = static_cast<const uint16_t*>(dout);
   auto* dQ = static_cast<uint16_t*>(dq);
+  const int succ = dq256_succ();
   if (causal)
     hipLaunchKernelGGL(mxk_attn_bwd_dq256_kernel<true>, dim3(nwg), dim3(256), 0, stream, Q, K, V, O,
-                       dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+                       dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale, nullptr, succ);
   else
     hipLaunchKernelGGL(mxk_attn_bwd_dq256_kernel<false>, dim3(nwg), dim3(256), 0, stream, Q, K, V,
-                       O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale);
+                       O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale, nullptr, succ);
   MXK_RETURN_LAUNCH_STATUS();
 }
 
@@ -648,6 +709,6 @@ MXK_API int mxk_attn_bwd_dq256_stamps(const void* q, const void* k, const void* 
                      static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k),
                      static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o),
                      static_cast<const uint16_t*>(dout), lse, static_cast<uint16_t*>(dq), rowc, S,
-                     Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps);
+                     Hq, Hkv, q_tok, k_tok, v_tok, scale, stamps, dq256_succ());
   MXK_RETURN_LAUNCH_STATUS();
 }
