@@ -579,11 +579,18 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
 #pragma unroll
     for (int db = 0; db < 4; ++db) asm volatile("" : "+a"(dqa[g][db]));
 
-  // ---- dQ = scale (dQ^T)^T: lane = query row, registers 4 rg .. 4 rg + 3 ->
-  // dims 32 db + 8 rg + 4 h .. + 3 (one 8-B store each)
+  // ---- dQ = scale (dQ^T)^T, staged through LDS so every global store
+  // writes 4 whole 256-B rows (straight from the lanes each store touched 32
+  // rows with 16 B each: store-bound, 8 % of the kernel's cycles).  Lane
+  // (r32, h) holds row 32 g + r32, dims 32 db + 8 rg + 4 h .. + 3: one 8-B
+  // LDS write each into the wave's 16-KiB row-major image (16-B chunks
+  // XOR-swizzled by swz()); every wave is past its tail first (the last
+  // tile's slot may be any wave's image region).
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  char* img = smem + wave * 16384;
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    uint16_t* dr = dq + (static_cast<long>(b) * S + q0 + 32 * g + r32) * tokd + static_cast<long>(hq) * D;
+  for (int g = 0; g < 2; ++g)
 #pragma unroll
     for (int db = 0; db < 4; ++db)
 #pragma unroll
@@ -591,8 +598,17 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
         uint2 pk;
         pk.x = pk2(dqa[g][db][4 * rg] * scale, dqa[g][db][4 * rg + 1] * scale);
         pk.y = pk2(dqa[g][db][4 * rg + 2] * scale, dqa[g][db][4 * rg + 3] * scale);
-        *reinterpret_cast<uint2*>(dr + 32 * db + 8 * rg + 4 * h) = pk;
+        *reinterpret_cast<uint2*>(img + swz(32 * g + r32, 4 * db + rg) + 8 * h) = pk;
       }
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // own image: no other wave reads it
+  // lane l: chunk l & 15 of rows (l >> 4) + 4 i
+  const int crow0 = lane >> 4, cch = lane & 15;
+  uint16_t* dbase = dq + (static_cast<long>(b) * S + q0) * tokd + static_cast<long>(hq) * D + cch * 8;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = crow0 + 4 * i;
+    const uint4 x = *reinterpret_cast<const uint4*>(img + swz(row, cch));
+    *reinterpret_cast<uint4*>(dbase + static_cast<long>(row) * tokd) = x;
   }
   stamp(4);
   };   // run_item
