@@ -23,9 +23,8 @@
 //     bf16 IS the B operand of dQ^T += K^T dS^T (K^T by ds_read_b64_tr_b16
 //     from the row-major K image), no LDS round trip;
 //   * per 32-key step j two phases, each with VALU work beside its MFMAs:
-//       A(j)    S^T, dP^T of step j (32 MFMAs)   beside the rest of softmax(j-1)
-//       B(j-1)  dQ^T += K^T dS^T(j-1) (16)       beside 2/3 of softmax(j) of g0
-//     (48 single-element items a step, one per MFMA gap)
+//       A(j)    S^T, dP^T of step j (32 MFMAs)   beside softmax(j-1) of g1
+//       B(j-1)  dQ^T += K^T dS^T(j-1) (16)       beside softmax(j)   of g0
 //     (softmax: P = exp2(c S - lse log2 e), the causal mask on the two
 //     diagonal steps, dS = P (dP - delta), bf16 pairs);
 //   * K / V tiles of 64 keys by LDS-DMA into a 4-slot ring (two tiles of
@@ -354,13 +353,10 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
       for (int r = 0; r < 16; ++r) dqa[g][db][r] = 0.f;
   f32x16_t sacc[2][2], pacc[2][2];    // [step parity][g]: rows key = crow, lane = query
   bf16x8_t dsf[2][2][2];              // dS^T operands [step parity][g][k-step of 16 keys]
-  // step -1 (a no-op): the softmax items it runs in A(0) see S = -inf (P = 0,
-  // dS = 0) and the rest of its operands are zero, so B(-1) adds K^T . 0
-  // (tile 0's finite keys)
+  // step -1 (a no-op): its g1 softmax sees S = -inf (P = 0, dS = 0) and its
+  // g0 operands are zero, so B(-1) adds K^T . 0 (tile 0's finite keys)
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    sacc[1][0][r] = -INFINITY;
-    pacc[1][0][r] = 0.f;
     sacc[1][1][r] = -INFINITY;
     pacc[1][1][r] = 0.f;
   }
@@ -376,8 +372,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   // diagonal steps): key kv0 + crow(r, h) past query q0 + 32 g + r32, i.e.
   // (r & 3) + 8 (r >> 2) > lim, one compare a score.
   uint32_t dsw[2][2][2][4];           // the operands as bf16 pairs, [parity][g][kk][word]
-  float xe[2][2] = {{0.f, 0.f}, {0.f, 0.f}};   // [g]: a unit's two elements between its items
-  dsw[1][0][1][0] = 0u;               // step -1: the g0 word A(0) does not compute
+  float xe[2];                        // the unit's two elements between their items
   auto smi = [&](auto par_c, int g, int n, int lim, auto mask_c) {
     constexpr int P = decltype(par_c)::value;
     constexpr bool MASK = decltype(mask_c)::value;
@@ -390,9 +385,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
       if constexpr (DBG == 1) x = p > 0.f ? 1.f : 0.f;
       if constexpr (DBG == 2) x = p > 0.f ? sacc[P][g][r] : 0.f;
       if constexpr (DBG == 3) x = p > 0.f ? pacc[P][g][r] : 0.f;
-      xe[g][kind] = x;
+      xe[kind] = x;
     } else {
-      dsw[P][g][u >> 2][u & 3] = pk2(xe[g][0], xe[g][1]);
+      dsw[P][g][u >> 2][u & 3] = pk2(xe[0], xe[1]);
       if ((u & 3) == 3) {
         const uint32_t* w = dsw[P][g][u >> 2];
         dsf[P][g][u >> 2] = __builtin_bit_cast(bf16x8_t, u32x4_t{w[0], w[1], w[2], w[3]});
@@ -420,7 +415,7 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     constexpr int PA = decltype(par_c)::value;
     constexpr bool PRE = decltype(pre_c)::value;
     using prv = std::integral_constant<int, PA ^ 1>;
-    const int lim = lim_of(j - 1, 1), lim0 = lim_of(j - 1, 0);
+    const int lim = lim_of(j - 1, 1);
     // the successor prefetch goes out ahead of this phase's DMA pieces: the
     // tile's barrier (vmcnt 8: only the pieces may fly) then covers it
     if (pf) prefetch_next();
@@ -428,18 +423,8 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     bf16x8_t ka = PRE ? pre_k : lds_b128(kt + koff[0]);
     bf16x8_t va = PRE ? pre_v : lds_b128(kt + TILE_BYTES + koff[0]);
     int item = 0;
-    // items 0..7: 16..23 of softmax(j-1) of g0 (its items 0..15 ran beside
-    // B(j-2)), items 8..31: all 24 of g1 - one item a gap, where B's 16 gaps
-    // carried 24 items (VALU-bound at 756 cycles for 512 of MFMA)
-    // (k-step 7's four MFMAs are one fenced statement, so there are 28
-    // gaps: gaps 24..27 take two items each)
-    auto one = [&](int n) {
-      if (n < 8) smi(prv{}, 0, 16 + n, lim0, mask_c);
-      else smi(prv{}, 1, n - 8, lim, mask_c);
-    };
     auto beside = [&]() {
-      one(item);
-      if (item >= 24) one(item + 4);
+      if (item < 24) smi(prv{}, 1, item, lim, mask_c);
       ++item;
     };
 #pragma unroll
@@ -514,10 +499,13 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
         pre_v = lds_b128(nexta + TILE_BYTES + koff[0]);
       }
       ma(dqa[0][i >> 1], a, dsf[PB][0][i & 1]);
-      if (SOFT) smi(cur{}, 0, 2 * i, lim, mask_c);
+      if (SOFT) smi(cur{}, 0, 3 * i, lim, mask_c);
       __builtin_amdgcn_sched_barrier(0);
       ma(dqa[1][i >> 1], a, dsf[PB][1][i & 1]);
-      if (SOFT) smi(cur{}, 0, 2 * i + 1, lim, mask_c);
+      if (SOFT) {
+        smi(cur{}, 0, 3 * i + 1, lim, mask_c);
+        smi(cur{}, 0, 3 * i + 2, lim, mask_c);
+      }
       __builtin_amdgcn_sched_barrier(0);
       a = a1;
       a1 = n;
@@ -570,13 +558,10 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   // tail: softmax(J-1) of g1, then B(J-1)
   {
     const int j = 2 * T - 1;
-    const int lim = lim_of(j, 1), lim0 = lim_of(j, 0);
+    const int lim = lim_of(j, 1);
     const char* kt = smem + ((T + 1) & 3) * QSLOT + 32 * 256;
     pre_b0 = kread(kt, 0);
     pre_b1 = kread(kt, 1);
-#pragma unroll
-    for (int n = 16; n < 24; ++n)
-      smi(std::integral_constant<int, 1>{}, 0, n, lim0, std::integral_constant<bool, CAUSAL>{});
 #pragma unroll
     for (int n = 0; n < 24; ++n)
       smi(std::integral_constant<int, 1>{}, 1, n, lim, std::integral_constant<bool, CAUSAL>{});
