@@ -76,7 +76,7 @@ def attn_fwd(q, k, v, causal: bool = True, scale: float | None = None, variant: 
     return o, lse
 
 
-_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "6"))
+_BWD_VARIANT = int(os.environ.get("MXK_ATTN_BWD_VARIANT", "9"))
 
 
 def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = None,
@@ -85,7 +85,15 @@ def attn_bwd(q, k, v, o, lse, dout, causal: bool = True, scale: float | None = N
 
     ``dk``/``dv`` may be preallocated views (e.g. slices of a fused dQKV
     buffer) with a token stride; by default they are fresh contiguous tensors.
-    ``variant`` 6 (default; S % 256 == 0, else 5): variant 5's dQ kernel (it
+    ``variant`` 9 (default; Hq / Hkv a multiple of 4 and S % 256 == 0, else
+    6): dQ by workgroups of the 4 query heads of a GQA quad x 64 rows, one
+    wave per SIMD (attention_dq256.hip: Q / dO resident as MFMA operands in
+    the accumulator file, K / V by LDS-DMA shared by the four heads, dO / O /
+    Q staged through LDS, the delta pass folded in), then variant 6's
+    256-key dK / dV: bit-identical to variant 6 and 1-3 % faster per
+    Llama-3-8B layer at B 8 (1.02-1.04 vs 1.045-1.057 ms,
+    profiles/r6_dq256/SUMMARY.md).
+    6: variant 5's dQ kernel (it
     also writes the row constants -lse/scale and -delta), then dK / dV by the
     256-key workgroups of attention_bwd256.hip (one wave per SIMD, dK^T / dV^T
     in accumulators, S / dP of both key tiles from one read of each Q / dO
