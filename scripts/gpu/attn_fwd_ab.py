@@ -5,6 +5,7 @@ checks that the variants agree bit for bit."""
 import os
 import statistics
 import sys
+import time
 
 import torch
 
@@ -27,6 +28,12 @@ def main():
         print(f"RESULT variant={vv} bit-identical to variant={variants[0]}: {same}", flush=True)
     fl = 4 * B * Hq * S * S * D / (2 if causal else 1)
     ts = {vv: [] for vv in variants}
+    # time-floored warm-up (the clock ramps over ~1 s; bench.py's protocol)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < float(os.environ.get("WARM_S", 2.0)):
+        for vv in variants:
+            A.attn_fwd(q, k, v, causal=causal, variant=vv)
+        torch.cuda.synchronize()
     for _ in range(10):
         for vv in variants:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
