@@ -198,7 +198,7 @@ __device__ __forceinline__ void zero16(f32x16_t& x) {
 // STAMP (diagnostic build, mxk_attn_bwd_dkdv256_stamps): each wave adds up
 // the shader cycles of the step's phases (AB, softmax 0, C, D) and its
 // end-of-step wait + barrier, and writes them with its total to
-// stamps[wave id][6]
+// stamps[wave id][9] (+ prologue, the last pending tile, the stores)
 template <bool CAUSAL, int DQ = 0, bool STAMP = false>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
@@ -208,7 +208,8 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
                             long k_tok, long v_tok, long dk_tok, long dv_tok, float scale,
                             void* __restrict__ dqo = nullptr,
                             unsigned long long* __restrict__ stamps = nullptr) {
-  unsigned long long st_t0 = 0, st_ph[5] = {0, 0, 0, 0, 0}, st_c = 0;
+  unsigned long long st_t0 = 0, st_ph[5] = {0, 0, 0, 0, 0}, st_c = 0, st_loop = 0, st_tail = 0,
+                     st_drain = 0;
   if constexpr (STAMP) st_t0 = __builtin_readcyclecounter();
   auto stamp = [&](int ph) {
     if constexpr (STAMP) {
@@ -654,6 +655,7 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     stamp(4);
     if constexpr (STAMP) st_c = 0;
   };
+  if constexpr (STAMP) st_loop = __builtin_readcyclecounter();
   // unrolled by the ring depth: every slot offset is a compile-time immediate
   for (int i = 0; i < niter; i += NSLOT) {
     step(i, std::integral_constant<int, 0>{});
@@ -662,6 +664,7 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     if constexpr (NSLOT > 3)
       if (i + 3 < niter) step(i + 3, std::integral_constant<int, 3>{});
   }
+  if constexpr (STAMP) st_tail = __builtin_readcyclecounter();
   if constexpr (DQ != 0) dq_item(niter - 1);
   if constexpr (DQ == 0) {   // the last pending tile 1
     const char* pq = smem + L::RCB + ((niter - 1) % NSLOT) * 2 * QIMG;
@@ -672,6 +675,7 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
     dkdv(pq, pq + QIMG, 1, pf1, sf1, [](int) {});
   }
   mfma_drain_acc(dva, dka);
+  if constexpr (STAMP) st_drain = __builtin_readcyclecounter();
 
   // ---- dK = scale * (dK^T)^T, dV: lane = key, registers r -> d = 32 db + crow(r, h)
 #pragma unroll
@@ -696,10 +700,13 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
   }
   if constexpr (STAMP) {
     if (lane == 0) {
-      unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 6;
+      unsigned long long* w = stamps + (static_cast<long>(blockIdx.x) * 4 + wave) * 9;
       w[0] = __builtin_readcyclecounter() - st_t0;
 #pragma unroll
       for (int e = 0; e < 5; ++e) w[1 + e] = st_ph[e];
+      w[6] = st_loop - st_t0;                // prologue
+      w[7] = st_drain - st_tail;             // last pending tile + drain
+      w[8] = w[0] - (st_drain - st_t0);      // dK / dV stores
     }
   }
 }
@@ -858,8 +865,9 @@ MXK_API int mxk_attn_bwd_onepass(const void* q, const void* k, const void* v, co
 }
 
 // Diagnostic: the dK / dV kernel with per-wave segment cycle counts
-// (stamps: [B * Hkv * S / 256 workgroups][4 waves][total, A, B, C, D,
-// end-of-step wait + barrier]); arguments as mxk_attn_bwd_dkdv256.
+// (stamps: [B * Hkv * S / 256 workgroups][4 waves][9]: total, AB, C, D, copies,
+// end-of-step wait + barrier, prologue, last pending tile, stores]); arguments as
+// mxk_attn_bwd_dkdv256.
 MXK_API int mxk_attn_bwd_dkdv256_stamps(const void* q, const void* k, const void* v,
                                         const void* dout, const float* rowc, void* dk, void* dv,
                                         int B, int S, int Hq, int Hkv, long q_tok, long k_tok,

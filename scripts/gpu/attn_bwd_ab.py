@@ -28,6 +28,17 @@ def main():
     for vv in variants[1:]:
         same = all(torch.equal(x, y) for x, y in zip(outs[variants[0]], outs[vv]))
         print(f"RESULT variant={vv} bit-identical to variant={variants[0]}: {same}", flush=True)
+    # SAVE: the first variant's (dq, dk, dv) to a file; against a saved file
+    # from another kernel library (MXK_KERNELS_LIB), bit for bit
+    if os.environ.get("SAVE"):
+        path = os.environ["SAVE"]
+        cur = [x.cpu() for x in outs[variants[0]]]
+        if os.path.exists(path):
+            ref = torch.load(path, weights_only=True)
+            same = all(torch.equal(x, y) for x, y in zip(cur, ref))
+            print(f"RESULT variant={variants[0]} bit-identical to {path}: {same}", flush=True)
+        else:
+            torch.save(cur, path)
     # time-floored warm-up (the clock ramps over ~1 s; bench.py's protocol)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < float(os.environ.get("WARM_S", 2.0)):

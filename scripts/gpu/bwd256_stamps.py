@@ -29,7 +29,7 @@ rowc = torch.stack([-lse / scale, torch.zeros_like(lse)], dim=-1).contiguous()
 dk = torch.empty_like(k)
 dv = torch.empty_like(v)
 nwg = B * Hkv * (S // 256)
-st = torch.zeros(nwg * 4 * 6, dtype=torch.int64, device=dev)
+st = torch.zeros(nwg * 4 * 9, dtype=torch.int64, device=dev)
 f = _lib.lib().mxk_attn_bwd_dkdv256_stamps
 vp, i_, l_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 f.restype = i_
@@ -41,17 +41,20 @@ for _ in range(3):
            st.data_ptr(), _lib.stream_ptr(dev))
     assert rc == 0, rc
 torch.cuda.synchronize()
-s = st.view(nwg, 4, 6).double().cpu()
+s = st.view(nwg, 4, 9).double().cpu()
 tot = s[:, :, 0]
-names = ["AB", "softmax0", "C", "D", "wait+barrier"]
+names = ["AB", "C(pending dkdv + softmax0)", "D(dkdv tile 0)", "copies", "wait+barrier",
+         "prologue", "tail", "stores"]
 share = {n: (s[:, :, 1 + e].sum() / tot.sum()).item() for e, n in enumerate(names)}
 other = 1 - sum(share.values())
 # steps: a key block kb of the (b, hkv) pair sweeps 4 heads x (S - 256 kb) / 32 slices
 kb = torch.arange(nwg) // (B * Hkv)
 steps = (4 * (S - 256 * kb) // 32).double()
-per_step = {n: (s[:, :, 1 + e].sum(1) / 4 / steps).median().item() for e, n in enumerate(names)}
+per_step = {n: (s[:, :, 1 + e].sum(1) / 4 / steps).median().item() for e, n in enumerate(names[:5])}
 print("share of wave cycles: " + ", ".join(f"{n} {v:.3f}" for n, v in share.items()) +
       f", other {other:.3f}")
 print("median cycles per step (64 MFMAs = 2048 at the roof; AB 32 = 1024, C / D 16 = 512): " +
       ", ".join(f"{n} {v:.0f}" for n, v in per_step.items()))
+print("median per wave: total %.0f, prologue %.0f, tail %.0f, stores %.0f cycles" % (
+    tot.median().item(), s[:, :, 6].median().item(), s[:, :, 7].median().item(), s[:, :, 8].median().item()))
 print("done", flush=True)
