@@ -26,7 +26,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.attention import flash_attention, supported as flash_supported
+from ..ops.attention import flash_attention, qkv_rope_attention, supported as flash_supported
 from ..ops.linear import Linear, SwiGLULinear, swiglu_mlp
 from ..ops.xent import cross_entropy
 from ..ops.fused import add_rmsnorm, qkv_rope, rmsnorm, rope_tables
@@ -94,6 +94,11 @@ class Attention(nn.Module):
         c = self.cfg
         hd = c.head_dim
         qkv = self.wqkv(x)
+        # split + RoPE + flash attention as one node: its backward returns
+        # d(qkv) with the RoPE backward fused into the attention kernels
+        o = qkv_rope_attention(qkv, cos, sin, c.n_heads, c.n_kv_heads, hd)
+        if o is not None:
+            return self.wo(o.reshape(B, S, c.n_heads * hd))
         # q, k rotated straight out of their qkv slices; v a view into qkv
         # (token stride (Hq+2Hkv)*hd); one d(qkv) buffer in the backward
         q, k, v = qkv_rope(qkv, cos, sin, c.n_heads, c.n_kv_heads, hd)

@@ -151,6 +151,81 @@ class _FlashAttention(torch.autograd.Function):
         return dq, dk, dv, None, None
 
 
+# The fused projection's split + RoPE + attention as one autograd node
+# (MXK_FUSED_ROPE_BWD=0 turns it off): the forward rotates q / k out of
+# their qkv slices (the stand-alone RoPE pass) and runs the flash forward;
+# the backward writes d(qkv) of the UN-rotated projection straight into one
+# buffer - the RoPE backward fused into the dQ / dK stores of variant 9
+# (mxk_attn_bwd_rope), dV in place - instead of separate dq / dk / dv, two
+# RoPE passes over them and a dV copy (~400 MB of HBM traffic per
+# Llama-3-8B layer at micro-batch 8).
+_FUSED_ROPE_BWD = os.environ.get("MXK_FUSED_ROPE_BWD", "1") != "0"
+
+
+class _QKVRoPEAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, hq: int, hkv: int, hd: int, causal: bool, scale):
+        from .fused import _rope_launch
+        B, S, _ = qkv.shape
+        q = _rope_launch(qkv[..., :hq * hd].view(B, S, hq, hd), cos, sin, 1.0)
+        k = _rope_launch(qkv[..., hq * hd:(hq + hkv) * hd].view(B, S, hkv, hd), cos, sin, 1.0)
+        v = qkv[..., (hq + hkv) * hd:].view(B, S, hkv, hd)
+        o, lse = attn_fwd(q, k, v, causal=causal, scale=scale)
+        ctx.save_for_backward(q, k, v, o, lse, cos, sin)
+        ctx.causal, ctx.scale, ctx.dims = causal, scale, (hq, hkv, hd)
+        return o
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .fused import _rope_launch
+        q, k, v, o, lse, cos, sin = ctx.saved_tensors
+        hq, hkv, hd = ctx.dims
+        B, S = q.shape[:2]
+        scale = ctx.scale if ctx.scale is not None else 1.0 / math.sqrt(hd)
+        dqkv = torch.empty((B, S, (hq + 2 * hkv) * hd), dtype=q.dtype, device=q.device)
+        dq = dqkv[..., :hq * hd].view(B, S, hq, hd)
+        dk = dqkv[..., hq * hd:(hq + hkv) * hd].view(B, S, hkv, hd)
+        dv = dqkv[..., (hq + hkv) * hd:].view(B, S, hkv, hd)
+        dout = dout.contiguous()
+        if _BWD_VARIANT == 9:
+            L = _lib.lib()
+            ws = torch.empty(L.mxk_attn_bwd_workspace_variant(B, S, hq, 9) // 4,
+                             dtype=torch.float32, device=q.device)
+            st = L.mxk_attn_bwd_rope(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                     dout.data_ptr(), lse.data_ptr(), dq.data_ptr(), dk.data_ptr(),
+                                     dv.data_ptr(), ws.data_ptr(), B, S, hq, hkv, hd, q.stride(1),
+                                     k.stride(1), v.stride(1), dq.stride(1), dk.stride(1),
+                                     dv.stride(1), cos.data_ptr(), sin.data_ptr(), float(scale),
+                                     int(ctx.causal), _lib.stream_ptr(q.device))
+            if st == 0:
+                return dqkv, None, None, None, None, None, None, None
+            if st != 1:     # 1 = hipErrorInvalidValue: a layout variant 9 does not take
+                _lib.check(st, "mxk_attn_bwd_rope")
+        # other variants: the backward into the slices, then the RoPE passes
+        gq, _, _ = attn_bwd(q, k, v, o, lse, dout, causal=ctx.causal, scale=scale, dk=dk, dv=dv)
+        _rope_launch(gq, cos, sin, -1.0, out=dq)
+        _rope_launch(dk, cos, sin, -1.0, out=dk)     # in place: a thread reads both halves first
+        return dqkv, None, None, None, None, None, None, None
+
+
+def qkv_rope_attention(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, hq: int, hkv: int,
+                       hd: int, causal: bool = True, scale: float | None = None):
+    """Attention output o [B, S, hq, hd] of a fused projection qkv [B, S,
+    (hq + 2 hkv) hd] with rotary embedding on q and k, as one autograd node
+    whose backward returns d(qkv) from the fused kernels; None when the
+    layout is not the fused path's (the caller then runs qkv_rope +
+    flash_attention)."""
+    if not (_FUSED_ROPE_BWD and qkv.is_cuda and qkv.dtype == torch.bfloat16 and qkv.dim() == 3
+            and qkv.is_contiguous() and qkv.data_ptr() % 16 == 0 and hd == HEAD_DIM
+            and hkv > 0 and hq % hkv == 0 and (hq // hkv) % 4 == 0
+            and qkv.shape[-1] == (hq + 2 * hkv) * hd and qkv.shape[1] % 256 == 0
+            and cos.shape[0] >= qkv.shape[1]):
+        return None
+    S = qkv.shape[1]
+    return _QKVRoPEAttention.apply(qkv, cos[:S].float().contiguous(), sin[:S].float().contiguous(),
+                                   hq, hkv, hd, causal, scale)
+
+
 def flash_attention(q, k, v, causal: bool = True, scale: float | None = None) -> torch.Tensor:
     """Attention o [B,S,Hq,D] for q [B,S,Hq,D], k/v [B,S,Hkv,D] (GQA).
 

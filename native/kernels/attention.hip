@@ -1727,6 +1727,31 @@ MXK_API long mxk_attn_bwd_workspace_variant(int B, int S, int Hq, int variant) {
   if (variant == 7 || variant == 8) return mxk_attn_bwd_onepass_workspace(B, S, Hq, variant == 8);
   return rows * 4 + (variant == 0 ? 2 * rows * D * 4 : 0);
 }
+// Backward variant 9 with the rotary-embedding backward fused into the dQ
+// and dK stores: q / k are the ROTATED projections the forward ran on, and
+// dq / dk come out as gradients of the un-rotated ones (rcos / rsin: the
+// forward's [S][D/2] fp32 tables), so the fused-QKV projection's backward
+// takes d(QKV) straight from here (dq / dk / dv at token strides, e.g.
+// slices of one buffer).  Workspace: mxk_attn_bwd_workspace_variant(.., 9).
+// hipErrorInvalidValue when variant 9 does not take the layout (the caller
+// then runs mxk_attn_bwd_variant and the stand-alone RoPE pass).
+MXK_API int mxk_attn_bwd_rope(const void* q, const void* k, const void* v, const void* o,
+                              const void* dout, const float* lse, void* dq, void* dk, void* dv,
+                              void* workspace, int B, int S, int Hq, int Hkv, int head_dim,
+                              long q_tok, long k_tok, long v_tok, long dq_tok, long dk_tok,
+                              long dv_tok, const float* rcos, const float* rsin, float scale,
+                              int causal, hipStream_t stream) {
+  if (head_dim != D || B < 1 || S < 256 || S % 256 || Hkv < 1 || Hq % Hkv || (Hq / Hkv) % 4 ||
+      !workspace || !rcos || !rsin ||
+      static_cast<long>(S) * (q_tok > static_cast<long>(Hq) * D ? q_tok : Hq * D) * 2 >= (1L << 32))
+    return static_cast<int>(hipErrorInvalidValue);
+  float* rowc = static_cast<float*>(workspace);
+  const int st = mxk_attn_bwd_dq256_rope(q, k, v, o, dout, lse, dq, rowc, B, S, Hq, Hkv, q_tok,
+                                         k_tok, v_tok, dq_tok, rcos, rsin, scale, causal, stream);
+  if (st) return st;
+  return mxk_attn_bwd_dkdv256_rope(q, k, v, dout, rowc, dk, dv, B, S, Hq, Hkv, q_tok, k_tok, v_tok,
+                                   dk_tok, dv_tok, rcos, rsin, scale, causal, stream);
+}
 MXK_API long mxk_attn_bwd_workspace(int B, int S, int Hq) {
   return mxk_attn_bwd_workspace_variant(B, S, Hq, 0);
 }

@@ -199,7 +199,11 @@ __device__ __forceinline__ void zero16(f32x16_t& x) {
 // the shader cycles of the step's phases (AB, softmax 0, C, D) and its
 // end-of-step wait + barrier, and writes them with its total to
 // stamps[wave id][9] (+ prologue, the last pending tile, the stores)
-template <bool CAUSAL, int DQ = 0, bool STAMP = false>
+// ROPE: dK leaves through the rotary-embedding backward (the inverse
+// rotation of its (d, d + 64) pairs at the key's position; both halves of a
+// pair are in the same lane, d tiles db and db + 2), rounded to bf16 before
+// and after exactly as the stand-alone pass (fused_ops.hip) does.
+template <bool CAUSAL, int DQ = 0, bool STAMP = false, bool ROPE = false>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                             const uint16_t* __restrict__ v, const uint16_t* __restrict__ dout,
@@ -207,7 +211,9 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
                             uint16_t* __restrict__ dv, int S, int Hq, int Hkv, long q_tok,
                             long k_tok, long v_tok, long dk_tok, long dv_tok, float scale,
                             void* __restrict__ dqo = nullptr,
-                            unsigned long long* __restrict__ stamps = nullptr) {
+                            unsigned long long* __restrict__ stamps = nullptr,
+                            const float* __restrict__ rcos = nullptr,
+                            const float* __restrict__ rsin = nullptr) {
   unsigned long long st_t0 = 0, st_ph[5] = {0, 0, 0, 0, 0}, st_c = 0, st_loop = 0, st_tail = 0,
                      st_drain = 0;
   if constexpr (STAMP) st_t0 = __builtin_readcyclecounter();
@@ -689,9 +695,29 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
       for (int g = 0; g < 4; ++g) {
         const int d = 32 * db + 8 * g + 4 * h;
         uint2 pk;
-        pk.x = mxk::pack2bf(dka[db][kt][4 * g] * scale, dka[db][kt][4 * g + 1] * scale);
-        pk.y = mxk::pack2bf(dka[db][kt][4 * g + 2] * scale, dka[db][kt][4 * g + 3] * scale);
-        *reinterpret_cast<uint2*>(dkr + d) = pk;
+        if (!ROPE) {
+          pk.x = mxk::pack2bf(dka[db][kt][4 * g] * scale, dka[db][kt][4 * g + 1] * scale);
+          pk.y = mxk::pack2bf(dka[db][kt][4 * g + 2] * scale, dka[db][kt][4 * g + 3] * scale);
+          *reinterpret_cast<uint2*>(dkr + d) = pk;
+        } else if (db < 2) {
+          // pair (d, d + 64): tiles db, db + 2, same register
+          const float4 c4 = *reinterpret_cast<const float4*>(rcos + key * (D / 2) + d);
+          const float4 s4 = *reinterpret_cast<const float4*>(rsin + key * (D / 2) + d);
+          const float cs[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
+          float oa[4], ob[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float a = mxk::bf2f(mxk::f2bf(dka[db][kt][4 * g + j] * scale));
+            const float bb = mxk::bf2f(mxk::f2bf(dka[db + 2][kt][4 * g + j] * scale));
+            mxk::rope_pair(a, bb, cs[j], -sn[j], oa[j], ob[j]);
+          }
+          pk.x = mxk::pack2bf(oa[0], oa[1]);
+          pk.y = mxk::pack2bf(oa[2], oa[3]);
+          *reinterpret_cast<uint2*>(dkr + d) = pk;
+          pk.x = mxk::pack2bf(ob[0], ob[1]);
+          pk.y = mxk::pack2bf(ob[2], ob[3]);
+          *reinterpret_cast<uint2*>(dkr + d + 64) = pk;
+        }
         pk.x = mxk::pack2bf(dva[db][kt][4 * g], dva[db][kt][4 * g + 1]);
         pk.y = mxk::pack2bf(dva[db][kt][4 * g + 2], dva[db][kt][4 * g + 3]);
         *reinterpret_cast<uint2*>(dvr + d) = pk;
@@ -712,12 +738,14 @@ mxk_attn_bwd_dkdv256_kernel(const uint16_t* __restrict__ q, const uint16_t* __re
 }
 
 // dK / dV of the 256-key kernel.  rowc: [B, Hq, S] x {-lse/scale, -delta}
-// (written by the dQ kernel of attention.hip with ROWC).  Returns a HIP
-// status; hipErrorInvalidValue when a layout does not fit.
-MXK_API int mxk_attn_bwd_dkdv256(const void* q, const void* k, const void* v, const void* dout,
-                                 const float* rowc, void* dk, void* dv, int B, int S, int Hq,
-                                 int Hkv, long q_tok, long k_tok, long v_tok, long dk_tok,
-                                 long dv_tok, float scale, int causal, hipStream_t stream) {
+// (written by the dQ kernel of attention.hip with ROWC).  rcos / rsin
+// (both or neither): the rotary-embedding backward fused into the dK store.
+// Returns a HIP status; hipErrorInvalidValue when a layout does not fit.
+static int dkdv256_launch(const void* q, const void* k, const void* v, const void* dout,
+                          const float* rowc, void* dk, void* dv, int B, int S, int Hq, int Hkv,
+                          long q_tok, long k_tok, long v_tok, long dk_tok, long dv_tok,
+                          const float* rcos, const float* rsin, float scale, int causal,
+                          hipStream_t stream) {
   if (B < 1 || S < KBLK || S % KBLK || Hkv < 1 || Hq % Hkv || q_tok % 8 || k_tok % 8 ||
       v_tok % 8 || dk_tok % 4 || dv_tok % 4 ||
       static_cast<long>(S) * q_tok * 2 >= (1L << 32) ||
@@ -725,8 +753,10 @@ MXK_API int mxk_attn_bwd_dkdv256(const void* q, const void* k, const void* v, co
       static_cast<long>(S) * Hq * D * 2 >= (1L << 32) ||
       (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
        reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(dout) |
-       reinterpret_cast<uintptr_t>(rowc)) % 16 ||
-      (reinterpret_cast<uintptr_t>(dk) | reinterpret_cast<uintptr_t>(dv)) % 8)
+       reinterpret_cast<uintptr_t>(rowc) | reinterpret_cast<uintptr_t>(rcos) |
+       reinterpret_cast<uintptr_t>(rsin)) % 16 ||
+      (reinterpret_cast<uintptr_t>(dk) | reinterpret_cast<uintptr_t>(dv)) % 8 ||
+      (rcos == nullptr) != (rsin == nullptr))
     return static_cast<int>(hipErrorInvalidValue);
   const int nwg = B * Hkv * (S / KBLK);
   const auto* Q = static_cast<const uint16_t*>(q);
@@ -735,15 +765,35 @@ MXK_API int mxk_attn_bwd_dkdv256(const void* q, const void* k, const void* v, co
   const auto* dO = static_cast<const uint16_t*>(dout);
   auto* dK = static_cast<uint16_t*>(dk);
   auto* dV = static_cast<uint16_t*>(dv);
-  if (causal)
-    hipLaunchKernelGGL(mxk_attn_bwd_dkdv256_kernel<true>, dim3(nwg), dim3(256), 0, stream,
-                       Q, K, V, dO, rowc, dK, dV, S, Hq, Hkv, q_tok, k_tok, v_tok, dk_tok, dv_tok,
-                       scale);
-  else
-    hipLaunchKernelGGL(mxk_attn_bwd_dkdv256_kernel<false>, dim3(nwg), dim3(256), 0, stream,
-                       Q, K, V, dO, rowc, dK, dV, S, Hq, Hkv, q_tok, k_tok, v_tok, dk_tok, dv_tok,
-                       scale);
+#define MXK_DKDV256(C, R)                                                                    \
+  hipLaunchKernelGGL((mxk_attn_bwd_dkdv256_kernel<C, 0, false, R>), dim3(nwg), dim3(256), 0, \
+                     stream, Q, K, V, dO, rowc, dK, dV, S, Hq, Hkv, q_tok, k_tok, v_tok, dk_tok, \
+                     dv_tok, scale, nullptr, nullptr, rcos, rsin)
+  if (rcos) {
+    if (causal) MXK_DKDV256(true, true);
+    else MXK_DKDV256(false, true);
+  } else {
+    if (causal) MXK_DKDV256(true, false);
+    else MXK_DKDV256(false, false);
+  }
+#undef MXK_DKDV256
   MXK_RETURN_LAUNCH_STATUS();
+}
+MXK_API int mxk_attn_bwd_dkdv256(const void* q, const void* k, const void* v, const void* dout,
+                                 const float* rowc, void* dk, void* dv, int B, int S, int Hq,
+                                 int Hkv, long q_tok, long k_tok, long v_tok, long dk_tok,
+                                 long dv_tok, float scale, int causal, hipStream_t stream) {
+  return dkdv256_launch(q, k, v, dout, rowc, dk, dv, B, S, Hq, Hkv, q_tok, k_tok, v_tok, dk_tok,
+                        dv_tok, nullptr, nullptr, scale, causal, stream);
+}
+MXK_API int mxk_attn_bwd_dkdv256_rope(const void* q, const void* k, const void* v, const void* dout,
+                                      const float* rowc, void* dk, void* dv, int B, int S, int Hq,
+                                      int Hkv, long q_tok, long k_tok, long v_tok, long dk_tok,
+                                      long dv_tok, const float* rcos, const float* rsin,
+                                      float scale, int causal, hipStream_t stream) {
+  if (!rcos || !rsin) return static_cast<int>(hipErrorInvalidValue);
+  return dkdv256_launch(q, k, v, dout, rowc, dk, dv, B, S, Hq, Hkv, q_tok, k_tok, v_tok, dk_tok,
+                        dv_tok, rcos, rsin, scale, causal, stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -137,6 +137,19 @@ MXK_API int mxk_attn_bwd_dq256(const void* q, const void* k, const void* v, cons
                                const void* dout, const float* lse, void* dq, float* rowc, int B,
                                int S, int Hq, int Hkv, long q_tok, long k_tok, long v_tok,
                                float scale, int causal, hipStream_t stream);
+// the same two kernels with the rotary-embedding backward fused into their
+// stores (rcos / rsin: [S][D/2] fp32 tables; dQ / dK leave un-rotated, i.e.
+// as the gradient of the pre-RoPE projection) and dQ at a token stride
+MXK_API int mxk_attn_bwd_dkdv256_rope(const void* q, const void* k, const void* v, const void* dout,
+                                      const float* rowc, void* dk, void* dv, int B, int S, int Hq,
+                                      int Hkv, long q_tok, long k_tok, long v_tok, long dk_tok,
+                                      long dv_tok, const float* rcos, const float* rsin,
+                                      float scale, int causal, hipStream_t stream);
+MXK_API int mxk_attn_bwd_dq256_rope(const void* q, const void* k, const void* v, const void* o,
+                                    const void* dout, const float* lse, void* dq, float* rowc,
+                                    int B, int S, int Hq, int Hkv, long q_tok, long k_tok,
+                                    long v_tok, long dq_tok, const float* rcos, const float* rsin,
+                                    float scale, int causal, hipStream_t stream);
 // forward variant 10 (attention_fwd256.hip)
 MXK_API int mxk_attn_fwd256(const void* q, const void* k, const void* v, void* o, float* lse,
                             int B, int S, int Hq, int Hkv, long q_tok, long k_tok, long v_tok,

@@ -123,14 +123,21 @@ __device__ __forceinline__ uint32_t pk2(float lo, float hi) { return mxk::pack2b
 // measured within 0.2 % of this launch, 1.0275 vs 1.0293 ms per layer
 // backward, and spilled once the prologue staged through LDS; not kept,
 // profiles/r6_dq256/.)
-template <bool CAUSAL, int DBG = 0, bool STAMP = false>
+// ROPE: dQ leaves through the rotary-embedding backward (each lane reads
+// its 16-B chunk and the pair partner 64 dims away from the row image and
+// writes its own chunk rotated back at the row's position), rounded to bf16
+// before and after exactly as the stand-alone pass (fused_ops.hip) does;
+// dq_tok (> 0): dQ's token stride (a slice of a fused d(QKV) buffer).
+template <bool CAUSAL, int DBG = 0, bool STAMP = false, bool ROPE = false>
 __global__ void __launch_bounds__(256, 1)
 mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                           const uint16_t* __restrict__ v, const uint16_t* __restrict__ o,
                           const uint16_t* __restrict__ dout, const float* __restrict__ lse,
                           uint16_t* __restrict__ dq, float* __restrict__ rowc, int S, int Hq,
                           int Hkv, long q_tok, long k_tok, long v_tok, float scale,
-                          unsigned long long* __restrict__ stamps = nullptr, int succ = 0) {
+                          unsigned long long* __restrict__ stamps = nullptr, int succ = 0,
+                          long dq_tok = 0, const float* __restrict__ rcos = nullptr,
+                          const float* __restrict__ rsin = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[QLDS + 4 * 256];   // ring | prefetch sinks
   unsigned long long st_0 = 0, st_c = 0, st_seg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if constexpr (STAMP) st_0 = st_c = __builtin_readcyclecounter();
@@ -603,12 +610,41 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   __builtin_amdgcn_s_waitcnt(0xC07F);   // own image: no other wave reads it
   // lane l: chunk l & 15 of rows (l >> 4) + 4 i
   const int crow0 = lane >> 4, cch = lane & 15;
-  uint16_t* dbase = dq + (static_cast<long>(b) * S + q0) * tokd + static_cast<long>(hq) * D + cch * 8;
+  const long dqt = dq_tok > 0 ? dq_tok : tokd;
+  uint16_t* dbase = dq + (static_cast<long>(b) * S + q0) * dqt + static_cast<long>(hq) * D + cch * 8;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int row = crow0 + 4 * i;
-    const uint4 x = *reinterpret_cast<const uint4*>(img + swz(row, cch));
-    *reinterpret_cast<uint4*>(dbase + static_cast<long>(row) * tokd) = x;
+    uint4 x = *reinterpret_cast<const uint4*>(img + swz(row, cch));
+    if constexpr (ROPE) {
+      // chunks cch < 8 hold a (dims 8 cch ..), the partner cch ^ 8 holds b
+      const uint4 y = *reinterpret_cast<const uint4*>(img + swz(row, cch ^ 8));
+      const long tb = static_cast<long>(q0 + row) * (D / 2) + 8 * (cch & 7);
+      const float4 c0 = *reinterpret_cast<const float4*>(rcos + tb);
+      const float4 c1 = *reinterpret_cast<const float4*>(rcos + tb + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(rsin + tb);
+      const float4 s1 = *reinterpret_cast<const float4*>(rsin + tb + 4);
+      const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const uint32_t xw[4] = {x.x, x.y, x.z, x.w}, yw[4] = {y.x, y.y, y.z, y.w};
+      const bool lo = cch < 8;
+      uint32_t ow[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        float o2[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const float own = __uint_as_float(e ? xw[w] & 0xFFFF0000u : xw[w] << 16);
+          const float par = __uint_as_float(e ? yw[w] & 0xFFFF0000u : yw[w] << 16);
+          float oa, ob;
+          mxk::rope_pair(lo ? own : par, lo ? par : own, cs[2 * w + e], -sn[2 * w + e], oa, ob);
+          o2[e] = lo ? oa : ob;
+        }
+        ow[w] = pk2(o2[0], o2[1]);
+      }
+      x = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    }
+    *reinterpret_cast<uint4*>(dbase + static_cast<long>(row) * dqt) = x;
   }
   stamp(4);
   };   // run_item
@@ -682,6 +718,42 @@ MXK_API int mxk_attn_bwd_dq256(const void* q, const void* k, const void* v, cons
   else
     hipLaunchKernelGGL(mxk_attn_bwd_dq256_kernel<false>, dim3(nwg), dim3(256), 0, stream, Q, K, V,
                        O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale, nullptr, succ);
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
+// mxk_attn_bwd_dq256 with the rotary-embedding backward fused into the dQ
+// store (rcos / rsin: [S][D/2] fp32) and dQ at token stride dq_tok
+MXK_API int mxk_attn_bwd_dq256_rope(const void* q, const void* k, const void* v, const void* o,
+                                    const void* dout, const float* lse, void* dq, float* rowc,
+                                    int B, int S, int Hq, int Hkv, long q_tok, long k_tok,
+                                    long v_tok, long dq_tok, const float* rcos, const float* rsin,
+                                    float scale, int causal, hipStream_t stream) {
+  if (B < 1 || S < QW || S % QW || Hkv < 1 || Hq % Hkv || (Hq / Hkv) % 4 || q_tok % 8 ||
+      k_tok % 8 || v_tok % 8 || dq_tok < static_cast<long>(Hq) * D || dq_tok % 8 || !rcos ||
+      !rsin || static_cast<long>(S) * k_tok * 2 >= (1L << 32) ||
+      static_cast<long>(S) * v_tok * 2 >= (1L << 32) ||
+      (reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
+       reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
+       reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
+       reinterpret_cast<uintptr_t>(rowc) | reinterpret_cast<uintptr_t>(rcos) |
+       reinterpret_cast<uintptr_t>(rsin)) % 16)
+    return static_cast<int>(hipErrorInvalidValue);
+  const int nwg = B * (Hq / 4) * (S / QW);
+  const auto* Q = static_cast<const uint16_t*>(q);
+  const auto* K = static_cast<const uint16_t*>(k);
+  const auto* V = static_cast<const uint16_t*>(v);
+  const auto* O = static_cast<const uint16_t*>(o);
+  const auto* dO = static_cast<const uint16_t*>(dout);
+  auto* dQ = static_cast<uint16_t*>(dq);
+  const int succ = dq256_succ();
+  if (causal)
+    hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<true, 0, false, true>), dim3(nwg), dim3(256), 0,
+                       stream, Q, K, V, O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale,
+                       nullptr, succ, dq_tok, rcos, rsin);
+  else
+    hipLaunchKernelGGL((mxk_attn_bwd_dq256_kernel<false, 0, false, true>), dim3(nwg), dim3(256), 0,
+                       stream, Q, K, V, O, dO, lse, dQ, rowc, S, Hq, Hkv, q_tok, k_tok, v_tok, scale,
+                       nullptr, succ, dq_tok, rcos, rsin);
   MXK_RETURN_LAUNCH_STATUS();
 }
 

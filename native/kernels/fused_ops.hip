@@ -335,11 +335,7 @@ mxk_rope_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
     sa[4] = s1.x; sa[5] = s1.y; sa[6] = s1.z; sa[7] = s1.w;
     float oa[8], ob[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float s = sign * sa[e];
-      oa[e] = a[e] * ca[e] - b[e] * s;
-      ob[e] = b[e] * ca[e] + a[e] * s;
-    }
+    for (int e = 0; e < 8; ++e) mxk::rope_pair(a[e], b[e], ca[e], sign * sa[e], oa[e], ob[e]);
     uint16_t* yr = y + tok * y_tok + static_cast<long>(hd) * D;
     store8(yr + p0, oa);
     store8(yr + half + p0, ob);

@@ -50,6 +50,16 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, b);
 }
 
+// Rotary embedding of one (i, i + D/2) pair ("rotate-half"): a' = a cos -
+// b s, b' = b cos + a s, with s = sign * sin (sign -1: the inverse rotation,
+// the backward).  Explicit fmas, so the stand-alone kernel (fused_ops.hip)
+// and the epilogues that fuse it (attention backward) round identically.
+__device__ __forceinline__ void rope_pair(float a, float b, float c, float s, float& oa,
+                                          float& ob) {
+  oa = __builtin_fmaf(a, c, -(b * s));
+  ob = __builtin_fmaf(b, c, a * s);
+}
+
 // Bijective XCD-aware remap of a 1-D block id: blocks b and b+8 share an
 // XCD (round-robin dispatch), so give each XCD a contiguous run of logical
 // work ids.  Speed-only: correctness never depends on placement.

@@ -227,3 +227,53 @@ def test_attn_bwd_dq256_v9(cuda_device, B, S, Hq, Hkv, causal, fused):
     if (Hq // Hkv) % 4:
         assert torch.equal(d6[0], dq)     # the fallback is variant 6 itself
 
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
+    (1, 256, 8, 2, True),
+    (2, 512, 8, 2, False),
+    (1, 512, 16, 4, True),
+    (1, 256, 8, 1, True),
+])
+def test_qkv_rope_attention_fused_backward(cuda_device, B, S, Hq, Hkv, causal, monkeypatch):
+    """The fused projection's split + RoPE + attention node
+    (A.qkv_rope_attention): the forward equals qkv_rope + flash_attention
+    bit for bit; its backward (variant 9 with the RoPE backward fused into
+    the dQ / dK stores, mxk_attn_bwd_rope) returns the same d(qkv) as the
+    unfused chain bit for bit, and matches the fp32 reference; the fallback
+    (another backward variant: attention into the slices, then the RoPE
+    passes) too."""
+    from mxk8s.ops.fused import qkv_rope, rope_ref, rope_tables
+    hd = 128
+    g = torch.Generator(device=cuda_device).manual_seed(41)
+    qkv = (torch.randn(B, S, (Hq + 2 * Hkv) * hd, device=cuda_device, generator=g) * 2).bfloat16()
+    dout = torch.randn(B, S, Hq, hd, device=cuda_device, generator=g).bfloat16()
+    cos, sin = rope_tables(S + 64, hd, device=cuda_device)
+
+    x1 = qkv.clone().requires_grad_()
+    o1 = A.qkv_rope_attention(x1, cos, sin, Hq, Hkv, hd, causal=causal)
+    assert o1 is not None
+    o1.backward(dout)
+
+    x2 = qkv.clone().requires_grad_()
+    q, k, v = qkv_rope(x2, cos, sin, Hq, Hkv, hd)
+    o2 = A.flash_attention(q, k, v, causal=causal)
+    o2.backward(dout)
+    assert torch.equal(o1, o2)
+    assert torch.equal(x1.grad, x2.grad)
+
+    xr = qkv.float().requires_grad_()
+    qr, kr, vr = xr.split([Hq * hd, Hkv * hd, Hkv * hd], dim=-1)
+    qr = rope_ref(qr.reshape(B, S, Hq, hd), cos, sin)
+    kr = rope_ref(kr.reshape(B, S, Hkv, hd), cos, sin)
+    A.attention_ref(qr, kr, vr.reshape(B, S, Hkv, hd), causal=causal).backward(dout.float())
+    err = (x1.grad.float() - xr.grad).abs().max().item()
+    tol = 3e-2 * max(1.0, xr.grad.abs().max().item())
+    assert err < tol, (err, tol)
+
+    # the fallback inside the node's backward (variant 6 + stand-alone RoPE)
+    monkeypatch.setattr(A, "_BWD_VARIANT", 6)
+    x3 = qkv.clone().requires_grad_()
+    A.qkv_rope_attention(x3, cos, sin, Hq, Hkv, hd, causal=causal).backward(dout)
+    err = (x3.grad.float() - xr.grad).abs().max().item()
+    assert err < tol, ("fallback", err, tol)
