@@ -26,7 +26,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.attention import flash_attention, qkv_rope_attention, supported as flash_supported
+from ..ops.attention import (flash_attention, proj_rope_attention, qkv_rope_attention,
+                              supported as flash_supported)
 from ..ops.linear import Linear, SwiGLULinear, swiglu_mlp
 from ..ops.xent import cross_entropy
 from ..ops.fused import add_rmsnorm, qkv_rope, rmsnorm, rope_tables
@@ -93,6 +94,12 @@ class Attention(nn.Module):
         B, S, _ = x.shape
         c = self.cfg
         hd = c.head_dim
+        # projection + RoPE (in the GEMM's epilogue) + flash attention as one
+        # node; its backward takes d(qkv) from the attention kernels with the
+        # RoPE backward fused into their stores
+        o = proj_rope_attention(x, self.wqkv.weight, cos, sin, c.n_heads, c.n_kv_heads, hd)
+        if o is not None:
+            return self.wo(o.reshape(B, S, c.n_heads * hd))
         qkv = self.wqkv(x)
         # split + RoPE + flash attention as one node: its backward returns
         # d(qkv) with the RoPE backward fused into the attention kernels

@@ -93,6 +93,7 @@ _SIGNATURES = {
                                        _l, _f, _vp, _vp]),
     "mxk_attn_bwd_variant": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i,
                                   _i, _l, _l, _l, _l, _l, _f, _i, _i, _vp]),
+    "mxk_gemm_bf16_rope": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp]),
     "mxk_attn_bwd_rope": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i,
                                _l, _l, _l, _l, _l, _l, _vp, _vp, _f, _i, _vp]),
     "mxk_attn_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i,

@@ -177,35 +177,114 @@ class _QKVRoPEAttention(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        from .fused import _rope_launch
         q, k, v, o, lse, cos, sin = ctx.saved_tensors
-        hq, hkv, hd = ctx.dims
-        B, S = q.shape[:2]
-        scale = ctx.scale if ctx.scale is not None else 1.0 / math.sqrt(hd)
-        dqkv = torch.empty((B, S, (hq + 2 * hkv) * hd), dtype=q.dtype, device=q.device)
-        dq = dqkv[..., :hq * hd].view(B, S, hq, hd)
-        dk = dqkv[..., hq * hd:(hq + hkv) * hd].view(B, S, hkv, hd)
-        dv = dqkv[..., (hq + hkv) * hd:].view(B, S, hkv, hd)
-        dout = dout.contiguous()
-        if _BWD_VARIANT == 9:
-            L = _lib.lib()
-            ws = torch.empty(L.mxk_attn_bwd_workspace_variant(B, S, hq, 9) // 4,
-                             dtype=torch.float32, device=q.device)
-            st = L.mxk_attn_bwd_rope(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
-                                     dout.data_ptr(), lse.data_ptr(), dq.data_ptr(), dk.data_ptr(),
-                                     dv.data_ptr(), ws.data_ptr(), B, S, hq, hkv, hd, q.stride(1),
-                                     k.stride(1), v.stride(1), dq.stride(1), dk.stride(1),
-                                     dv.stride(1), cos.data_ptr(), sin.data_ptr(), float(scale),
-                                     int(ctx.causal), _lib.stream_ptr(q.device))
-            if st == 0:
-                return dqkv, None, None, None, None, None, None, None
-            if st != 1:     # 1 = hipErrorInvalidValue: a layout variant 9 does not take
-                _lib.check(st, "mxk_attn_bwd_rope")
-        # other variants: the backward into the slices, then the RoPE passes
-        gq, _, _ = attn_bwd(q, k, v, o, lse, dout, causal=ctx.causal, scale=scale, dk=dk, dv=dv)
-        _rope_launch(gq, cos, sin, -1.0, out=dq)
-        _rope_launch(dk, cos, sin, -1.0, out=dk)     # in place: a thread reads both halves first
+        dqkv = _rope_attn_backward(q, k, v, o, lse, cos, sin, dout, ctx.dims, ctx.causal, ctx.scale)
         return dqkv, None, None, None, None, None, None, None
+
+
+def _rope_attn_backward(q, k, v, o, lse, cos, sin, dout, dims, causal, scale):
+    """d(qkv) [B, S, (hq + 2 hkv) hd] of the un-rotated projection from the
+    rotated q / k the forward attended with."""
+    from .fused import _rope_launch
+    hq, hkv, hd = dims
+    B, S = q.shape[:2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(hd)
+    dqkv = torch.empty((B, S, (hq + 2 * hkv) * hd), dtype=q.dtype, device=q.device)
+    dq = dqkv[..., :hq * hd].view(B, S, hq, hd)
+    dk = dqkv[..., hq * hd:(hq + hkv) * hd].view(B, S, hkv, hd)
+    dv = dqkv[..., (hq + hkv) * hd:].view(B, S, hkv, hd)
+    dout = dout.contiguous()
+    if _BWD_VARIANT == 9:
+        L = _lib.lib()
+        ws = torch.empty(L.mxk_attn_bwd_workspace_variant(B, S, hq, 9) // 4,
+                         dtype=torch.float32, device=q.device)
+        st = L.mxk_attn_bwd_rope(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                 dout.data_ptr(), lse.data_ptr(), dq.data_ptr(), dk.data_ptr(),
+                                 dv.data_ptr(), ws.data_ptr(), B, S, hq, hkv, hd, q.stride(1),
+                                 k.stride(1), v.stride(1), dq.stride(1), dk.stride(1),
+                                 dv.stride(1), cos.data_ptr(), sin.data_ptr(), float(scale),
+                                 int(causal), _lib.stream_ptr(q.device))
+        if st == 0:
+            return dqkv
+        if st != 1:     # 1 = hipErrorInvalidValue: a layout variant 9 does not take
+            _lib.check(st, "mxk_attn_bwd_rope")
+    # other variants: the backward into the slices, then the RoPE passes
+    gq, _, _ = attn_bwd(q, k, v, o, lse, dout, causal=causal, scale=scale, dk=dk, dv=dv)
+    _rope_launch(gq, cos, sin, -1.0, out=dq)
+    _rope_launch(dk, cos, sin, -1.0, out=dk)     # in place: a thread reads both halves first
+    return dqkv
+
+
+class _ProjRoPEAttention(torch.autograd.Function):
+    """x -> qkv = x W^T -> RoPE(q, k) -> flash attention -> o as one node:
+    the projection GEMM applies the rotary embedding in its epilogue
+    (mxk_gemm_bf16_rope: q / k leave the GEMM rotated, no stand-alone RoPE
+    pass and no rotated copies), the attention runs on q / k / v as strided
+    views of that one buffer, and the backward takes d(qkv) of the
+    un-rotated projection from the fused attention backward into the
+    projection's input- and weight-gradient GEMMs (the weight gradient
+    straight into the flat gradient buffer, as Linear does)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, cos, sin, hq: int, hkv: int, hd: int, causal: bool, scale):
+        from .fused import _rope_launch
+        from .linear import _fwd
+        B, S, K = x.shape
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        N = weight.shape[0]
+        qkv = torch.empty((B * S, N), dtype=x.dtype, device=x.device)
+        st = _lib.lib().mxk_gemm_bf16_rope(x2.data_ptr(), weight.data_ptr(), qkv.data_ptr(),
+                                           B * S, N, K, x2.stride(0), weight.stride(0),
+                                           qkv.stride(0), cos.data_ptr(), sin.data_ptr(), S,
+                                           (hq + hkv) * hd, _lib.stream_ptr(x.device))
+        qkv = qkv.view(B, S, N)
+        q = qkv[..., :hq * hd].view(B, S, hq, hd)
+        k = qkv[..., hq * hd:(hq + hkv) * hd].view(B, S, hkv, hd)
+        v = qkv[..., (hq + hkv) * hd:].view(B, S, hkv, hd)
+        if st != 0:
+            if st != 1:
+                _lib.check(st, "mxk_gemm_bf16_rope")
+            qkv.copy_(_fwd(x2, weight).view(B, S, N))
+            _rope_launch(q, cos, sin, 1.0, out=q)      # in place
+            _rope_launch(k, cos, sin, 1.0, out=k)
+        o, lse = attn_fwd(q, k, v, causal=causal, scale=scale)
+        ctx.save_for_backward(x2, weight, q, k, v, o, lse, cos, sin)
+        ctx.causal, ctx.scale, ctx.dims, ctx.xshape = causal, scale, (hq, hkv, hd), x.shape
+        return o
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .linear import _dgrad, _weight_grad
+        x2, weight, q, k, v, o, lse, cos, sin = ctx.saved_tensors
+        dqkv = _rope_attn_backward(q, k, v, o, lse, cos, sin, dout, ctx.dims, ctx.causal, ctx.scale)
+        dqkv2 = dqkv.view(-1, dqkv.shape[-1])
+        need_x, need_w = ctx.needs_input_grad[:2]
+        dx = _dgrad(dqkv2, weight).view(ctx.xshape) if need_x else None
+        dw = _weight_grad(weight, dqkv2, x2) if need_w else None
+        return dx, dw, None, None, None, None, None, None, None
+
+
+def proj_rope_attention(x: torch.Tensor, weight: torch.Tensor, cos: torch.Tensor,
+                        sin: torch.Tensor, hq: int, hkv: int, hd: int, causal: bool = True,
+                        scale: float | None = None):
+    """o [B, S, hq, hd] = attention(RoPE(split(x W^T))) as one node (see
+    _ProjRoPEAttention); None when the layout is not the fused path's."""
+    if not (_FUSED_ROPE_BWD and _FUSED_ROPE_FWD and x.is_cuda and x.dtype == torch.bfloat16
+            and weight.dtype == torch.bfloat16 and x.dim() == 3 and weight.is_contiguous()
+            and weight.shape[0] == (hq + 2 * hkv) * hd and hd == HEAD_DIM and hkv > 0
+            and hq % hkv == 0 and (hq // hkv) % 4 == 0 and x.shape[1] % 256 == 0
+            and cos.shape[0] >= x.shape[1]):
+        return None
+    S = x.shape[1]
+    return _ProjRoPEAttention.apply(x, weight, cos[:S].float().contiguous(),
+                                    sin[:S].float().contiguous(), hq, hkv, hd, causal, scale)
+
+
+# the rotary embedding in the fused QKV projection's GEMM epilogue
+# (MXK_FUSED_ROPE_FWD=0: the GEMM, then the stand-alone RoPE pass)
+_FUSED_ROPE_FWD = os.environ.get("MXK_FUSED_ROPE_FWD", "1") != "0"
 
 
 def qkv_rope_attention(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, hq: int, hkv: int,

@@ -620,29 +620,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
       // chunks cch < 8 hold a (dims 8 cch ..), the partner cch ^ 8 holds b
       const uint4 y = *reinterpret_cast<const uint4*>(img + swz(row, cch ^ 8));
       const long tb = static_cast<long>(q0 + row) * (D / 2) + 8 * (cch & 7);
-      const float4 c0 = *reinterpret_cast<const float4*>(rcos + tb);
-      const float4 c1 = *reinterpret_cast<const float4*>(rcos + tb + 4);
-      const float4 s0 = *reinterpret_cast<const float4*>(rsin + tb);
-      const float4 s1 = *reinterpret_cast<const float4*>(rsin + tb + 4);
-      const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-      const uint32_t xw[4] = {x.x, x.y, x.z, x.w}, yw[4] = {y.x, y.y, y.z, y.w};
-      const bool lo = cch < 8;
-      uint32_t ow[4];
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        float o2[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const float own = __uint_as_float(e ? xw[w] & 0xFFFF0000u : xw[w] << 16);
-          const float par = __uint_as_float(e ? yw[w] & 0xFFFF0000u : yw[w] << 16);
-          float oa, ob;
-          mxk::rope_pair(lo ? own : par, lo ? par : own, cs[2 * w + e], -sn[2 * w + e], oa, ob);
-          o2[e] = lo ? oa : ob;
-        }
-        ow[w] = pk2(o2[0], o2[1]);
-      }
-      x = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+      const u32x4_t o = mxk::rope8_bf16(u32x4_t{x.x, x.y, x.z, x.w}, u32x4_t{y.x, y.y, y.z, y.w},
+                                        cch < 8, rcos + tb, rsin + tb, -1.f);
+      x = make_uint4(o[0], o[1], o[2], o[3]);
     }
     *reinterpret_cast<uint4*>(dbase + static_cast<long>(row) * dqt) = x;
   }

@@ -693,6 +693,27 @@ MXK_API int mxk_gemm_bf16_w13_swiglu(const void* x, const void* w13, void* gu, v
   MXK_RETURN_LAUNCH_STATUS();
 }
 
+// C = A . Bt^T with the rotary embedding applied to output columns
+// [0, rope_cols) in the epilogue (the q / k heads of a fused QKV
+// projection, head_dim 128; row t at position t % S; rcos / rsin [S][64]
+// fp32): the default schedule's K loop (52) with EPI 5, so q / k leave
+// rotated and the stand-alone RoPE pass over them disappears.  Bit for bit
+// the GEMM followed by that pass.  Tiled shapes only (M, N % 256, K % 64,
+// S % 256, M % S, rope_cols % 128); hipErrorInvalidValue otherwise.
+MXK_API int mxk_gemm_bf16_rope(const void* A, const void* Bt, void* C, int M, int N, int K,
+                               int lda, int ldb, int ldc, const float* rcos, const float* rsin,
+                               int S, int rope_cols, hipStream_t stream) {
+  auto al = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK || lda % 8 || ldb % 8 ||
+      ldc % 8 || S <= 0 || S % 256 || M % S || rope_cols < 0 || rope_cols % 128 ||
+      rope_cols > N || !al(A) || !al(Bt) || !al(C) || !rcos || !rsin || !al(rcos) || !al(rsin))
+    return static_cast<int>(hipErrorInvalidValue);
+  MXK_LAUNCH_GEMM((mxk_gemm_bf16_tn_w4k<1, 5, 0, 1>), dim3((M / BM) * (N / BN)), dim3(W4_THREADS),
+                  stream, static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(Bt),
+                  static_cast<uint16_t*>(C), M, N, K, lda, ldb, ldc, rcos, rsin, S, rope_cols);
+  MXK_RETURN_LAUNCH_STATUS();
+}
+
 // 1 if (M, N, K) takes the tiled MFMA fast path.
 MXK_API int mxk_gemm_bf16_tn_is_fast(int M, int N, int K) {
   return (M % BM == 0) && (N % BN == 0) && (K % BK == 0);

@@ -651,7 +651,10 @@ __device__ __forceinline__ void w4k_mainloop(f32x4_t (&acc)[8][8], char* smem, c
 template <int MAP, int EPI, int ABL = 0, int ORDER = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
-                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc) {
+                     uint16_t* __restrict__ C, int M, int N, int K, int lda, int ldb, int ldc,
+                     const float* __restrict__ rcos = nullptr,
+                     const float* __restrict__ rsin = nullptr, int rope_S = 0,
+                     int rope_cols = 0) {
   __shared__ __attribute__((aligned(16))) char smem[A3_LDS];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -674,6 +677,19 @@ mxk_gemm_bf16_tn_w4k(const uint16_t* __restrict__ A, const uint16_t* __restrict_
     __builtin_amdgcn_s_barrier();
     mxk::store_block_lds<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane,
                                smem + wave_s * mxk::kStoreLdsWave);
+  } else if constexpr (EPI == 5) {
+    // EPI 4 with the rotary embedding of the columns below rope_cols (the
+    // q / k heads of a fused QKV projection; each wave's 128 columns are one
+    // head)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    // an opaque lane id: the epilogue's lane-derived addresses are formed
+    // here, not hoisted above the K loop (where they spilled)
+    int lane_e = lane;
+    asm volatile("" : "+v"(lane_e));
+    mxk::store_block_lds_rope<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane_e,
+                                    smem + wave_s * mxk::kStoreLdsWave, rcos, rsin, rope_S,
+                                    n0 + wn * 128 < rope_cols);
   } else if constexpr (EPI == 2) store_block_wide<true>(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
   else store_block_narrow(acc, C, ldc, m0 + wm * 128, n0 + wn * 128, lane);
 }

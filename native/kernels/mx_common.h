@@ -60,6 +60,37 @@ __device__ __forceinline__ void rope_pair(float a, float b, float c, float s, fl
   ob = __builtin_fmaf(b, c, a * s);
 }
 
+// Eight bf16 elements of one rotate-half row rotated: `own` holds dims
+// i0 .. i0 + 7 of the lower half (lo) or of the upper half, `par` the same
+// dims of the other half; cs / sn: cos / sin at the row's position for
+// frequencies i0 .. i0 + 7 (8 floats each, 16-B aligned); sign -1: the
+// inverse rotation.  Returns the 8 rotated elements of `own`'s half, rounded
+// as the stand-alone pass (fused_ops.hip) rounds them.
+__device__ __forceinline__ u32x4_t rope8_bf16(u32x4_t own, u32x4_t par, bool lo, const float* cs,
+                                              const float* sn, float sign) {
+  const float4 c0 = *reinterpret_cast<const float4*>(cs);
+  const float4 c1 = *reinterpret_cast<const float4*>(cs + 4);
+  const float4 s0 = *reinterpret_cast<const float4*>(sn);
+  const float4 s1 = *reinterpret_cast<const float4*>(sn + 4);
+  const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  u32x4_t out;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    float o2[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float x = __uint_as_float(e ? own[w] & 0xFFFF0000u : own[w] << 16);
+      const float y = __uint_as_float(e ? par[w] & 0xFFFF0000u : par[w] << 16);
+      float oa, ob;
+      rope_pair(lo ? x : y, lo ? y : x, c[2 * w + e], sign * sv[2 * w + e], oa, ob);
+      o2[e] = lo ? oa : ob;
+    }
+    out[w] = pack2bf(o2[0], o2[1]);
+  }
+  return out;
+}
+
 // Bijective XCD-aware remap of a 1-D block id: blocks b and b+8 share an
 // XCD (round-robin dispatch), so give each XCD a contiguous run of logical
 // work ids.  Speed-only: correctness never depends on placement.
@@ -335,6 +366,49 @@ __device__ __forceinline__ void store_block_lds(const f32x4_t (&acc)[8][8], uint
       uint16_t* cp = C + static_cast<size_t>(row0 + (p ^ rot) * 64 + r) * ldc + col0 + cc;
       if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(cp));
       else *reinterpret_cast<u32x4_t*>(cp) = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __asm__ volatile("" ::: "memory");
+  }
+}
+
+// store_block_lds with the rotary embedding applied on the way out: the
+// block's 128 columns are one head (col0 % 128 == 0), row t (token) sits at
+// position t % S of its sequence (S % 64 == 0, row0 % 64 == 0); each lane
+// reads its 16-B chunk and the partner 64 columns away from the LDS rows and
+// stores its chunk rotated (rcos / rsin: [S][64] fp32).
+// rope false (wave-uniform): store_block_lds itself.
+template <bool NT = true>
+__device__ __forceinline__ void store_block_lds_rope(const f32x4_t (&acc)[8][8], uint16_t* C,
+                                                     int ldc, int row0, int col0, int lane,
+                                                     char* lds, const float* rcos,
+                                                     const float* rsin, int S, bool rope) {
+  const int crow = lane & 15, q = lane >> 4;
+  const int rr = lane >> 4, cc = (lane & 15) * 8;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint2 pk;
+        pk.x = pack2bf(acc[4 * p + ii][j][0], acc[4 * p + ii][j][1]);
+        pk.y = pack2bf(acc[4 * p + ii][j][2], acc[4 * p + ii][j][3]);
+        *reinterpret_cast<uint2*>(lds + (ii * 16 + crow) * kStoreLdsRow + (j * 16 + q * 4) * 2) = pk;
+      }
+    const int pos0 = (row0 + p * 64) % S;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int r = it * 4 + rr;
+      u32x4_t o = *reinterpret_cast<const u32x4_t*>(lds + r * kStoreLdsRow + cc * 2);
+      if (rope) {
+        const u32x4_t w = *reinterpret_cast<const u32x4_t*>(lds + r * kStoreLdsRow + (cc ^ 64) * 2);
+        const long tb = static_cast<long>(pos0 + r) * 64 + (cc & 63);
+        o = rope8_bf16(o, w, cc < 64, rcos + tb, rsin + tb, 1.f);
+      }
+      uint16_t* cp = C + static_cast<size_t>(row0 + p * 64 + r) * ldc + col0 + cc;
+      if constexpr (NT) __builtin_nontemporal_store(o, reinterpret_cast<u32x4_t*>(cp));
+      else *reinterpret_cast<u32x4_t*>(cp) = o;
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __asm__ volatile("" ::: "memory");

@@ -277,3 +277,53 @@ def test_qkv_rope_attention_fused_backward(cuda_device, B, S, Hq, Hkv, causal, m
     A.qkv_rope_attention(x3, cos, sin, Hq, Hkv, hd, causal=causal).backward(dout)
     err = (x3.grad.float() - xr.grad).abs().max().item()
     assert err < tol, ("fallback", err, tol)
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
+    (1, 256, 8, 2, True),
+    (2, 512, 16, 4, True),
+    (1, 512, 8, 1, False),
+])
+def test_proj_rope_attention_fused(cuda_device, B, S, Hq, Hkv, causal):
+    """The QKV projection with the rotary embedding in its GEMM epilogue
+    (mxk_gemm_bf16_rope), attention on strided views of its output, and the
+    fused RoPE backward (A.proj_rope_attention): the output bit for bit that
+    of the same GEMM (schedule 52, no split tail) + qkv_rope +
+    flash_attention; dx / dW those of the same chain's d(qkv) through the
+    input- and weight-gradient GEMMs; all close to the fp32 reference."""
+    from mxk8s.ops.fused import qkv_rope, rope_ref, rope_tables
+    from mxk8s.ops.gemm import gemm_bf16_tn
+    from mxk8s.ops.linear import _dgrad, _weight_grad
+    hd, dim = 128, 256
+    g = torch.Generator(device=cuda_device).manual_seed(43)
+    x = torch.randn(B, S, dim, device=cuda_device, generator=g).bfloat16()
+    w = (torch.randn((Hq + 2 * Hkv) * hd, dim, device=cuda_device, generator=g) / 8).bfloat16()
+    dout = torch.randn(B, S, Hq, hd, device=cuda_device, generator=g).bfloat16()
+    cos, sin = rope_tables(S, hd, device=cuda_device)
+
+    x1, w1 = x.clone().requires_grad_(), w.clone().requires_grad_()
+    o1 = A.proj_rope_attention(x1, w1, cos, sin, Hq, Hkv, hd, causal=causal)
+    assert o1 is not None
+    o1.backward(dout)
+
+    qkv = torch.empty(B * S, w.shape[0], device=cuda_device, dtype=torch.bfloat16)
+    gemm_bf16_tn(x.reshape(-1, dim), w, qkv)
+    qkv = qkv.view(B, S, -1).requires_grad_()
+    q, k, v = qkv_rope(qkv, cos, sin, Hq, Hkv, hd)
+    o2 = A.flash_attention(q, k, v, causal=causal)
+    o2.backward(dout)
+    assert torch.equal(o1, o2)
+    dqkv = qkv.grad.view(B * S, -1)
+    assert torch.equal(x1.grad, _dgrad(dqkv, w).view(B, S, dim))
+    assert torch.equal(w1.grad, _weight_grad(w, dqkv, x.reshape(-1, dim)))
+
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    qkvr = xr @ wr.t()
+    qr, kr, vr = qkvr.split([Hq * hd, Hkv * hd, Hkv * hd], dim=-1)
+    qr = rope_ref(qr.reshape(B, S, Hq, hd), cos, sin)
+    kr = rope_ref(kr.reshape(B, S, Hkv, hd), cos, sin)
+    A.attention_ref(qr, kr, vr.reshape(B, S, Hkv, hd), causal=causal).backward(dout.float())
+    for name, got, want in (("dx", x1.grad, xr.grad), ("dw", w1.grad, wr.grad)):
+        err = (got.float() - want).abs().max().item()
+        tol = 5e-2 * max(1.0, want.abs().max().item())
+        assert err < tol, (name, err, tol)
