@@ -595,6 +595,24 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
   // tile's slot may be any wave's image region).
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
+  // ROPE: the cos / sin rows of the block's 64 positions (16 KiB each,
+  // shared by the 4 heads) by LDS-DMA into slots 2-3 (free now), 8 pieces a
+  // wave, read from LDS by the row loop instead of one L2 round trip per row
+  const char* rtab = smem + 65536;
+  if constexpr (ROPE) {
+#pragma unroll
+    for (int pc = 0; pc < 8; ++pc) {
+      const int tbl = pc >> 2, piece = 4 * wave + (pc & 3);
+      const mxk::u32x4 rs = mxk::make_rsrc((tbl ? rsin : rcos) + static_cast<long>(q0) * (D / 2),
+                                           static_cast<unsigned>(QW * (D / 2) * 4));
+      uint32_t d0 = sm32 + 65536 + tbl * 16384 + piece * 1024;
+      asm volatile("" : "+s"(d0));
+      asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+                   :
+                   : "v"(static_cast<uint32_t>(piece * 1024 + lane * 16)), "s"(rs), "{m0}"(d0)
+                   : "memory");
+    }
+  }
   char* img = smem + wave * 16384;
 #pragma unroll
   for (int g = 0; g < 2; ++g)
@@ -608,6 +626,10 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
         *reinterpret_cast<uint2*>(img + swz(32 * g + r32, 4 * db + rg) + 8 * h) = pk;
       }
   __builtin_amdgcn_s_waitcnt(0xC07F);   // own image: no other wave reads it
+  if constexpr (ROPE) {
+    vmw<0>();                            // the table pieces, every wave's
+    __builtin_amdgcn_s_barrier();
+  }
   // lane l: chunk l & 15 of rows (l >> 4) + 4 i
   const int crow0 = lane >> 4, cch = lane & 15;
   const long dqt = dq_tok > 0 ? dq_tok : tokd;
@@ -619,9 +641,9 @@ mxk_attn_bwd_dq256_kernel(const uint16_t* __restrict__ q, const uint16_t* __rest
     if constexpr (ROPE) {
       // chunks cch < 8 hold a (dims 8 cch ..), the partner cch ^ 8 holds b
       const uint4 y = *reinterpret_cast<const uint4*>(img + swz(row, cch ^ 8));
-      const long tb = static_cast<long>(q0 + row) * (D / 2) + 8 * (cch & 7);
+      const float* ct = reinterpret_cast<const float*>(rtab) + row * (D / 2) + 8 * (cch & 7);
       const u32x4_t o = mxk::rope8_bf16(u32x4_t{x.x, x.y, x.z, x.w}, u32x4_t{y.x, y.y, y.z, y.w},
-                                        cch < 8, rcos + tb, rsin + tb, -1.f);
+                                        cch < 8, ct, ct + QW * (D / 2), -1.f);
       x = make_uint4(o[0], o[1], o[2], o[3]);
     }
     *reinterpret_cast<uint4*>(dbase + static_cast<long>(row) * dqt) = x;
