@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""In-process A/B of the attention backward between the default kernel
+"""In-process A/B of the attention backward (MODE=fwd: the forward,
+FWD_VARIANT) between the default kernel
 library and an alternative build (ALT=path.so, loaded beside it with
 RTLD_LOCAL): interleaved timing blocks on the same clock, outputs compared
 bit for bit.  Llama-3-8B step shape (B 8, S 2048, 32 q / 8 kv heads,
@@ -36,8 +37,12 @@ def main():
     o, lse = A.attn_fwd(q, k, v, causal=True)
     dout = torch.randn(B, S, Hq, D, device=dev, generator=g).bfloat16()
 
+    fwd = os.environ.get("MODE", "bwd") == "fwd"
+
     def run(name):
         _lib._lib = libs[name]
+        if fwd:
+            return A.attn_fwd(q, k, v, causal=True, variant=int(os.environ.get("FWD_VARIANT", 4)))
         return A.attn_bwd(q, k, v, o, lse, dout, variant=variant)
 
     outs = {n: [x.clone() for x in run(n)] for n in libs}
