@@ -62,6 +62,25 @@ def main():
     unfused()
     print(f"RESULT fused bit-identical to unfused: {torch.equal(fa, fb)}", flush=True)
     runs = {"fused": fused, "unfused": unfused, "plain_v9": plain}
+    if os.environ.get("ALT"):
+        # the fused call from another build of the library (in-process A/B)
+        import ctypes
+        alt = ctypes.CDLL(os.environ["ALT"], mode=ctypes.RTLD_LOCAL)
+        fn = alt.mxk_attn_bwd_rope
+        fn.restype, fn.argtypes = _lib._SIGNATURES["mxk_attn_bwd_rope"]
+        fd = torch.empty_like(qkv)
+
+        def fused_alt():
+            dq, dk, dv = slices(fd)
+            st = fn(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
+                    lse.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), ws.data_ptr(), B, S, hq,
+                    hkv, hd, q.stride(1), k.stride(1), v.stride(1), dq.stride(1), dk.stride(1),
+                    dv.stride(1), cos.data_ptr(), sin.data_ptr(), scale, 1, _lib.stream_ptr(dev))
+            assert st == 0, st
+
+        fused_alt()
+        print(f"RESULT fused bit-identical to fused_alt: {torch.equal(fa, fd)}", flush=True)
+        runs["fused_alt"] = fused_alt
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 2.0:
         for f in runs.values():
