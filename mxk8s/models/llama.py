@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -30,6 +31,7 @@ from ..ops.attention import (flash_attention, proj_rope_attention, qkv_rope_atte
                               supported as flash_supported)
 from ..ops.linear import Linear, SwiGLULinear, swiglu_mlp
 from ..ops.xent import cross_entropy
+from ..ops.embedding import Embedding
 from ..ops.fused import add_rmsnorm, qkv_rope, rmsnorm, rope_tables
 
 
@@ -157,7 +159,10 @@ class Llama(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.cfg = cfg
-        self.embed = nn.Embedding(cfg.vocab_size, cfg.dim)
+        # the weight gradient straight into the flat buffer (mxk8s.ops.embedding);
+        # MXK_DIRECT_EMBED=1 (off until measured on the GPU): nn.Embedding + AccumulateGrad otherwise
+        direct = os.environ.get("MXK_DIRECT_EMBED", "0") == "1"
+        self.embed = (Embedding if direct else nn.Embedding)(cfg.vocab_size, cfg.dim)
         self.layers = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layers)])
         self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
         self.lm_head = Linear(cfg.dim, cfg.vocab_size)
