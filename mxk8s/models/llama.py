@@ -160,8 +160,9 @@ class Llama(nn.Module):
         super().__init__()
         self.cfg = cfg
         # the weight gradient straight into the flat buffer (mxk8s.ops.embedding);
-        # MXK_DIRECT_EMBED=1 (off until measured on the GPU): nn.Embedding + AccumulateGrad otherwise
-        direct = os.environ.get("MXK_DIRECT_EMBED", "0") == "1"
+        # MXK_DIRECT_EMBED=0: nn.Embedding + AccumulateGrad (A/B; same-box step
+        # -1.1 / -1.3 ms, bit-identical losses: profiles/r6_embed/)
+        direct = os.environ.get("MXK_DIRECT_EMBED", "1") != "0"
         self.embed = (Embedding if direct else nn.Embedding)(cfg.vocab_size, cfg.dim)
         self.layers = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layers)])
         self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
