@@ -79,6 +79,9 @@ class RMSNorm(nn.Module):
         super().__init__()
         self.eps = eps
         self.weight = nn.Parameter(torch.ones(dim))
+        # gradient straight into the flat buffer (mxk8s.ops.fused._deliver_dw);
+        # MXK_DIRECT_NORM=1 (off until measured on the GPU)
+        self.weight._mxk_direct_grad = os.environ.get("MXK_DIRECT_NORM", "0") == "1"
 
     def forward(self, x):
         return rmsnorm(x, self.weight, self.eps)

@@ -50,6 +50,70 @@ def rope_ref(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, sign: float 
 # ----------------------------------------------------------------------------
 
 
+# Norm weights marked ``_mxk_direct_grad`` (mxk8s.models.llama.RMSNorm) take
+# the protocol of mxk8s.ops.linear: their gradient goes straight into
+# ``weight.main_grad`` (the kernel writes it there on the first backward
+# after zero_grad, later micro-batches add) and the DDP bucketer is told,
+# instead of autograd's AccumulateGrad add into a zero-filled flat range.
+def _direct_sink(w: torch.Tensor):
+    if getattr(w, "_mxk_direct_grad", False) and getattr(w, "main_grad", None) is not None:
+        return w.main_grad
+    return None
+
+
+def _deliver_dw(w: torch.Tensor, dw: torch.Tensor | None):
+    """Finish a norm weight's gradient: None for autograd when it went to
+    main_grad (``dw`` None: the kernel wrote it there), else ``dw``."""
+    sink = _direct_sink(w)
+    if sink is None:
+        return dw
+    if dw is not None:
+        if w._mxk_grad_fresh:
+            sink.copy_(dw)
+        else:
+            sink.add_(dw)
+    w._mxk_grad_fresh = False
+    ready = getattr(w, "_mxk_grad_ready", None)
+    if ready is not None:
+        ready()
+    return None
+
+
+def _dw_out(w: torch.Tensor) -> tuple[torch.Tensor, bool]:
+    """(buffer the kernel writes dw into, whether that is main_grad)."""
+    sink = _direct_sink(w)
+    if sink is not None and w._mxk_grad_fresh and sink.dtype == w.dtype and sink.is_contiguous():
+        return sink, True
+    return torch.empty_like(w), False
+
+
+class _RMSNormRef(torch.autograd.Function):
+    """The fp32 reference (CPU / non-bf16) with the direct-gradient protocol
+    for the weight."""
+
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        ctx.save_for_backward(x, w)
+        ctx.eps = eps
+        return rmsnorm_ref(x, w, eps)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        with torch.enable_grad():
+            xx = x.detach().requires_grad_(ctx.needs_input_grad[0])
+            ww = w.detach().requires_grad_(True)
+            y = rmsnorm_ref(xx, ww, ctx.eps)
+            ins = (xx, ww) if ctx.needs_input_grad[0] else (ww,)
+            grads = torch.autograd.grad(y, ins, dy)
+        dx = grads[0] if ctx.needs_input_grad[0] else None
+        dw = grads[-1] if ctx.needs_input_grad[1] else None
+        if dw is not None:
+            dw = _deliver_dw(w, dw)
+        return dx, dw, None
+
+
+
 class _RMSNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, eps):
@@ -72,7 +136,7 @@ class _RMSNorm(torch.autograd.Function):
         rows, H = x2.shape
         dy2 = dy.contiguous().view(rows, H)
         dx = torch.empty_like(x2)
-        dw = torch.empty_like(w)
+        dw, direct = _dw_out(w)
         L = _lib.lib()
         ws = torch.empty(L.mxk_rmsnorm_bwd_workspace(rows, H) // 4, dtype=torch.float32,
                          device=x2.device)
@@ -80,7 +144,7 @@ class _RMSNorm(torch.autograd.Function):
                                None, dx.data_ptr(), dw.data_ptr(), None, ws.data_ptr(), rows, H,
                                _lib.stream_ptr(x2.device))
         _lib.check(st, "mxk_rmsnorm_bwd")
-        return dx.view(ctx.shape), dw, None
+        return dx.view(ctx.shape), _deliver_dw(w, None if direct else dw), None
 
 
 class _AddRMSNorm(torch.autograd.Function):
@@ -110,7 +174,7 @@ class _AddRMSNorm(torch.autograd.Function):
         h, w, rstd = ctx.saved_tensors
         rows, H = h.shape
         L = _lib.lib()
-        dw = torch.empty_like(w)
+        dw, direct = _dw_out(w)
         if dy is None:
             dy = torch.zeros_like(h)
         dy2 = dy.contiguous().view(rows, H)
@@ -124,7 +188,7 @@ class _AddRMSNorm(torch.autograd.Function):
                                _lib.stream_ptr(h.device))
         _lib.check(st, "mxk_rmsnorm_bwd")
         dx = dx.view(ctx.shape)
-        return dx, dx, dw, None
+        return dx, dx, _deliver_dw(w, None if direct else dw), None
 
 
 def add_rmsnorm(x: torch.Tensor, delta: torch.Tensor, w: torch.Tensor,
@@ -138,9 +202,9 @@ def add_rmsnorm(x: torch.Tensor, delta: torch.Tensor, w: torch.Tensor,
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     if x.device.type == "cpu" or x.dtype != torch.bfloat16:
-        xf = x.float()
-        rstd = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
-        return (xf * rstd * w.float()).to(x.dtype)
+        if getattr(w, "_mxk_direct_grad", False) and torch.is_grad_enabled():
+            return _RMSNormRef.apply(x, w, eps)
+        return rmsnorm_ref(x, w, eps)
     return _RMSNorm.apply(x, w, eps)
 
 
