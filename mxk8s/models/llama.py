@@ -80,7 +80,7 @@ class RMSNorm(nn.Module):
         self.eps = eps
         self.weight = nn.Parameter(torch.ones(dim))
         # gradient straight into the flat buffer (mxk8s.ops.fused._deliver_dw);
-        # MXK_DIRECT_NORM=1 (off until measured on the GPU)
+        # MXK_DIRECT_NORM=1 (opt-in: step-neutral, profiles/r6_norm/)
         self.weight._mxk_direct_grad = os.environ.get("MXK_DIRECT_NORM", "0") == "1"
 
     def forward(self, x):
